@@ -1,0 +1,142 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: distributed Lloyd K-Means, N=10M points per GPU, D=128, K=1024, bf16.
+
+Metric (BASELINE.json): points assigned / s (whole job) and iters / s.  One *step* is one
+full Lloyd iteration on every rank: bf16 MFMA distance + fused argmin (HIP), LDS centroid
+update (HIP), ONE packed RCCL all-reduce of [sums | counts], centroid finalize (HIP).
+Nothing is skipped inside the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N
+
+Data: synthetic Gaussian blobs generated on each GPU (counter-based, world-size
+invariant), random-row centroid init.  Weak scaling: each GPU owns ``--n-per-gpu`` points.
+The reference's best published K-Means number is 177.7 M points assigned/s
+(N=25M, D=5, K=3, 8 GPUs, fp64; scripts/executions_log.csv:320) -> ``vs_baseline``.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+BASELINE_POINTS_PER_SEC = 177.7e6
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n-per-gpu", type=int, default=10_000_000)
+    ap.add_argument("--dim", type=int, default=128)
+    ap.add_argument("--k", type=int, default=1024)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp64"])
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--profile-steps", action="store_true",
+                    help="print a per-phase breakdown after the timed region")
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    a = parse(argv)
+    import torch
+    import tensorflow_distributed_clustering_amd as tdc
+    from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs
+    from tensorflow_distributed_clustering_amd.models.kmeans import LloydEngine
+    from tensorflow_distributed_clustering_amd.parallel.dist import init_comm, shard_bounds
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != a.gpus and world_env > 1:
+        print(f"[bench] warning: WORLD_SIZE={world_env} but --gpus={a.gpus}", file=sys.stderr)
+    if a.gpus > 1 and world_env == 1:
+        # self-launch one process per GPU (before touching the GPU in this process)
+        import subprocess
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={a.gpus}", "--master-addr=127.0.0.1",
+               f"--master-port={29500 + (os.getpid() % 1000)}", os.path.abspath(__file__)] + \
+              (sys.argv[1:] if argv is None else list(argv))
+        sys.exit(subprocess.call(cmd))
+
+    comm = init_comm("cuda" if torch.cuda.is_available() else "cpu")
+    dev = comm.device
+    world, rank = comm.world_size, comm.rank
+    n_global = a.n_per_gpu * world if a.scaling == "weak" else a.n_per_gpu
+    s, e = shard_bounds(n_global, world, rank)
+    dt = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp64": torch.float64}[a.dtype]
+    x = gaussian_blobs(e - s, a.dim, a.k, seed=a.seed, row_offset=s, dtype=dt, device=dev)
+    cfg = tdc.ClusterConfig(n_clusters=a.k, max_iter=a.steps, dtype=a.dtype, init="random",
+                            seed=a.seed, compute_inertia=False)
+    eng = LloydEngine(x, cfg, comm, n_global, s)
+
+    for _ in range(a.warmup):
+        eng.step()
+    comm.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        eng.step()
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    comm.barrier()
+    elapsed = comm.max_scalar(time.perf_counter() - t0)
+
+    ms = elapsed / max(1, a.steps) * 1e3
+    pps = n_global * a.steps / elapsed
+    breakdown = None
+    if a.profile_steps and dev.type == "cuda":
+        breakdown = phase_breakdown(eng, torch, dev)
+    if rank == 0:
+        out = {
+            "metric": "points_assigned_per_sec",
+            "value": pps,
+            "unit": "points/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": ms,
+            "higher_is_better": True,
+            "scaling": a.scaling,
+            "vs_baseline": pps / BASELINE_POINTS_PER_SEC,
+            "dtype": a.dtype,
+            "data": "synthetic gaussian blobs (on-device, counter-based), random-row init",
+            "iters_per_sec": 1e3 / ms,
+            "backend": eng.local.name,
+            "config": {"model": "kmeans-lloyd", "global_batch": n_global, "seq_len": a.dim,
+                       "K": a.k, "D": a.dim, "points_per_gpu": e - s,
+                       "parallelism": f"dp{world}"},
+        }
+        if breakdown:
+            out["phase_ms"] = breakdown
+        print(json.dumps(out), flush=True)
+
+
+def phase_breakdown(eng, torch, dev, reps: int = 5):
+    """Per-phase device time of one step (events; diagnostic only, after the timed run)."""
+    ev = lambda: torch.cuda.Event(enable_timing=True)
+    names = ["zero", "assign", "update", "allreduce", "finalize"]
+    tot = {n: 0.0 for n in names}
+    loc = eng.local
+    for _ in range(reps):
+        e = [ev() for _ in range(len(names) + 1)]
+        e[0].record()
+        eng.buf.zero_(); e[1].record()
+        if hasattr(loc, "cm2"):
+            loc.ops.assign_bf16(loc.x, loc.cm2, loc.cnorm, eng.labels, None); e[2].record()
+            loc.ops.update(loc.x, eng.labels, eng.sums, eng.counts); e[3].record()
+        else:
+            loc.step(eng.C, eng.labels, None, eng.sums, eng.counts); e[2].record(); e[3].record()
+        eng.comm.allreduce_bucketed_(eng.buf, eng.bucket_bytes); e[4].record()
+        loc.finalize(eng.sums, eng.counts, eng.C, None); e[5].record()
+        torch.cuda.synchronize(dev)
+        for i, n in enumerate(names):
+            tot[n] += e[i].elapsed_time(e[i + 1]) / reps
+    return {k: round(v, 4) for k, v in tot.items()}
+
+
+if __name__ == "__main__":
+    main()

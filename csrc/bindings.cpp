@@ -1,0 +1,218 @@
+// torch.ops.tdc.* custom ops over the HIP launchers in kernels.h.
+// Out-parameter style (no allocation inside an op) so an iteration can be captured into
+// a HIP graph and so the engine owns every buffer (one packed comm buffer per run).
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+
+#include <mutex>
+#include <unordered_map>
+
+#include "kernels.h"
+
+namespace {
+
+// PyTorch-ROCm exposes HIP devices as device type "cuda" ("masquerading"): use the
+// masquerading guard/stream so we launch on exactly torch.cuda.current_stream().
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+using DevGuard = at::hip::HIPGuardMasqueradingAsCUDA;
+
+int num_cus(int dev) {
+  static std::mutex mu;
+  static std::unordered_map<int, int> cache;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(dev);
+  if (it != cache.end()) return it->second;
+  int v = 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+    v = 256;
+  cache[dev] = v;
+  return v;
+}
+
+int dcode(at::ScalarType t) {
+  switch (t) {
+    case at::kFloat: return TDC_F32;
+    case at::kDouble: return TDC_F64;
+    case at::kBFloat16: return TDC_BF16;
+    default: TORCH_CHECK(false, "tdc: unsupported dtype ", t);
+  }
+  return -1;
+}
+
+void check(int err, const char* what) {
+  TORCH_CHECK(err == 0, "tdc: ", what, " failed: ", hipGetErrorString((hipError_t)err),
+              " (code ", err, ")");
+}
+
+void check_cuda(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "tdc: ", name, " must be a GPU tensor");
+}
+
+void* opt_ptr(const std::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? t->data_ptr() : nullptr;
+}
+
+void check_rows(const at::Tensor& X, const char* name) {
+  TORCH_CHECK(X.dim() == 2, "tdc: ", name, " must be 2-D");
+  TORCH_CHECK(X.stride(1) == 1, "tdc: ", name, " rows must be contiguous");
+}
+
+// ------------------------------------------------------------------------------------
+void assign_bf16(const at::Tensor& X, const at::Tensor& Cm2, const at::Tensor& cnorm,
+                 at::Tensor& labels, const std::optional<at::Tensor>& mind) {
+  check_cuda(X, "X");
+  check_rows(X, "X");
+  TORCH_CHECK(X.scalar_type() == at::kBFloat16 && Cm2.scalar_type() == at::kBFloat16,
+              "tdc.assign_bf16: X and Cm2 must be bfloat16");
+  TORCH_CHECK(cnorm.scalar_type() == at::kFloat && labels.scalar_type() == at::kInt,
+              "tdc.assign_bf16: cnorm fp32, labels int32");
+  TORCH_CHECK(Cm2.is_contiguous() && cnorm.is_contiguous() && labels.is_contiguous(),
+              "tdc.assign_bf16: Cm2/cnorm/labels must be contiguous");
+  const int64_t N = X.size(0);
+  const int DP = (int)Cm2.size(1);
+  const int Kp = (int)Cm2.size(0);
+  TORCH_CHECK(DP == 32 || DP == 64 || DP == 128 || DP == 256,
+              "tdc.assign_bf16: padded dim must be 32/64/128/256, got ", DP);
+  TORCH_CHECK(X.size(1) >= DP, "tdc.assign_bf16: X has fewer columns than Cm2");
+  TORCH_CHECK(X.stride(0) % 8 == 0 && (reinterpret_cast<uintptr_t>(X.data_ptr()) % 16) == 0,
+              "tdc.assign_bf16: X rows must be 16-byte aligned");
+  TORCH_CHECK(Kp % 64 == 0 && cnorm.numel() >= Kp, "tdc.assign_bf16: Kp must be a multiple of 64");
+  TORCH_CHECK(labels.numel() >= N, "tdc.assign_bf16: labels too small");
+  float* md = nullptr;
+  if (mind.has_value() && mind->defined()) {
+    TORCH_CHECK(mind->scalar_type() == at::kFloat && mind->numel() >= N && mind->is_contiguous(),
+                "tdc.assign_bf16: mind must be fp32 [N]");
+    md = mind->data_ptr<float>();
+  }
+  const DevGuard guard(X.device());
+  check(tdc_assign_mfma_bf16(X.data_ptr(), N, X.stride(0), DP, Cm2.data_ptr(),
+                             cnorm.data_ptr<float>(), Kp, labels.data_ptr<int32_t>(), md,
+                             cur_stream()),
+        "assign_bf16");
+}
+
+void assign_simt(const at::Tensor& X, const at::Tensor& C, at::Tensor& labels,
+                 const std::optional<at::Tensor>& mind) {
+  check_cuda(X, "X");
+  check_rows(X, "X");
+  TORCH_CHECK(C.scalar_type() == X.scalar_type() && C.is_contiguous(), "tdc.assign_simt: C");
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.numel() >= X.size(0), "tdc.assign_simt: labels");
+  const DevGuard guard(X.device());
+  check(tdc_assign_simt(dcode(X.scalar_type()), X.data_ptr(), X.size(0), X.stride(0),
+                        (int)C.size(1), C.data_ptr(), (int)C.size(0), labels.data_ptr<int32_t>(),
+                        opt_ptr(mind), cur_stream()),
+        "assign_simt");
+}
+
+bool lloyd_small_supported(at::ScalarType dtype, int64_t K, int64_t D) {
+  if (dtype != at::kFloat && dtype != at::kDouble) return false;
+  return tdc_lloyd_small_supported(dcode(dtype), (int)K, (int)D) != 0;
+}
+
+void lloyd_small(const at::Tensor& X, const at::Tensor& C, at::Tensor& labels,
+                 const std::optional<at::Tensor>& mind, at::Tensor& sums, at::Tensor& counts) {
+  check_cuda(X, "X");
+  check_rows(X, "X");
+  TORCH_CHECK(C.scalar_type() == X.scalar_type() && C.is_contiguous(), "tdc.lloyd_small: C");
+  TORCH_CHECK(sums.scalar_type() == counts.scalar_type(), "tdc.lloyd_small: sums/counts dtype");
+  TORCH_CHECK(sums.is_contiguous() && counts.is_contiguous(), "tdc.lloyd_small: contiguity");
+  const DevGuard guard(X.device());
+  check(tdc_lloyd_small(dcode(X.scalar_type()), dcode(sums.scalar_type()), X.data_ptr(),
+                        X.size(0), X.stride(0), (int)C.size(1), C.data_ptr(), (int)C.size(0),
+                        labels.data_ptr<int32_t>(), opt_ptr(mind), sums.data_ptr(),
+                        counts.data_ptr(), cur_stream()),
+        "lloyd_small");
+}
+
+void update(const at::Tensor& X, const at::Tensor& labels, at::Tensor& sums, at::Tensor& counts) {
+  check_cuda(X, "X");
+  check_rows(X, "X");
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous(), "tdc.update: labels int32");
+  TORCH_CHECK(sums.dim() == 2 && sums.is_contiguous() && counts.is_contiguous(), "tdc.update: sums");
+  TORCH_CHECK(sums.scalar_type() == counts.scalar_type(), "tdc.update: sums/counts dtype");
+  TORCH_CHECK(X.size(1) >= sums.size(1), "tdc.update: X narrower than sums");
+  TORCH_CHECK(labels.numel() >= X.size(0), "tdc.update: labels shorter than X");
+  TORCH_CHECK(counts.numel() >= sums.size(0), "tdc.update: counts shorter than K");
+  const DevGuard guard(X.device());
+  check(tdc_update_lds(dcode(X.scalar_type()), dcode(sums.scalar_type()), X.data_ptr(), X.size(0),
+                       X.stride(0), (int)sums.size(1), labels.data_ptr<int32_t>(),
+                       (int)sums.size(0), sums.data_ptr(), counts.data_ptr(),
+                       num_cus(X.device().index()), cur_stream()),
+        "update");
+}
+
+bool fcm_small_supported(at::ScalarType dtype, int64_t K, int64_t D) {
+  if (dtype != at::kFloat && dtype != at::kDouble) return false;
+  return tdc_fcm_small_supported(dcode(dtype), (int)K, (int)D) != 0;
+}
+
+void fcm_small(const at::Tensor& X, const at::Tensor& C, double m, bool nan_to_zero,
+               at::Tensor& labels, at::Tensor& wx, at::Tensor& ws) {
+  check_cuda(X, "X");
+  check_rows(X, "X");
+  TORCH_CHECK(C.scalar_type() == X.scalar_type() && C.is_contiguous(), "tdc.fcm_small: C");
+  TORCH_CHECK(wx.scalar_type() == ws.scalar_type() && wx.is_contiguous() && ws.is_contiguous(),
+              "tdc.fcm_small: wx/ws");
+  const DevGuard guard(X.device());
+  check(tdc_fcm_small(dcode(X.scalar_type()), dcode(wx.scalar_type()), X.data_ptr(), X.size(0),
+                      X.stride(0), (int)C.size(1), C.data_ptr(), (int)C.size(0), m,
+                      nan_to_zero ? 1 : 0, labels.data_ptr<int32_t>(), wx.data_ptr(),
+                      ws.data_ptr(), cur_stream()),
+        "fcm_small");
+}
+
+void finalize(const std::optional<at::Tensor>& sums, const std::optional<at::Tensor>& counts,
+              at::Tensor& C, int64_t policy, const std::optional<at::Tensor>& shift,
+              const std::optional<at::Tensor>& Cm2, const std::optional<at::Tensor>& cnorm) {
+  check_cuda(C, "C");
+  TORCH_CHECK(C.is_contiguous() && C.dim() == 2, "tdc.finalize: C");
+  const int K = (int)C.size(0), D = (int)C.size(1);
+  int acc = TDC_F64;
+  if (sums.has_value() && sums->defined()) {
+    TORCH_CHECK(counts.has_value() && counts->defined(), "tdc.finalize: counts required");
+    TORCH_CHECK(sums->is_contiguous() && sums->numel() == (int64_t)K * D, "tdc.finalize: sums");
+    acc = dcode(sums->scalar_type());
+  }
+  int Kp = K, DP = D;
+  if (Cm2.has_value() && Cm2->defined()) {
+    TORCH_CHECK(Cm2->scalar_type() == at::kBFloat16 && Cm2->is_contiguous(), "tdc.finalize: Cm2");
+    TORCH_CHECK(cnorm.has_value() && cnorm->defined(), "tdc.finalize: cnorm required with Cm2");
+    Kp = (int)Cm2->size(0);
+    DP = (int)Cm2->size(1);
+    TORCH_CHECK(Kp >= K && DP >= D, "tdc.finalize: Cm2 smaller than C");
+  }
+  float* sh = nullptr;
+  if (shift.has_value() && shift->defined()) {
+    TORCH_CHECK(shift->scalar_type() == at::kFloat, "tdc.finalize: shift fp32");
+    sh = shift->data_ptr<float>();
+  }
+  const DevGuard guard(C.device());
+  check(tdc_finalize(acc, dcode(C.scalar_type()), opt_ptr(sums), opt_ptr(counts), K, D,
+                     C.data_ptr(), (int)policy, sh, opt_ptr(Cm2),
+                     static_cast<float*>(opt_ptr(cnorm)), Kp, DP, cur_stream()),
+        "finalize");
+}
+
+}  // namespace
+
+TORCH_LIBRARY(tdc, m) {
+  m.def("assign_bf16(Tensor X, Tensor Cm2, Tensor cnorm, Tensor(a!) labels, Tensor(b!)? mind) -> ()");
+  m.def("assign_simt(Tensor X, Tensor C, Tensor(a!) labels, Tensor(b!)? mind) -> ()");
+  m.def("lloyd_small_supported(ScalarType dtype, int K, int D) -> bool", &lloyd_small_supported);
+  m.def("lloyd_small(Tensor X, Tensor C, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!) sums, Tensor(d!) counts) -> ()");
+  m.def("update(Tensor X, Tensor labels, Tensor(a!) sums, Tensor(b!) counts) -> ()");
+  m.def("fcm_small_supported(ScalarType dtype, int K, int D) -> bool", &fcm_small_supported);
+  m.def("fcm_small(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) wx, Tensor(c!) ws) -> ()");
+  m.def("finalize(Tensor? sums, Tensor? counts, Tensor(a!) C, int policy, Tensor(b!)? shift, Tensor(c!)? Cm2, Tensor(d!)? cnorm) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(tdc, CUDA, m) {
+  m.impl("assign_bf16", &assign_bf16);
+  m.impl("assign_simt", &assign_simt);
+  m.impl("lloyd_small", &lloyd_small);
+  m.impl("update", &update);
+  m.impl("fcm_small", &fcm_small);
+  m.impl("finalize", &finalize);
+}

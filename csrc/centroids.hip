@@ -1,0 +1,98 @@
+// N3: centroid finalize + next-iteration operand prep, one wave per centroid row.
+//
+// Reference (scripts/distribuitedClustering.py:257-263): on /cpu:0, AddN of the tower
+// partials, Tile/Reshape of the counts, Div, Transpose, Assign.  Here every rank runs this
+// on its replicated copy right after the all-reduce:
+//   c_k = sums_k / count_k            (empty cluster: keep | NaN (reference) | zero)
+//   shift = max_k ||c_k - c_k_old||^2  (for the optional tolerance stop)
+// and, for the bf16 MFMA assignment, writes its operands in the same pass:
+//   Cm2[k] = -2 * bf16(c_k)   (exact scaling), cnorm[k] = ||bf16(c_k)||^2 (fp32),
+//   pad rows k >= K: Cm2 = 0, cnorm = 3e38 (never selected).
+#include "tdc_common.h"
+#include "kernels.h"
+
+namespace tdc {
+
+template <typename ACC, typename CT>
+__global__ __launch_bounds__(256) void finalize_kernel(const ACC* __restrict__ sums,
+                                                       const ACC* __restrict__ counts, int K,
+                                                       int D, CT* __restrict__ C, int policy,
+                                                       float* __restrict__ shift,
+                                                       __bf16* __restrict__ Cm2,
+                                                       float* __restrict__ cnorm, int Kp, int DP) {
+  const int lane = threadIdx.x & 63;
+  const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k >= Kp) return;
+  if (k >= K) {
+    if (Cm2)
+      for (int d = lane; d < DP; d += 64) Cm2[(int64_t)k * DP + d] = (__bf16)0.f;
+    if (cnorm && lane == 0) cnorm[k] = 3.0e38f;
+    return;
+  }
+  float sh = 0.f, nrm = 0.f;
+  ACC cnt = sums ? counts[k] : (ACC)1;
+  const int dend = Cm2 ? (DP > D ? DP : D) : D;
+  for (int d = lane; d < dend; d += 64) {
+    if (d < D) {
+      const CT old = C[(int64_t)k * D + d];
+      CT nw = old;
+      if (sums) {
+        if (cnt > (ACC)0) {
+          nw = (CT)(sums[(int64_t)k * D + d] / cnt);
+        } else if (policy == 1) {
+          nw = (CT)NAN;
+        } else if (policy == 2) {
+          nw = (CT)0;
+        }
+        C[(int64_t)k * D + d] = nw;
+        const float df = (float)nw - (float)old;
+        sh += df * df;
+      }
+      if (Cm2) {
+        const __bf16 b = (__bf16)(float)nw;
+        const float bf = (float)b;
+        Cm2[(int64_t)k * DP + d] = (__bf16)(-2.f * bf);
+        nrm = fmaf(bf, bf, nrm);
+      }
+    } else if (Cm2 && d < DP) {
+      Cm2[(int64_t)k * DP + d] = (__bf16)0.f;
+    }
+  }
+  if (sums && shift) {
+    sh = wave_sum(sh);
+    if (lane == 0) atomicMax(reinterpret_cast<unsigned*>(shift), __float_as_uint(sh));
+  }
+  if (cnorm) {
+    nrm = wave_sum(nrm);
+    if (lane == 0) cnorm[k] = nrm;
+  }
+}
+
+template <typename ACC, typename CT>
+int launch_finalize(const void* sums, const void* counts, int K, int D, void* C, int policy,
+                    float* shift, void* Cm2, float* cnorm, int Kp, int DP, hipStream_t s) {
+  const int rows = Cm2 ? (Kp > K ? Kp : K) : K;
+  hipLaunchKernelGGL((finalize_kernel<ACC, CT>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0,
+                     s, (const ACC*)sums, (const ACC*)counts, K, D, (CT*)C, policy, shift,
+                     (__bf16*)Cm2, cnorm, Kp, DP);
+  TDC_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace tdc
+
+using namespace tdc;
+
+int tdc_finalize(int acc_dtype, int c_dtype, const void* sums, const void* counts, int K, int D,
+                 void* C, int policy, float* shift, void* Cm2, float* cnorm, int Kp, int DP,
+                 hipStream_t s) {
+  if (acc_dtype == TDC_F64 && c_dtype == TDC_F32)
+    return launch_finalize<double, float>(sums, counts, K, D, C, policy, shift, Cm2, cnorm, Kp, DP, s);
+  if (acc_dtype == TDC_F32 && c_dtype == TDC_F32)
+    return launch_finalize<float, float>(sums, counts, K, D, C, policy, shift, Cm2, cnorm, Kp, DP, s);
+  if (acc_dtype == TDC_F64 && c_dtype == TDC_F64)
+    return launch_finalize<double, double>(sums, counts, K, D, C, policy, shift, Cm2, cnorm, Kp, DP, s);
+  if (acc_dtype == TDC_F32 && c_dtype == TDC_F64)
+    return launch_finalize<float, double>(sums, counts, K, D, C, policy, shift, Cm2, cnorm, Kp, DP, s);
+  return (int)hipErrorInvalidValue;
+}

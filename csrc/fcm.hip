@@ -1,0 +1,175 @@
+// N4/N5: fused Fuzzy C-Means tower for small K x D (the reference's FCM configs:
+// D=5, K<=15, fp64; image segmentation D=3, K=3).
+//
+// Reference op chain per GPU per iteration (scripts/distribuitedClustering.py:108-137):
+//   Tile x2, Sub, Square, Sum, Sqrt  -> d [N,K]
+//   Pow(d, -2/(M-1)), Transpose, Sum, Div -> u [K,N]
+//   IsNan/Select (NaN -> 0), Pow(u, M) -> W
+//   MatMul(W, X) [K,D], Sum(W, 1) [K]           (+ CPU argmax label pass :141)
+// Here ONE kernel reads each point once and keeps sum_i w_ki x_i and sum_i w_ki in
+// VGPRs (static register tiles), then reduces wave -> LDS -> one global atomic per
+// output per block.  d^(-2/(m-1)) is computed as exp2(log2(d^2) * -1/(m-1)) so no
+// sqrt is needed; the argmax label comes for free.
+//
+// nan_to_zero = 1 reproduces the reference guard (a point ON a centroid gets zero
+// membership everywhere, :125-126); 0 gives the correct one-hot membership.
+#include "tdc_common.h"
+#include "kernels.h"
+
+namespace tdc {
+
+__device__ __forceinline__ float tdc_exp2(float v) { return exp2f(v); }
+__device__ __forceinline__ double tdc_exp2(double v) { return exp2(v); }
+__device__ __forceinline__ float tdc_log2(float v) { return log2f(v); }
+__device__ __forceinline__ double tdc_log2(double v) { return log2(v); }
+
+template <typename T, typename ACC, int KMAX, int DMAX>
+__global__ __launch_bounds__(256) void fcm_small_kernel(
+    const T* __restrict__ X, int64_t N, int64_t ldx, int D, const T* __restrict__ C, int K,
+    T expo, T m, int nan_to_zero, int32_t* __restrict__ labels, ACC* __restrict__ wx,
+    ACC* __restrict__ ws) {
+  __shared__ T s_c[KMAX * DMAX];
+  __shared__ T s_red[4][KMAX * (DMAX + 1)];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < KMAX * DMAX; i += 256) {
+    const int k = i / DMAX, d = i % DMAX;
+    s_c[i] = (k < K && d < D) ? C[k * D + d] : (T)0;
+  }
+  __syncthreads();
+
+  T acc[KMAX][DMAX];
+  T wsum[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    wsum[k] = 0;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) acc[k][d] = 0;
+  }
+  const T inf = (T)INFINITY;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + tid; i < N; i += stride) {
+    T x[DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) x[d] = (d < D) ? X[i * ldx + d] : (T)0;
+    T t[KMAX];
+    T tsum = 0;
+    int nzero = 0;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      T dd = 0;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) {
+        const T df = x[d] - s_c[k * DMAX + d];
+        dd = fma(df, df, dd);
+      }
+      const bool on = (k < K);
+      t[k] = !on ? (T)0 : (dd == (T)0 ? inf : tdc_exp2(tdc_log2(dd) * expo));
+      nzero += (on && dd == (T)0);
+      tsum += t[k];
+    }
+    // memberships u_k, argmax label, weights w_k = u_k^m (all in t[])
+    int best = 0;
+    T bu = (T)-1;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      T u;
+      if (nzero == 0) {
+        u = t[k] / tsum;
+      } else if (nan_to_zero) {
+        u = (T)0;  // inf/inf = NaN -> 0 and finite/inf = 0  (reference guard)
+      } else {
+        u = (t[k] == inf) ? (T)1 / (T)nzero : (T)0;
+      }
+      if (k < K && u > bu) {
+        bu = u;
+        best = k;
+      }
+      t[k] = (u > (T)0) ? tdc_exp2(m * tdc_log2(u)) : (T)0;
+    }
+    labels[i] = best;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      wsum[k] += t[k];
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) acc[k][d] = fma(t[k], x[d], acc[k][d]);
+    }
+  }
+
+  const int lane = tid & 63, w = tid >> 6;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+#pragma unroll
+    for (int d = 0; d <= DMAX; ++d) {
+      T v = (d < DMAX) ? acc[k][d] : wsum[k];
+      v = wave_sum(v);
+      if (lane == 0) s_red[w][k * (DMAX + 1) + d] = v;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < K * (DMAX + 1); i += 256) {
+    const int k = i / (DMAX + 1), d = i % (DMAX + 1);
+    if (d >= D && d != DMAX) continue;
+    const T v = s_red[0][i] + s_red[1][i] + s_red[2][i] + s_red[3][i];
+    if (v == (T)0) continue;
+    if (d == DMAX) atomic_add(&ws[k], (ACC)v);
+    else atomic_add(&wx[k * D + d], (ACC)v);
+  }
+}
+
+template <typename T, typename ACC, int KMAX, int DMAX>
+int launch_fcm(const void* X, int64_t N, int64_t ldx, int D, const void* C, int K, double m,
+               int nan_to_zero, int32_t* labels, void* wx, void* ws, hipStream_t s) {
+  int64_t g = (N + 256 * 8 - 1) / (256 * 8);
+  if (g < 1) g = 1;
+  if (g > 2048) g = 2048;
+  const T expo = (T)(-1.0 / (m - 1.0));
+  hipLaunchKernelGGL((fcm_small_kernel<T, ACC, KMAX, DMAX>), dim3((unsigned)g), dim3(256), 0, s,
+                     (const T*)X, N, ldx, D, (const T*)C, K, expo, (T)m, nan_to_zero, labels,
+                     (ACC*)wx, (ACC*)ws);
+  TDC_CHECK_LAUNCH();
+  return 0;
+}
+
+template <typename T, typename ACC>
+int dispatch_fcm(const void* X, int64_t N, int64_t ldx, int D, const void* C, int K, double m,
+                 int nz, int32_t* labels, void* wx, void* ws, hipStream_t s) {
+#define TDC_FCM(KM, DM) \
+  if (K <= KM && D <= DM) return launch_fcm<T, ACC, KM, DM>(X, N, ldx, D, C, K, m, nz, labels, wx, ws, s);
+  TDC_FCM(4, 4)
+  TDC_FCM(4, 8)
+  TDC_FCM(8, 4)
+  TDC_FCM(8, 8)
+  TDC_FCM(16, 4)
+  if constexpr (sizeof(T) == 4) {
+    TDC_FCM(16, 8)
+    TDC_FCM(32, 4)
+  } else {
+    TDC_FCM(16, 5)
+  }
+#undef TDC_FCM
+  return (int)hipErrorInvalidValue;
+}
+
+}  // namespace tdc
+
+using namespace tdc;
+
+int tdc_fcm_small_supported(int dtype, int K, int D) {
+  if (dtype == TDC_F32) return (K <= 16 && D <= 8) || (K <= 32 && D <= 4);
+  if (dtype == TDC_F64) return (K <= 8 && D <= 8) || (K <= 16 && D <= 5);
+  return 0;
+}
+
+int tdc_fcm_small(int dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
+                  const void* C, int K, double m, int nan_to_zero, int32_t* labels, void* wx,
+                  void* ws, hipStream_t s) {
+  if (N <= 0) return 0;
+  if (dtype == TDC_F32) {
+    if (acc_dtype == TDC_F64)
+      return dispatch_fcm<float, double>(X, N, ldx, D, C, K, m, nan_to_zero, labels, wx, ws, s);
+    return dispatch_fcm<float, float>(X, N, ldx, D, C, K, m, nan_to_zero, labels, wx, ws, s);
+  }
+  if (dtype == TDC_F64)
+    return dispatch_fcm<double, double>(X, N, ldx, D, C, K, m, nan_to_zero, labels, wx, ws, s);
+  return (int)hipErrorInvalidValue;
+}

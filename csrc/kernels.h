@@ -1,0 +1,47 @@
+// Host-side launcher API of the tdc HIP kernels (raw pointers + stream; no torch
+// dependency, so the kernels compile with hipcc alone and the torch bindings with g++).
+// Every launcher returns 0 or a hipError_t code.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// dtype codes shared with the bindings
+enum TdcDtype { TDC_F32 = 0, TDC_F64 = 1, TDC_BF16 = 2, TDC_FP8 = 3 };
+
+// N1/N6  bf16 MFMA distance + argmin. X [N, ldx] bf16 (first DP columns used, DP in
+// {32,64,128,256}), Cm2 [Kp, DP] bf16 = -2*c, cnorm [Kp] fp32 (pad rows: 0 / 3e38),
+// Kp % 64 == 0.  labels int32 [N]; mind fp32 [N] (nullable) = min squared distance.
+int tdc_assign_mfma_bf16(const void* X, int64_t N, int64_t ldx, int DP, const void* Cm2,
+                         const float* cnorm, int Kp, int32_t* labels, float* mind,
+                         hipStream_t stream);
+
+// N1 (exact)  SIMT difference-form assignment for fp32/fp64, any K, D <= 64.
+int tdc_assign_simt(int dtype, const void* X, int64_t N, int64_t ldx, int D, const void* C,
+                    int K, int32_t* labels, void* mind, hipStream_t stream);
+
+// Fused small-K Lloyd step (assign + per-cluster sums/counts in registers), fp32/fp64.
+// Returns hipErrorInvalidValue if (K, D) exceeds the compiled register tiles.
+int tdc_lloyd_small(int dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
+                    const void* C, int K, int32_t* labels, void* mind, void* sums,
+                    void* counts, hipStream_t stream);
+int tdc_lloyd_small_supported(int dtype, int K, int D);
+
+// N2  LDS-privatised, D-sliced per-cluster sums/counts. sums [K, D], counts [K] must be
+// zeroed by the caller (accumulated with global atomics).  x_dtype: f32/f64/bf16.
+int tdc_update_lds(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
+                   const int32_t* labels, int K, void* sums, void* counts, int num_cus,
+                   hipStream_t stream);
+
+// N4/N5  fused small-K Fuzzy C-Means tower: sum_i w_ki x_i, sum_i w_ki, argmax labels.
+int tdc_fcm_small(int dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
+                  const void* C, int K, double m, int nan_to_zero, int32_t* labels, void* wx,
+                  void* ws, hipStream_t stream);
+int tdc_fcm_small_supported(int dtype, int K, int D);
+
+// N3  finalize: C = sums/counts (empty policy), max shift^2 -> shift (float, atomic max),
+// optional bf16 prep of the next assignment (Cm2 [Kp, DP] = -2*bf16(c), cnorm [Kp]).
+// sums == nullptr: prep only (C unchanged).
+// policy: 0 keep, 1 nan, 2 zero.
+int tdc_finalize(int acc_dtype, int c_dtype, const void* sums, const void* counts, int K,
+                 int D, void* C, int policy, float* shift, void* Cm2, float* cnorm, int Kp,
+                 int DP, hipStream_t stream);

@@ -1,0 +1,388 @@
+// Exact-arithmetic (fp32 / fp64) K-Means kernels for low-dimensional data, and the
+// LDS-privatised centroid update (N2) used by every dtype.
+//
+// * lloyd_small: ONE pass over the shard computes labels AND per-cluster sums/counts.
+//   This is the whole reference K-Means tower (scripts/distribuitedClustering.py:217-248:
+//   Tile/Sub/Square/Sum/ArgMin + K x (Where, Gather, Mean) + CPU Bincount) for the
+//   reference's own configs (D=5, K<=15, fp64).  Distances use the difference form
+//   sum((x-c)^2) like the reference; the per-cluster partials live in VGPRs
+//   (predicated FMA, static indices) so there is no atomic contention even at K=3,
+//   and are reduced wave -> LDS -> one global atomic per (cluster, dim) per block.
+// * assign_simt: difference-form argmin for larger K (centroids staged through LDS).
+// * update_lds: per-block LDS histogram of sum(x) and count, sliced over D so that
+//   K x D_slice fits LDS; one flush of global atomics per block.
+#include "tdc_common.h"
+#include "kernels.h"
+
+namespace tdc {
+
+// ------------------------------------------------------------------------------------
+// fused small-K Lloyd step
+// ------------------------------------------------------------------------------------
+template <typename T, typename ACC, int KMAX, int DMAX>
+__global__ __launch_bounds__(256) void lloyd_small_kernel(
+    const T* __restrict__ X, int64_t N, int64_t ldx, int D, const T* __restrict__ C, int K,
+    int32_t* __restrict__ labels, T* __restrict__ mind, ACC* __restrict__ sums,
+    ACC* __restrict__ counts) {
+  __shared__ T s_c[KMAX * DMAX];
+  __shared__ T s_red[4][KMAX * (DMAX + 1)];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < KMAX * DMAX; i += 256) {
+    const int k = i / DMAX, d = i % DMAX;
+    s_c[i] = (k < K && d < D) ? C[k * D + d] : (T)0;
+  }
+  __syncthreads();
+
+  T acc[KMAX][DMAX];
+  int cnt[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    cnt[k] = 0;
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) acc[k][d] = 0;
+  }
+
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + tid; i < N; i += stride) {
+    T x[DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) x[d] = (d < D) ? X[i * ldx + d] : (T)0;
+    T bd = (T)0;
+    int best = 0;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      if (k < K) {
+        T dd = 0;
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) {
+          const T df = x[d] - s_c[k * DMAX + d];
+          dd = fma(df, df, dd);
+        }
+        if (k == 0 || dd < bd) {  // strict: first minimum wins (TF ArgMin)
+          bd = dd;
+          best = k;
+        }
+      }
+    }
+    labels[i] = best;
+    if (mind) mind[i] = bd;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const T sel = (k == best) ? (T)1 : (T)0;
+      cnt[k] += (k == best);
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) acc[k][d] = fma(sel, x[d], acc[k][d]);
+    }
+  }
+
+  // wave reduce -> LDS -> block total -> one global atomic per (k, d)
+  const int lane = tid & 63, w = tid >> 6;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+#pragma unroll
+    for (int d = 0; d <= DMAX; ++d) {
+      T v = (d < DMAX) ? acc[k][d] : (T)cnt[k];
+      v = wave_sum(v);
+      if (lane == 0) s_red[w][k * (DMAX + 1) + d] = v;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < K * (DMAX + 1); i += 256) {
+    const int k = i / (DMAX + 1), d = i % (DMAX + 1);
+    if (d >= D && d != DMAX) continue;
+    const T v = s_red[0][i] + s_red[1][i] + s_red[2][i] + s_red[3][i];
+    if (d == DMAX) {
+      if (v != (T)0) atomic_add(&counts[k], (ACC)v);
+    } else if (v != (T)0) {
+      atomic_add(&sums[k * D + d], (ACC)v);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// exact assignment, any K (centroid tiles through LDS), D <= DMAX
+// ------------------------------------------------------------------------------------
+template <typename T, int DMAX>
+__global__ __launch_bounds__(256) void assign_simt_kernel(const T* __restrict__ X, int64_t N,
+                                                          int64_t ldx, int D,
+                                                          const T* __restrict__ C, int K,
+                                                          int32_t* __restrict__ labels,
+                                                          T* __restrict__ mind) {
+  constexpr int KT = 256;  // centroids per LDS tile
+  __shared__ T s_c[KT * DMAX];
+  const int tid = threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * 256 + tid;
+  T x[DMAX];
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) x[d] = (i < N && d < D) ? X[i * ldx + d] : (T)0;
+  T bd = (T)0;
+  int best = -1;
+  for (int k0 = 0; k0 < K; k0 += KT) {
+    const int kt = min(KT, K - k0);
+    __syncthreads();
+    for (int j = tid; j < kt * DMAX; j += 256) {
+      const int k = j / DMAX, d = j % DMAX;
+      s_c[j] = (d < D) ? C[(int64_t)(k0 + k) * D + d] : (T)0;
+    }
+    __syncthreads();
+    for (int k = 0; k < kt; ++k) {
+      T dd = 0;
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d) {
+        const T df = x[d] - s_c[k * DMAX + d];
+        dd = fma(df, df, dd);
+      }
+      if (best < 0 || dd < bd) {
+        bd = dd;
+        best = k0 + k;
+      }
+    }
+  }
+  if (i < N) {
+    labels[i] = best;
+    if (mind) mind[i] = bd;
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// LDS-privatised, D-sliced centroid update
+// ------------------------------------------------------------------------------------
+template <typename XT, int VEC> struct VecLoad;
+template <> struct VecLoad<float, 4> {
+  __device__ static void load(const float* p, float (&v)[4]) {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  }
+};
+template <> struct VecLoad<double, 2> {
+  __device__ static void load(const double* p, double (&v)[2]) {
+    const double2 t = *reinterpret_cast<const double2*>(p);
+    v[0] = t.x; v[1] = t.y;
+  }
+};
+template <> struct VecLoad<__bf16, 4> {
+  __device__ static void load(const __bf16* p, float (&v)[4]) {
+    const uint2 t = *reinterpret_cast<const uint2*>(p);
+    v[0] = __uint_as_float(t.x << 16); v[1] = __uint_as_float(t.x & 0xffff0000u);
+    v[2] = __uint_as_float(t.y << 16); v[3] = __uint_as_float(t.y & 0xffff0000u);
+  }
+};
+template <typename XT> struct VecLoad1 {
+  template <typename LT> __device__ static void load(const XT* p, LT (&v)[1]) { v[0] = (LT)p[0]; }
+};
+// LDS accumulation type: fp64 data keeps fp64 partials (compat mode), else fp32
+template <typename XT> struct LdsT { typedef float type; };
+template <> struct LdsT<double> { typedef double type; };
+
+template <typename XT, typename ACC, int VEC>
+__global__ __launch_bounds__(256) void update_lds_kernel(const XT* __restrict__ X, int64_t N,
+                                                         int64_t ldx, int D, int DS,
+                                                         const int32_t* __restrict__ labels,
+                                                         int K, ACC* __restrict__ sums,
+                                                         ACC* __restrict__ counts,
+                                                         int nslices, int64_t rows_per_block) {
+  typedef typename LdsT<XT>::type LT;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int stride = DS + 1;  // pad: breaks the power-of-2 bank aliasing across clusters
+  LT* s_sum = reinterpret_cast<LT*>(smem_raw);
+  int* s_cnt = reinterpret_cast<int*>(s_sum + (size_t)K * stride);
+  const int tid = threadIdx.x;
+  const int slice = blockIdx.x % nslices;
+  const int64_t chunk = blockIdx.x / nslices;
+  const int d0 = slice * DS;
+  const int ds = min(DS, D - d0);
+  for (int i = tid; i < K * stride; i += 256) s_sum[i] = (LT)0;
+  for (int i = tid; i < K; i += 256) s_cnt[i] = 0;
+  __syncthreads();
+
+  const int tpr = DS / VEC;   // threads per row
+  const int rpi = 256 / tpr;  // rows per block iteration
+  const int j = tid % tpr, rsub = tid / tpr;
+  const int dd = j * VEC;
+  const int64_t r0 = chunk * rows_per_block;
+  const int64_t r1 = min(N, r0 + rows_per_block);
+  for (int64_t row = r0 + rsub; row < r1; row += rpi) {
+    const int lab = labels[row];
+    if ((unsigned)lab >= (unsigned)K) continue;  // never index LDS out of range
+    if (dd < ds) {
+      LT v[VEC];
+      if constexpr (VEC == 1) VecLoad1<XT>::load(X + row * ldx + d0 + dd, v);
+      else VecLoad<XT, VEC>::load(X + row * ldx + d0 + dd, v);
+      LT* dst = s_sum + lab * stride + dd;
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) atomicAdd(dst + e, v[e]);
+    }
+    if (j == 0) atomicAdd(s_cnt + lab, 1);
+  }
+  __syncthreads();
+  for (int i = tid; i < K * ds; i += 256) {
+    const int k = i / ds, d = i % ds;
+    if (s_cnt[k]) atomic_add(&sums[(int64_t)k * D + d0 + d], (ACC)s_sum[k * stride + d]);
+  }
+  if (slice == 0)
+    for (int k = tid; k < K; k += 256)
+      if (s_cnt[k]) atomic_add(&counts[k], (ACC)s_cnt[k]);
+}
+
+}  // namespace tdc
+
+using namespace tdc;
+
+// ------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------
+namespace {
+
+int grid_for(int64_t N, int per_block, int cap) {
+  int64_t g = (N + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+template <typename T, typename ACC, int KMAX, int DMAX>
+int launch_small(const void* X, int64_t N, int64_t ldx, int D, const void* C, int K,
+                 int32_t* labels, void* mind, void* sums, void* counts, hipStream_t s) {
+  const int g = grid_for(N, 256 * 8, 2048);
+  hipLaunchKernelGGL((lloyd_small_kernel<T, ACC, KMAX, DMAX>), dim3(g), dim3(256), 0, s,
+                     (const T*)X, N, ldx, D, (const T*)C, K, labels, (T*)mind, (ACC*)sums,
+                     (ACC*)counts);
+  TDC_CHECK_LAUNCH();
+  return 0;
+}
+
+// (KMAX, DMAX) register tiles compiled for the fused kernel
+template <typename T, typename ACC>
+int dispatch_small(const void* X, int64_t N, int64_t ldx, int D, const void* C, int K,
+                   int32_t* labels, void* mind, void* sums, void* counts, hipStream_t s) {
+#define TDC_SMALL(KM, DM)                                                          \
+  if (K <= KM && D <= DM)                                                          \
+    return launch_small<T, ACC, KM, DM>(X, N, ldx, D, C, K, labels, mind, sums, counts, s);
+  TDC_SMALL(4, 4)
+  TDC_SMALL(4, 8)
+  TDC_SMALL(8, 4)
+  TDC_SMALL(8, 8)
+  TDC_SMALL(16, 4)
+  if constexpr (sizeof(T) == 4) {
+    TDC_SMALL(16, 8)
+    TDC_SMALL(8, 16)
+  }
+  TDC_SMALL(4, 16)
+  if constexpr (sizeof(T) == 4) {
+    TDC_SMALL(32, 4)
+  } else {
+    TDC_SMALL(16, 6)
+  }
+#undef TDC_SMALL
+  return (int)hipErrorInvalidValue;
+}
+
+}  // namespace
+
+int tdc_lloyd_small_supported(int dtype, int K, int D) {
+  if (dtype == TDC_F32) return (K <= 16 && D <= 8) || (K <= 8 && D <= 16) || (K <= 32 && D <= 4);
+  if (dtype == TDC_F64) return (K <= 8 && D <= 8) || (K <= 16 && D <= 6) || (K <= 4 && D <= 16);
+  return 0;
+}
+
+int tdc_lloyd_small(int dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
+                    const void* C, int K, int32_t* labels, void* mind, void* sums, void* counts,
+                    hipStream_t s) {
+  if (N <= 0) return 0;
+  if (dtype == TDC_F32) {
+    if (acc_dtype == TDC_F64)
+      return dispatch_small<float, double>(X, N, ldx, D, C, K, labels, mind, sums, counts, s);
+    return dispatch_small<float, float>(X, N, ldx, D, C, K, labels, mind, sums, counts, s);
+  }
+  if (dtype == TDC_F64)
+    return dispatch_small<double, double>(X, N, ldx, D, C, K, labels, mind, sums, counts, s);
+  return (int)hipErrorInvalidValue;
+}
+
+int tdc_assign_simt(int dtype, const void* X, int64_t N, int64_t ldx, int D, const void* C,
+                    int K, int32_t* labels, void* mind, hipStream_t s) {
+  if (N <= 0) return 0;
+  const dim3 grid((unsigned)((N + 255) / 256));
+#define TDC_AS(T, DM)                                                                      \
+  if (D <= DM) {                                                                           \
+    hipLaunchKernelGGL((assign_simt_kernel<T, DM>), grid, dim3(256), 0, s, (const T*)X, N, \
+                       ldx, D, (const T*)C, K, labels, (T*)mind);                          \
+    TDC_CHECK_LAUNCH();                                                                    \
+    return 0;                                                                              \
+  }
+  if (dtype == TDC_F32) {
+    TDC_AS(float, 4) TDC_AS(float, 8) TDC_AS(float, 16) TDC_AS(float, 32) TDC_AS(float, 64)
+  } else if (dtype == TDC_F64) {
+    TDC_AS(double, 4) TDC_AS(double, 8) TDC_AS(double, 16) TDC_AS(double, 32)
+  }
+#undef TDC_AS
+  return (int)hipErrorInvalidValue;
+}
+
+namespace {
+template <typename XT, typename ACC, int VEC>
+int launch_update(const void* X, int64_t N, int64_t ldx, int D, int DS, const int32_t* labels,
+                  int K, void* sums, void* counts, int num_cus, hipStream_t s) {
+  const int nslices = (D + DS - 1) / DS;
+  const size_t lds = (size_t)K * (DS + 1) * sizeof(typename LdsT<XT>::type) + (size_t)K * sizeof(int);
+  const int blocks_per_cu = lds <= 40 * 1024 ? 4 : (lds <= 80 * 1024 ? 2 : 1);
+  const int tpr = DS / VEC, rpi = 256 / tpr;
+  int64_t target_chunks = (int64_t)num_cus * blocks_per_cu / nslices;
+  if (target_chunks < 1) target_chunks = 1;
+  const int64_t max_chunks = (N + rpi - 1) / rpi;
+  int64_t chunks = target_chunks < max_chunks ? target_chunks : max_chunks;
+  if (chunks < 1) chunks = 1;
+  const int64_t rpb = (N + chunks - 1) / chunks;
+  chunks = (N + rpb - 1) / rpb;
+  if (lds > 64 * 1024)
+    hipFuncSetAttribute((const void*)update_lds_kernel<XT, ACC, VEC>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((update_lds_kernel<XT, ACC, VEC>), dim3((unsigned)(chunks * nslices)),
+                     dim3(256), lds, s, (const XT*)X, N, ldx, D, DS, labels, K, (ACC*)sums,
+                     (ACC*)counts, nslices, rpb);
+  TDC_CHECK_LAUNCH();
+  return 0;
+}
+
+template <typename ACC>
+int dispatch_update(int x_dtype, const void* X, int64_t N, int64_t ldx, int D,
+                    const int32_t* labels, int K, void* sums, void* counts, int num_cus,
+                    hipStream_t s) {
+  // slice width: largest power of two (<= next_pow2(D), <= 256) whose LDS image fits 140 KB
+  const size_t es = (x_dtype == TDC_F64) ? 8 : 4;
+  auto bytes = [&](int ds) { return (size_t)K * (ds + 1) * es + (size_t)K * 4; };
+  int dmax = 1;
+  while (dmax < D && dmax < 256) dmax <<= 1;
+  int DS = dmax;
+  while (DS > 1 && bytes(DS) > 140 * 1024) DS >>= 1;
+  if (bytes(DS) > 140 * 1024) return (int)hipErrorInvalidValue;
+  // prefer two blocks per CU when it only costs half the slice width
+  if (DS >= 16 && bytes(DS) > 80 * 1024 && bytes(DS / 2) <= 80 * 1024) DS >>= 1;
+  const bool aligned = ((uintptr_t)X % 16 == 0);
+  if (x_dtype == TDC_BF16) {
+    if (aligned && D % 4 == 0 && ldx % 4 == 0 && DS >= 4)
+      return launch_update<__bf16, ACC, 4>(X, N, ldx, D, DS, labels, K, sums, counts, num_cus, s);
+    return launch_update<__bf16, ACC, 1>(X, N, ldx, D, DS, labels, K, sums, counts, num_cus, s);
+  }
+  if (x_dtype == TDC_F32) {
+    if (aligned && D % 4 == 0 && ldx % 4 == 0 && DS >= 4)
+      return launch_update<float, ACC, 4>(X, N, ldx, D, DS, labels, K, sums, counts, num_cus, s);
+    return launch_update<float, ACC, 1>(X, N, ldx, D, DS, labels, K, sums, counts, num_cus, s);
+  }
+  if (x_dtype == TDC_F64) {
+    if (aligned && D % 2 == 0 && ldx % 2 == 0 && DS >= 2)
+      return launch_update<double, ACC, 2>(X, N, ldx, D, DS, labels, K, sums, counts, num_cus, s);
+    return launch_update<double, ACC, 1>(X, N, ldx, D, DS, labels, K, sums, counts, num_cus, s);
+  }
+  return (int)hipErrorInvalidValue;
+}
+}  // namespace
+
+int tdc_update_lds(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
+                   const int32_t* labels, int K, void* sums, void* counts, int num_cus,
+                   hipStream_t s) {
+  if (N <= 0) return 0;
+  if (acc_dtype == TDC_F64)
+    return dispatch_update<double>(x_dtype, X, N, ldx, D, labels, K, sums, counts, num_cus, s);
+  return dispatch_update<float>(x_dtype, X, N, ldx, D, labels, K, sums, counts, num_cus, s);
+}

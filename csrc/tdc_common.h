@@ -1,0 +1,48 @@
+// Shared device helpers for the tdc (tensorflow-distributed-clustering, MI355X-native)
+// HIP kernels.  gfx950 / CDNA4 only: 64-lane waves, MFMA, 160 KiB LDS per CU.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define TDC_WAVE 64
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define TDC_CHECK_LAUNCH()                                                         \
+  do {                                                                             \
+    hipError_t _e = hipGetLastError();                                             \
+    if (_e != hipSuccess) return (int)_e;                                          \
+  } while (0)
+
+namespace tdc {
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Typed element load/convert helpers (X may be bf16 / fp32 / fp64).
+template <typename T> __device__ __forceinline__ float to_f(T v) { return (float)v; }
+template <typename T, typename A> __device__ __forceinline__ A to_acc(T v) { return (A)v; }
+
+// Atomic add on global memory for float / double (gfx950 has native
+// global_atomic_add_f32 / _f64; agent scope is the default).
+__device__ __forceinline__ void atomic_add(float* p, float v) { atomicAdd(p, v); }
+__device__ __forceinline__ void atomic_add(double* p, double v) { atomicAdd(p, v); }
+
+}  // namespace tdc

@@ -1,0 +1,79 @@
+"""Frozen run configuration threaded through every layer.
+
+The reference hard-codes its knobs: fixed iteration count with no tolerance
+(`scripts/distribuitedClustering.py:163,277`), fuzzifier ``m := D``
+(`:97,121,129`), k-means++ init (`:82,191`), NaN on empty clusters (`:240,248`).
+Here each of those is an explicit field whose *default* is the correct
+semantics and whose ``compat`` value reproduces the reference behaviour.
+"""
+from __future__ import annotations
+
+import dataclasses
+from dataclasses import dataclass, field
+from typing import Optional
+
+METHODS = ("distributedKMeans", "distributedFuzzyCMeans", "miniBatchKMeans")
+DTYPES = ("fp64", "fp32", "bf16", "fp8")
+INITS = ("random", "first_k", "kmeans++", "given")
+EMPTY_POLICIES = ("keep", "nan", "reseed", "zero")
+BACKENDS = ("auto", "hip", "torch")
+
+
+@dataclass(frozen=True)
+class ClusterConfig:
+    """All knobs of one clustering run.
+
+    n_clusters      K
+    max_iter        fixed iteration budget (reference: ``--n_max_iters``)
+    tol             stop when max centroid shift^2 <= tol (0 = run all iters,
+                    the reference behaviour, `distribuitedClustering.py:163`)
+    dtype           compute dtype of the distance kernel. bf16/fp8 use MFMA;
+                    fp32/fp64 use exact-difference SIMT kernels.
+    init            centroid init (reference script: k-means++; CSV era: first-K)
+    fuzzifier       FCM m. ``None`` = compat value D (`:121,129`).
+    fcm_nan_to_zero compat: membership NaN (point on a centroid) -> 0 (`:125-126`);
+                    False gives the correct one-hot membership.
+    empty_cluster   'keep' (default) | 'nan' (reference) | 'reseed' | 'zero'
+    backend         'hip' native kernels, 'torch' reference ops, 'auto'
+    deterministic   ordered per-block reduction instead of float atomics
+    chunk_rows      rows per streamed chunk (0 = whole shard resident)
+    hbm_budget_gb   planner budget per GPU (MI355X has 288 GB)
+    """
+
+    n_clusters: int
+    max_iter: int = 20
+    tol: float = 0.0
+    dtype: str = "bf16"
+    init: str = "random"
+    seed: int = 0
+    fuzzifier: Optional[float] = None
+    fcm_nan_to_zero: bool = True
+    empty_cluster: str = "keep"
+    backend: str = "auto"
+    deterministic: bool = False
+    chunk_rows: int = 0
+    hbm_budget_gb: float = 0.0
+    compute_inertia: bool = True
+    label_pass: bool = True
+    batch_size: int = 0  # mini-batch K-Means: rows per rank per step
+    log_every: int = 0
+
+    def __post_init__(self):
+        if self.n_clusters <= 0:
+            raise ValueError(f"n_clusters must be positive, got {self.n_clusters}")
+        if self.max_iter < 0:
+            raise ValueError("max_iter must be >= 0")
+        if self.dtype not in DTYPES:
+            raise ValueError(f"dtype must be one of {DTYPES}, got {self.dtype!r}")
+        if self.init not in INITS:
+            raise ValueError(f"init must be one of {INITS}, got {self.init!r}")
+        if self.empty_cluster not in EMPTY_POLICIES:
+            raise ValueError(f"empty_cluster must be one of {EMPTY_POLICIES}")
+        if self.backend not in BACKENDS:
+            raise ValueError(f"backend must be one of {BACKENDS}")
+
+    def replace(self, **kw) -> "ClusterConfig":
+        return dataclasses.replace(self, **kw)
+
+    def to_dict(self) -> dict:
+        return dataclasses.asdict(self)

@@ -1,0 +1,149 @@
+"""Distributed centroid initialisation.
+
+Reference variants:
+* k-means++ via sklearn's private ``k_means_._init_centroids`` on the host, per batch
+  (`scripts/distribuitedClustering.py:82,191`);
+* first-K rows ``X[0:K]`` (`:325`; the CSV-era revision);
+* K random rows without replacement (`ckpt/Testing Images-checkpoint.ipynb:290-291`).
+
+Here every method is *world-size invariant*: the chosen global row indices depend only
+on ``seed`` and ``N``, and each rank contributes the rows it owns to one SUM all-reduce,
+so a 1-GPU and an 8-GPU run start from bit-identical centroids.  k-means++ runs on the
+device shards (distributed D^2 sampling: one all-reduce of per-rank potentials + one of
+the candidate rows per step) instead of on a host copy of the whole dataset.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..parallel.dist import Comm
+
+
+def floyd_sample(n: int, k: int, seed: int) -> List[int]:
+    """k distinct integers from [0, n) in O(k) (Floyd's algorithm), order randomised."""
+    if k > n:
+        raise ValueError(f"cannot draw {k} distinct rows from {n}")
+    rng = np.random.default_rng(seed)
+    chosen = {}
+    out = []
+    for j in range(n - k, n):
+        t = int(rng.integers(0, j + 1))
+        if t in chosen:
+            t = j
+        chosen[t] = True
+        out.append(t)
+    rng.shuffle(out)
+    return out
+
+
+def gather_global_rows(x_local: torch.Tensor, row_offset: int, idx: Sequence[int],
+                       comm: Comm, dtype=torch.float64) -> torch.Tensor:
+    """Rows ``idx`` (global indices) of the sharded matrix, replicated on every rank."""
+    d = x_local.shape[1]
+    out = torch.zeros(len(idx), d, dtype=dtype, device=x_local.device)
+    n_local = x_local.shape[0]
+    if len(idx):
+        gi = torch.as_tensor(list(idx), dtype=torch.int64)
+        mine = (gi >= row_offset) & (gi < row_offset + n_local)
+        if bool(mine.any()):
+            pos = torch.nonzero(mine).flatten()
+            rows = (gi[mine] - row_offset).to(x_local.device)
+            out[pos.to(x_local.device)] = x_local.index_select(0, rows).to(dtype)
+    comm.allreduce_(out)
+    return out
+
+
+def init_random(x_local, row_offset, n_global, k, comm, seed):
+    idx = floyd_sample(n_global, k, seed)
+    return gather_global_rows(x_local, row_offset, idx, comm)
+
+
+def init_first_k(x_local, row_offset, n_global, k, comm, seed=0):
+    if k > n_global:
+        raise ValueError("K larger than the number of points")
+    return gather_global_rows(x_local, row_offset, range(k), comm)
+
+
+def _sqdist_to(x: torch.Tensor, c: torch.Tensor, chunk: int = 1 << 22) -> torch.Tensor:
+    """||x_i - c_j||^2 for a handful of candidate rows c [T, D] -> [T, n] (fp32/fp64)."""
+    out = torch.empty(c.shape[0], x.shape[0], dtype=c.dtype, device=x.device)
+    cc = (c * c).sum(1)[:, None]
+    for s in range(0, x.shape[0], chunk):
+        xs = x[s:s + chunk].to(c.dtype)
+        xx = (xs * xs).sum(1)[None, :]
+        out[:, s:s + chunk] = (torch.addmm(cc, c, xs.t(), alpha=-2.0) + xx).clamp_min_(0)
+    return out
+
+
+def init_kmeanspp(x_local, row_offset, n_global, k, comm: Comm, seed,
+                  n_local_trials: Optional[int] = None, work_dtype=None):
+    """Distributed greedy k-means++ (sklearn's variant: 2 + ln K trials per step)."""
+    if n_local_trials is None:
+        n_local_trials = 2 + int(math.log(k))
+    dev = x_local.device
+    wd = work_dtype or (torch.float64 if x_local.dtype == torch.float64 or dev.type == "cpu"
+                        else torch.float32)
+    rng = np.random.default_rng(seed)
+    n_local = x_local.shape[0]
+    sizes = comm.all_gather_sizes(n_local)
+    offsets = np.concatenate([[0], np.cumsum(sizes)])
+    centers = torch.empty(k, x_local.shape[1], dtype=torch.float64, device=dev)
+    first = int(rng.integers(0, n_global))
+    centers[0] = gather_global_rows(x_local, row_offset, [first], comm)[0]
+    closest = _sqdist_to(x_local, centers[:1].to(wd))[0]
+    for c in range(1, k):
+        pots = torch.zeros(comm.world_size, dtype=torch.float64, device=dev)
+        pots[comm.rank] = closest.sum().double()
+        comm.allreduce_(pots)
+        pots_h = pots.cpu().numpy()
+        total = float(pots_h.sum())
+        if total <= 0.0:
+            cand_idx = [int(v) for v in rng.integers(0, n_global, size=n_local_trials)]
+        else:
+            r = rng.random(n_local_trials) * total
+            cum = np.cumsum(pots_h)
+            owners = np.searchsorted(cum, r, side="right").clip(0, comm.world_size - 1)
+            cand_idx = [0] * n_local_trials
+            local_cs = None
+            for t in range(n_local_trials):
+                if owners[t] == comm.rank:
+                    if local_cs is None:
+                        local_cs = torch.cumsum(closest.double(), 0)
+                    rr = r[t] - (cum[owners[t]] - pots_h[owners[t]])
+                    li = int(torch.searchsorted(local_cs, torch.tensor([rr], dtype=torch.float64,
+                                                                       device=dev)).item())
+                    cand_idx[t] = row_offset + min(li, n_local - 1)
+            ci = torch.tensor(cand_idx, dtype=torch.int64, device=dev)
+            comm.allreduce_(ci)  # only the owner wrote a non-zero (owners differ per trial)
+            cand_idx = [int(v) for v in ci.tolist()]
+        cand = gather_global_rows(x_local, row_offset, cand_idx, comm)
+        dist = torch.minimum(_sqdist_to(x_local, cand.to(wd)), closest[None, :])
+        tp = dist.double().sum(1)
+        comm.allreduce_(tp)
+        best = int(torch.argmin(tp).item())
+        closest = dist[best].contiguous()
+        centers[c] = cand[best]
+    return centers
+
+
+def init_centers(method: str, x_local: torch.Tensor, row_offset: int, n_global: int, k: int,
+                 comm: Comm, seed: int = 0, given: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[K, D] float64 on the shard's device, identical on every rank."""
+    if given is not None or method == "given":
+        if given is None:
+            raise ValueError("init='given' needs init_centers")
+        g = torch.as_tensor(np.asarray(given), dtype=torch.float64).to(x_local.device)
+        if g.shape != (k, x_local.shape[1]):
+            raise ValueError(f"init_centers must be [{k}, {x_local.shape[1]}], got {tuple(g.shape)}")
+        return g
+    if method == "random":
+        return init_random(x_local, row_offset, n_global, k, comm, seed)
+    if method == "first_k":
+        return init_first_k(x_local, row_offset, n_global, k, comm, seed)
+    if method == "kmeans++":
+        return init_kmeanspp(x_local, row_offset, n_global, k, comm, seed)
+    raise ValueError(f"unknown init {method!r}")

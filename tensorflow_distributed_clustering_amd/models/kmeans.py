@@ -1,0 +1,214 @@
+"""Distributed Lloyd K-Means (data-parallel over points, replicated centroids).
+
+Reference: ``distribuited_k_means`` (`scripts/distribuitedClustering.py:180-294`).
+Per iteration the reference ran one TF session step that (1) materialised [N_g,K,D]
+tiles per GPU, (2) gathered per-cluster means with K dynamic-shape Where/Gather chains,
+(3) copied labels to the host for a CPU bincount, (4) reduced everything on a CPU
+parameter server, and then (5) re-ran the whole distance computation for an untimed
+CPU label pass (`:277-282`).
+
+Here one iteration on each rank is:
+
+    comm_buf.zero_()                       # [sums K*D | counts K], one flat buffer
+    local.step(C, labels, ..., sums, counts)   # HIP: N1 assign (+N2 update) on the shard
+    all_reduce(comm_buf)                   # ONE RCCL call over xGMI (gloo on CPU)
+    local.finalize(sums, counts, C)        # N3: divide + next-iteration operand prep
+
+Labels are produced by the same kernel that feeds the update, so there is no
+separate label pass inside the loop; a final label pass against the *final*
+centroids (what the reference returns as ``cluster_idx``) runs after the timed loop.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from ..config import ClusterConfig
+from ..ops import acc_dtype_for, make_lloyd_ops
+from ..parallel.dist import Comm, local_comm
+from ..utils.timers import DeviceTimer, sync
+from .init import gather_global_rows, init_centers, floyd_sample
+
+
+@dataclass
+class ClusterResult:
+    centers: np.ndarray                 # [K, D] float64 (host)
+    init_centers: np.ndarray            # [K, D] float64
+    labels: Optional[torch.Tensor]      # this rank's labels (int32, on device)
+    counts: Optional[np.ndarray]        # [K] global cluster sizes of the last update
+    n_iter: int
+    inertia: Optional[float]
+    setup_time: float
+    initialization_time: float
+    computation_time: float
+    backend: str = ""
+    history: List[dict] = field(default_factory=list)
+    n_global: int = 0
+
+    @property
+    def points_per_sec(self) -> float:
+        return self.n_global * self.n_iter / self.computation_time if self.computation_time > 0 else 0.0
+
+    @property
+    def iters_per_sec(self) -> float:
+        return self.n_iter / self.computation_time if self.computation_time > 0 else 0.0
+
+
+def _shard_geometry(x_local: torch.Tensor, comm: Comm):
+    sizes = comm.all_gather_sizes(int(x_local.shape[0]))
+    return int(sum(sizes)), int(sum(sizes[: comm.rank]))
+
+
+class LloydEngine:
+    """Resident state of one distributed Lloyd run: shard operands, centroids, buffers.
+
+    ``step()`` is exactly one iteration (assign + update + all-reduce + finalize); it is
+    what ``bench.py`` times and what :meth:`KMeans.fit` loops over.
+    """
+
+    def __init__(self, x_local: torch.Tensor, cfg: ClusterConfig, comm: Comm,
+                 n_global: int, row_offset: int, init_centers_=None):
+        self.cfg, self.comm = cfg, comm
+        self.device = dev = x_local.device
+        self.n_global, self.row_offset = n_global, row_offset
+        k, d = cfg.n_clusters, int(x_local.shape[1])
+        self.k, self.d = k, d
+        self.local = make_lloyd_ops(x_local, k, cfg.dtype, cfg.backend, cfg.empty_cluster)
+        self.x_local = x_local
+        self.c0 = init_centers(cfg.init, x_local, row_offset, n_global, k, comm, cfg.seed,
+                               given=init_centers_)
+        self.C = self.c0.to(self.local.c_dtype).contiguous()
+        self.local.prepare(self.C)
+        acc = acc_dtype_for(cfg.dtype, k, d)
+        self.buf = torch.zeros(k * d + k, dtype=acc, device=dev)
+        self.sums = self.buf[: k * d].view(k, d)
+        self.counts = self.buf[k * d:]
+        self.labels = torch.zeros(self.local.n, dtype=torch.int32, device=dev)
+        self.mind = torch.zeros(self.local.n, dtype=torch.float64 if self.local.c_dtype == torch.float64
+                                else torch.float32, device=dev) if cfg.compute_inertia else None
+        self.need_shift = cfg.tol > 0 or cfg.log_every > 0
+        self.shift = torch.zeros(1, dtype=torch.float32, device=dev) if self.need_shift else None
+        self.bucket_bytes = 64 << 20
+        self.n_iter = 0
+
+    def step(self):
+        self.buf.zero_()
+        self.local.step(self.C, self.labels, None, self.sums, self.counts)
+        self.comm.allreduce_bucketed_(self.buf, self.bucket_bytes)
+        if self.shift is not None:
+            self.shift.zero_()
+        self.local.finalize(self.sums, self.counts, self.C, self.shift)
+        if self.cfg.empty_cluster == "reseed":
+            self._reseed()
+        self.n_iter += 1
+
+    def _reseed(self):
+        empty = torch.nonzero(self.counts == 0).flatten().cpu().tolist()
+        if not empty:
+            return
+        idx = floyd_sample(self.n_global, len(empty), self.cfg.seed + 7919 * (self.n_iter + 1))
+        rows = gather_global_rows(self.x_local, self.row_offset, idx, self.comm)
+        self.C[torch.as_tensor(empty, device=self.C.device)] = rows.to(self.C.dtype)
+        self.local.prepare(self.C)
+
+    def label_pass(self) -> Optional[float]:
+        """Assign against the current centroids; returns the global inertia if tracked."""
+        self.local.assign(self.C, self.labels, self.mind)
+        if self.mind is None:
+            return None
+        return self.comm.sum_scalar(float(self.mind.double().sum()))
+
+
+class KMeans:
+    """sklearn-like front end over the distributed engine.
+
+    >>> km = KMeans(ClusterConfig(n_clusters=8, dtype="fp32")).fit(x)
+    >>> km.result_.centers
+    """
+
+    def __init__(self, cfg: ClusterConfig, comm: Optional[Comm] = None, device=None):
+        self.cfg = cfg
+        self.comm = comm
+        self.device = device
+        self.result_: Optional[ClusterResult] = None
+        self.local_ = None
+
+    # ------------------------------------------------------------------ helpers
+    def _comm_for(self, x: torch.Tensor) -> Comm:
+        if self.comm is None:
+            self.comm = local_comm(x.device)
+        return self.comm
+
+    @property
+    def cluster_centers_(self) -> np.ndarray:
+        return self.result_.centers
+
+    @property
+    def labels_(self) -> torch.Tensor:
+        return self.result_.labels
+
+    # ---------------------------------------------------------------------- fit
+    def fit(self, x_local, init_centers_: Optional[np.ndarray] = None,
+            n_global: Optional[int] = None, row_offset: Optional[int] = None) -> "KMeans":
+        cfg = self.cfg
+        t_init0 = time.perf_counter()
+        x_local = torch.as_tensor(x_local)
+        dev = torch.device(self.device) if self.device is not None else (
+            self.comm.device if self.comm is not None else x_local.device)
+        if x_local.device != dev:
+            x_local = x_local.to(dev, non_blocking=False)
+        comm = self._comm_for(x_local)
+        if n_global is None or row_offset is None:
+            n_global, row_offset = _shard_geometry(x_local, comm)
+        sync(dev)
+        initialization_time = time.perf_counter() - t_init0
+
+        t_setup0 = time.perf_counter()
+        eng = LloydEngine(x_local, cfg, comm, n_global, row_offset, init_centers_)
+        sync(dev)
+        setup_time = time.perf_counter() - t_setup0
+
+        # ------------------------------------------------------------ timed loop
+        history = []
+        timer = DeviceTimer(dev)
+        timer.start()
+        for _ in range(cfg.max_iter):
+            eng.step()
+            n = eng.n_iter
+            if eng.need_shift and (cfg.tol > 0 or n % cfg.log_every == 0):
+                sv = float(eng.shift.item())
+                history.append({"iter": n, "shift": sv})
+                if cfg.log_every and comm.is_root and n % cfg.log_every == 0:
+                    print(f"[kmeans] iter {n} max centroid shift^2 {sv:.3e}", flush=True)
+                if cfg.tol > 0 and sv <= cfg.tol:
+                    break
+        computation_time = timer.stop()
+
+        # ------------------------------------------- final label pass (untimed)
+        inertia = eng.label_pass() if cfg.label_pass else None
+        n_iter = eng.n_iter
+        cnt = eng.counts.double().cpu().numpy() if n_iter > 0 else None
+        self.engine_ = eng
+        self.local_ = eng.local
+        self.result_ = ClusterResult(
+            centers=eng.C.double().cpu().numpy(), init_centers=eng.c0.cpu().numpy(),
+            labels=eng.labels, counts=cnt, n_iter=n_iter, inertia=inertia,
+            setup_time=setup_time, initialization_time=initialization_time,
+            computation_time=computation_time, backend=eng.local.name, history=history,
+            n_global=n_global)
+        return self
+
+    def predict(self, x: torch.Tensor) -> torch.Tensor:
+        """Labels of new points against the fitted centroids (local, no collectives)."""
+        x = torch.as_tensor(x)
+        cfg = self.cfg
+        local = make_lloyd_ops(x, cfg.n_clusters, cfg.dtype, cfg.backend, cfg.empty_cluster)
+        C = torch.as_tensor(self.result_.centers).to(x.device, local.c_dtype).contiguous()
+        local.prepare(C)
+        labels = torch.empty(local.n, dtype=torch.int32, device=x.device)
+        local.assign(C, labels, None)
+        return labels

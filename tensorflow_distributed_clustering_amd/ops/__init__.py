@@ -1,0 +1,278 @@
+"""Op layer: the local (per-rank) part of one clustering iteration.
+
+Each *local-ops* object owns the shard in the layout its kernels want and exposes
+three calls used by the algorithm drivers in :mod:`..models`:
+
+``step(C, labels, mind, sums, counts)``   assignment + per-cluster partials
+``assign(C, labels, mind)``               label pass only (reference `:282`)
+``finalize(sums, counts, C, policy, shift)`` centroid divide (+ operand prep)
+
+Variants (picked by :func:`make_lloyd_ops`):
+
+========================  =====================================================
+``HipBf16Lloyd``          bf16 MFMA distance+argmin (N1) + LDS update (N2) + N3
+``HipSmallLloyd``         fused fp32/fp64 assign+accumulate (reference configs)
+``HipSimtLloyd``          fp32/fp64 exact SIMT assign + LDS update
+``HipGemmLloyd``          fp32/fp64 large-D: library GEMM assign + LDS update
+``TorchLloyd``            plain PyTorch (CPU ranks, oracle)
+========================  =====================================================
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .. import _native
+from . import reference as ref
+
+POLICY_CODES = {"keep": 0, "reseed": 0, "nan": 1, "zero": 2}
+TORCH_DTYPES = {"fp64": torch.float64, "fp32": torch.float32, "bf16": torch.bfloat16,
+                "fp8": torch.bfloat16}
+MFMA_DIMS = (32, 64, 128, 256)
+
+
+def acc_dtype_for(dtype: str, k: int, d: int) -> torch.dtype:
+    """Accumulation / all-reduce dtype of the per-cluster partials.
+
+    fp64 whenever the buffer is small (latency-bound all-reduce: the extra bytes are
+    free and counts stay exact past 2^24); fp32 for big K x D buffers.
+    """
+    if dtype == "fp64" or k * (d + 1) <= 65536:
+        return torch.float64
+    return torch.float32
+
+
+def padded_dim(d: int) -> Optional[int]:
+    for p in MFMA_DIMS:
+        if d <= p:
+            return p
+    return None
+
+
+def use_native(device: torch.device, backend: str) -> bool:
+    if backend == "torch" or device.type != "cuda":
+        if backend == "hip" and device.type != "cuda":
+            raise RuntimeError("backend='hip' requires a GPU tensor")
+        return False
+    _native.require()  # GPU + hip/auto: the native path is mandatory (fail loudly)
+    return True
+
+
+class _LocalOpsBase:
+    name = "base"
+
+    def __init__(self, x: torch.Tensor, k: int, empty_cluster: str = "keep"):
+        self.n, self.d = x.shape
+        self.k = k
+        self.device = x.device
+        self.policy = POLICY_CODES[empty_cluster]
+        self.empty_cluster = empty_cluster
+
+    # centroid dtype kept by the driver
+    c_dtype = torch.float32
+
+    def prepare(self, C: torch.Tensor):
+        """(Re)derive kernel operands from C (called after init / external edits)."""
+
+    def finalize(self, sums, counts, C, shift):
+        ref_new = ref.finalize(sums, counts, C, self.empty_cluster)
+        if shift is not None:
+            d = (ref_new.double() - C.double())
+            shift.fill_(float((d * d).sum(1).max()) if d.numel() else 0.0)
+        C.copy_(ref_new)
+        self.prepare(C)
+
+
+class TorchLloyd(_LocalOpsBase):
+    name = "torch"
+
+    def __init__(self, x, k, dtype="fp64", empty_cluster="keep", exact=None):
+        super().__init__(x, k, empty_cluster)
+        tdt = TORCH_DTYPES[dtype] if dtype in ("fp64", "fp32") else torch.float32
+        self.x = x.to(tdt).contiguous()
+        self.c_dtype = tdt
+        self.exact = (dtype == "fp64") if exact is None else exact
+
+    def step(self, C, labels, mind, sums, counts):
+        lab, md = ref.assign(self.x, C.to(self.x.dtype), exact=self.exact)
+        labels.copy_(lab)
+        if mind is not None:
+            mind.copy_(md)
+        s, c = ref.cluster_sums(self.x, lab, self.k, acc_dtype=sums.dtype)
+        sums.add_(s)
+        counts.add_(c)
+
+    def assign(self, C, labels, mind):
+        lab, md = ref.assign(self.x, C.to(self.x.dtype), exact=self.exact)
+        labels.copy_(lab)
+        if mind is not None:
+            mind.copy_(md)
+
+
+class HipBf16Lloyd(_LocalOpsBase):
+    """bf16 shard [N, DP] (zero-padded to an MFMA-friendly width) + fp32 centroids."""
+    name = "hip_bf16_mfma"
+    c_dtype = torch.float32
+
+    def __init__(self, x, k, empty_cluster="keep"):
+        super().__init__(x, k, empty_cluster)
+        self.ops = _native.require()
+        dp = padded_dim(self.d)
+        if dp is None:
+            raise ValueError(f"bf16 MFMA path supports D <= {MFMA_DIMS[-1]}, got {self.d}")
+        self.dp = dp
+        if x.dtype == torch.bfloat16 and self.d == dp and x.is_contiguous():
+            self.x = x
+        else:
+            xb = torch.zeros(self.n, dp, dtype=torch.bfloat16, device=x.device)
+            xb[:, : self.d] = x
+            self.x = xb
+        self.kp = ((k + 63) // 64) * 64
+        self.cm2 = torch.zeros(self.kp, dp, dtype=torch.bfloat16, device=x.device)
+        self.cnorm = torch.zeros(self.kp, dtype=torch.float32, device=x.device)
+
+    def prepare(self, C):
+        self.ops.finalize(None, None, C, 0, None, self.cm2, self.cnorm)
+
+    def step(self, C, labels, mind, sums, counts):
+        self.ops.assign_bf16(self.x, self.cm2, self.cnorm, labels, mind)
+        self.ops.update(self.x, labels, sums, counts)
+
+    def assign(self, C, labels, mind):
+        self.ops.assign_bf16(self.x, self.cm2, self.cnorm, labels, mind)
+
+    def finalize(self, sums, counts, C, shift):
+        self.ops.finalize(sums, counts, C, self.policy, shift, self.cm2, self.cnorm)
+
+
+class _HipExactBase(_LocalOpsBase):
+    def __init__(self, x, k, dtype, empty_cluster):
+        super().__init__(x, k, empty_cluster)
+        self.ops = _native.require()
+        tdt = TORCH_DTYPES[dtype]
+        self.x = x.to(tdt).contiguous()
+        self.c_dtype = tdt
+
+    def finalize(self, sums, counts, C, shift):
+        self.ops.finalize(sums, counts, C, self.policy, shift, None, None)
+
+
+class HipSmallLloyd(_HipExactBase):
+    name = "hip_small_fused"
+
+    def step(self, C, labels, mind, sums, counts):
+        self.ops.lloyd_small(self.x, C, labels, mind, sums, counts)
+
+    def assign(self, C, labels, mind):
+        self.ops.assign_simt(self.x, C, labels, mind)
+
+
+class HipSimtLloyd(_HipExactBase):
+    name = "hip_simt"
+
+    def step(self, C, labels, mind, sums, counts):
+        self.ops.assign_simt(self.x, C, labels, mind)
+        self.ops.update(self.x, labels, sums, counts)
+
+    def assign(self, C, labels, mind):
+        self.ops.assign_simt(self.x, C, labels, mind)
+
+
+class HipGemmLloyd(_HipExactBase):
+    """Large-D fp32/fp64: distance via the vendor GEMM (plain library GEMM), native update."""
+    name = "hip_gemm"
+
+    def step(self, C, labels, mind, sums, counts):
+        self.assign(C, labels, mind)
+        self.ops.update(self.x, labels, sums, counts)
+
+    def assign(self, C, labels, mind):
+        lab, md = ref.assign(self.x, C, exact=False)
+        labels.copy_(lab)
+        if mind is not None:
+            mind.copy_(md.to(mind.dtype))
+
+
+def make_lloyd_ops(x: torch.Tensor, k: int, dtype: str = "bf16", backend: str = "auto",
+                   empty_cluster: str = "keep"):
+    """Pick the fastest local implementation for (device, dtype, K, D)."""
+    d = x.shape[1]
+    if not use_native(x.device, backend):
+        return TorchLloyd(x, k, dtype if dtype in ("fp64", "fp32") else "fp32", empty_cluster)
+    if dtype == "fp8":
+        raise NotImplementedError("fp8 distance path: use dtype='bf16' (fp8 MFMA kernel pending)")
+    if dtype == "bf16":
+        if padded_dim(d) is not None:
+            return HipBf16Lloyd(x, k, empty_cluster)
+        return HipGemmLloyd(x, k, "fp32", empty_cluster)
+    tdt = TORCH_DTYPES[dtype]
+    ops = _native.require()
+    if ops.lloyd_small_supported(tdt, k, d):
+        return HipSmallLloyd(x, k, dtype, empty_cluster)
+    if d <= (64 if dtype == "fp32" else 32):
+        return HipSimtLloyd(x, k, dtype, empty_cluster)
+    return HipGemmLloyd(x, k, dtype, empty_cluster)
+
+
+# ----------------------------------------------------------------------------- FCM
+class TorchFCM(_LocalOpsBase):
+    name = "torch_fcm"
+
+    def __init__(self, x, k, dtype="fp64", m=2.0, nan_to_zero=True):
+        super().__init__(x, k, "keep")
+        tdt = torch.float64 if dtype == "fp64" else torch.float32
+        self.x = x.to(tdt).contiguous()
+        self.c_dtype = tdt
+        self.m = float(m)
+        self.nan_to_zero = nan_to_zero
+
+    def step(self, C, labels, wx, ws):
+        a, b, lab = ref.fcm_partial(self.x, C.to(self.x.dtype), self.m, self.nan_to_zero,
+                                    acc_dtype=wx.dtype)
+        wx.add_(a)
+        ws.add_(b)
+        labels.copy_(lab)
+
+    def assign(self, C, labels):
+        u = ref.fcm_memberships(self.x, C.to(self.x.dtype), self.m, self.nan_to_zero)
+        labels.copy_(u.argmax(1).to(torch.int32))
+
+
+class HipSmallFCM(_LocalOpsBase):
+    name = "hip_fcm_small"
+
+    def __init__(self, x, k, dtype="fp64", m=2.0, nan_to_zero=True):
+        super().__init__(x, k, "keep")
+        self.ops = _native.require()
+        tdt = torch.float64 if dtype == "fp64" else torch.float32
+        self.x = x.to(tdt).contiguous()
+        self.c_dtype = tdt
+        self.m = float(m)
+        self.nan_to_zero = nan_to_zero
+        self._wx = None
+
+    def step(self, C, labels, wx, ws):
+        self.ops.fcm_small(self.x, C, self.m, self.nan_to_zero, labels, wx, ws)
+
+    def assign(self, C, labels):
+        if self._wx is None:
+            self._wx = torch.zeros(self.k, self.d, dtype=torch.float64, device=self.device)
+            self._ws = torch.zeros(self.k, dtype=torch.float64, device=self.device)
+        self.ops.fcm_small(self.x, C, self.m, self.nan_to_zero, labels, self._wx, self._ws)
+
+    def finalize(self, sums, counts, C, shift):
+        self.ops.finalize(sums, counts, C, 0, shift, None, None)
+
+
+def make_fcm_ops(x: torch.Tensor, k: int, dtype: str = "fp64", m: float = 2.0,
+                 nan_to_zero: bool = True, backend: str = "auto"):
+    d = x.shape[1]
+    if dtype in ("bf16", "fp8"):
+        dtype = "fp32"  # memberships need exact-difference distances; see docs
+    if not use_native(x.device, backend):
+        return TorchFCM(x, k, dtype, m, nan_to_zero)
+    tdt = torch.float64 if dtype == "fp64" else torch.float32
+    if _native.require().fcm_small_supported(tdt, k, d):
+        return HipSmallFCM(x, k, dtype, m, nan_to_zero)
+    return TorchFCM(x, k, dtype, m, nan_to_zero)

@@ -1,0 +1,186 @@
+"""Process-group runtime: one process per GPU, RCCL over xGMI (gloo on CPU).
+
+Replaces the reference's in-graph replication + CPU parameter server
+(`scripts/distribuitedClustering.py:84-148,193-263`): there every tower's
+partial sums went device->host and were `tf.add_n`-ed on `/cpu:0` every
+iteration.  Here each rank owns a contiguous row shard
+(``np.array_split`` semantics, `:76,184`), keeps its partial sums on device and
+the ranks combine them with ONE packed all-reduce per iteration; every rank then
+finalises the (replicated) centroids itself, so no broadcast is needed.
+
+Launch with ``torchrun --nproc-per-node G`` (``backend="nccl"`` is RCCL on
+ROCm).  On a CPU-only host the same code runs with ``gloo``.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def shard_bounds(n: int, world: int, rank: int) -> Tuple[int, int]:
+    """[start, end) of ``rank``'s rows under ``np.array_split(range(n), world)``.
+
+    The first ``n % world`` shards get one extra row (`distribuitedClustering.py:76`).
+    """
+    base, extra = divmod(n, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def shard_sizes(n: int, world: int) -> List[int]:
+    return [shard_bounds(n, world, r)[1] - shard_bounds(n, world, r)[0] for r in range(world)]
+
+
+class Comm:
+    """Thin handle over the default process group (or a single-process no-op)."""
+
+    def __init__(self, device: torch.device, rank: int = 0, world_size: int = 1,
+                 local_rank: int = 0, group=None):
+        self.device = device
+        self.rank = rank
+        self.world_size = world_size
+        self.local_rank = local_rank
+        self.group = group
+
+    # ------------------------------------------------------------------ props
+    @property
+    def is_distributed(self) -> bool:
+        return self.world_size > 1
+
+    @property
+    def is_root(self) -> bool:
+        return self.rank == 0
+
+    def shard(self, n: int) -> Tuple[int, int]:
+        return shard_bounds(n, self.world_size, self.rank)
+
+    # ------------------------------------------------------------ collectives
+    def allreduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        if self.world_size > 1:
+            rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
+                   "min": dist.ReduceOp.MIN}[op]
+            dist.all_reduce(t, op=rop, group=self.group)
+        return t
+
+    def allreduce_bucketed_(self, flat: torch.Tensor, bucket_bytes: int = 0) -> torch.Tensor:
+        """SUM all-reduce of a flat buffer, optionally split into buckets.
+
+        xGMI is point-to-point (7 links x ~153 GB/s per MI355X): one large
+        ring all-reduce is per-link bound, so very large buffers (K=65536 x
+        D=768 partial sums ~ 201 MB) are issued as several async buckets that
+        RCCL can run on separate channels; small buffers (K=1024: ~0.5 MB) are
+        latency bound and go as ONE call.
+        """
+        if self.world_size <= 1:
+            return flat
+        nbytes = flat.numel() * flat.element_size()
+        if bucket_bytes <= 0 or nbytes <= bucket_bytes:
+            dist.all_reduce(flat, group=self.group)
+            return flat
+        per = max(1, bucket_bytes // flat.element_size())
+        works = [dist.all_reduce(flat[s:s + per], group=self.group, async_op=True)
+                 for s in range(0, flat.numel(), per)]
+        for w in works:
+            w.wait()
+        return flat
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if self.world_size > 1:
+            dist.broadcast(t, src=src, group=self.group)
+        return t
+
+    def barrier(self):
+        if self.world_size > 1:
+            if self.device.type == "cuda":
+                dist.barrier(group=self.group, device_ids=[self.device.index])
+            else:
+                dist.barrier(group=self.group)
+
+    def max_scalar(self, v: float) -> float:
+        if self.world_size <= 1:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device=self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return float(t.item())
+
+    def sum_scalar(self, v: float) -> float:
+        if self.world_size <= 1:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device=self.device)
+        dist.all_reduce(t, group=self.group)
+        return float(t.item())
+
+    def all_gather_sizes(self, n_local: int) -> List[int]:
+        if self.world_size <= 1:
+            return [n_local]
+        t = torch.zeros(self.world_size, dtype=torch.int64, device=self.device)
+        t[self.rank] = n_local
+        dist.all_reduce(t, group=self.group)
+        return [int(v) for v in t.tolist()]
+
+    def gather_rows_to_root(self, local: torch.Tensor) -> Optional[torch.Tensor]:
+        """Concatenate every rank's rows on rank 0 (variable sizes; for outputs only)."""
+        if self.world_size <= 1:
+            return local
+        sizes = self.all_gather_sizes(local.shape[0])
+        mx = max(sizes)
+        buf = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=self.device)
+        buf[: local.shape[0]] = local
+        if self.rank == 0:
+            bufs = [torch.empty_like(buf) for _ in range(self.world_size)]
+            dist.gather(buf, gather_list=bufs, dst=0, group=self.group)
+            return torch.cat([b[:s] for b, s in zip(bufs, sizes)])
+        dist.gather(buf, dst=0, group=self.group)
+        return None
+
+
+_COMM: Optional[Comm] = None
+
+
+def init_comm(device_type: Optional[str] = None, timeout_s: float = 600.0) -> Comm:
+    """Initialise (once) from torchrun's env:// variables.
+
+    device_type: 'cuda' | 'cpu' | None (auto: cuda if visible).
+    """
+    global _COMM
+    if _COMM is not None:
+        return _COMM
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if device_type is None:
+        device_type = "cuda" if torch.cuda.is_available() else "cpu"
+    if device_type == "cuda":
+        ndev = torch.cuda.device_count()
+        dev_index = local_rank % max(1, ndev)
+        torch.cuda.set_device(dev_index)
+        device = torch.device("cuda", dev_index)
+    else:
+        device = torch.device("cpu")
+    group = None
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if device_type == "cuda" else "gloo"
+        kw = dict(backend=backend, init_method="env://", world_size=world, rank=rank,
+                  timeout=datetime.timedelta(seconds=timeout_s))
+        if device_type == "cuda":
+            kw["device_id"] = device
+        dist.init_process_group(**kw)
+    _COMM = Comm(device, rank, world, local_rank, group)
+    return _COMM
+
+
+def local_comm(device: torch.device) -> Comm:
+    """A single-rank communicator (no process group)."""
+    return Comm(device, 0, 1, 0, None)
+
+
+def destroy_comm():
+    global _COMM
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    _COMM = None

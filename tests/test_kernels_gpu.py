@@ -1,0 +1,199 @@
+"""Numerics of every HIP kernel against a plain-PyTorch fp64 reference of the same op.
+
+Label checks tolerate only *near ties*: a row may pick a different centroid than the
+fp64 oracle only if that centroid's exact distance is within the kernel's arithmetic
+error of the optimum.
+"""
+import pytest
+import torch
+
+from tensorflow_distributed_clustering_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf16_case(n, d, k, dev, seed=0, spread=3.0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    c = torch.randn(k, d, generator=g, dtype=torch.float64) * spread
+    lab = torch.randint(0, k, (n,), generator=g)
+    x = c[lab] + torch.randn(n, d, generator=g, dtype=torch.float64)
+    return x.to(torch.bfloat16).to(dev), c.to(dev)
+
+
+def _check_labels(x64, c64, labels, rel=2e-5):
+    d = ref.pairwise_sqdist(x64, c64, exact=True)
+    best, _ = d.min(1)
+    got = d.gather(1, labels.long()[:, None]).squeeze(1)
+    scale = (x64 * x64).sum(1) + (c64 * c64).sum(1).max()
+    bad = (got - best) > rel * scale + 1e-9
+    assert int(bad.sum()) == 0, f"{int(bad.sum())} rows not at a (near-)minimum"
+    return best
+
+
+@pytest.mark.parametrize("n,d,k", [(1000, 5, 3), (4097, 32, 64), (12345, 64, 100),
+                                   (30000, 128, 1024), (5000, 100, 257), (3000, 256, 130),
+                                   (777, 128, 15)])
+def test_assign_bf16_mfma(gpu, n, d, k):
+    from tensorflow_distributed_clustering_amd.ops import HipBf16Lloyd
+    xb, c = _bf16_case(n, d, k, gpu, seed=n + d + k)
+    loc = HipBf16Lloyd(xb, k)
+    C = c.float().contiguous()
+    loc.prepare(C)
+    labels = torch.full((n,), -1, dtype=torch.int32, device=gpu)
+    mind = torch.zeros(n, dtype=torch.float32, device=gpu)
+    loc.assign(C, labels, mind)
+    torch.cuda.synchronize()
+    assert int(labels.min()) >= 0 and int(labels.max()) < k
+    x64 = xb.double()
+    c64 = C.to(torch.bfloat16).double()  # the kernel sees bf16-rounded centroids
+    best = _check_labels(x64, c64, labels)
+    scale = (x64 * x64).sum(1) + (c64 * c64).sum(1).max()
+    assert torch.all((mind.double() - best).abs() <= 5e-5 * scale + 1e-4)
+
+
+def test_assign_bf16_exact_integers(gpu):
+    """Small-integer data: every product and sum is exact -> labels must match exactly."""
+    from tensorflow_distributed_clustering_amd.ops import HipBf16Lloyd
+    g = torch.Generator().manual_seed(5)
+    n, d, k = 2048, 128, 192
+    x = torch.randint(-4, 5, (n, d), generator=g).to(torch.float64)
+    c = torch.randint(-4, 5, (k, d), generator=g).to(torch.float64)
+    c[7] = c[3]  # exact duplicate centroid: ties must resolve to the lower index
+    loc = HipBf16Lloyd(x.to(torch.bfloat16).to(gpu), k)
+    C = c.float().to(gpu).contiguous()
+    loc.prepare(C)
+    labels = torch.empty(n, dtype=torch.int32, device=gpu)
+    mind = torch.empty(n, dtype=torch.float32, device=gpu)
+    loc.assign(C, labels, mind)
+    dref = ref.pairwise_sqdist(x, c, exact=True)
+    vref, lref = dref.min(1)
+    assert torch.equal(mind.double().cpu(), vref)
+    # exact distances; with the 5-bit index embedding an exact tie may pick either
+    # of the tied centroids but never a non-minimal one
+    got = dref.gather(1, labels.long().cpu()[:, None]).squeeze(1)
+    assert torch.equal(got, vref)
+    # centroids 3 and 7 sit in different lane halves: the cross-half tie-break picks 3
+    assert not bool((labels.cpu() == 7).any())
+
+
+@pytest.mark.parametrize("xdt", [torch.bfloat16, torch.float32, torch.float64])
+@pytest.mark.parametrize("n,d,k", [(10000, 5, 3), (20000, 128, 1024), (5000, 33, 70), (3000, 300, 40)])
+def test_update_lds(gpu, xdt, n, d, k):
+    from tensorflow_distributed_clustering_amd import _native
+    ops = _native.require()
+    g = torch.Generator().manual_seed(n + d)
+    x = torch.randn(n, d, generator=g).to(xdt).to(gpu)
+    lab = torch.randint(0, k, (n,), generator=g, dtype=torch.int32).to(gpu)
+    lab[:7] = 0  # make sure a hot cluster exists
+    for acc in (torch.float32, torch.float64):
+        sums = torch.zeros(k, d, dtype=acc, device=gpu)
+        counts = torch.zeros(k, dtype=acc, device=gpu)
+        ops.update(x, lab, sums, counts)
+        s_ref, c_ref = ref.cluster_sums(x.double(), lab, k, acc_dtype=torch.float64)
+        assert torch.equal(counts.double(), c_ref)
+        tol = 1e-3 if acc == torch.float32 or xdt != torch.float64 else 1e-9
+        torch.testing.assert_close(sums.double(), s_ref, rtol=tol, atol=tol * 10)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64])
+@pytest.mark.parametrize("k,d", [(3, 5), (15, 5), (8, 2), (16, 8), (4, 16), (32, 3)])
+def test_lloyd_small_fused(gpu, dt, k, d):
+    from tensorflow_distributed_clustering_amd import _native
+    ops = _native.require()
+    if not ops.lloyd_small_supported(dt, k, d):
+        pytest.skip("tile not compiled for this dtype")
+    g = torch.Generator().manual_seed(k * 100 + d)
+    n = 50000
+    x = torch.randn(n, d, generator=g, dtype=torch.float64).to(dt).to(gpu)
+    c = torch.randn(k, d, generator=g, dtype=torch.float64).to(dt).to(gpu)
+    labels = torch.empty(n, dtype=torch.int32, device=gpu)
+    mind = torch.empty(n, dtype=dt, device=gpu)
+    sums = torch.zeros(k, d, dtype=torch.float64, device=gpu)
+    counts = torch.zeros(k, dtype=torch.float64, device=gpu)
+    ops.lloyd_small(x, c, labels, mind, sums, counts)
+    x64, c64 = x.double(), c.double()
+    lref, mref = ref.assign(x64, c64, exact=True)
+    if dt == torch.float64:
+        assert torch.equal(labels, lref)
+    else:
+        _check_labels(x64, c64, labels, rel=1e-6)
+    s_ref, c_ref = ref.cluster_sums(x64, labels, k)
+    assert torch.equal(counts, c_ref)
+    tol = 1e-10 if dt == torch.float64 else 2e-4
+    torch.testing.assert_close(sums, s_ref, rtol=tol, atol=tol)
+    torch.testing.assert_close(mind.double(), mref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64])
+@pytest.mark.parametrize("k,d", [(300, 5), (1000, 17), (64, 32)])
+def test_assign_simt(gpu, dt, k, d):
+    from tensorflow_distributed_clustering_amd import _native
+    ops = _native.require()
+    g = torch.Generator().manual_seed(k + d)
+    n = 20000
+    x = torch.randn(n, d, generator=g, dtype=torch.float64).to(dt).to(gpu)
+    c = torch.randn(k, d, generator=g, dtype=torch.float64).to(dt).to(gpu)
+    labels = torch.empty(n, dtype=torch.int32, device=gpu)
+    mind = torch.empty(n, dtype=dt, device=gpu)
+    ops.assign_simt(x, c, labels, mind)
+    lref, mref = ref.assign(x.double(), c.double(), exact=True)
+    if dt == torch.float64:
+        assert torch.equal(labels, lref)
+    else:
+        _check_labels(x.double(), c.double(), labels, rel=1e-6)
+    torch.testing.assert_close(mind.double(), mref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64])
+@pytest.mark.parametrize("k,d,m", [(3, 5, 5.0), (15, 5, 5.0), (3, 3, 2.0), (8, 2, 2.0), (6, 4, 1.7)])
+@pytest.mark.parametrize("nan_to_zero", [True, False])
+def test_fcm_small(gpu, dt, k, d, m, nan_to_zero):
+    from tensorflow_distributed_clustering_amd import _native
+    ops = _native.require()
+    if not ops.fcm_small_supported(dt, k, d):
+        pytest.skip("tile not compiled")
+    g = torch.Generator().manual_seed(k + d)
+    n = 20000
+    x = torch.randn(n, d, generator=g, dtype=torch.float64)
+    c = torch.randn(k, d, generator=g, dtype=torch.float64)
+    x[5] = c[1]  # a point exactly on a centroid exercises the NaN guard
+    x, c = x.to(dt).to(gpu), c.to(dt).to(gpu)
+    labels = torch.empty(n, dtype=torch.int32, device=gpu)
+    wx = torch.zeros(k, d, dtype=torch.float64, device=gpu)
+    ws = torch.zeros(k, dtype=torch.float64, device=gpu)
+    ops.fcm_small(x, c, m, nan_to_zero, labels, wx, ws)
+    a, b, lr = ref.fcm_partial(x.double(), c.double(), m, nan_to_zero)
+    tol = 1e-9 if dt == torch.float64 else 2e-4
+    torch.testing.assert_close(ws, b, rtol=tol, atol=tol)
+    torch.testing.assert_close(wx, a, rtol=tol, atol=tol * 10)
+    agree = (labels == lr).double().mean().item()
+    assert agree > (0.9999 if dt == torch.float64 else 0.999)
+
+
+@pytest.mark.parametrize("policy", ["keep", "nan", "zero"])
+def test_finalize_and_prep(gpu, policy):
+    from tensorflow_distributed_clustering_amd import _native
+    from tensorflow_distributed_clustering_amd.ops import POLICY_CODES
+    ops = _native.require()
+    k, d = 70, 100
+    g = torch.Generator().manual_seed(1)
+    sums = torch.randn(k, d, generator=g, dtype=torch.float64).to(gpu)
+    counts = torch.randint(0, 5, (k,), generator=g).double().to(gpu)
+    counts[3] = 0
+    C = torch.randn(k, d, generator=g).to(gpu)
+    old = C.clone()
+    shift = torch.zeros(1, device=gpu)
+    cm2 = torch.zeros(128, 128, dtype=torch.bfloat16, device=gpu)
+    cn = torch.zeros(128, device=gpu)
+    ops.finalize(sums, counts, C, POLICY_CODES[policy], shift, cm2, cn)
+    exp = ref.finalize(sums, counts, old, policy)
+    torch.testing.assert_close(C, exp, equal_nan=True)
+    cb = C.to(torch.bfloat16)
+    assert torch.equal(cm2[:k, :d], (-2 * cb.float()).to(torch.bfloat16))
+    assert torch.all(cm2[:, d:] == 0) and torch.all(cm2[k:] == 0)
+    assert torch.all(cn[k:] > 1e38)
+    fin = torch.isfinite(C).all(1)
+    torch.testing.assert_close(cn[:k][fin], (cb.float() ** 2).sum(1)[fin], rtol=1e-5, atol=1e-5)
+    if policy == "keep":
+        dd = ((C.double() - old.double()) ** 2).sum(1).max()
+        torch.testing.assert_close(shift.double()[0], dd, rtol=1e-4, atol=1e-6)
