@@ -127,7 +127,7 @@ def phase_breakdown(eng, torch, dev, reps: int = 5):
         eng.buf.zero_(); e[1].record()
         if hasattr(loc, "cm2"):
             loc.ops.assign_bf16(loc.x, loc.cm2, loc.cnorm, eng.labels, None); e[2].record()
-            loc.ops.update(loc.x, eng.labels, eng.sums, eng.counts); e[3].record()
+            loc.update(loc.x, eng.labels, eng.sums, eng.counts); e[3].record()
         else:
             loc.step(eng.C, eng.labels, None, eng.sums, eng.counts); e[2].record(); e[3].record()
         eng.comm.allreduce_bucketed_(eng.buf, eng.bucket_bytes); e[4].record()

@@ -143,6 +143,29 @@ void update(const at::Tensor& X, const at::Tensor& labels, at::Tensor& sums, at:
         "update");
 }
 
+int64_t update_sorted_workspace(int64_t N, int64_t K) { return tdc_update_sorted_workspace(N, (int)K); }
+
+void update_sorted(const at::Tensor& X, const at::Tensor& labels, at::Tensor& sums,
+                   at::Tensor& counts, at::Tensor& work) {
+  check_cuda(X, "X");
+  check_rows(X, "X");
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous() && labels.numel() >= X.size(0),
+              "tdc.update_sorted: labels int32 [N]");
+  TORCH_CHECK(sums.dim() == 2 && sums.is_contiguous() && counts.is_contiguous(), "tdc.update_sorted: sums");
+  TORCH_CHECK(sums.scalar_type() == counts.scalar_type() && counts.numel() >= sums.size(0),
+              "tdc.update_sorted: counts");
+  TORCH_CHECK(X.size(1) >= sums.size(1), "tdc.update_sorted: X narrower than sums");
+  TORCH_CHECK(work.scalar_type() == at::kInt && work.is_contiguous() &&
+                  work.numel() >= tdc_update_sorted_workspace(X.size(0), (int)sums.size(0)),
+              "tdc.update_sorted: workspace too small");
+  const DevGuard guard(X.device());
+  check(tdc_update_sorted(dcode(X.scalar_type()), dcode(sums.scalar_type()), X.data_ptr(),
+                          X.size(0), X.stride(0), (int)sums.size(1), labels.data_ptr<int32_t>(),
+                          (int)sums.size(0), sums.data_ptr(), counts.data_ptr(),
+                          work.data_ptr<int>(), num_cus(X.device().index()), cur_stream()),
+        "update_sorted");
+}
+
 bool fcm_small_supported(at::ScalarType dtype, int64_t K, int64_t D) {
   if (dtype != at::kFloat && dtype != at::kDouble) return false;
   return tdc_fcm_small_supported(dcode(dtype), (int)K, (int)D) != 0;
@@ -203,6 +226,8 @@ TORCH_LIBRARY(tdc, m) {
   m.def("lloyd_small_supported(ScalarType dtype, int K, int D) -> bool", &lloyd_small_supported);
   m.def("lloyd_small(Tensor X, Tensor C, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!) sums, Tensor(d!) counts) -> ()");
   m.def("update(Tensor X, Tensor labels, Tensor(a!) sums, Tensor(b!) counts) -> ()");
+  m.def("update_sorted_workspace(int N, int K) -> int", &update_sorted_workspace);
+  m.def("update_sorted(Tensor X, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work) -> ()");
   m.def("fcm_small_supported(ScalarType dtype, int K, int D) -> bool", &fcm_small_supported);
   m.def("fcm_small(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) wx, Tensor(c!) ws) -> ()");
   m.def("finalize(Tensor? sums, Tensor? counts, Tensor(a!) C, int policy, Tensor(b!)? shift, Tensor(c!)? Cm2, Tensor(d!)? cnorm) -> ()");
@@ -213,6 +238,7 @@ TORCH_LIBRARY_IMPL(tdc, CUDA, m) {
   m.impl("assign_simt", &assign_simt);
   m.impl("lloyd_small", &lloyd_small);
   m.impl("update", &update);
+  m.impl("update_sorted", &update_sorted);
   m.impl("fcm_small", &fcm_small);
   m.impl("finalize", &finalize);
 }

@@ -32,6 +32,14 @@ int tdc_update_lds(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t
                    const int32_t* labels, int K, void* sums, void* counts, int num_cus,
                    hipStream_t stream);
 
+// N2 (large K x D): counting sort by label + segmented row gather-sum.  work: int32
+// workspace of tdc_update_sorted_workspace(N, K) elements.  sums/counts are accumulated
+// (caller zeroes them once per pass).
+int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
+                      const int32_t* labels, int K, void* sums, void* counts, int* work,
+                      int num_cus, hipStream_t stream);
+int64_t tdc_update_sorted_workspace(int64_t N, int K);
+
 // N4/N5  fused small-K Fuzzy C-Means tower: sum_i w_ki x_i, sum_i w_ki, argmax labels.
 int tdc_fcm_small(int dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
                   const void* C, int K, double m, int nan_to_zero, int32_t* labels, void* wx,

@@ -201,18 +201,34 @@ __global__ __launch_bounds__(256) void update_lds_kernel(const XT* __restrict__ 
   const int dd = j * VEC;
   const int64_t r0 = chunk * rows_per_block;
   const int64_t r1 = min(N, r0 + rows_per_block);
-  for (int64_t row = r0 + rsub; row < r1; row += rpi) {
-    const int lab = labels[row];
-    if ((unsigned)lab >= (unsigned)K) continue;  // never index LDS out of range
-    if (dd < ds) {
-      LT v[VEC];
-      if constexpr (VEC == 1) VecLoad1<XT>::load(X + row * ldx + d0 + dd, v);
-      else VecLoad<XT, VEC>::load(X + row * ldx + d0 + dd, v);
-      LT* dst = s_sum + lab * stride + dd;
+  constexpr int R = 8;  // rows per thread in flight: hides the label -> row load chain
+  for (int64_t row0 = r0 + rsub; row0 < r1; row0 += (int64_t)rpi * R) {
+    int lab[R];
+    LT v[R][VEC];
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) atomicAdd(dst + e, v[e]);
+    for (int u = 0; u < R; ++u) {
+      const int64_t row = row0 + (int64_t)u * rpi;
+      lab[u] = row < r1 ? labels[row] : -1;
+      if ((unsigned)lab[u] >= (unsigned)K) lab[u] = -1;  // never index LDS out of range
     }
-    if (j == 0) atomicAdd(s_cnt + lab, 1);
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const int64_t row = row0 + (int64_t)u * rpi;
+      if (lab[u] >= 0 && dd < ds) {
+        if constexpr (VEC == 1) VecLoad1<XT>::load(X + row * ldx + d0 + dd, v[u]);
+        else VecLoad<XT, VEC>::load(X + row * ldx + d0 + dd, v[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      if (lab[u] < 0) continue;
+      if (dd < ds) {
+        LT* dst = s_sum + lab[u] * stride + dd;
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) atomicAdd(dst + e, v[u][e]);
+      }
+      if (j == 0) atomicAdd(s_cnt + lab[u], 1);
+    }
   }
   __syncthreads();
   for (int i = tid; i < K * ds; i += 256) {

@@ -1,0 +1,342 @@
+// N2 (large K x D): per-cluster sums via counting sort + segmented gather-sum.
+//
+// When K x D does not fit LDS (K=1024 x D=128 fp32 = 512 KB; K=65536 x D=768 = 201 MB)
+// the LDS histogram of update_lds would need D-slices and one flush of K x D_slice
+// global atomics per block, and its label -> row load chain is latency bound.  Instead:
+//
+//   1. hist     : labels -> per-cluster counts (LDS histogram per block, one global
+//                 atomic per non-empty bin per block)
+//   2. scan     : exclusive prefix sum -> segment offsets; counts also added (acc dtype)
+//                 straight into the all-reduce buffer
+//   3. scatter  : counting-sort the point indices by label (block-aggregated cursor
+//                 reservation: one returning global atomic per bin per block)
+//   4. segsum   : each wave walks a contiguous range of the sorted index, gathers whole
+//                 rows (16 B per lane, a row per 16/32/64 lanes), accumulates in fp32
+//                 registers and flushes with global atomics only at segment boundaries
+//                 (~1-3 flushes per wave instead of one atomic per element).
+//
+// X is read exactly once (as whole-row gathers); labels twice; the permutation once.
+#include "tdc_common.h"
+#include "kernels.h"
+
+namespace tdc {
+
+constexpr int LDS_HIST_MAX_K = 16384;
+
+__global__ __launch_bounds__(256) void hist_kernel(const int32_t* __restrict__ labels, int64_t N,
+                                                   int K, int* __restrict__ cnt,
+                                                   int64_t per_block) {
+  extern __shared__ int s_h[];
+  const int tid = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * per_block;
+  const int64_t r1 = min(N, r0 + per_block);
+  const bool lds = K <= LDS_HIST_MAX_K;
+  if (lds) {
+    for (int k = tid; k < K; k += 256) s_h[k] = 0;
+    __syncthreads();
+  }
+  int64_t i = r0 + tid;
+  for (; i + 3 * 256 < r1; i += 4 * 256) {
+    const int a = labels[i], b = labels[i + 256], c = labels[i + 512], d = labels[i + 768];
+    if (lds) {
+      if ((unsigned)a < (unsigned)K) atomicAdd(s_h + a, 1);
+      if ((unsigned)b < (unsigned)K) atomicAdd(s_h + b, 1);
+      if ((unsigned)c < (unsigned)K) atomicAdd(s_h + c, 1);
+      if ((unsigned)d < (unsigned)K) atomicAdd(s_h + d, 1);
+    } else {
+      if ((unsigned)a < (unsigned)K) atomicAdd(cnt + a, 1);
+      if ((unsigned)b < (unsigned)K) atomicAdd(cnt + b, 1);
+      if ((unsigned)c < (unsigned)K) atomicAdd(cnt + c, 1);
+      if ((unsigned)d < (unsigned)K) atomicAdd(cnt + d, 1);
+    }
+  }
+  for (; i < r1; i += 256) {
+    const int a = labels[i];
+    if ((unsigned)a < (unsigned)K) atomicAdd(lds ? s_h + a : cnt + a, 1);
+  }
+  if (lds) {
+    __syncthreads();
+    for (int k = tid; k < K; k += 256)
+      if (s_h[k]) atomicAdd(cnt + k, s_h[k]);
+  }
+}
+
+// single block, 1024 threads: offsets[0..K] (exclusive), cursor = offsets, counts_acc = cnt
+template <typename ACC>
+__global__ __launch_bounds__(1024) void scan_kernel(const int* __restrict__ cnt, int K,
+                                                    int* __restrict__ offsets,
+                                                    int* __restrict__ cursor,
+                                                    ACC* __restrict__ counts_acc) {
+  __shared__ int s_part[1024];
+  const int tid = threadIdx.x;
+  const int per = (K + 1023) / 1024;
+  const int k0 = tid * per, k1 = min(K, k0 + per);
+  int s = 0;
+  for (int k = k0; k < k1; ++k) s += cnt[k];
+  s_part[tid] = s;
+  __syncthreads();
+  // Hillis-Steele inclusive scan over 1024 partials
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int v = tid >= o ? s_part[tid - o] : 0;
+    __syncthreads();
+    s_part[tid] += v;
+    __syncthreads();
+  }
+  int run = s_part[tid] - s;  // exclusive prefix of this thread's range
+  for (int k = k0; k < k1; ++k) {
+    const int c = cnt[k];
+    offsets[k] = run;
+    cursor[k] = run;
+    if (counts_acc) counts_acc[k] += (ACC)c;  // accumulate: streamed chunks add up
+    run += c;
+  }
+  if (tid == 1023) offsets[K] = s_part[1023];
+}
+
+// block-aggregated counting-sort scatter: perm[offset[label] + rank] = i
+__global__ __launch_bounds__(256) void scatter_kernel(const int32_t* __restrict__ labels, int64_t N,
+                                                      int K, int* __restrict__ cursor,
+                                                      int32_t* __restrict__ perm,
+                                                      int64_t per_block) {
+  constexpr int R = 16;  // labels per thread per pass (4096 per block pass)
+  extern __shared__ int s_mem[];
+  int* s_cnt = s_mem;
+  int* s_base = s_mem + K;
+  const int tid = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * per_block;
+  const int64_t r1 = min(N, r0 + per_block);
+  const bool agg = K <= 4096;
+  for (int64_t p0 = r0; p0 < r1; p0 += 256 * R) {
+    int lab[R], rank[R];
+    if (agg) {
+      for (int k = tid; k < K; k += 256) s_cnt[k] = 0;
+      __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int64_t i = p0 + j * 256 + tid;
+      lab[j] = (i < r1) ? labels[i] : -1;
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      rank[j] = -1;
+      if ((unsigned)lab[j] < (unsigned)K)
+        rank[j] = agg ? atomicAdd(s_cnt + lab[j], 1) : atomicAdd(cursor + lab[j], 1);
+    }
+    if (agg) {
+      __syncthreads();
+      for (int k = tid; k < K; k += 256) {
+        const int c = s_cnt[k];
+        s_base[k] = c ? atomicAdd(cursor + k, c) : 0;
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      if (rank[j] >= 0) {
+        const int pos = agg ? s_base[lab[j]] + rank[j] : rank[j];
+        perm[pos] = (int32_t)(p0 + j * 256 + tid);
+      }
+    }
+    if (agg) __syncthreads();
+  }
+}
+
+template <typename XT, int VEC> struct RowLoad;
+template <> struct RowLoad<__bf16, 8> {
+  typedef float acc_t;
+  __device__ static void add(const __bf16* p, float (&a)[8]) {
+    const uint4 t = *reinterpret_cast<const uint4*>(p);
+    a[0] += __uint_as_float(t.x << 16); a[1] += __uint_as_float(t.x & 0xffff0000u);
+    a[2] += __uint_as_float(t.y << 16); a[3] += __uint_as_float(t.y & 0xffff0000u);
+    a[4] += __uint_as_float(t.z << 16); a[5] += __uint_as_float(t.z & 0xffff0000u);
+    a[6] += __uint_as_float(t.w << 16); a[7] += __uint_as_float(t.w & 0xffff0000u);
+  }
+};
+template <> struct RowLoad<float, 4> {
+  typedef float acc_t;
+  __device__ static void add(const float* p, float (&a)[4]) {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    a[0] += t.x; a[1] += t.y; a[2] += t.z; a[3] += t.w;
+  }
+};
+template <> struct RowLoad<double, 2> {
+  typedef double acc_t;
+  __device__ static void add(const double* p, double (&a)[2]) {
+    const double2 t = *reinterpret_cast<const double2*>(p);
+    a[0] += t.x; a[1] += t.y;
+  }
+};
+template <typename XT> struct RowLoad1 {
+  typedef typename std::conditional<sizeof(XT) == 8, double, float>::type acc_t;
+  __device__ static void add(const XT* p, acc_t (&a)[1]) { a[0] += (acc_t)p[0]; }
+};
+
+// each wave: rows [a, b) of the sorted permutation; TPR lanes per row, G = 64/TPR rows
+// in flight per wave-instruction, columns [c0, c0 + TPR*VEC) per pass
+template <typename XT, typename ACC, int VEC, int TPR>
+__global__ __launch_bounds__(256) void segsum_kernel(const XT* __restrict__ X, int64_t ldx, int D,
+                                                     const int32_t* __restrict__ perm,
+                                                     const int* __restrict__ offsets, int K,
+                                                     int64_t N, ACC* __restrict__ sums,
+                                                     int64_t rows_per_wave) {
+  typedef typename RowLoad1<XT>::acc_t AT;  // fp64 data -> fp64 partials, else fp32
+  constexpr int G = 64 / TPR;
+  constexpr int U = 4;  // rows per group in flight
+  const int lane = threadIdx.x & 63;
+  const int g = lane / TPR, t = lane % TPR;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t a = wave * rows_per_wave;
+  if (a >= N) return;
+  const int64_t b = min(N, a + rows_per_wave);
+  // segment containing a: largest k with offsets[k] <= a
+  int lo = 0, hi = K;  // invariant offsets[lo] <= a < offsets[hi]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (offsets[mid] <= a) lo = mid; else hi = mid;
+  }
+  for (int c0 = 0; c0 < D; c0 += TPR * VEC) {
+    const int col = c0 + t * VEC;
+    const bool colok = col < D;
+    int k = lo;
+    int64_t kend = offsets[k + 1];
+    AT acc[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) acc[e] = 0;
+#define TDC_FLUSH(KK)                                                                 \
+  do {                                                                                \
+    if (colok) {                                                                      \
+      _Pragma("unroll") for (int e = 0; e < VEC; ++e) if (col + e < D && acc[e] != (AT)0) \
+          atomic_add(&sums[(int64_t)(KK) * D + col + e], (ACC)acc[e]);                \
+    }                                                                                 \
+    _Pragma("unroll") for (int e = 0; e < VEC; ++e) acc[e] = 0;                       \
+  } while (0)
+    int64_t j = a + g;
+    // fast path: U rows of this group all inside the current segment
+    while (j < b) {
+      if (j + (U - 1) * G < min(b, kend)) {
+        int32_t idx[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) idx[u] = perm[j + u * G];
+        if (colok) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            if constexpr (VEC == 1) RowLoad1<XT>::add(X + (int64_t)idx[u] * ldx + col, acc);
+            else RowLoad<XT, VEC>::add(X + (int64_t)idx[u] * ldx + col, acc);
+          }
+        }
+        j += U * G;
+      } else {
+        while (j >= kend) {  // crossed into a later segment
+          TDC_FLUSH(k);
+          ++k;
+          kend = offsets[k + 1];
+        }
+        const int32_t idx = perm[j];
+        if (colok) {
+          if constexpr (VEC == 1) RowLoad1<XT>::add(X + (int64_t)idx * ldx + col, acc);
+          else RowLoad<XT, VEC>::add(X + (int64_t)idx * ldx + col, acc);
+        }
+        j += G;
+      }
+    }
+    TDC_FLUSH(k);
+  }
+#undef TDC_FLUSH
+}
+
+}  // namespace tdc
+
+using namespace tdc;
+
+namespace {
+
+template <typename XT, typename ACC, int VEC>
+int launch_segsum(const void* X, int64_t ldx, int D, const int32_t* perm, const int* offsets,
+                  int K, int64_t N, void* sums, int num_cus, hipStream_t s) {
+  const int lanes_needed = (D + VEC - 1) / VEC;
+  int64_t waves = (int64_t)num_cus * 32;  // ~8 resident 256-thread blocks per CU
+  int64_t rpw = (N + waves - 1) / waves;
+  if (rpw < 256) rpw = 256;
+  waves = (N + rpw - 1) / rpw;
+  const dim3 grid((unsigned)((waves + 3) / 4));
+#define TDC_SEG(TPRV)                                                                       \
+  hipLaunchKernelGGL((segsum_kernel<XT, ACC, VEC, TPRV>), grid, dim3(256), 0, s, (const XT*)X, \
+                     ldx, D, perm, offsets, K, N, (ACC*)sums, rpw)
+  if (lanes_needed <= 4) TDC_SEG(4);
+  else if (lanes_needed <= 8) TDC_SEG(8);
+  else if (lanes_needed <= 16) TDC_SEG(16);
+  else if (lanes_needed <= 32) TDC_SEG(32);
+  else TDC_SEG(64);
+#undef TDC_SEG
+  TDC_CHECK_LAUNCH();
+  return 0;
+}
+
+template <typename ACC>
+int dispatch_segsum(int x_dtype, const void* X, int64_t ldx, int D, const int32_t* perm,
+                    const int* offsets, int K, int64_t N, void* sums, int num_cus, hipStream_t s) {
+  const bool a16 = ((uintptr_t)X % 16) == 0;
+  if (x_dtype == TDC_BF16) {
+    if (a16 && D % 8 == 0 && ldx % 8 == 0)
+      return launch_segsum<__bf16, ACC, 8>(X, ldx, D, perm, offsets, K, N, sums, num_cus, s);
+    return launch_segsum<__bf16, ACC, 1>(X, ldx, D, perm, offsets, K, N, sums, num_cus, s);
+  }
+  if (x_dtype == TDC_F32) {
+    if (a16 && D % 4 == 0 && ldx % 4 == 0)
+      return launch_segsum<float, ACC, 4>(X, ldx, D, perm, offsets, K, N, sums, num_cus, s);
+    return launch_segsum<float, ACC, 1>(X, ldx, D, perm, offsets, K, N, sums, num_cus, s);
+  }
+  if (x_dtype == TDC_F64) {
+    if (a16 && D % 2 == 0 && ldx % 2 == 0)
+      return launch_segsum<double, ACC, 2>(X, ldx, D, perm, offsets, K, N, sums, num_cus, s);
+    return launch_segsum<double, ACC, 1>(X, ldx, D, perm, offsets, K, N, sums, num_cus, s);
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+}  // namespace
+
+int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
+                      const int32_t* labels, int K, void* sums, void* counts, int* work,
+                      int num_cus, hipStream_t s) {
+  if (N <= 0) return 0;
+  if (N >= (int64_t)1 << 31) return (int)hipErrorInvalidValue;
+  // workspace layout (ints): cnt[K] | offsets[K+1] | cursor[K] | perm[N]
+  int* cnt = work;
+  int* offsets = cnt + K;
+  int* cursor = offsets + K + 1;
+  int32_t* perm = cursor + K;
+  if (hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)K, s) != hipSuccess) return (int)hipErrorUnknown;
+  {
+    int64_t blocks = (int64_t)num_cus * 4;
+    int64_t per = (N + blocks - 1) / blocks;
+    if (per < 4096) per = 4096;
+    blocks = (N + per - 1) / per;
+    const size_t lds = K <= LDS_HIST_MAX_K ? sizeof(int) * (size_t)K : 0;
+    hipLaunchKernelGGL(hist_kernel, dim3((unsigned)blocks), dim3(256), lds, s, labels, N, K, cnt, per);
+    TDC_CHECK_LAUNCH();
+  }
+  if (acc_dtype == TDC_F64)
+    hipLaunchKernelGGL(scan_kernel<double>, dim3(1), dim3(1024), 0, s, cnt, K, offsets, cursor,
+                       (double*)counts);
+  else
+    hipLaunchKernelGGL(scan_kernel<float>, dim3(1), dim3(1024), 0, s, cnt, K, offsets, cursor,
+                       (float*)counts);
+  TDC_CHECK_LAUNCH();
+  {
+    int64_t blocks = (int64_t)num_cus * 4;
+    int64_t per = (N + blocks - 1) / blocks;
+    per = ((per + 4095) / 4096) * 4096;
+    blocks = (N + per - 1) / per;
+    const size_t lds = K <= 4096 ? 2 * sizeof(int) * (size_t)K : 0;
+    hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)blocks), dim3(256), lds, s, labels, N, K,
+                       cursor, perm, per);
+    TDC_CHECK_LAUNCH();
+  }
+  if (acc_dtype == TDC_F64)
+    return dispatch_segsum<double>(x_dtype, X, ldx, D, perm, offsets, K, N, sums, num_cus, s);
+  return dispatch_segsum<float>(x_dtype, X, ldx, D, perm, offsets, K, N, sums, num_cus, s);
+}
+
+int64_t tdc_update_sorted_workspace(int64_t N, int K) { return 3 * (int64_t)K + 1 + N; }

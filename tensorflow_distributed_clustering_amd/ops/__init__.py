@@ -59,6 +59,31 @@ def use_native(device: torch.device, backend: str) -> bool:
     return True
 
 
+class NativeUpdate:
+    """N2 dispatcher: LDS-privatised histogram when K x D fits one LDS slice, otherwise
+    counting sort + segmented gather-sum (workspace allocated once per shard)."""
+
+    LDS_BUDGET = 64 * 1024
+
+    def __init__(self, ops, n: int, k: int, d: int, x_dtype: torch.dtype, device):
+        self.ops = ops
+        es = 8 if x_dtype == torch.float64 else 4
+        self.kind = "lds" if k * (d + 1) * es + 4 * k <= self.LDS_BUDGET else "sorted"
+        self.work = None
+        if self.kind == "sorted":
+            self.work = torch.empty(int(ops.update_sorted_workspace(n, k)), dtype=torch.int32,
+                                    device=device)
+
+    def __call__(self, x, labels, sums, counts):
+        if self.kind == "lds":
+            self.ops.update(x, labels, sums, counts)
+        else:
+            if self.work.numel() < int(self.ops.update_sorted_workspace(x.shape[0], sums.shape[0])):
+                self.work = torch.empty(int(self.ops.update_sorted_workspace(x.shape[0], sums.shape[0])),
+                                        dtype=torch.int32, device=x.device)
+            self.ops.update_sorted(x, labels, sums, counts, self.work)
+
+
 class _LocalOpsBase:
     name = "base"
 
@@ -131,13 +156,14 @@ class HipBf16Lloyd(_LocalOpsBase):
         self.kp = ((k + 63) // 64) * 64
         self.cm2 = torch.zeros(self.kp, dp, dtype=torch.bfloat16, device=x.device)
         self.cnorm = torch.zeros(self.kp, dtype=torch.float32, device=x.device)
+        self.update = NativeUpdate(self.ops, self.n, k, self.d, torch.bfloat16, x.device)
 
     def prepare(self, C):
         self.ops.finalize(None, None, C, 0, None, self.cm2, self.cnorm)
 
     def step(self, C, labels, mind, sums, counts):
         self.ops.assign_bf16(self.x, self.cm2, self.cnorm, labels, mind)
-        self.ops.update(self.x, labels, sums, counts)
+        self.update(self.x, labels, sums, counts)
 
     def assign(self, C, labels, mind):
         self.ops.assign_bf16(self.x, self.cm2, self.cnorm, labels, mind)
@@ -153,6 +179,7 @@ class _HipExactBase(_LocalOpsBase):
         tdt = TORCH_DTYPES[dtype]
         self.x = x.to(tdt).contiguous()
         self.c_dtype = tdt
+        self.update = NativeUpdate(self.ops, self.n, k, self.d, tdt, x.device)
 
     def finalize(self, sums, counts, C, shift):
         self.ops.finalize(sums, counts, C, self.policy, shift, None, None)
@@ -173,7 +200,7 @@ class HipSimtLloyd(_HipExactBase):
 
     def step(self, C, labels, mind, sums, counts):
         self.ops.assign_simt(self.x, C, labels, mind)
-        self.ops.update(self.x, labels, sums, counts)
+        self.update(self.x, labels, sums, counts)
 
     def assign(self, C, labels, mind):
         self.ops.assign_simt(self.x, C, labels, mind)
@@ -185,7 +212,7 @@ class HipGemmLloyd(_HipExactBase):
 
     def step(self, C, labels, mind, sums, counts):
         self.assign(C, labels, mind)
-        self.ops.update(self.x, labels, sums, counts)
+        self.update(self.x, labels, sums, counts)
 
     def assign(self, C, labels, mind):
         lab, md = ref.assign(self.x, C, exact=False)

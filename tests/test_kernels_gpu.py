@@ -95,6 +95,28 @@ def test_update_lds(gpu, xdt, n, d, k):
         torch.testing.assert_close(sums.double(), s_ref, rtol=tol, atol=tol * 10)
 
 
+@pytest.mark.parametrize("xdt", [torch.bfloat16, torch.float32, torch.float64])
+@pytest.mark.parametrize("n,d,k", [(10000, 5, 3), (50000, 128, 1024), (5000, 33, 70),
+                                   (3000, 300, 40), (20000, 64, 5000), (4000, 768, 20000)])
+def test_update_sorted(gpu, xdt, n, d, k):
+    from tensorflow_distributed_clustering_amd import _native
+    ops = _native.require()
+    g = torch.Generator().manual_seed(n + d + 1)
+    x = torch.randn(n, d, generator=g).to(xdt).to(gpu)
+    lab = torch.randint(0, k, (n,), generator=g, dtype=torch.int32).to(gpu)
+    lab[: n // 3] = 1  # one long segment spanning many waves
+    work = torch.empty(int(ops.update_sorted_workspace(n, k)), dtype=torch.int32, device=gpu)
+    s_ref, c_ref = ref.cluster_sums(x.double(), lab, k, acc_dtype=torch.float64)
+    for acc in (torch.float32, torch.float64):
+        sums = torch.zeros(k, d, dtype=acc, device=gpu)
+        counts = torch.zeros(k, dtype=acc, device=gpu)
+        ops.update_sorted(x, lab, sums, counts, work)
+        ops.update_sorted(x, lab, sums, counts, work)  # accumulates (streamed chunks)
+        assert torch.equal(counts.double(), 2 * c_ref)
+        tol = 1e-3 if acc == torch.float32 or xdt != torch.float64 else 1e-9
+        torch.testing.assert_close(sums.double(), 2 * s_ref, rtol=tol, atol=tol * 10)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.float64])
 @pytest.mark.parametrize("k,d", [(3, 5), (15, 5), (8, 2), (16, 8), (4, 16), (32, 3)])
 def test_lloyd_small_fused(gpu, dt, k, d):
@@ -189,7 +211,8 @@ def test_finalize_and_prep(gpu, policy):
     exp = ref.finalize(sums, counts, old, policy)
     torch.testing.assert_close(C, exp, equal_nan=True)
     cb = C.to(torch.bfloat16)
-    assert torch.equal(cm2[:k, :d], (-2 * cb.float()).to(torch.bfloat16))
+    torch.testing.assert_close(cm2[:k, :d], (-2 * cb.float()).to(torch.bfloat16), rtol=0, atol=0,
+                               equal_nan=True)
     assert torch.all(cm2[:, d:] == 0) and torch.all(cm2[k:] == 0)
     assert torch.all(cn[k:] > 1e38)
     fin = torch.isfinite(C).all(1)
