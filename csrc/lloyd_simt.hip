@@ -47,7 +47,7 @@ __global__ __launch_bounds__(256) void lloyd_small_kernel(
     T x[DMAX];
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) x[d] = (d < D) ? X[i * ldx + d] : (T)0;
-    T bd = (T)0;
+    T bd = (T)INFINITY;  // NaN distances (poisoned centroid, empty_cluster='nan') never win
     int best = 0;
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void lloyd_small_kernel(
           const T df = x[d] - s_c[k * DMAX + d];
           dd = fma(df, df, dd);
         }
-        if (k == 0 || dd < bd) {  // strict: first minimum wins (TF ArgMin)
+        if (dd < bd) {  // strict: first minimum wins (TF ArgMin)
           bd = dd;
           best = k;
         }
@@ -115,8 +115,8 @@ __global__ __launch_bounds__(256) void assign_simt_kernel(const T* __restrict__ 
   T x[DMAX];
 #pragma unroll
   for (int d = 0; d < DMAX; ++d) x[d] = (i < N && d < D) ? X[i * ldx + d] : (T)0;
-  T bd = (T)0;
-  int best = -1;
+  T bd = (T)INFINITY;
+  int best = 0;
   for (int k0 = 0; k0 < K; k0 += KT) {
     const int kt = min(KT, K - k0);
     __syncthreads();
@@ -132,7 +132,7 @@ __global__ __launch_bounds__(256) void assign_simt_kernel(const T* __restrict__ 
         const T df = x[d] - s_c[k * DMAX + d];
         dd = fma(df, df, dd);
       }
-      if (best < 0 || dd < bd) {
+      if (dd < bd) {
         bd = dd;
         best = k0 + k;
       }

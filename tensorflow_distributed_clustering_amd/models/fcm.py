@@ -57,7 +57,7 @@ class FuzzyCMeans:
         t1 = time.perf_counter()
         c0 = init_centers(cfg.init, x_local, row_offset, n_global, k, comm, cfg.seed,
                           given=init_centers_)
-        C = c0.to(local.c_dtype).contiguous()
+        C = c0.to(local.c_dtype).clone().contiguous()
         buf = torch.zeros(k * d + k, dtype=torch.float64, device=dev)
         wx = buf[: k * d].view(k, d)
         ws = buf[k * d:]

@@ -133,6 +133,8 @@ def init_kmeanspp(x_local, row_offset, n_global, k, comm: Comm, seed,
 def init_centers(method: str, x_local: torch.Tensor, row_offset: int, n_global: int, k: int,
                  comm: Comm, seed: int = 0, given: Optional[torch.Tensor] = None) -> torch.Tensor:
     """[K, D] float64 on the shard's device, identical on every rank."""
+    if given is None and method != "given" and k > n_global:
+        raise ValueError(f"K={k} is larger than the number of points N={n_global}")
     if given is not None or method == "given":
         if given is None:
             raise ValueError("init='given' needs init_centers")

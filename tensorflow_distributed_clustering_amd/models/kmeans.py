@@ -81,7 +81,7 @@ class LloydEngine:
         self.x_local = x_local
         self.c0 = init_centers(cfg.init, x_local, row_offset, n_global, k, comm, cfg.seed,
                                given=init_centers_)
-        self.C = self.c0.to(self.local.c_dtype).contiguous()
+        self.C = self.c0.to(self.local.c_dtype).clone().contiguous()  # never alias c0
         self.local.prepare(self.C)
         acc = acc_dtype_for(cfg.dtype, k, d)
         self.buf = torch.zeros(k * d + k, dtype=acc, device=dev)

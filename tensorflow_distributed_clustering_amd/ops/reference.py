@@ -54,6 +54,7 @@ def assign(x: torch.Tensor, c: torch.Tensor, exact: bool = False,
     step = _chunk_rows(n, k, chunk_elems)
     for s in range(0, n, step):
         d = pairwise_sqdist(x[s:s + step], c, exact=exact)
+        d = torch.nan_to_num(d, nan=float("inf"))  # a NaN (poisoned) centroid never wins
         v, i = d.min(1)
         labels[s:s + step] = i.to(torch.int32)
         mind[s:s + step] = v

@@ -1,0 +1,80 @@
+"""Data-parallel correctness without GPUs: world sizes 2/3/4 on the gloo backend must
+reproduce the single-process result (fp64; equal up to the summation order of the
+packed all-reduce).  Replaces the reference's lack of any fake-cluster testing.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, method, init, q, n, d, k, iters, seed, extra):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    import tensorflow_distributed_clustering_amd as tdc
+    from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs
+    from tensorflow_distributed_clustering_amd.parallel import dist as D
+    D._COMM = None
+    comm = D.init_comm("cpu")
+    s, e = comm.shard(n)
+    x = gaussian_blobs(e - s, d, k, seed=seed, row_offset=s, dtype=torch.float64)
+    cfg = tdc.ClusterConfig(n_clusters=k, max_iter=iters, dtype="fp64", init=init, seed=seed, **extra)
+    model = (tdc.KMeans if method == "kmeans" else tdc.FuzzyCMeans)(cfg, comm)
+    model.fit(x, n_global=n, row_offset=s)
+    r = model.result_
+    labels = comm.gather_rows_to_root(r.labels)
+    if rank == 0:
+        q.put((r.centers, labels.numpy(), r.inertia, r.n_iter, r.init_centers))
+    D.destroy_comm()
+
+
+def run_world(world, method="kmeans", init="random", n=6001, d=3, k=5, iters=6, seed=11, extra=None):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, method, init, q, n, d, k, iters,
+                                                seed, extra or {}))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("init", ["random", "kmeans++"])
+def test_kmeans_dp_equals_single(world, init):
+    c1, l1, in1, it1, i1 = run_world(1, init=init)
+    cw, lw, inw, itw, iw = run_world(world, init=init)
+    np.testing.assert_array_equal(i1, iw)  # init is world-size invariant
+    np.testing.assert_allclose(cw, c1, rtol=1e-12, atol=1e-12)
+    np.testing.assert_array_equal(lw, l1)
+    assert abs(inw - in1) <= 1e-9 * abs(in1)
+    assert itw == it1
+
+
+def test_fcm_dp_equals_single():
+    c1, l1, *_ = run_world(1, method="fcm", init="first_k", d=4, k=3)
+    c4, l4, *_ = run_world(4, method="fcm", init="first_k", d=4, k=3)
+    np.testing.assert_allclose(c4, c1, rtol=1e-12, atol=1e-12)
+    np.testing.assert_array_equal(l4, l1)
+
+
+def test_dp_tolerance_stop_consistent():
+    c1, _, _, it1, _ = run_world(1, iters=200, extra={"tol": 1e-10})
+    c2, _, _, it2, _ = run_world(2, iters=200, extra={"tol": 1e-10})
+    assert it1 == it2 and it1 < 200
+    np.testing.assert_allclose(c2, c1, rtol=1e-12, atol=1e-12)
