@@ -8,9 +8,10 @@ PyTorch-ROCm for memory/streams.  See SURVEY.md for the reference map.
 from .config import ClusterConfig
 from .models.kmeans import KMeans, ClusterResult
 from .models.fcm import FuzzyCMeans
+from .models.minibatch import MiniBatchKMeans
 from .parallel.dist import Comm, init_comm, local_comm, shard_bounds
 
 __version__ = "0.1.0"
 
-__all__ = ["ClusterConfig", "KMeans", "FuzzyCMeans", "ClusterResult", "Comm", "init_comm",
+__all__ = ["ClusterConfig", "KMeans", "FuzzyCMeans", "MiniBatchKMeans", "ClusterResult", "Comm", "init_comm",
            "local_comm", "shard_bounds", "__version__"]

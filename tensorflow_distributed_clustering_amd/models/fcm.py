@@ -47,7 +47,7 @@ class FuzzyCMeans:
             self.comm = local_comm(dev)
         comm = self.comm
         if n_global is None or row_offset is None:
-            n_global, row_offset = _shard_geometry(x_local, comm)
+            n_global, row_offset = _shard_geometry(int(x_local.shape[0]), comm)
         k, d = cfg.n_clusters, int(x_local.shape[1])
         m = self.fuzzifier(d)
         local = make_fcm_ops(x_local, k, cfg.dtype, m, cfg.fcm_nan_to_zero, cfg.backend)

@@ -149,3 +149,68 @@ def init_centers(method: str, x_local: torch.Tensor, row_offset: int, n_global: 
     if method == "kmeans++":
         return init_kmeanspp(x_local, row_offset, n_global, k, comm, seed)
     raise ValueError(f"unknown init {method!r}")
+
+
+# ------------------------------------------------------------------ chunk sources
+def _source_rows(source, local_idx, d: int) -> torch.Tensor:
+    """float64 rows (local indices) of a chunk source, on the source's device."""
+    from ..data.stream import HostSource, ResidentSource, SyntheticSource
+    from ..data.synth import gaussian_blob_rows
+    if isinstance(source, ResidentSource):
+        idx = torch.as_tensor(local_idx, dtype=torch.int64, device=source.x.device)
+        return source.x.index_select(0, idx)[:, :d].double()
+    if isinstance(source, HostSource):
+        rows = np.asarray(source.x[np.asarray(local_idx, dtype=np.int64)], dtype=np.float64)
+        return torch.from_numpy(rows).to(source.device)
+    if isinstance(source, SyntheticSource):
+        g = [source.row_offset + int(i) for i in local_idx]
+        return gaussian_blob_rows(g, d, source.n_centers, source.seed, source.cluster_std,
+                                  dtype=torch.float64, device=source.device)
+    raise TypeError(f"unsupported source {type(source).__name__}")
+
+
+def gather_rows_from_source(source, row_offset: int, idx, comm: Comm, d: int) -> torch.Tensor:
+    """Global rows ``idx`` of a sharded chunk source, replicated on every rank."""
+    dev = comm.device
+    out = torch.zeros(len(idx), d, dtype=torch.float64, device=dev)
+    n_local = int(source.n_rows)
+    pos, loc = [], []
+    for p, g in enumerate(idx):
+        if row_offset <= g < row_offset + n_local:
+            pos.append(p)
+            loc.append(g - row_offset)
+    if pos:
+        out[torch.as_tensor(pos, device=dev)] = _source_rows(source, loc, d).to(dev)
+    comm.allreduce_(out)
+    return out
+
+
+def init_centers_from_source(method: str, source, row_offset: int, n_global: int, k: int,
+                             comm: Comm, seed: int = 0, given=None, d: int = None,
+                             rows=None) -> torch.Tensor:
+    """Init for streamed / generated shards (rows are gathered from the source).
+
+    k-means++ on a source that is not device-resident runs on a uniform random sample of
+    max(50 K, 256 k) rows (replicated), the standard sample-based seeding for data that
+    cannot be swept K times.
+    """
+    if rows is not None:
+        return gather_rows_from_source(source, row_offset, rows, comm, d)
+    if given is not None or method == "given":
+        g = torch.as_tensor(np.asarray(given), dtype=torch.float64).to(comm.device)
+        if g.shape != (k, d):
+            raise ValueError(f"init_centers must be [{k}, {d}], got {tuple(g.shape)}")
+        return g
+    if k > n_global:
+        raise ValueError(f"K={k} is larger than the number of points N={n_global}")
+    if method == "random":
+        return gather_rows_from_source(source, row_offset, floyd_sample(n_global, k, seed), comm, d)
+    if method == "first_k":
+        return gather_rows_from_source(source, row_offset, range(k), comm, d)
+    if method == "kmeans++":
+        m = min(n_global, max(50_000, 256 * k))
+        sample = gather_rows_from_source(source, row_offset, floyd_sample(n_global, m, seed + 1),
+                                         comm, d)
+        from ..parallel.dist import local_comm
+        return init_kmeanspp(sample, 0, m, k, local_comm(sample.device), seed)
+    raise ValueError(f"unknown init {method!r}")

@@ -5,18 +5,21 @@ Per iteration the reference ran one TF session step that (1) materialised [N_g,K
 tiles per GPU, (2) gathered per-cluster means with K dynamic-shape Where/Gather chains,
 (3) copied labels to the host for a CPU bincount, (4) reduced everything on a CPU
 parameter server, and then (5) re-ran the whole distance computation for an untimed
-CPU label pass (`:277-282`).
+CPU label pass (`:277-282`).  When the data did not fit, it split N into batches that
+were clustered *independently* and averaged their centers (`:296-360`).
 
 Here one iteration on each rank is:
 
-    comm_buf.zero_()                       # [sums K*D | counts K], one flat buffer
-    local.step(C, labels, ..., sums, counts)   # HIP: N1 assign (+N2 update) on the shard
-    all_reduce(comm_buf)                   # ONE RCCL call over xGMI (gloo on CPU)
-    local.finalize(sums, counts, C)        # N3: divide + next-iteration operand prep
+    comm_buf.zero_()                               # [sums K*D | counts K], one flat buffer
+    for chunk in source.chunks(chunk_rows):        # one chunk when the shard is resident
+        local.bind(chunk).step(C, labels, ..., sums, counts)   # N1 assign + N2 update (HIP)
+    all_reduce(comm_buf)                           # ONE RCCL call over xGMI (gloo on CPU)
+    local.finalize(sums, counts, C)                # N3 divide + next-iteration operand prep
 
-Labels are produced by the same kernel that feeds the update, so there is no
-separate label pass inside the loop; a final label pass against the *final*
-centroids (what the reference returns as ``cluster_idx``) runs after the timed loop.
+so a streamed pass (host-resident or generated data, larger than HBM) is the *exact*
+Lloyd step -- partial sums accumulate over all chunks before the single all-reduce.
+Labels come out of the same kernel that feeds the update; a final label pass against
+the *final* centroids (what the reference returns as ``cluster_idx``) runs untimed.
 """
 from __future__ import annotations
 
@@ -28,10 +31,11 @@ import numpy as np
 import torch
 
 from ..config import ClusterConfig
-from ..ops import acc_dtype_for, make_lloyd_ops
+from ..data.stream import HostSource, ResidentSource, plan_chunk_rows
+from ..ops import acc_dtype_for, make_lloyd_ops, padded_dim
 from ..parallel.dist import Comm, local_comm
 from ..utils.timers import DeviceTimer, sync
-from .init import gather_global_rows, init_centers, floyd_sample
+from .init import floyd_sample, init_centers, init_centers_from_source
 
 
 @dataclass
@@ -48,6 +52,7 @@ class ClusterResult:
     backend: str = ""
     history: List[dict] = field(default_factory=list)
     n_global: int = 0
+    streamed: bool = False
 
     @property
     def points_per_sec(self) -> float:
@@ -58,46 +63,79 @@ class ClusterResult:
         return self.n_iter / self.computation_time if self.computation_time > 0 else 0.0
 
 
-def _shard_geometry(x_local: torch.Tensor, comm: Comm):
-    sizes = comm.all_gather_sizes(int(x_local.shape[0]))
+def _shard_geometry(n_local: int, comm: Comm):
+    sizes = comm.all_gather_sizes(int(n_local))
     return int(sum(sizes)), int(sum(sizes[: comm.rank]))
 
 
 class LloydEngine:
-    """Resident state of one distributed Lloyd run: shard operands, centroids, buffers.
+    """Resident state of one distributed Lloyd run: operands, centroids, buffers.
 
-    ``step()`` is exactly one iteration (assign + update + all-reduce + finalize); it is
-    what ``bench.py`` times and what :meth:`KMeans.fit` loops over.
+    ``source`` is a device tensor (the resident shard) or a chunk source from
+    :mod:`..data.stream`.  ``step()`` is exactly one iteration (assign + update +
+    all-reduce + finalize); it is what ``bench.py`` times and what :meth:`KMeans.fit`
+    loops over.
     """
 
-    def __init__(self, x_local: torch.Tensor, cfg: ClusterConfig, comm: Comm,
-                 n_global: int, row_offset: int, init_centers_=None):
+    def __init__(self, source, cfg: ClusterConfig, comm: Comm, n_global: int, row_offset: int,
+                 init_centers_=None, chunk_rows: int = 0):
         self.cfg, self.comm = cfg, comm
-        self.device = dev = x_local.device
         self.n_global, self.row_offset = n_global, row_offset
-        k, d = cfg.n_clusters, int(x_local.shape[1])
-        self.k, self.d = k, d
-        self.local = make_lloyd_ops(x_local, k, cfg.dtype, cfg.backend, cfg.empty_cluster)
-        self.x_local = x_local
-        self.c0 = init_centers(cfg.init, x_local, row_offset, n_global, k, comm, cfg.seed,
-                               given=init_centers_)
+        k = cfg.n_clusters
+        self.k = k
+        if isinstance(source, torch.Tensor):
+            x0 = source
+            self.local = make_lloyd_ops(source, k, cfg.dtype, cfg.backend, cfg.empty_cluster)
+            self.source = ResidentSource(self.local.x, self.local.layout, row_offset)
+            self.local.x = self.source.x
+            self.device = source.device
+            self.d = int(source.shape[1])
+            self.n_local = int(source.shape[0])
+        else:
+            self.source = source
+            self.device = torch.device(getattr(source, "device", comm.device))
+            self.d = int(source.d)
+            self.n_local = int(source.n_rows)
+            probe = torch.zeros(1, self.d, dtype=torch.float32, device=self.device)
+            self.local = make_lloyd_ops(probe, k, cfg.dtype, cfg.backend, cfg.empty_cluster)
+            if tuple(self.local.layout) != tuple(source.layout):
+                raise ValueError(f"source layout {source.layout} != kernel layout {self.local.layout}")
+            x0 = None
+        self.chunk_rows = chunk_rows
+        self.streamed = not isinstance(self.source, ResidentSource) or chunk_rows > 0
+        dev = self.device
+        if x0 is not None:
+            self.c0 = init_centers(cfg.init, x0, row_offset, n_global, k, comm, cfg.seed,
+                                   given=init_centers_)
+        else:
+            self.c0 = init_centers_from_source(cfg.init, self.source, row_offset, n_global, k,
+                                               comm, cfg.seed, given=init_centers_, d=self.d)
         self.C = self.c0.to(self.local.c_dtype).clone().contiguous()  # never alias c0
         self.local.prepare(self.C)
-        acc = acc_dtype_for(cfg.dtype, k, d)
-        self.buf = torch.zeros(k * d + k, dtype=acc, device=dev)
-        self.sums = self.buf[: k * d].view(k, d)
-        self.counts = self.buf[k * d:]
-        self.labels = torch.zeros(self.local.n, dtype=torch.int32, device=dev)
-        self.mind = torch.zeros(self.local.n, dtype=torch.float64 if self.local.c_dtype == torch.float64
-                                else torch.float32, device=dev) if cfg.compute_inertia else None
+        acc = acc_dtype_for(cfg.dtype, k, self.d)
+        self.buf = torch.zeros(k * self.d + k, dtype=acc, device=dev)
+        self.sums = self.buf[: k * self.d].view(k, self.d)
+        self.counts = self.buf[k * self.d:]
+        self.labels = torch.zeros(self.n_local, dtype=torch.int32, device=dev)
+        mdt = torch.float64 if self.local.c_dtype == torch.float64 else torch.float32
+        self.mind = torch.zeros(self.n_local, dtype=mdt, device=dev) if cfg.compute_inertia else None
         self.need_shift = cfg.tol > 0 or cfg.log_every > 0
         self.shift = torch.zeros(1, dtype=torch.float32, device=dev) if self.need_shift else None
         self.bucket_bytes = 64 << 20
         self.n_iter = 0
 
+    def _chunks(self):
+        return self.source.chunks(self.chunk_rows)
+
     def step(self):
         self.buf.zero_()
-        self.local.step(self.C, self.labels, None, self.sums, self.counts)
+        if not self.streamed:
+            self.local.step(self.C, self.labels, None, self.sums, self.counts)
+        else:
+            for start, chunk in self._chunks():
+                s = start - self.source.row_offset  # chunk starts are source-global
+                self.local.bind(chunk).step(self.C, self.labels[s:s + chunk.shape[0]], None,
+                                            self.sums, self.counts)
         self.comm.allreduce_bucketed_(self.buf, self.bucket_bytes)
         if self.shift is not None:
             self.shift.zero_()
@@ -111,13 +149,21 @@ class LloydEngine:
         if not empty:
             return
         idx = floyd_sample(self.n_global, len(empty), self.cfg.seed + 7919 * (self.n_iter + 1))
-        rows = gather_global_rows(self.x_local, self.row_offset, idx, self.comm)
+        rows = init_centers_from_source("rows", self.source, self.row_offset, self.n_global,
+                                        len(empty), self.comm, 0, rows=idx, d=self.d)
         self.C[torch.as_tensor(empty, device=self.C.device)] = rows.to(self.C.dtype)
         self.local.prepare(self.C)
 
     def label_pass(self) -> Optional[float]:
         """Assign against the current centroids; returns the global inertia if tracked."""
-        self.local.assign(self.C, self.labels, self.mind)
+        if not self.streamed:
+            self.local.assign(self.C, self.labels, self.mind)
+        else:
+            for start, chunk in self._chunks():
+                s = start - self.source.row_offset
+                e = s + chunk.shape[0]
+                self.local.bind(chunk).assign(self.C, self.labels[s:e],
+                                              None if self.mind is None else self.mind[s:e])
         if self.mind is None:
             return None
         return self.comm.sum_scalar(float(self.mind.double().sum()))
@@ -128,6 +174,11 @@ class KMeans:
 
     >>> km = KMeans(ClusterConfig(n_clusters=8, dtype="fp32")).fit(x)
     >>> km.result_.centers
+
+    ``x_local`` is this rank's row shard: a device tensor (resident), a CPU tensor or
+    numpy array (moved to the device, or streamed from host memory when it does not fit
+    the HBM budget or ``cfg.chunk_rows`` is set), or a chunk source from
+    :mod:`..data.stream`.
     """
 
     def __init__(self, cfg: ClusterConfig, comm: Optional[Comm] = None, device=None):
@@ -137,12 +188,6 @@ class KMeans:
         self.result_: Optional[ClusterResult] = None
         self.local_ = None
 
-    # ------------------------------------------------------------------ helpers
-    def _comm_for(self, x: torch.Tensor) -> Comm:
-        if self.comm is None:
-            self.comm = local_comm(x.device)
-        return self.comm
-
     @property
     def cluster_centers_(self) -> np.ndarray:
         return self.result_.centers
@@ -151,24 +196,53 @@ class KMeans:
     def labels_(self) -> torch.Tensor:
         return self.result_.labels
 
-    # ---------------------------------------------------------------------- fit
+    def _target_device(self, x):
+        if self.device is not None:
+            return torch.device(self.device)
+        if self.comm is not None:
+            return self.comm.device
+        if isinstance(x, torch.Tensor):
+            return x.device
+        return torch.device(getattr(x, "device", "cpu"))
+
+    def _make_source(self, x_local, dev, row_offset):
+        """(source, chunk_rows): resident tensor, or a HostSource when the shard stays on
+        the host (does not fit the HBM budget, or cfg.chunk_rows forces streaming)."""
+        cfg = self.cfg
+        if hasattr(x_local, "chunks"):
+            return x_local, cfg.chunk_rows or (1 << 22)
+        if isinstance(x_local, torch.Tensor) and x_local.device.type != "cpu":
+            return x_local.to(dev), cfg.chunk_rows
+        xn = x_local.numpy() if isinstance(x_local, torch.Tensor) else np.asarray(x_local)
+        if dev.type == "cuda" and cfg.dtype in ("bf16", "fp32"):
+            d = xn.shape[1]
+            width = padded_dim(d) if cfg.dtype == "bf16" else d
+            if width is not None:
+                es = 2 if cfg.dtype == "bf16" else 4
+                chunk = cfg.chunk_rows or plan_chunk_rows(xn.shape[0], width * es,
+                                                          cfg.n_clusters, d, dev, cfg.hbm_budget_gb)
+                if chunk:
+                    layout = (torch.bfloat16 if cfg.dtype == "bf16" else torch.float32, width)
+                    return HostSource(xn, layout, dev, row_offset), chunk
+        return torch.as_tensor(xn).to(dev), cfg.chunk_rows
+
     def fit(self, x_local, init_centers_: Optional[np.ndarray] = None,
             n_global: Optional[int] = None, row_offset: Optional[int] = None) -> "KMeans":
         cfg = self.cfg
         t_init0 = time.perf_counter()
-        x_local = torch.as_tensor(x_local)
-        dev = torch.device(self.device) if self.device is not None else (
-            self.comm.device if self.comm is not None else x_local.device)
-        if x_local.device != dev:
-            x_local = x_local.to(dev, non_blocking=False)
-        comm = self._comm_for(x_local)
+        dev = self._target_device(x_local)
+        if self.comm is None:
+            self.comm = local_comm(dev)
+        comm = self.comm
+        n_local = int(x_local.n_rows if hasattr(x_local, "n_rows") else x_local.shape[0])
         if n_global is None or row_offset is None:
-            n_global, row_offset = _shard_geometry(x_local, comm)
+            n_global, row_offset = _shard_geometry(n_local, comm)
+        source, chunk_rows = self._make_source(x_local, dev, row_offset)
         sync(dev)
         initialization_time = time.perf_counter() - t_init0
 
         t_setup0 = time.perf_counter()
-        eng = LloydEngine(x_local, cfg, comm, n_global, row_offset, init_centers_)
+        eng = LloydEngine(source, cfg, comm, n_global, row_offset, init_centers_, chunk_rows)
         sync(dev)
         setup_time = time.perf_counter() - t_setup0
 
@@ -199,7 +273,7 @@ class KMeans:
             labels=eng.labels, counts=cnt, n_iter=n_iter, inertia=inertia,
             setup_time=setup_time, initialization_time=initialization_time,
             computation_time=computation_time, backend=eng.local.name, history=history,
-            n_global=n_global)
+            n_global=n_global, streamed=eng.streamed)
         return self
 
     def predict(self, x: torch.Tensor) -> torch.Tensor:

@@ -97,6 +97,19 @@ class _LocalOpsBase:
     # centroid dtype kept by the driver
     c_dtype = torch.float32
 
+    @property
+    def layout(self):
+        """(dtype, width) of the row layout the kernels consume (for chunk sources)."""
+        return (self.x.dtype, self.x.shape[1])
+
+    def bind(self, x: torch.Tensor):
+        """Point the kernels at another chunk already in :attr:`layout` (streaming)."""
+        if x.dtype != self.x.dtype or x.shape[1] != self.x.shape[1]:
+            raise ValueError(f"chunk layout {(x.dtype, x.shape[1])} != {self.layout}")
+        self.x = x
+        self.n = x.shape[0]
+        return self
+
     def prepare(self, C: torch.Tensor):
         """(Re)derive kernel operands from C (called after init / external edits)."""
 
