@@ -24,6 +24,14 @@ import time
 
 BASELINE_POINTS_PER_SEC = 177.7e6
 
+# BASELINE.json configs (the default is the headline metric/config)
+PRESETS = {
+    "headline": dict(n_per_gpu=10_000_000, dim=128, k=1024, scaling="weak", mode="lloyd"),
+    "dp100m": dict(n_per_gpu=100_000_000, dim=128, k=1024, scaling="strong", mode="lloyd"),
+    "minibatch1b": dict(n_per_gpu=1_000_000_000, dim=64, k=4096, scaling="strong",
+                        mode="minibatch", batch_size=1 << 20),
+}
+
 
 def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
@@ -36,9 +44,19 @@ def parse(argv=None):
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp64"])
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--preset", default="headline", choices=sorted(PRESETS),
+                    help="BASELINE config: headline (N=10M/GPU D=128 K=1024, default), "
+                         "dp100m (N=100M total), minibatch1b (mini-batch N=1B D=64 K=4096)")
+    ap.add_argument("--batch-size", type=int, default=0, help="mini-batch rows per rank")
     ap.add_argument("--profile-steps", action="store_true",
                     help="print a per-phase breakdown after the timed region")
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    p = PRESETS[a.preset]
+    given = set(x.split("=")[0].lstrip("-").replace("-", "_") for x in (argv or sys.argv[1:]))
+    for key, val in p.items():
+        if key not in given:
+            setattr(a, key, val)
+    return a
 
 
 def main(argv=None):
@@ -70,7 +88,14 @@ def main(argv=None):
     x = gaussian_blobs(e - s, a.dim, a.k, seed=a.seed, row_offset=s, dtype=dt, device=dev)
     cfg = tdc.ClusterConfig(n_clusters=a.k, max_iter=a.steps, dtype=a.dtype, init="random",
                             seed=a.seed, compute_inertia=False)
-    eng = LloydEngine(x, cfg, comm, n_global, s)
+    if a.mode == "minibatch":
+        from tensorflow_distributed_clustering_amd.models.minibatch import MiniBatchStepper
+        eng = MiniBatchStepper(x, cfg.replace(batch_size=a.batch_size or (1 << 20)), comm,
+                               n_global, s)
+        points_per_step = eng.batch_rows * world
+    else:
+        eng = LloydEngine(x, cfg, comm, n_global, s)
+        points_per_step = n_global
 
     for _ in range(a.warmup):
         eng.step()
@@ -86,9 +111,9 @@ def main(argv=None):
     elapsed = comm.max_scalar(time.perf_counter() - t0)
 
     ms = elapsed / max(1, a.steps) * 1e3
-    pps = n_global * a.steps / elapsed
+    pps = points_per_step * a.steps / elapsed
     breakdown = None
-    if a.profile_steps and dev.type == "cuda":
+    if a.profile_steps and dev.type == "cuda" and a.mode == "lloyd":
         breakdown = phase_breakdown(eng, torch, dev)
     if rank == 0:
         out = {
@@ -104,9 +129,11 @@ def main(argv=None):
             "vs_baseline": pps / BASELINE_POINTS_PER_SEC,
             "dtype": a.dtype,
             "data": "synthetic gaussian blobs (on-device, counter-based), random-row init",
+            "preset": a.preset,
             "iters_per_sec": 1e3 / ms,
             "backend": eng.local.name,
-            "config": {"model": "kmeans-lloyd", "global_batch": n_global, "seq_len": a.dim,
+            "config": {"model": "kmeans-minibatch" if a.mode == "minibatch" else "kmeans-lloyd",
+                       "global_batch": points_per_step, "seq_len": a.dim, "N": n_global,
                        "K": a.k, "D": a.dim, "points_per_gpu": e - s,
                        "parallelism": f"dp{world}"},
         }

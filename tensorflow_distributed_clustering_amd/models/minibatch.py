@@ -32,6 +32,95 @@ from .init import init_centers, init_centers_from_source
 from .kmeans import ClusterResult, _shard_geometry
 
 
+class MiniBatchStepper:
+    """Resident state of a distributed mini-batch run; ``step()`` is one mini-batch update
+    (sample/stream a batch, HIP assign+update on it, one all-reduce, Sculley update)."""
+
+    def __init__(self, source, cfg: ClusterConfig, comm: Comm, n_global: int, row_offset: int,
+                 init_centers_=None):
+        if cfg.batch_size <= 0:
+            cfg = cfg.replace(batch_size=1 << 16)
+        self.cfg, self.comm = cfg, comm
+        self.n_global, self.row_offset = n_global, row_offset
+        k = self.k = cfg.n_clusters
+        if isinstance(source, torch.Tensor):
+            dev = source.device
+            self.local = make_lloyd_ops(source, k, cfg.dtype, cfg.backend, cfg.empty_cluster)
+            self.source = ResidentSource(self.local.x, self.local.layout, row_offset)
+            self.d = int(source.shape[1])
+            self.c0 = init_centers(cfg.init, source, row_offset, n_global, k, comm, cfg.seed,
+                                   given=init_centers_)
+        else:
+            dev = torch.device(getattr(source, "device", "cpu"))
+            self.source = source
+            self.d = int(source.d)
+            self.local = make_lloyd_ops(torch.zeros(1, self.d, device=dev), k, cfg.dtype,
+                                        cfg.backend, cfg.empty_cluster)
+            self.c0 = init_centers_from_source(cfg.init, source, row_offset, n_global, k, comm,
+                                               cfg.seed, given=init_centers_, d=self.d)
+        self.device = dev
+        self.n_local = int(self.source.n_rows)
+        d = self.d
+        self.C = self.c0.to(self.local.c_dtype).clone().contiguous()
+        self.local.prepare(self.C)
+        acc = acc_dtype_for(cfg.dtype, k, d)
+        self.buf = torch.zeros(k * d + k, dtype=acc, device=dev)
+        self.sums, self.counts = self.buf[: k * d].view(k, d), self.buf[k * d:]
+        self.v = torch.zeros(k, dtype=torch.float64, device=dev)
+        self.batch_rows = B = min(cfg.batch_size, self.n_local)
+        self.blabels = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.gen = torch.Generator(device=dev).manual_seed(cfg.seed * 1000003 + comm.rank)
+        self._stream_iter = None
+        self.shift = None
+        self.n_iter = 0
+
+    @property
+    def resident(self) -> bool:
+        return isinstance(self.source, ResidentSource)
+
+    def next_batch(self) -> torch.Tensor:
+        if self.resident:
+            idx = torch.randint(self.n_local, (self.batch_rows,), generator=self.gen,
+                                device=self.device)
+            return self.source.rows(idx)
+        for _ in range(2):
+            if self._stream_iter is None:
+                self._stream_iter = self.source.chunks(self.batch_rows)
+            try:
+                return next(self._stream_iter)[1]
+            except StopIteration:
+                self._stream_iter = None  # next epoch over the shard
+        raise RuntimeError("empty source")
+
+    def step(self):
+        batch = self.next_batch()
+        self.buf.zero_()
+        self.local.bind(batch).step(self.C, self.blabels[: batch.shape[0]], None, self.sums,
+                                    self.counts)
+        self.comm.allreduce_bucketed_(self.buf, 64 << 20)
+        C64 = self.C.double()
+        cnt = self.counts.double()
+        nv = self.v + cnt
+        upd = (cnt > 0)[:, None]
+        newc = (self.v[:, None] * C64 + self.sums.double()) / nv.clamp_min(1.0)[:, None]
+        self.shift = ((newc - C64) ** 2).sum(1).masked_fill(~upd[:, 0], 0).max()
+        self.C.copy_(torch.where(upd, newc, C64).to(self.C.dtype))
+        self.v = nv
+        self.local.prepare(self.C)
+        self.n_iter += 1
+
+    def label_pass(self):
+        dev = self.device
+        labels = torch.zeros(self.n_local, dtype=torch.int32, device=dev)
+        mind = torch.zeros(self.n_local, dtype=torch.float64 if self.local.c_dtype == torch.float64
+                           else torch.float32, device=dev)
+        for start, chunk in self.source.chunks(max(self.batch_rows, 1 << 20)):
+            s = start - self.source.row_offset
+            e = s + chunk.shape[0]
+            self.local.bind(chunk).assign(self.C, labels[s:e], mind[s:e])
+        return labels, self.comm.sum_scalar(float(mind.double().sum()))
+
+
 class MiniBatchKMeans:
     def __init__(self, cfg: ClusterConfig, comm: Optional[Comm] = None, device=None):
         if cfg.batch_size <= 0:
@@ -49,106 +138,46 @@ class MiniBatchKMeans:
         cfg = self.cfg
         t0 = time.perf_counter()
         if hasattr(x_local, "chunks"):
-            source = x_local
-            dev = torch.device(getattr(source, "device", "cpu"))
+            dev = torch.device(getattr(x_local, "device", "cpu"))
         else:
             x_local = torch.as_tensor(x_local)
             dev = torch.device(self.device) if self.device is not None else (
                 self.comm.device if self.comm is not None else x_local.device)
             x_local = x_local.to(dev)
-            source = None
         if self.comm is None:
             self.comm = local_comm(dev)
         comm = self.comm
-        n_local = int(source.n_rows if source is not None else x_local.shape[0])
+        n_local = int(x_local.n_rows if hasattr(x_local, "n_rows") else x_local.shape[0])
         if n_global is None or row_offset is None:
             n_global, row_offset = _shard_geometry(n_local, comm)
-        k = cfg.n_clusters
-        if source is None:
-            local = make_lloyd_ops(x_local, k, cfg.dtype, cfg.backend, cfg.empty_cluster)
-            source = ResidentSource(local.x, local.layout, row_offset)
-            d = int(x_local.shape[1])
-        else:
-            d = int(source.d)
-            local = make_lloyd_ops(torch.zeros(1, d, device=dev), k, cfg.dtype, cfg.backend,
-                                   cfg.empty_cluster)
         sync(dev)
         initialization_time = time.perf_counter() - t0
 
         t1 = time.perf_counter()
-        if isinstance(source, ResidentSource):
-            c0 = init_centers(cfg.init, source.x[:, :d], row_offset, n_global, k, comm, cfg.seed,
-                              given=init_centers_)
-        else:
-            c0 = init_centers_from_source(cfg.init, source, row_offset, n_global, k, comm,
-                                          cfg.seed, given=init_centers_, d=d)
-        C = c0.to(local.c_dtype).clone().contiguous()
-        local.prepare(C)
-        acc = acc_dtype_for(cfg.dtype, k, d)
-        buf = torch.zeros(k * d + k, dtype=acc, device=dev)
-        sums, counts = buf[: k * d].view(k, d), buf[k * d:]
-        v = torch.zeros(k, dtype=torch.float64, device=dev)
-        B = min(cfg.batch_size, n_local)
-        blabels = torch.zeros(B, dtype=torch.int32, device=dev)
-        gen = torch.Generator(device=dev).manual_seed(cfg.seed * 1000003 + comm.rank)
-        stream_iter = None
+        eng = MiniBatchStepper(x_local, cfg, comm, n_global, row_offset, init_centers_)
         sync(dev)
         setup_time = time.perf_counter() - t1
 
-        def next_batch():
-            nonlocal stream_iter
-            if isinstance(source, ResidentSource):
-                idx = torch.randint(n_local, (B,), generator=gen, device=dev)
-                return source.rows(idx)
-            for _ in range(2):
-                if stream_iter is None:
-                    stream_iter = source.chunks(B)
-                try:
-                    return next(stream_iter)[1]
-                except StopIteration:
-                    stream_iter = None  # next epoch
-            raise RuntimeError("empty source")
-
         timer = DeviceTimer(dev)
         timer.start()
-        n_iter = 0
         history = []
-        for it in range(cfg.max_iter):
-            batch = next_batch()
-            buf.zero_()
-            local.bind(batch).step(C, blabels[: batch.shape[0]], None, sums, counts)
-            comm.allreduce_bucketed_(buf, 64 << 20)
-            cnt = counts.double()
-            nv = v + cnt
-            upd = (cnt > 0)[:, None]
-            newc = (v[:, None] * C.double() + sums.double()) / nv.clamp_min(1.0)[:, None]
-            shift = ((newc - C.double()) ** 2).sum(1).masked_fill(~upd[:, 0], 0).max()
-            C.copy_(torch.where(upd, newc, C.double()).to(C.dtype))
-            v = nv
-            local.prepare(C)
-            n_iter = it + 1
-            if cfg.tol > 0 or (cfg.log_every and n_iter % cfg.log_every == 0):
-                sv = float(shift)
-                history.append({"iter": n_iter, "shift": sv})
+        for _ in range(cfg.max_iter):
+            eng.step()
+            n = eng.n_iter
+            if cfg.tol > 0 or (cfg.log_every and n % cfg.log_every == 0):
+                sv = float(eng.shift)
+                history.append({"iter": n, "shift": sv})
                 if cfg.tol > 0 and sv <= cfg.tol:
                     break
         computation_time = timer.stop()
 
-        labels, inertia = None, None
-        if cfg.label_pass:
-            labels = torch.zeros(n_local, dtype=torch.int32, device=dev)
-            mind = torch.zeros(n_local, dtype=torch.float64 if local.c_dtype == torch.float64
-                               else torch.float32, device=dev)
-            for start, chunk in source.chunks(max(B, 1 << 20)):
-                s = start - source.row_offset
-                e = s + chunk.shape[0]
-                local.bind(chunk).assign(C, labels[s:e], mind[s:e])
-            inertia = comm.sum_scalar(float(mind.double().sum()))
+        labels, inertia = eng.label_pass() if cfg.label_pass else (None, None)
+        self.engine_ = eng
         self.result_ = ClusterResult(
-            centers=C.double().cpu().numpy(), init_centers=c0.cpu().numpy(), labels=labels,
-            counts=v.cpu().numpy(), n_iter=n_iter, inertia=inertia, setup_time=setup_time,
-            initialization_time=initialization_time, computation_time=computation_time,
-            backend=local.name, history=history, n_global=n_global,
-            streamed=not isinstance(source, ResidentSource))
-        self.points_processed_ = n_iter * B * comm.world_size
+            centers=eng.C.double().cpu().numpy(), init_centers=eng.c0.cpu().numpy(),
+            labels=labels, counts=eng.v.cpu().numpy(), n_iter=eng.n_iter, inertia=inertia,
+            setup_time=setup_time, initialization_time=initialization_time,
+            computation_time=computation_time, backend=eng.local.name, history=history,
+            n_global=n_global, streamed=not eng.resident)
+        self.points_processed_ = eng.n_iter * eng.batch_rows * comm.world_size
         return self
