@@ -30,6 +30,8 @@ PRESETS = {
     "dp100m": dict(n_per_gpu=100_000_000, dim=128, k=1024, scaling="strong", mode="lloyd"),
     "minibatch1b": dict(n_per_gpu=1_000_000_000, dim=64, k=4096, scaling="strong",
                         mode="minibatch", batch_size=1 << 20),
+    "embed50m_fp8": dict(n_per_gpu=50_000_000, dim=768, k=65536, scaling="strong", mode="lloyd",
+                         dtype="fp8"),
 }
 
 
@@ -41,12 +43,13 @@ def parse(argv=None):
     ap.add_argument("--n-per-gpu", type=int, default=10_000_000)
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--k", type=int, default=1024)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp64"])
+    ap.add_argument("--dtype", default="bf16", choices=["fp8", "bf16", "fp32", "fp64"])
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--preset", default="headline", choices=sorted(PRESETS),
                     help="BASELINE config: headline (N=10M/GPU D=128 K=1024, default), "
-                         "dp100m (N=100M total), minibatch1b (mini-batch N=1B D=64 K=4096)")
+                         "dp100m (N=100M total), minibatch1b (mini-batch N=1B D=64 K=4096), "
+                         "embed50m_fp8 (N=50M D=768 K=65536, fp8 block-scaled MFMA)")
     ap.add_argument("--batch-size", type=int, default=0, help="mini-batch rows per rank")
     ap.add_argument("--profile-steps", action="store_true",
                     help="print a per-phase breakdown after the timed region")
@@ -84,7 +87,8 @@ def main(argv=None):
     world, rank = comm.world_size, comm.rank
     n_global = a.n_per_gpu * world if a.scaling == "weak" else a.n_per_gpu
     s, e = shard_bounds(n_global, world, rank)
-    dt = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp64": torch.float64}[a.dtype]
+    dt = {"fp8": torch.bfloat16, "bf16": torch.bfloat16, "fp32": torch.float32,
+          "fp64": torch.float64}[a.dtype]
     x = gaussian_blobs(e - s, a.dim, a.k, seed=a.seed, row_offset=s, dtype=dt, device=dev)
     cfg = tdc.ClusterConfig(n_clusters=a.k, max_iter=a.steps, dtype=a.dtype, init="random",
                             seed=a.seed, compute_inertia=False)
@@ -144,6 +148,7 @@ def main(argv=None):
 
 def phase_breakdown(eng, torch, dev, reps: int = 5):
     """Per-phase device time of one step (events; diagnostic only, after the timed run)."""
+    from tensorflow_distributed_clustering_amd.ops import NativeUpdate
     ev = lambda: torch.cuda.Event(enable_timing=True)
     names = ["zero", "assign", "update", "allreduce", "finalize"]
     tot = {n: 0.0 for n in names}
@@ -152,8 +157,8 @@ def phase_breakdown(eng, torch, dev, reps: int = 5):
         e = [ev() for _ in range(len(names) + 1)]
         e[0].record()
         eng.buf.zero_(); e[1].record()
-        if hasattr(loc, "cm2"):
-            loc.ops.assign_bf16(loc.x, loc.cm2, loc.cnorm, eng.labels, None); e[2].record()
+        if isinstance(getattr(loc, "update", None), NativeUpdate):
+            loc.assign(eng.C, eng.labels, None); e[2].record()
             loc.update(loc.x, eng.labels, eng.sums, eng.counts); e[3].record()
         else:
             loc.step(eng.C, eng.labels, None, eng.sums, eng.counts); e[2].record(); e[3].record()

@@ -1,0 +1,495 @@
+// N1/N8 for wide embeddings: fused distance + argmin for D in (256, 512] (bf16) and for
+// block-scaled fp8 (OCP e4m3 + E8M0 scales, D a multiple of 256 up to 1024), plus the
+// fp8 row quantiser.  BASELINE config 5: N=50M, D=768, K=65536.
+//
+// Reference: the same K-Means tower (`scripts/distribuitedClustering.py:221-234`); the
+// reference had no reduced-precision path at all (float64 everywhere).
+//
+// Why a second kernel (vs assign_mfma.hip, D <= 256):
+//   * a 32-point B fragment set is D/8 VGPRs per lane in the fp8 MX layout (96 at D=768)
+//     and D/4 in bf16 (128 at D=512): one point tile per wave, 8 waves per workgroup, so
+//     one centroid stage in LDS is reused by 256 points;
+//   * the centroid table no longer fits an XCD's 4 MiB L2 (65536 x 768 fp8 = 48 MiB), so
+//     the K loop is split into GROUPS of ~3 MiB and the grid is ordered XCD-major:
+//     block b runs on XCD b % 8, and the work items of one XCD are a contiguous
+//     (group-major) range, so every XCD keeps exactly one centroid group L2-resident
+//     while it sweeps the points.  Per-group winners are merged with a 64-bit atomicMin
+//     on (order-preserving score bits << 32 | centroid id): min score, lowest id on ties;
+//   * fp8 uses v_mfma_scale_f32_32x32x64_f8f6f4 (2x the bf16 MFMA rate on CDNA4; the
+//     unscaled fp8 MFMA only runs at the bf16 rate).  Each lane feeds 32 bytes
+//     features of one row as two 16-feature halves of two consecutive scale blocks
+//     (layout probed on the hardware, see fp8_off), so the per-lane E8M0 scale operand
+//     is one of the row's block exponents.  The -2 of the expansion is folded
+//     into the centroid operand (sign bit + 1 in the exponent), the accumulator is
+//     initialised with ||c~||^2, so the epilogue is pure min.
+//
+// Schedule per workgroup (WAVES waves x 32 points): centroid tiles of 32 rows stream
+// through an NST-deep LDS ring filled by global_load_lds (LDS-DMA, 16 B per lane,
+// XOR-swizzled on the source side so ds_read_b128 lane groups are conflict-free);
+// per-tile norms / scales for tile t+1 are loaded one stage early, BEFORE the ring
+// refill, so the only vmcnt wait per stage is the counted one on the ring.
+#include <stdlib.h>
+
+#include "kernels.h"
+#include "tdc_common.h"
+
+namespace tdc {
+namespace bigd {
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+constexpr float BIGN = 3.0e38f;
+
+struct OpBf16 {
+  static constexpr int ES = 2;   // storage bytes per feature
+  static constexpr int FB = 16;  // operand bytes per lane per MFMA
+  static constexpr bool SCALED = false;
+  typedef bf16x8 frag;
+};
+struct OpFp8 {
+  static constexpr int ES = 1;
+  static constexpr int FB = 32;
+  static constexpr bool SCALED = true;
+  typedef i32x8 frag;
+};
+
+template <int RB>
+__device__ __forceinline__ int swz(int r, int c) {
+  constexpr int CPR = RB / 16;
+  constexpr int G = CPR < 16 ? CPR : 16;
+  constexpr int RPB = 16 / G;
+  return c ^ ((r / RPB) & (G - 1));
+}
+
+__device__ __forceinline__ unsigned ord_bits(float v) {
+  const unsigned u = __float_as_uint(v);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unord_bits(unsigned o) {
+  return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+
+// Operand layout of v_mfma_scale_f32_32x32x64_f8f6f4 (probed with tools/probe_mfma_scale.hip):
+// byte j of lane (r, h) is k = 32*(j/16) + 16*h + (j%16), and the E8M0 scale of K-block b
+// (k in [32b, 32b+32)) comes from lane r + 32*b.  So one 32-feature quantisation block
+// is split over both lane halves (16 features each), and MFMA step kk covers blocks
+// 2kk and 2kk+1: lane half h reads features 64kk + 16h + [0,16) and 64kk + 32 + 16h +
+// [0,16), and supplies the scale of block 2kk + h.
+__device__ __forceinline__ int fp8_off(int kk, int h, int u) { return 64 * kk + 32 * u + 16 * h; }
+
+template <class OP>
+__device__ __forceinline__ f32x16 mma(const typename OP::frag& a, const typename OP::frag& b,
+                                      const f32x16& c, int sa, int sb) {
+  if constexpr (OP::SCALED) {
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
+  } else {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+}
+
+// D: padded feature count.  X rows: ldx BYTES apart.  Xs/Cs: E8M0 scales [rows, D/32].
+// ABL (timing ablations, 0 in production; results are invalid otherwise):
+//   1 = no ring refill after the prologue, 2 = no per-stage barrier, 4 = no epilogue
+template <class OP, int D, int WAVES, int NST, int ABL = 0>
+__global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
+    const uint8_t* __restrict__ X, const uint8_t* __restrict__ Xs, int64_t N, int64_t ldx,
+    const uint8_t* __restrict__ Cm2, const uint8_t* Cs,
+    const float* cnorm, int ntiles, int kg_tiles, int64_t npb, int64_t n_items,
+    int64_t items_per_xcd, const float* __restrict__ xnorm, int32_t* __restrict__ labels,
+    float* __restrict__ mind, unsigned long long* __restrict__ keys) {
+  constexpr int RB = D * OP::ES;        // bytes per row
+  constexpr int HALFB = RB / 2;         // lane half h covers bytes [h*HALFB, (h+1)*HALFB)
+  constexpr int NK = HALFB / OP::FB;    // MFMAs per 32x32 tile
+  constexpr int CPR = RB / 16;
+  constexpr int UPF = OP::FB / 16;      // 16-B LDS reads per fragment
+  constexpr int TILE_B = 32 * RB;
+  constexpr int PIECES = TILE_B / 1024;
+  constexpr int PPW = PIECES / WAVES;
+  constexpr int SB = D / 32;            // scale bytes per row
+  constexpr int NSW = OP::SCALED ? NK / 2 : 1;  // scale dwords per lane (= the row's)
+  static_assert(RB % 256 == 0, "row bytes must be a multiple of 256");
+  static_assert(PIECES % WAVES == 0, "stage must split evenly over the waves");
+  static_assert(!OP::SCALED || NK % 2 == 0, "fp8: D must be a multiple of 128");
+  constexpr unsigned EMB = 15u;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  // ---- XCD-major work item: (centroid group g, point block pb) ----
+  const int64_t b = blockIdx.x;
+  const int64_t item = (b & 7) * items_per_xcd + (b >> 3);
+  if (item >= n_items) return;  // whole block, before any barrier
+  const int g = (int)(item / npb);
+  const int64_t pb = item - (int64_t)g * npb;
+  const int t0 = g * kg_tiles;
+  const int t1 = min(ntiles, t0 + kg_tiles);
+  const int nt = t1 - t0;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const int64_t prow = pb * (WAVES * 32) + w * 32 + r;
+  const int64_t xrow = prow < N ? prow : N - 1;
+
+  // ---- point fragments (B operand), resident for the whole group ----
+  typename OP::frag bq[NK];
+  if constexpr (OP::SCALED) {
+    const uint8_t* src = X + xrow * ldx;
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      const i32x4 lo = *reinterpret_cast<const i32x4*>(src + fp8_off(kk, h, 0));
+      const i32x4 hi = *reinterpret_cast<const i32x4*>(src + fp8_off(kk, h, 1));
+      bq[kk] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+  } else {
+    const uint8_t* src = X + xrow * ldx + h * HALFB;
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk)
+      bq[kk] = *reinterpret_cast<const typename OP::frag*>(src + kk * OP::FB);
+  }
+  int xs[NSW];
+  if constexpr (OP::SCALED) {
+    const int* s = reinterpret_cast<const int*>(Xs + xrow * SB);
+#pragma unroll
+    for (int i = 0; i < NSW; ++i) xs[i] = s[i];
+  }
+  const int hsh = 8 * h;  // byte of the lane half inside a scale dword pair
+  const unsigned lds_base =
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+
+  auto issue = [&](int t, int slot) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int piece = w * PPW + i;
+      const int L = piece * 64 + lane;  // 16-B chunk index inside the stage
+      const int row = L / CPR, cp = L % CPR;
+      const uint8_t* src = Cm2 + ((int64_t)t * 32 + row) * RB + swz<RB>(row, cp) * 16;
+      __builtin_amdgcn_global_load_lds(
+          (const void*)src,
+          (__attribute__((address_space(3))) void*)(smem + slot * TILE_B + piece * 1024), 16, 0, 0);
+    }
+  };
+  // per-tile operands that do not go through LDS: ||c||^2 rows of this lane, A scales.
+  // Issued with inline asm so the compiler does not track them: its waitcnt pass puts a
+  // conservative vmcnt(0) before their first use inside the ring loop (= waiting for the
+  // refill DMAs just issued).  They are issued before the stage's refill and consumed one
+  // stage later, after the counted end-of-stage vmcnt wait has retired them.
+  auto load_norm = [&](int t, f32x16& init, int* sa) __attribute__((always_inline)) {
+    const float* ns = cnorm + (int64_t)t * 32 + 4 * h;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 v;
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(ns + 8 * q) : "memory");
+      init[4 * q + 0] = v[0];
+      init[4 * q + 1] = v[1];
+      init[4 * q + 2] = v[2];
+      init[4 * q + 3] = v[3];
+    }
+    if constexpr (OP::SCALED) {
+      const int* s = reinterpret_cast<const int*>(Cs + ((int64_t)t * 32 + r) * SB);
+#pragma unroll
+      for (int i = 0; i < NSW; ++i)
+        asm volatile("global_load_dword %0, %1, off" : "=v"(sa[i]) : "v"(s + i) : "memory");
+    }
+  };
+
+  float best = INFINITY;
+  int bt = 0;
+  // one ring stage; cur/nxt are distinct register sets (the loop is unrolled by two and
+  // swaps them), so consuming the prefetched norms never needs a copy -- a copy would
+  // force a vmcnt wait on the freshly issued ring DMAs.
+  auto stage = [&](int i, const f32x16& init_cur, const int* sa_cur, f32x16& init_nxt,
+                   int* sa_nxt) __attribute__((always_inline)) {
+    const int t = t0 + i;
+    const int slot = i % NST;
+    load_norm(i + 1 < nt ? t + 1 : t, init_nxt, sa_nxt);
+    asm volatile("" ::: "memory");  // keep these loads older than the refill (vmcnt order)
+    if constexpr (!(ABL & 1)) {
+      const int in = i + NST - 1;
+      issue(t0 + (in < nt ? in : nt - 1), in % NST);
+    }
+    // LDS byte address of this lane's row in the slot
+    const unsigned rbase = lds_base + slot * TILE_B + r * RB;
+    // A fragments via inline-asm ds_read_b128: the compiler cannot prove they do not
+    // alias the in-flight LDS-DMA ring refill, so compiler-visible LDS reads get a
+    // vmcnt(0) in front of them (= waiting for the refill just issued, every stage).
+    // Issued two MFMAs ahead; the lgkmcnt waits are explicit.
+    auto lds_frag = [&](int kk) __attribute__((always_inline)) {
+      typename OP::frag a;
+      i32x4 lo, hi;
+      if constexpr (UPF == 1) {
+        asm volatile("ds_read_b128 %0, %1" : "=v"(lo) : "v"(rbase + swz<RB>(r, h * (CPR / 2) + kk) * 16));
+        a = __builtin_bit_cast(typename OP::frag, lo);
+      } else {
+        asm volatile("ds_read_b128 %0, %1" : "=v"(lo) : "v"(rbase + swz<RB>(r, fp8_off(kk, h, 0) / 16) * 16));
+        asm volatile("ds_read_b128 %0, %1" : "=v"(hi) : "v"(rbase + swz<RB>(r, fp8_off(kk, h, 1) / 16) * 16));
+        a = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+      return a;
+    };
+    f32x16 acc = init_cur;
+    typename OP::frag a0 = lds_frag(0);
+    typename OP::frag a1 = lds_frag(NK > 1 ? 1 : 0);
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      typename OP::frag a2 = a1;
+      if (kk + 2 < NK) a2 = lds_frag(kk + 2);
+      // reads still allowed in flight when a0 is consumed: those of a1 and a2
+      constexpr int PER = UPF;  // ds_read instructions per fragment
+      if (kk + 2 < NK) asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(2 * PER) : "memory");
+      else if (kk + 1 < NK) asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(PER) : "memory");
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      int sa = 0, sb = 0;
+      if constexpr (OP::SCALED) {  // block 2kk+h: dword kk>>1, byte 2(kk&1)+h
+        sa = (sa_cur[kk >> 1] >> (16 * (kk & 1) + hsh)) & 0xff;
+        sb = (xs[kk >> 1] >> (16 * (kk & 1) + hsh)) & 0xff;
+      }
+      acc = mma<OP>(a0, bq[kk], acc, sa, sb);
+      __builtin_amdgcn_sched_barrier(0);
+      a0 = a1;
+      a1 = a2;
+    }
+    if constexpr (ABL & 4) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) asm volatile("" ::"v"(acc[j]));
+    } else {
+      float m = INFINITY;
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        m = __builtin_fminf(m, __uint_as_float((__float_as_uint(acc[j]) & ~EMB) | (unsigned)j));
+      const bool up = m < best;
+      best = up ? m : best;
+      bt = up ? t : bt;
+    }
+    if constexpr (ABL & 1) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * PPW) : "memory");  // stage i+1 landed
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (!(ABL & 2)) __builtin_amdgcn_s_barrier();  // ... for every wave's pieces
+  };
+
+  f32x16 init_a, init_b;
+  int sa_a[NSW], sa_b[NSW];
+  load_norm(t0, init_a, sa_a);
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s) issue(t0 + (s < nt ? s : nt - 1), s);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * PPW) : "memory");
+  __builtin_amdgcn_s_barrier();
+
+  for (int i = 0; i < nt; i += 2) {
+    stage(i, init_a, sa_a, init_b, sa_b);
+    if (i + 1 < nt) stage(i + 1, init_b, sa_b, init_a, sa_a);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  const float ob = __shfl_xor(best, 32, 64);
+  const int obt = __shfl_xor(bt, 32, 64);
+  const unsigned e0 = __float_as_uint(best) & EMB, e1 = __float_as_uint(ob) & EMB;
+  const int l0 = bt * 32 + (int)(e0 & 3) + 8 * (int)(e0 >> 2) + 4 * h;
+  const int l1 = obt * 32 + (int)(e1 & 3) + 8 * (int)(e1 >> 2) + 4 * (1 - h);
+  const float v0 = __uint_as_float(__float_as_uint(best) & ~EMB);
+  const float v1 = __uint_as_float(__float_as_uint(ob) & ~EMB);
+  const bool other = (v1 < v0) || (v1 == v0 && l1 < l0);
+  if (h == 0 && prow < N) {
+    const int lab = other ? l1 : l0;
+    const float v = other ? v1 : v0;
+    if (keys) {
+      const unsigned long long key = ((unsigned long long)ord_bits(v) << 32) | (unsigned)lab;
+      atomicMin(keys + prow, key);
+    } else {
+      labels[prow] = lab;
+      if (mind) mind[prow] = fmaxf(v + xnorm[prow], 0.f);
+    }
+  }
+}
+
+// keys -> labels / mind, and reset keys for the next pass
+__global__ __launch_bounds__(256) void keys_finalize_kernel(unsigned long long* __restrict__ keys,
+                                                            int64_t N, const float* __restrict__ xnorm,
+                                                            int32_t* __restrict__ labels,
+                                                            float* __restrict__ mind) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= N) return;
+  const unsigned long long k = keys[i];
+  labels[i] = (int32_t)(unsigned)(k & 0xffffffffull);
+  if (mind) mind[i] = fmaxf(unord_bits((unsigned)(k >> 32)) + xnorm[i], 0.f);
+  keys[i] = ~0ull;
+}
+
+// ------------------------------------------------------------------ fp8 quantiser (N8)
+template <typename T>
+__device__ __forceinline__ float ldf(const T* p) { return (float)*p; }
+
+// One wave per row.  Lane l owns features [base + 8l, base + 8l + 8) of each 512-wide span;
+// a 32-feature scale block = 4 consecutive lanes.  E8M0 exponent e = ilogb(amax) - 7 puts
+// the block max in [128, 256) (no saturation, 13 binades of headroom below it).
+// neg2: centroid operand (-2*c): sign flipped, exponent + 1, and norm = ||c~||^2 of the
+// UN-negated dequantised row.  Rows >= valid: zero bytes, scale 1.0, norm = BIGN.
+template <typename T>
+__global__ __launch_bounds__(256) void quant_fp8_kernel(const T* __restrict__ X, int64_t rows,
+                                                        int64_t valid, int d, int64_t ldx, int DP,
+                                                        int neg2, uint8_t* __restrict__ Q,
+                                                        uint8_t* __restrict__ S,
+                                                        float* __restrict__ norm) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const bool pad = row >= valid;
+  float nsum = 0.f;
+  for (int base = 0; base < DP; base += 512) {
+    const int c0 = base + 8 * lane;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      v[j] = (!pad && c < d) ? ldf(X + row * ldx + c) : 0.f;
+    }
+    float am = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(v[j]));
+    am = fmaxf(am, __shfl_xor(am, 1, 64));
+    am = fmaxf(am, __shfl_xor(am, 2, 64));
+    if (c0 >= DP) continue;  // after the shuffles (all lanes took part)
+    int e = am > 0.f ? ilogbf(am) - 7 : -127;
+    e = e < -127 ? -127 : (e > 126 ? 126 : e);
+    const float inv = ldexpf(1.f, -e);
+    const float sc = ldexpf(1.f, e);
+    int p0 = 0, p1 = 0;
+    p0 = __builtin_amdgcn_cvt_pk_fp8_f32(v[0] * inv, v[1] * inv, p0, false);
+    p0 = __builtin_amdgcn_cvt_pk_fp8_f32(v[2] * inv, v[3] * inv, p0, true);
+    p1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[4] * inv, v[5] * inv, p1, false);
+    p1 = __builtin_amdgcn_cvt_pk_fp8_f32(v[6] * inv, v[7] * inv, p1, true);
+    float f[8];
+    f[0] = __builtin_amdgcn_cvt_f32_fp8(p0, 0); f[1] = __builtin_amdgcn_cvt_f32_fp8(p0, 1);
+    f[2] = __builtin_amdgcn_cvt_f32_fp8(p0, 2); f[3] = __builtin_amdgcn_cvt_f32_fp8(p0, 3);
+    f[4] = __builtin_amdgcn_cvt_f32_fp8(p1, 0); f[5] = __builtin_amdgcn_cvt_f32_fp8(p1, 1);
+    f[6] = __builtin_amdgcn_cvt_f32_fp8(p1, 2); f[7] = __builtin_amdgcn_cvt_f32_fp8(p1, 3);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float x = f[j] * sc;
+      nsum = fmaf(x, x, nsum);
+    }
+    if (neg2 && !pad) {
+      p0 ^= 0x80808080;
+      p1 ^= 0x80808080;
+    }
+    int2 pk;
+    pk.x = p0;
+    pk.y = p1;
+    *reinterpret_cast<int2*>(Q + row * DP + c0) = pk;
+    if ((lane & 3) == 0) S[row * (DP / 32) + c0 / 32] = (uint8_t)(e + 127 + (neg2 ? 1 : 0));
+  }
+  nsum = wave_sum(nsum);
+  if (lane == 0 && norm) norm[row] = pad ? BIGN : nsum;
+}
+
+}  // namespace bigd
+}  // namespace tdc
+
+using namespace tdc::bigd;
+
+namespace {
+template <class OP, int D, int WAVES, int NST, int ABL = 0>
+int launch_bigd(const void* X, const void* Xs, int64_t N, int64_t ldx_bytes, const void* Cm2,
+                const void* Cs, const float* cnorm, int Kp, int kg_tiles, const float* xnorm,
+                int32_t* labels, float* mind, unsigned long long* keys, hipStream_t stream) {
+  constexpr int TILE_B = 32 * D * OP::ES;
+  const size_t lds = (size_t)NST * TILE_B;
+  auto kern = assign_bigd_kernel<OP, D, WAVES, NST, ABL>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  const int ntiles = Kp / 32;
+  if (kg_tiles <= 0 || kg_tiles > ntiles) kg_tiles = ntiles;
+  const int ngroups = (ntiles + kg_tiles - 1) / kg_tiles;
+  if (ngroups > 1 && keys == nullptr) return (int)hipErrorInvalidValue;
+  const int64_t per = (int64_t)WAVES * 32;
+  const int64_t npb = (N + per - 1) / per;
+  const int64_t n_items = npb * ngroups;
+  const int64_t ipx = (n_items + 7) / 8;
+  dim3 grid((unsigned)(ipx * 8));
+  hipLaunchKernelGGL(kern, grid, dim3(WAVES * 64), lds, stream, (const uint8_t*)X,
+                     (const uint8_t*)Xs, N, ldx_bytes, (const uint8_t*)Cm2, (const uint8_t*)Cs,
+                     cnorm, ntiles, kg_tiles, npb, n_items, ipx, xnorm, labels, mind,
+                     ngroups > 1 ? keys : nullptr);
+  TDC_CHECK_LAUNCH();
+  if (ngroups > 1) {
+    hipLaunchKernelGGL(keys_finalize_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
+                       stream, keys, N, xnorm, labels, mind);
+    TDC_CHECK_LAUNCH();
+  }
+  return 0;
+}
+}  // namespace
+
+int tdc_assign_bigd_supported(int dtype, int DP) {
+  // (bf16 D > 512 would need > 256 VGPRs of resident point fragments: spills)
+  if (dtype == TDC_FP8) return DP == 256 || DP == 512 || DP == 768 || DP == 1024;
+  if (dtype == TDC_BF16) return DP == 384 || DP == 512;
+  return 0;
+}
+
+int tdc_assign_bigd(int dtype, const void* X, const void* Xs, int64_t N, int64_t ldx, int DP,
+                    const void* Cm2, const void* Cs, const float* cnorm, int Kp, int kg_tiles,
+                    const float* xnorm, int32_t* labels, float* mind, unsigned long long* keys,
+                    hipStream_t stream) {
+  if (N <= 0) return 0;
+  if (Kp % 32 != 0) return (int)hipErrorInvalidValue;
+  if (dtype == TDC_FP8) {
+    switch (DP) {
+      case 256: return launch_bigd<OpFp8, 256, 8, 4>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
+      case 512: return launch_bigd<OpFp8, 512, 8, 4>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
+      case 768: {
+        static const int abl = getenv("TDC_BIGD_ABL") ? atoi(getenv("TDC_BIGD_ABL")) : 0;
+        switch (abl) {  // timing ablations (tools only)
+          case 1: return launch_bigd<OpFp8, 768, 8, 4, 1>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
+          case 2: return launch_bigd<OpFp8, 768, 8, 4, 2>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
+          case 4: return launch_bigd<OpFp8, 768, 8, 4, 4>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
+          case 7: return launch_bigd<OpFp8, 768, 8, 4, 7>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
+          default: return launch_bigd<OpFp8, 768, 8, 4>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
+        }
+      }
+      case 1024: return launch_bigd<OpFp8, 1024, 8, 4>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
+    }
+  } else if (dtype == TDC_BF16) {
+    const int64_t ldb = ldx * 2;
+    switch (DP) {
+      case 384: return launch_bigd<OpBf16, 384, 8, 4>(X, nullptr, N, ldb, Cm2, nullptr, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
+      case 512: return launch_bigd<OpBf16, 512, 8, 4>(X, nullptr, N, ldb, Cm2, nullptr, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
+    }
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+int tdc_quant_fp8(int src_dtype, const void* X, int64_t rows, int64_t valid, int d, int64_t ldx,
+                  int DP, int neg2, void* Q, void* S, float* norm, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (DP % 32 != 0 || d > DP) return (int)hipErrorInvalidValue;
+  dim3 grid((unsigned)((rows + 3) / 4));
+  switch (src_dtype) {
+    case TDC_F32:
+      hipLaunchKernelGGL(quant_fp8_kernel<float>, grid, dim3(256), 0, stream, (const float*)X, rows,
+                         valid, d, ldx, DP, neg2, (uint8_t*)Q, (uint8_t*)S, norm);
+      break;
+    case TDC_F64:
+      hipLaunchKernelGGL(quant_fp8_kernel<double>, grid, dim3(256), 0, stream, (const double*)X,
+                         rows, valid, d, ldx, DP, neg2, (uint8_t*)Q, (uint8_t*)S, norm);
+      break;
+    case TDC_BF16:
+      hipLaunchKernelGGL(quant_fp8_kernel<__bf16>, grid, dim3(256), 0, stream, (const __bf16*)X,
+                         rows, valid, d, ldx, DP, neg2, (uint8_t*)Q, (uint8_t*)S, norm);
+      break;
+    default:
+      return (int)hipErrorInvalidValue;
+  }
+  TDC_CHECK_LAUNCH();
+  return 0;
+}

@@ -26,6 +26,8 @@
 //   * feature order inside a k-step is permuted (lane half h covers features
 //     [h*DP/2, (h+1)*DP/2)); A and B use the same map, so the dot product is
 //     unchanged and each lane's B loads are contiguous.
+#include <stdlib.h>
+
 #include "assign_mfma_impl.h"
 #include "kernels.h"
 
@@ -39,15 +41,20 @@ int tdc_assign_mfma_bf16(const void* X, int64_t N, int64_t ldx, int DP, const vo
   const int ntiles = Kp / BN;
   const __bf16* x = (const __bf16*)X;
   const __bf16* c = (const __bf16*)Cm2;
-  // LDS-DMA ring variant, 4 waves x P x 32 points per workgroup, 64-centroid stages
-  // (tools/ablate_assign.hip: 1.53 PF/s at N=10M, D=128 vs 1.07 for register staging)
+  // LDS-DMA ring, 4 waves x P x 32 points per workgroup, 64-centroid stages.
+  // TDC_ASSIGN_RING=1 selects the first ring variant (kept for A/B timing).
+  static const int ring = getenv("TDC_ASSIGN_RING") ? atoi(getenv("TDC_ASSIGN_RING")) : 2;
   switch (DP) {
 #define TDC_CASE(DPV, PV, NSTV)                                                              \
   case DPV: {                                                                                \
     const int64_t per = 4 * PV * 32;                                                         \
     dim3 grid((unsigned)((N + per - 1) / per));                                              \
-    hipLaunchKernelGGL((assign_mfma_bf16_ring_kernel<DPV, PV, NSTV, 4, 2>), grid, dim3(256), \
-                       0, stream, x, N, ldx, c, cnorm, ntiles, labels, mind);                \
+    if (ring == 1)                                                                           \
+      hipLaunchKernelGGL((assign_mfma_bf16_ring_kernel<DPV, PV, NSTV, 4, 2>), grid, dim3(256), \
+                         0, stream, x, N, ldx, c, cnorm, ntiles, labels, mind);              \
+    else                                                                                     \
+      hipLaunchKernelGGL((assign_mfma_bf16_ring2_kernel<DPV, PV, NSTV, 4, 2>), grid,         \
+                         dim3(256), 0, stream, x, N, ldx, c, cnorm, ntiles, labels, mind);   \
     break;                                                                                   \
   }
     TDC_CASE(32, 4, 3)

@@ -370,4 +370,188 @@ void assign_mfma_bf16_ring_kernel(const __bf16* __restrict__ X, int64_t N, int64
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Variant 3 ("ring2"): the ring above, with the two stalls it had removed.
+//  * the compiler cannot prove that a plain LDS read does not alias an in-flight
+//    LDS-DMA, so every phase of "ring" started with s_waitcnt vmcnt(0): each stage
+//    waited for the refill it had just issued (NST-1 stages ahead -> 0 ahead).  Here the
+//    A fragments are read with inline-asm ds_read_b128 (explicit, counted lgkmcnt);
+//  * the centroid norms ride in the ring with their tile (one extra 16-B-per-lane DMA of
+//    NPW lanes per wave, so every wave issues the same count), instead of global loads
+//    that also forced a vmcnt(0) at their use.
+// A fragments are prefetched two k-steps ahead.
+// ------------------------------------------------------------------------------------
+template <int DP, int P, int NST, int WAVES, int QT>
+__global__ __launch_bounds__(WAVES * 64, (WAVES % 4 == 0 ? (WAVES / 4 > 1 ? WAVES / 4 : 3) : 2))
+void assign_mfma_bf16_ring2_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
+                                   const __bf16* __restrict__ Cm2, const float* __restrict__ cnorm,
+                                   int ntiles, int32_t* __restrict__ labels,
+                                   float* __restrict__ mind) {
+  constexpr int BNL = 32 * QT;                     // centroids per stage
+  constexpr int CPR = DP / 8;
+  constexpr int KS = DP / 16;
+  constexpr int HALF = DP / 2;
+  constexpr int TILE_B = BNL * DP * 2;
+  constexpr int NORM_B = BNL * 4;
+  constexpr int STAGE_B = TILE_B + NORM_B;
+  constexpr int PIECES = TILE_B / 1024;
+  constexpr int PPW = PIECES / WAVES;
+  constexpr int NCH = NORM_B / 16;                 // 16-B norm chunks per stage
+  constexpr int NPW = NCH / WAVES;                 // ... per wave
+  constexpr int VPS = PPW + 1;                     // vmem instructions per wave per stage
+  static_assert(PIECES % WAVES == 0 && NCH % WAVES == 0 && NPW >= 1, "stage split");
+  constexpr unsigned EMB = QT * 16 <= 32 ? 31u : 63u;
+  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE_B];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const int64_t pbase = (int64_t)blockIdx.x * (WAVES * P * 32) + (int64_t)w * (P * 32);
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+
+  bf16x8 bq[P][KS];
+  float xn[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    int64_t row = pbase + p * 32 + r;
+    if (row >= N) row = N - 1;
+    const bf16x8* src = reinterpret_cast<const bf16x8*>(X + row * ldx + h * HALF);
+    float s = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      bq[p][kk] = src[kk];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float f = (float)bq[p][kk][j];
+        s = fmaf(f, f, s);
+      }
+    }
+    xn[p] = s + __shfl_xor(s, 32, 64);
+  }
+
+  auto issue = [&](int t, int slot) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int piece = w * PPW + i;
+      const int L = piece * 64 + lane;
+      const int row = L / CPR, cp = L % CPR;
+      const int csrc = swz<DP>(row, cp);
+      const __bf16* src = Cm2 + ((int64_t)t * BNL + row) * DP + csrc * 8;
+      __builtin_amdgcn_global_load_lds(
+          (const void*)src,
+          (__attribute__((address_space(3))) void*)(smem + slot * STAGE_B + piece * 1024), 16, 0, 0);
+    }
+    if (lane < NPW) {
+      const float* src = cnorm + (int64_t)t * BNL + (w * NPW + lane) * 4;
+      __builtin_amdgcn_global_load_lds(
+          (const void*)src,
+          (__attribute__((address_space(3))) void*)(smem + slot * STAGE_B + TILE_B + w * NPW * 16),
+          16, 0, 0);
+    }
+  };
+
+#pragma unroll
+  for (int t = 0; t < NST - 1; ++t) issue(t < ntiles ? t : ntiles - 1, t);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * VPS) : "memory");
+  __builtin_amdgcn_s_barrier();
+
+  float best[P];
+  int bt[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    best[p] = INFINITY;
+    bt[p] = 0;
+  }
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int slot = t % NST;
+    {
+      const int tn = t + NST - 1;
+      issue(tn < ntiles ? tn : ntiles - 1, (t + NST - 1) % NST);
+    }
+    const unsigned sbase = lds0 + slot * STAGE_B;
+#pragma unroll
+    for (int q = 0; q < QT; ++q) {
+      const int row = q * 32 + r;
+      const unsigned abase = sbase + row * (DP * 2);
+      auto afrag = [&](int kk) __attribute__((always_inline)) {
+        bf16x8 a;
+        asm volatile("ds_read_b128 %0, %1" : "=v"(a) : "v"(abase + swz<DP>(row, h * (CPR / 2) + kk) * 16));
+        return a;
+      };
+      f32x4 n4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        asm volatile("ds_read_b128 %0, %1" : "=v"(n4[j]) : "v"(sbase + TILE_B + (q * 32 + 8 * j + 4 * h) * 4));
+      bf16x8 a0 = afrag(0);
+      bf16x8 a1 = afrag(KS > 1 ? 1 : 0);
+      f32x16 acc[P];
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        bf16x8 a2 = a1;
+        if (kk + 2 < KS) a2 = afrag(kk + 2);
+        if (kk + 2 < KS) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+        else if (kk + 1 < KS) asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if (kk == 0) {
+#pragma unroll
+          for (int p = 0; p < P; ++p) {
+            f32x16 init;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              init[4 * j + 0] = n4[j][0];
+              init[4 * j + 1] = n4[j][1];
+              init[4 * j + 2] = n4[j][2];
+              init[4 * j + 3] = n4[j][3];
+            }
+            acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq[p][0], init, 0, 0, 0);
+          }
+        } else {
+#pragma unroll
+          for (int p = 0; p < P; ++p)
+            acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq[p][kk], acc[p], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        a0 = a1;
+        a1 = a2;
+      }
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        float m = INFINITY;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float v = __uint_as_float((__float_as_uint(acc[p][i]) & ~EMB) | (unsigned)(q * 16 + i));
+          m = __builtin_fminf(m, v);
+        }
+        const bool up = m < best[p];
+        best[p] = up ? m : best[p];
+        bt[p] = up ? t : bt[p];
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * VPS) : "memory");  // stage t+1 landed
+    __builtin_amdgcn_s_barrier();  // ... for every wave's pieces
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const float ob = __shfl_xor(best[p], 32, 64);
+    const int obt = __shfl_xor(bt[p], 32, 64);
+    const unsigned e0 = __float_as_uint(best[p]) & EMB, e1 = __float_as_uint(ob) & EMB;
+    const int l0 = bt[p] * BNL + (int)(e0 >> 4) * 32 + (int)(e0 & 3) + 8 * (int)((e0 & 15) >> 2) + 4 * h;
+    const int l1 = obt * BNL + (int)(e1 >> 4) * 32 + (int)(e1 & 3) + 8 * (int)((e1 & 15) >> 2) + 4 * (1 - h);
+    const float v0 = __uint_as_float(__float_as_uint(best[p]) & ~EMB);
+    const float v1 = __uint_as_float(__float_as_uint(ob) & ~EMB);
+    const bool other = (v1 < v0) || (v1 == v0 && l1 < l0);
+    const int64_t row = pbase + p * 32 + r;
+    if (h == 0 && row < N) {
+      labels[row] = other ? l1 : l0;
+      if (mind) mind[row] = fmaxf((other ? v1 : v0) + xn[p], 0.f);
+    }
+  }
+}
+
 }  // namespace tdc

@@ -218,6 +218,94 @@ void finalize(const std::optional<at::Tensor>& sums, const std::optional<at::Ten
         "finalize");
 }
 
+bool assign_bigd_supported(at::ScalarType dtype, int64_t DP) {
+  const int code = dtype == at::kFloat8_e4m3fn ? TDC_FP8 : (dtype == at::kBFloat16 ? TDC_BF16 : -1);
+  return code >= 0 && tdc_assign_bigd_supported(code, (int)DP) != 0;
+}
+
+// X: bf16 [N, >=DP] or float8_e4m3fn [N, DP] (with Xs uint8 [N, DP/32]).
+void assign_bigd(const at::Tensor& X, const std::optional<at::Tensor>& Xs, const at::Tensor& xnorm,
+                 const at::Tensor& Cm2, const std::optional<at::Tensor>& Cs,
+                 const at::Tensor& cnorm, int64_t kg_tiles, at::Tensor& labels,
+                 const std::optional<at::Tensor>& mind, const std::optional<at::Tensor>& keys) {
+  check_cuda(X, "X");
+  check_rows(X, "X");
+  const bool fp8 = X.scalar_type() == at::kFloat8_e4m3fn;
+  TORCH_CHECK(fp8 || X.scalar_type() == at::kBFloat16, "tdc.assign_bigd: X must be bf16 or float8_e4m3fn");
+  TORCH_CHECK(Cm2.scalar_type() == X.scalar_type() && Cm2.is_contiguous() && Cm2.dim() == 2,
+              "tdc.assign_bigd: Cm2 dtype/contiguity");
+  const int64_t N = X.size(0);
+  const int DP = (int)Cm2.size(1);
+  const int Kp = (int)Cm2.size(0);
+  TORCH_CHECK(tdc_assign_bigd_supported(fp8 ? TDC_FP8 : TDC_BF16, DP), "tdc.assign_bigd: unsupported DP ", DP);
+  TORCH_CHECK(X.size(1) >= DP && Kp % 32 == 0, "tdc.assign_bigd: shapes");
+  const int64_t es = fp8 ? 1 : 2;
+  TORCH_CHECK((X.stride(0) * es) % 16 == 0 && reinterpret_cast<uintptr_t>(X.data_ptr()) % 16 == 0,
+              "tdc.assign_bigd: X rows must be 16-byte aligned");
+  TORCH_CHECK(cnorm.scalar_type() == at::kFloat && cnorm.is_contiguous() && cnorm.numel() >= Kp,
+              "tdc.assign_bigd: cnorm fp32 [Kp]");
+  TORCH_CHECK(xnorm.scalar_type() == at::kFloat && xnorm.is_contiguous() && xnorm.numel() >= N,
+              "tdc.assign_bigd: xnorm fp32 [N]");
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous() && labels.numel() >= N,
+              "tdc.assign_bigd: labels int32 [N]");
+  const void* xs = nullptr;
+  const void* cs = nullptr;
+  if (fp8) {
+    TORCH_CHECK(Xs.has_value() && Cs.has_value(), "tdc.assign_bigd: fp8 needs Xs and Cs");
+    TORCH_CHECK(Xs->scalar_type() == at::kByte && Xs->is_contiguous() && Xs->numel() >= N * (DP / 32),
+                "tdc.assign_bigd: Xs uint8 [N, DP/32]");
+    TORCH_CHECK(Cs->scalar_type() == at::kByte && Cs->is_contiguous() && Cs->numel() >= (int64_t)Kp * (DP / 32),
+                "tdc.assign_bigd: Cs uint8 [Kp, DP/32]");
+    TORCH_CHECK(X.stride(0) == DP, "tdc.assign_bigd: fp8 X must be [N, DP] contiguous");
+    xs = Xs->data_ptr();
+    cs = Cs->data_ptr();
+  }
+  float* md = nullptr;
+  if (mind.has_value() && mind->defined()) {
+    TORCH_CHECK(mind->scalar_type() == at::kFloat && mind->numel() >= N && mind->is_contiguous(),
+                "tdc.assign_bigd: mind fp32 [N]");
+    md = mind->data_ptr<float>();
+  }
+  unsigned long long* kp = nullptr;
+  if (keys.has_value() && keys->defined()) {
+    TORCH_CHECK(keys->scalar_type() == at::kLong && keys->is_contiguous() && keys->numel() >= N,
+                "tdc.assign_bigd: keys int64 [N]");
+    kp = reinterpret_cast<unsigned long long*>(keys->data_ptr());
+  }
+  const int ntiles = Kp / 32;
+  const int kg = (kg_tiles <= 0 || kg_tiles > ntiles) ? ntiles : (int)kg_tiles;
+  TORCH_CHECK(kg == ntiles || kp != nullptr, "tdc.assign_bigd: keys required with >1 centroid group");
+  const DevGuard guard(X.device());
+  check(tdc_assign_bigd(fp8 ? TDC_FP8 : TDC_BF16, X.data_ptr(), xs, N, X.stride(0), DP, Cm2.data_ptr(),
+                        cs, cnorm.data_ptr<float>(), Kp, kg, xnorm.data_ptr<float>(),
+                        labels.data_ptr<int32_t>(), md, kp, cur_stream()),
+        "assign_bigd");
+}
+
+void quant_fp8(const at::Tensor& X, int64_t valid, int64_t neg2, at::Tensor& Q, at::Tensor& S,
+               const std::optional<at::Tensor>& norm) {
+  check_cuda(X, "X");
+  check_rows(X, "X");
+  TORCH_CHECK(Q.scalar_type() == at::kFloat8_e4m3fn && Q.is_contiguous() && Q.dim() == 2,
+              "tdc.quant_fp8: Q float8_e4m3fn [rows, DP]");
+  const int64_t rows = Q.size(0);
+  const int DP = (int)Q.size(1);
+  TORCH_CHECK(DP % 32 == 0 && X.size(1) <= DP, "tdc.quant_fp8: DP");
+  TORCH_CHECK(valid <= X.size(0) && valid <= rows, "tdc.quant_fp8: valid rows");
+  TORCH_CHECK(S.scalar_type() == at::kByte && S.is_contiguous() && S.numel() >= rows * (DP / 32),
+              "tdc.quant_fp8: S uint8 [rows, DP/32]");
+  float* nm = nullptr;
+  if (norm.has_value() && norm->defined()) {
+    TORCH_CHECK(norm->scalar_type() == at::kFloat && norm->is_contiguous() && norm->numel() >= rows,
+                "tdc.quant_fp8: norm fp32 [rows]");
+    nm = norm->data_ptr<float>();
+  }
+  const DevGuard guard(X.device());
+  check(tdc_quant_fp8(dcode(X.scalar_type()), X.data_ptr(), rows, valid, (int)X.size(1), X.stride(0),
+                      DP, (int)neg2, Q.data_ptr(), S.data_ptr(), nm, cur_stream()),
+        "quant_fp8");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(tdc, m) {
@@ -230,6 +318,9 @@ TORCH_LIBRARY(tdc, m) {
   m.def("update_sorted(Tensor X, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work) -> ()");
   m.def("fcm_small_supported(ScalarType dtype, int K, int D) -> bool", &fcm_small_supported);
   m.def("fcm_small(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) wx, Tensor(c!) ws) -> ()");
+  m.def("assign_bigd_supported(ScalarType dtype, int DP) -> bool", &assign_bigd_supported);
+  m.def("assign_bigd(Tensor X, Tensor? Xs, Tensor xnorm, Tensor Cm2, Tensor? Cs, Tensor cnorm, int kg_tiles, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!)? keys) -> ()");
+  m.def("quant_fp8(Tensor X, int valid, int neg2, Tensor(a!) Q, Tensor(b!) S, Tensor(c!)? norm) -> ()");
   m.def("finalize(Tensor? sums, Tensor? counts, Tensor(a!) C, int policy, Tensor(b!)? shift, Tensor(c!)? Cm2, Tensor(d!)? cnorm) -> ()");
 }
 
@@ -241,4 +332,6 @@ TORCH_LIBRARY_IMPL(tdc, CUDA, m) {
   m.impl("update_sorted", &update_sorted);
   m.impl("fcm_small", &fcm_small);
   m.impl("finalize", &finalize);
+  m.impl("assign_bigd", &assign_bigd);
+  m.impl("quant_fp8", &quant_fp8);
 }

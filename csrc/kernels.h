@@ -53,3 +53,21 @@ int tdc_fcm_small_supported(int dtype, int K, int D);
 int tdc_finalize(int acc_dtype, int c_dtype, const void* sums, const void* counts, int K,
                  int D, void* C, int policy, float* shift, void* Cm2, float* cnorm, int Kp,
                  int DP, hipStream_t stream);
+
+// N1 wide-D / fp8 (assign_bigd.hip).  dtype TDC_BF16: X bf16 rows (ldx elements), Cm2
+// bf16 [Kp, DP] = -2c, DP in {384,512}.  dtype TDC_FP8: X e4m3 bytes (ldx bytes),
+// Xs E8M0 [N, DP/32]; Cm2 = quantised -2c with scales Cs [Kp, DP/32]; DP in {256..1024}/256.
+// cnorm [Kp] (pad 3e38), xnorm [N] (for mind).  Kp % 32 == 0.  The K loop is split into
+// groups of kg_tiles*32 centroids (0 = one group); with >1 group keys (uint64 [N], all
+// ones on entry; reset on exit) merges the group winners.
+int tdc_assign_bigd(int dtype, const void* X, const void* Xs, int64_t N, int64_t ldx, int DP,
+                    const void* Cm2, const void* Cs, const float* cnorm, int Kp, int kg_tiles,
+                    const float* xnorm, int32_t* labels, float* mind, unsigned long long* keys,
+                    hipStream_t stream);
+int tdc_assign_bigd_supported(int dtype, int DP);
+
+// N8 fp8 quantiser: rows of X (f32/f64/bf16, d valid columns, ldx elements) -> Q e4m3
+// [rows, DP] + E8M0 block scales S [rows, DP/32] + norm[rows] = ||dequant||^2.
+// neg2 != 0: centroid operand (-2c; norm of +c).  Rows >= valid are padding.
+int tdc_quant_fp8(int src_dtype, const void* X, int64_t rows, int64_t valid, int d, int64_t ldx,
+                  int DP, int neg2, void* Q, void* S, float* norm, hipStream_t stream);

@@ -4,14 +4,15 @@
 # than success or an ordinary test failure).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
+OUT="$PWD/gpurun_out"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 step() {  # step <seconds> <logname> <cmd...>
   local secs=$1 log=$2; shift 2
-  echo "== $(date +%T) $*" | tee -a gpurun_out/steps.log
-  timeout -k 10 "$secs" "$@" > "gpurun_out/$log" 2>&1
+  echo "== $(date +%T) $*" | tee -a "$OUT/steps.log"
+  timeout -k 10 "$secs" "$@" > "$OUT/$log" 2>&1
   local rc=$?
-  echo "   rc=$rc" | tee -a gpurun_out/steps.log
-  tail -5 "gpurun_out/$log"
+  echo "   rc=$rc" | tee -a "$OUT/steps.log"
+  tail -5 "$OUT/$log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after rc=$rc"; exit $rc; fi
   return 0
 }

@@ -11,6 +11,9 @@ Variants (picked by :func:`make_lloyd_ops`):
 
 ========================  =====================================================
 ``HipBf16Lloyd``          bf16 MFMA distance+argmin (N1) + LDS update (N2) + N3
+``HipWideBf16Lloyd``      bf16, 256 < D <= 512: K-grouped wide-D MFMA kernel
+``HipFp8Lloyd``           fp8 e4m3 + E8M0 block scales (N8), scaled-MFMA assign,
+                          update from the full-precision shard
 ``HipSmallLloyd``         fused fp32/fp64 assign+accumulate (reference configs)
 ``HipSimtLloyd``          fp32/fp64 exact SIMT assign + LDS update
 ``HipGemmLloyd``          fp32/fp64 large-D: library GEMM assign + LDS update
@@ -30,6 +33,10 @@ POLICY_CODES = {"keep": 0, "reseed": 0, "nan": 1, "zero": 2}
 TORCH_DTYPES = {"fp64": torch.float64, "fp32": torch.float32, "bf16": torch.bfloat16,
                 "fp8": torch.bfloat16}
 MFMA_DIMS = (32, 64, 128, 256)
+WIDE_BF16_DIMS = (384, 512)
+FP8_DIMS = (256, 512, 768, 1024)
+# centroid bytes one K-group may occupy (an XCD's L2 is 4 MiB; leave room for X/labels)
+KGROUP_BYTES = int(__import__("os").environ.get("TDC_KGROUP_BYTES", 3 << 20))
 
 
 def acc_dtype_for(dtype: str, k: int, d: int) -> torch.dtype:
@@ -48,6 +55,26 @@ def padded_dim(d: int) -> Optional[int]:
         if d <= p:
             return p
     return None
+
+
+def wide_bf16_dim(d: int) -> Optional[int]:
+    for p in WIDE_BF16_DIMS:
+        if d <= p:
+            return p
+    return None
+
+
+def fp8_dim(d: int) -> Optional[int]:
+    for p in FP8_DIMS:
+        if d <= p:
+            return p
+    return None
+
+
+def kgroup_tiles(row_bytes: int, kp: int) -> int:
+    """Centroid tiles (of 32) per K-group so a group stays L2-resident (0 = one group)."""
+    tiles = max(1, KGROUP_BYTES // (32 * row_bytes))
+    return 0 if tiles * 32 >= kp else int(tiles)
 
 
 def use_native(device: torch.device, backend: str) -> bool:
@@ -185,6 +212,153 @@ class HipBf16Lloyd(_LocalOpsBase):
         self.ops.finalize(sums, counts, C, self.policy, shift, self.cm2, self.cnorm)
 
 
+class _GroupedAssign:
+    """Shared state of the K-grouped wide-D kernels: point norms + merge keys."""
+
+    def _init_grouped(self, row_bytes: int):
+        self.kg = kgroup_tiles(row_bytes, self.kp)
+        self._keys = None
+
+    def _keys_for(self, n):
+        if self.kg == 0:
+            return None
+        if self._keys is None or self._keys.numel() < n:
+            self._keys = torch.full((max(n, 1),), -1, dtype=torch.int64, device=self.device)
+        return self._keys[:n]
+
+
+class HipWideBf16Lloyd(_GroupedAssign, _LocalOpsBase):
+    """bf16 shard [N, DP], 256 < D <= 512 (DP = 384 / 512): assign_bigd bf16 kernel."""
+    name = "hip_bf16_wide"
+    c_dtype = torch.float32
+
+    def __init__(self, x, k, empty_cluster="keep"):
+        super().__init__(x, k, empty_cluster)
+        self.ops = _native.require()
+        self.dp = wide_bf16_dim(self.d)
+        if self.dp is None:
+            raise ValueError(f"wide bf16 path supports D <= {WIDE_BF16_DIMS[-1]}, got {self.d}")
+        self.x = None
+        self.kp = ((k + 31) // 32) * 32
+        self.cm2 = torch.zeros(self.kp, self.dp, dtype=torch.bfloat16, device=x.device)
+        self.cnorm = torch.zeros(self.kp, dtype=torch.float32, device=x.device)
+        self._init_grouped(self.dp * 2 + 4)
+        self._set_x(x)
+        self.update = NativeUpdate(self.ops, self.n, k, self.d, torch.bfloat16, x.device)
+
+    def _set_x(self, x):
+        if x.dtype == torch.bfloat16 and x.shape[1] == self.dp and x.is_contiguous():
+            xb = x
+        else:
+            xb = torch.zeros(x.shape[0], self.dp, dtype=torch.bfloat16, device=x.device)
+            xb[:, : min(self.d, x.shape[1])] = x[:, : self.d]
+        self.x = xb
+        self.n = xb.shape[0]
+        self.xnorm = xb.float().pow_(2).sum(1)
+
+    @property
+    def layout(self):
+        return (torch.bfloat16, self.dp)
+
+    def bind(self, x):
+        if x is not self.x:
+            if x.dtype != torch.bfloat16 or x.shape[1] != self.dp:
+                raise ValueError(f"chunk layout {(x.dtype, x.shape[1])} != {self.layout}")
+            self._set_x(x)
+        return self
+
+    def prepare(self, C):
+        self.ops.finalize(None, None, C, 0, None, self.cm2, self.cnorm)
+
+    def assign(self, C, labels, mind):
+        self.ops.assign_bigd(self.x, None, self.xnorm, self.cm2, None, self.cnorm, self.kg,
+                             labels, mind, self._keys_for(self.n))
+
+    def step(self, C, labels, mind, sums, counts):
+        self.assign(C, labels, mind)
+        self.update(self.x, labels, sums, counts)
+
+    def finalize(self, sums, counts, C, shift):
+        self.ops.finalize(sums, counts, C, self.policy, shift, self.cm2, self.cnorm)
+
+
+class HipFp8Lloyd(_GroupedAssign, _LocalOpsBase):
+    """fp8 assignment (BASELINE config 5): the shard is quantised once to OCP e4m3 with
+    one E8M0 exponent per 32 features (N8, `quant_fp8`); centroids are re-quantised each
+    iteration as the -2c operand.  Distances run on the block-scaled MFMA; the update
+    sums the full-precision shard (bf16/fp32), so centroids are exact means of the
+    assigned points and fp8 only affects which centroid wins a near-tie."""
+    name = "hip_fp8_mfma"
+    c_dtype = torch.float32
+
+    def __init__(self, x, k, empty_cluster="keep"):
+        super().__init__(x, k, empty_cluster)
+        self.ops = _native.require()
+        self.dp = fp8_dim(self.d)
+        if self.dp is None:
+            raise ValueError(f"fp8 path supports D <= {FP8_DIMS[-1]}, got {self.d}")
+        self.kp = ((k + 31) // 32) * 32
+        dev = x.device
+        self.cm2 = torch.zeros(self.kp, self.dp, dtype=torch.float8_e4m3fn, device=dev)
+        self.cs = torch.zeros(self.kp, self.dp // 32, dtype=torch.uint8, device=dev)
+        self.cnorm = torch.zeros(self.kp, dtype=torch.float32, device=dev)
+        self._init_grouped(self.dp + self.dp // 32 + 4)
+        self.x8 = self.xs = self.xnorm = None
+        self.x = None
+        self._set_x(x)
+        self.update = NativeUpdate(self.ops, self.n, k, self.d, self.x.dtype, dev)
+
+    def _set_x(self, x):
+        if x.dtype == torch.float64:
+            x = x.float()
+        if not x.is_contiguous():
+            x = x.contiguous()
+        n = x.shape[0]
+        if self.x8 is None or self.x8.shape[0] < n:
+            self.x8 = torch.empty(n, self.dp, dtype=torch.float8_e4m3fn, device=x.device)
+            self.xs = torch.empty(n, self.dp // 32, dtype=torch.uint8, device=x.device)
+            self.xnorm = torch.empty(n, dtype=torch.float32, device=x.device)
+        self.x = x
+        self.n = n
+        self.ops.quant_fp8(x[:, : self.d], n, 0, self.x8[:n], self.xs[:n], self.xnorm[:n])
+
+    @property
+    def layout(self):
+        return (self.x.dtype, self.x.shape[1])
+
+    def bind(self, x):
+        if x is not self.x:
+            if x.shape[1] != self.x.shape[1]:
+                raise ValueError(f"chunk layout {(x.dtype, x.shape[1])} != {self.layout}")
+            self._set_x(x)
+        return self
+
+    def prepare(self, C):
+        self.ops.quant_fp8(C, self.k, 1, self.cm2, self.cs, self.cnorm)
+
+    def assign(self, C, labels, mind):
+        n = self.n
+        self.ops.assign_bigd(self.x8[:n], self.xs[:n], self.xnorm[:n], self.cm2, self.cs,
+                             self.cnorm, self.kg, labels, None, self._keys_for(n))
+        if mind is not None:
+            # inertia from the full-precision shard (the fp8 distances include the
+            # quantisation noise of both operands; they only pick the winner)
+            Cf = C.float()
+            step = max(1, (1 << 28) // max(1, 4 * self.d))
+            for s in range(0, n, step):
+                e = min(n, s + step)
+                diff = self.x[s:e, : self.d].float() - Cf.index_select(0, labels[s:e].long())
+                mind[s:e] = diff.pow_(2).sum(1).to(mind.dtype)
+
+    def step(self, C, labels, mind, sums, counts):
+        self.assign(C, labels, mind)
+        self.update(self.x, labels, sums, counts)
+
+    def finalize(self, sums, counts, C, shift):
+        self.ops.finalize(sums, counts, C, self.policy, shift, None, None)
+        self.prepare(C)
+
+
 class _HipExactBase(_LocalOpsBase):
     def __init__(self, x, k, dtype, empty_cluster):
         super().__init__(x, k, empty_cluster)
@@ -241,10 +415,14 @@ def make_lloyd_ops(x: torch.Tensor, k: int, dtype: str = "bf16", backend: str = 
     if not use_native(x.device, backend):
         return TorchLloyd(x, k, dtype if dtype in ("fp64", "fp32") else "fp32", empty_cluster)
     if dtype == "fp8":
-        raise NotImplementedError("fp8 distance path: use dtype='bf16' (fp8 MFMA kernel pending)")
+        if fp8_dim(d) is not None:
+            return HipFp8Lloyd(x, k, empty_cluster)
+        dtype = "bf16"  # D > 1024: bf16/fp32 paths below
     if dtype == "bf16":
         if padded_dim(d) is not None:
             return HipBf16Lloyd(x, k, empty_cluster)
+        if wide_bf16_dim(d) is not None:
+            return HipWideBf16Lloyd(x, k, empty_cluster)
         return HipGemmLloyd(x, k, "fp32", empty_cluster)
     tdt = TORCH_DTYPES[dtype]
     ops = _native.require()

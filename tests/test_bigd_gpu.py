@@ -1,0 +1,156 @@
+"""GPU: wide-D / fp8 assignment (csrc/assign_bigd.hip) and the fp8 quantiser (N8), against
+fp64 torch references of the same (quantised) operands."""
+import numpy as np
+import pytest
+import torch
+
+import tensorflow_distributed_clustering_amd as tdc
+from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs
+
+pytestmark = pytest.mark.gpu
+
+
+def ops():
+    return torch.ops.tdc
+
+
+def ref_quant(x: torch.Tensor, dp: int, neg2: bool = False):
+    """torch model of quant_fp8: E8M0 exponent ilogb(amax)-7 per 32-block, RNE to e4m3."""
+    n, d = x.shape
+    xp = torch.zeros(n, dp, dtype=torch.float32, device=x.device)
+    xp[:, :d] = x.float()
+    blk = xp.view(n, dp // 32, 32)
+    amax = blk.abs().amax(-1)
+    _, ex = torch.frexp(amax)
+    e = torch.where(amax > 0, ex - 1 - 7, torch.full_like(ex, -127)).clamp(-127, 126)
+    q = (blk / torch.exp2(e.float())[..., None]).to(torch.float8_e4m3fn)
+    deq = q.float() * torch.exp2(e.float())[..., None]
+    norm = (deq.reshape(n, dp).double() ** 2).sum(1).float()
+    if neg2:
+        q = (-q.float()).to(torch.float8_e4m3fn)
+        e = e + 1
+    return q.reshape(n, dp), (e + 127).to(torch.uint8), norm, deq.reshape(n, dp)
+
+
+@pytest.mark.parametrize("src", [torch.float32, torch.bfloat16, torch.float64])
+@pytest.mark.parametrize("d,dp", [(768, 768), (100, 256), (1000, 1024)])
+def test_quant_fp8_matches_torch(gpu, src, d, dp):
+    g = torch.Generator(device=gpu).manual_seed(0)
+    x = (torch.randn(3001, d, device=gpu, generator=g) * torch.logspace(-3, 3, d, device=gpu)).to(src)
+    q = torch.empty(3001, dp, dtype=torch.float8_e4m3fn, device=gpu)
+    s = torch.empty(3001, dp // 32, dtype=torch.uint8, device=gpu)
+    nrm = torch.empty(3001, dtype=torch.float32, device=gpu)
+    ops().quant_fp8(x, 3001, 0, q, s, nrm)
+    rq, rs, rn, _ = ref_quant(x.float(), dp)
+    assert torch.equal(s, rs)
+    assert torch.equal(q.view(torch.uint8), rq.view(torch.uint8))
+    torch.testing.assert_close(nrm, rn, rtol=1e-5, atol=1e-5)
+
+
+def test_quant_fp8_centroid_mode_and_padding(gpu):
+    c = torch.randn(40, 256, device=gpu)
+    q = torch.empty(64, 256, dtype=torch.float8_e4m3fn, device=gpu)
+    s = torch.empty(64, 8, dtype=torch.uint8, device=gpu)
+    nrm = torch.empty(64, dtype=torch.float32, device=gpu)
+    ops().quant_fp8(c, 40, 1, q, s, nrm)
+    rq, rs, rn, _ = ref_quant(c, 256, neg2=True)
+    assert torch.equal(q[:40].view(torch.uint8), rq.view(torch.uint8))
+    assert torch.equal(s[:40], rs)
+    torch.testing.assert_close(nrm[:40], rn, rtol=1e-5, atol=1e-5)
+    assert (q[40:].view(torch.uint8) == 0).all() and (nrm[40:] > 1e38).all()
+
+
+def _fp8_operands(x, c, dp, kp):
+    n, k = x.shape[0], c.shape[0]
+    dev = x.device
+    x8 = torch.empty(n, dp, dtype=torch.float8_e4m3fn, device=dev)
+    xs = torch.empty(n, dp // 32, dtype=torch.uint8, device=dev)
+    xn = torch.empty(n, dtype=torch.float32, device=dev)
+    ops().quant_fp8(x, n, 0, x8, xs, xn)
+    cm = torch.empty(kp, dp, dtype=torch.float8_e4m3fn, device=dev)
+    cs = torch.empty(kp, dp // 32, dtype=torch.uint8, device=dev)
+    cn = torch.empty(kp, dtype=torch.float32, device=dev)
+    ops().quant_fp8(c, k, 1, cm, cs, cn)
+    return x8, xs, xn, cm, cs, cn
+
+
+def _ref_assign(xd, cd):
+    d2 = torch.cdist(xd.double(), cd.double()) ** 2
+    md, lab = d2.min(1)
+    top2 = d2.topk(2, largest=False).values
+    gap = (top2[:, 1] - top2[:, 0]) / top2[:, 0].clamp_min(1e-9)
+    return lab.int(), md, gap
+
+
+@pytest.mark.parametrize("d,dp,k,kg", [(768, 768, 1000, 0), (768, 768, 4096, 8), (200, 256, 320, 3),
+                                       (512, 512, 2048, 0), (1024, 1024, 96, 1)])
+def test_assign_fp8_vs_dequantised_reference(gpu, d, dp, k, kg):
+    torch.manual_seed(1)
+    n = 20000
+    x = torch.randn(n, d, device=gpu) * 3
+    c = torch.randn(k, d, device=gpu) * 3
+    kp = (k + 31) // 32 * 32
+    x8, xs, xn, cm, cs, cn = _fp8_operands(x, c, dp, kp)
+    _, _, _, xd = ref_quant(x, dp)
+    _, _, _, cdq = ref_quant(c, dp)
+    lab = torch.empty(n, dtype=torch.int32, device=gpu)
+    mind = torch.empty(n, dtype=torch.float32, device=gpu)
+    keys = torch.full((n,), -1, dtype=torch.int64, device=gpu) if kg else None
+    ops().assign_bigd(x8, xs, xn, cm, cs, cn, kg, lab, mind, keys)
+    rlab, rmd, gap = _ref_assign(xd, cdq)
+    clear = gap > 1e-4  # fp32 accumulation can flip true near-ties only
+    assert clear.float().mean() > 0.9
+    assert torch.equal(lab[clear], rlab[clear])
+    torch.testing.assert_close(mind.double(), rmd, rtol=2e-3, atol=1e-2)
+    if keys is not None:
+        assert (keys == -1).all()  # reset for the next pass
+        lab2 = torch.empty_like(lab)
+        ops().assign_bigd(x8, xs, xn, cm, cs, cn, 0, lab2, None, None)  # one group
+        assert torch.equal(lab, lab2)
+
+
+@pytest.mark.parametrize("d,dp,k,kg", [(300, 384, 777, 0), (512, 512, 3000, 16), (384, 384, 64, 1)])
+def test_assign_wide_bf16(gpu, d, dp, k, kg):
+    torch.manual_seed(2)
+    n = 15000
+    x = torch.zeros(n, dp, dtype=torch.bfloat16, device=gpu)
+    x[:, :d] = (torch.randn(n, d, device=gpu) * 2).bfloat16()
+    c = (torch.randn(k, d, device=gpu) * 2).bfloat16().float()
+    kp = (k + 31) // 32 * 32
+    cm2 = torch.zeros(kp, dp, dtype=torch.bfloat16, device=gpu)
+    cn = torch.zeros(kp, dtype=torch.float32, device=gpu)
+    ops().finalize(None, None, c.contiguous(), 0, None, cm2, cn)
+    xn = x.float().pow(2).sum(1)
+    lab = torch.empty(n, dtype=torch.int32, device=gpu)
+    mind = torch.empty(n, dtype=torch.float32, device=gpu)
+    keys = torch.full((n,), -1, dtype=torch.int64, device=gpu) if kg else None
+    ops().assign_bigd(x, None, xn, cm2, None, cn, kg, lab, mind, keys)
+    rlab, rmd, gap = _ref_assign(x[:, :d].float(), c)
+    clear = gap > 1e-4
+    assert clear.float().mean() > 0.9
+    assert torch.equal(lab[clear], rlab[clear])
+    torch.testing.assert_close(mind.double(), rmd, rtol=2e-3, atol=1e-2)
+
+
+def test_kmeans_fp8_end_to_end(gpu):
+    n, d, k = 200_000, 768, 256
+    x = gaussian_blobs(n, d, k, seed=5, dtype=torch.bfloat16, device=gpu)
+    cfg = tdc.ClusterConfig(n_clusters=k, max_iter=8, dtype="fp8", seed=2, init="kmeans++")
+    a = tdc.KMeans(cfg, device=gpu).fit(x)
+    b = tdc.KMeans(cfg.replace(dtype="bf16"), device=gpu).fit(x)
+    assert a.result_.backend == "hip_fp8_mfma"
+    agree = (a.result_.labels == b.result_.labels).float().mean().item()
+    assert agree > 0.99
+    # inertia is measured on the full-precision data for both runs
+    assert a.result_.inertia <= 1.01 * b.result_.inertia
+
+
+def test_kmeans_wide_bf16_end_to_end(gpu):
+    n, d, k = 100_000, 400, 128
+    x = gaussian_blobs(n, d, k, seed=6, dtype=torch.bfloat16, device=gpu)
+    cfg = tdc.ClusterConfig(n_clusters=k, max_iter=6, dtype="bf16", seed=1, init="kmeans++")
+    a = tdc.KMeans(cfg, device=gpu).fit(x)
+    b = tdc.KMeans(cfg.replace(dtype="fp32"), device=gpu).fit(x.float())
+    assert a.result_.backend == "hip_bf16_wide"
+    agree = (a.result_.labels == b.result_.labels).float().mean().item()
+    assert agree > 0.99
