@@ -116,7 +116,7 @@ def build_parser():
                         type=lambda x: check_file_exists(parser, x),
                         help="Unable to find data file !!!")
     # ---- extensions (all optional) ----
-    parser.add_argument("--dtype", default="auto", choices=["auto", "fp64", "fp32", "bf16"])
+    parser.add_argument("--dtype", default="auto", choices=["auto", "fp64", "fp32", "bf16", "fp8"])
     parser.add_argument("--init", default="kmeans++", choices=["kmeans++", "first_k", "random"])
     parser.add_argument("--fuzzifier", type=float, default=None,
                         help="FCM m (default: the data dimension, as the reference)")
@@ -131,9 +131,16 @@ def build_parser():
     parser.add_argument("--extended_log", default=None, help="JSON-lines file with derived metrics")
     parser.add_argument("--compat", action="store_true",
                         help="reference bug-compat: NaN empty clusters, first-K init")
-    parser.add_argument("--checkpoint", default=None)
-    parser.add_argument("--checkpoint_every", type=int, default=0)
-    parser.add_argument("--resume", action="store_true")
+    parser.add_argument("--checkpoint", default=None,
+                        help="NPZ checkpoint of the centroids (written by rank 0)")
+    parser.add_argument("--checkpoint_every", type=int, default=0,
+                        help="iterations between checkpoints (0: only at the end)")
+    parser.add_argument("--resume", action="store_true",
+                        help="continue from --checkpoint if it exists")
+    parser.add_argument("--hbm_budget_gb", type=float, default=0.0,
+                        help="per-GPU memory budget for the stream planner (0: free HBM)")
+    parser.add_argument("--deterministic", action="store_true",
+                        help="run-to-run bitwise reproducible centroid update")
     return parser
 
 
@@ -185,7 +192,10 @@ def run(args) -> int:
         cfg = ClusterConfig(n_clusters=args.K, max_iter=args.n_max_iters, tol=args.tol,
                             dtype=dtype, init=init, seed=args.seed, fuzzifier=args.fuzzifier,
                             empty_cluster=empty, backend=args.backend,
-                            chunk_rows=args.chunk_rows, batch_size=args.batch_size)
+                            chunk_rows=args.chunk_rows, batch_size=args.batch_size,
+                            checkpoint_path=args.checkpoint or "",
+                            checkpoint_every=args.checkpoint_every, resume=args.resume,
+                            hbm_budget_gb=args.hbm_budget_gb, deterministic=args.deterministic)
         xt = torch.from_numpy(np.asarray(x))
         if args.method_name == "distributedKMeans":
             model = KMeans(cfg, comm)

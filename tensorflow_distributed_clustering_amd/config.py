@@ -38,6 +38,7 @@ class ClusterConfig:
     deterministic   ordered per-block reduction instead of float atomics
     chunk_rows      rows per streamed chunk (0 = whole shard resident)
     hbm_budget_gb   planner budget per GPU (MI355X has 288 GB)
+    checkpoint_*    periodic centroid checkpoints / resume (reference: none)
     """
 
     n_clusters: int
@@ -57,6 +58,10 @@ class ClusterConfig:
     label_pass: bool = True
     batch_size: int = 0  # mini-batch K-Means: rows per rank per step
     log_every: int = 0
+    checkpoint_path: str = ""   # NPZ written by rank 0 (utils/checkpoint.py)
+    checkpoint_every: int = 0   # iterations between checkpoints (0: final only)
+    resume: bool = False        # continue from checkpoint_path if it exists
+    max_oom_retries: int = 4    # setup OOM -> halve the streamed chunk and retry
 
     def __post_init__(self):
         if self.n_clusters <= 0:

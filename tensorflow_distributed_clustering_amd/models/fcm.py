@@ -20,6 +20,8 @@ import torch
 from ..config import ClusterConfig
 from ..ops import make_fcm_ops
 from ..parallel.dist import Comm, local_comm
+from ..utils import faults
+from ..utils.checkpoint import RunCheckpointer
 from ..utils.timers import DeviceTimer, sync
 from .init import init_centers
 from .kmeans import ClusterResult, _shard_geometry
@@ -55,6 +57,11 @@ class FuzzyCMeans:
         initialization_time = time.perf_counter() - t0
 
         t1 = time.perf_counter()
+        ckpt = RunCheckpointer(cfg, comm, "distributedFuzzyCMeans")
+        resumed = ckpt.load_for_resume(k, d)
+        start_iter = 0
+        if resumed is not None:
+            init_centers_, start_iter = resumed.centers, resumed.n_iter
         c0 = init_centers(cfg.init, x_local, row_offset, n_global, k, comm, cfg.seed,
                           given=init_centers_)
         C = c0.to(local.c_dtype).clone().contiguous()
@@ -69,9 +76,10 @@ class FuzzyCMeans:
 
         timer = DeviceTimer(dev)
         timer.start()
-        n_iter = 0
+        n_iter = start_iter
         history = []
-        for it in range(cfg.max_iter):
+        centers_host = lambda: C.double().cpu().numpy()
+        for it in range(start_iter, cfg.max_iter):
             buf.zero_()
             local.step(C, labels, wx, ws)
             comm.allreduce_(buf)
@@ -84,7 +92,10 @@ class FuzzyCMeans:
                 history.append({"iter": n_iter, "shift": sv})
                 if sv <= cfg.tol:
                     break
+            ckpt.maybe_save(n_iter, centers_host)
+            faults.maybe_fail(str(n_iter), comm.rank)
         computation_time = timer.stop()
+        ckpt.maybe_save(n_iter, centers_host, final=True)
 
         if cfg.label_pass:
             local.assign(C, labels)

@@ -34,6 +34,8 @@ from ..config import ClusterConfig
 from ..data.stream import HostSource, ResidentSource, plan_chunk_rows
 from ..ops import acc_dtype_for, make_lloyd_ops, padded_dim
 from ..parallel.dist import Comm, local_comm
+from ..utils import faults
+from ..utils.checkpoint import RunCheckpointer
 from ..utils.timers import DeviceTimer, sync
 from .init import floyd_sample, init_centers, init_centers_from_source
 
@@ -78,14 +80,15 @@ class LloydEngine:
     """
 
     def __init__(self, source, cfg: ClusterConfig, comm: Comm, n_global: int, row_offset: int,
-                 init_centers_=None, chunk_rows: int = 0):
+                 init_centers_=None, chunk_rows: int = 0, defer_init: bool = False):
         self.cfg, self.comm = cfg, comm
         self.n_global, self.row_offset = n_global, row_offset
         k = cfg.n_clusters
         self.k = k
         if isinstance(source, torch.Tensor):
             x0 = source
-            self.local = make_lloyd_ops(source, k, cfg.dtype, cfg.backend, cfg.empty_cluster)
+            self.local = make_lloyd_ops(source, k, cfg.dtype, cfg.backend, cfg.empty_cluster,
+                                        cfg.deterministic)
             self.source = ResidentSource(self.local.x, self.local.layout, row_offset)
             self.local.x = self.source.x
             self.device = source.device
@@ -97,21 +100,17 @@ class LloydEngine:
             self.d = int(source.d)
             self.n_local = int(source.n_rows)
             probe = torch.zeros(1, self.d, dtype=torch.float32, device=self.device)
-            self.local = make_lloyd_ops(probe, k, cfg.dtype, cfg.backend, cfg.empty_cluster)
+            self.local = make_lloyd_ops(probe, k, cfg.dtype, cfg.backend, cfg.empty_cluster,
+                                        cfg.deterministic)
             if tuple(self.local.layout) != tuple(source.layout):
                 raise ValueError(f"source layout {source.layout} != kernel layout {self.local.layout}")
             x0 = None
         self.chunk_rows = chunk_rows
         self.streamed = not isinstance(self.source, ResidentSource) or chunk_rows > 0
         dev = self.device
-        if x0 is not None:
-            self.c0 = init_centers(cfg.init, x0, row_offset, n_global, k, comm, cfg.seed,
-                                   given=init_centers_)
-        else:
-            self.c0 = init_centers_from_source(cfg.init, self.source, row_offset, n_global, k,
-                                               comm, cfg.seed, given=init_centers_, d=self.d)
-        self.C = self.c0.to(self.local.c_dtype).clone().contiguous()  # never alias c0
-        self.local.prepare(self.C)
+        self._x0 = x0
+        self._init_given = init_centers_
+        self.C = torch.zeros(k, self.d, dtype=self.local.c_dtype, device=dev)
         acc = acc_dtype_for(cfg.dtype, k, self.d)
         self.buf = torch.zeros(k * self.d + k, dtype=acc, device=dev)
         self.sums = self.buf[: k * self.d].view(k, self.d)
@@ -123,6 +122,25 @@ class LloydEngine:
         self.shift = torch.zeros(1, dtype=torch.float32, device=dev) if self.need_shift else None
         self.bucket_bytes = 64 << 20
         self.n_iter = 0
+        self.c0 = None
+        if not defer_init:
+            self.init_centroids()
+
+    def init_centroids(self):
+        """Centroid init (collective: every rank calls it, in the same order).  Kept out
+        of the constructor's local allocations so a setup OOM can be agreed on first."""
+        cfg, comm, k = self.cfg, self.comm, self.k
+        if self._x0 is not None:
+            c0 = init_centers(cfg.init, self._x0, self.row_offset, self.n_global, k, comm,
+                              cfg.seed, given=self._init_given)
+        else:
+            c0 = init_centers_from_source(cfg.init, self.source, self.row_offset, self.n_global,
+                                          k, comm, cfg.seed, given=self._init_given, d=self.d)
+        self.c0 = c0
+        self.C.copy_(c0.to(self.local.c_dtype))  # never alias c0
+        self.local.prepare(self.C)
+        self._x0 = None
+        return self
 
     def _chunks(self):
         return self.source.chunks(self.chunk_rows)
@@ -205,26 +223,66 @@ class KMeans:
             return x.device
         return torch.device(getattr(x, "device", "cpu"))
 
-    def _make_source(self, x_local, dev, row_offset):
+    def _make_source(self, x_local, dev, row_offset, chunk_override: int = 0):
         """(source, chunk_rows): resident tensor, or a HostSource when the shard stays on
-        the host (does not fit the HBM budget, or cfg.chunk_rows forces streaming)."""
+        the host (does not fit the HBM budget, or cfg.chunk_rows / an OOM retry forces
+        streaming)."""
         cfg = self.cfg
+        want = chunk_override or cfg.chunk_rows
         if hasattr(x_local, "chunks"):
-            return x_local, cfg.chunk_rows or (1 << 22)
+            return x_local, want or (1 << 22)
         if isinstance(x_local, torch.Tensor) and x_local.device.type != "cpu":
-            return x_local.to(dev), cfg.chunk_rows
+            return x_local.to(dev), want
         xn = x_local.numpy() if isinstance(x_local, torch.Tensor) else np.asarray(x_local)
         if dev.type == "cuda" and cfg.dtype in ("bf16", "fp32"):
             d = xn.shape[1]
             width = padded_dim(d) if cfg.dtype == "bf16" else d
             if width is not None:
                 es = 2 if cfg.dtype == "bf16" else 4
-                chunk = cfg.chunk_rows or plan_chunk_rows(xn.shape[0], width * es,
-                                                          cfg.n_clusters, d, dev, cfg.hbm_budget_gb)
+                chunk = want or plan_chunk_rows(xn.shape[0], width * es, cfg.n_clusters, d, dev,
+                                                cfg.hbm_budget_gb)
                 if chunk:
                     layout = (torch.bfloat16 if cfg.dtype == "bf16" else torch.float32, width)
                     return HostSource(xn, layout, dev, row_offset), chunk
-        return torch.as_tensor(xn).to(dev), cfg.chunk_rows
+        return torch.as_tensor(xn).to(dev), want
+
+    def _build_engine(self, first, x_local, dev, comm, n_global, row_offset, n_local,
+                      init_centers_, start_iter):
+        """LloydEngine with collective OOM handling: if any rank runs out of memory while
+        building the engine, every rank halves the streamed chunk and retries (the
+        reference doubled its batch count on ResourceExhaustedError,
+        `scripts/distribuitedClustering.py:331-360`, but clustered batches independently)."""
+        cfg = self.cfg
+        chunk = 0
+        for attempt in range(cfg.max_oom_retries + 1):
+            err = None
+            eng = source = None
+            try:
+                if attempt == 0:
+                    source, chunk_rows = first
+                else:
+                    source, chunk_rows = self._make_source(x_local, dev, row_offset, chunk)
+                first = None
+                faults.maybe_fail("setup", comm.rank)
+                eng = LloydEngine(source, cfg, comm, n_global, row_offset, init_centers_,
+                                  chunk_rows, defer_init=True)
+            except Exception as e:  # noqa: BLE001 - filtered right below
+                if not faults.is_oom(e):
+                    raise
+                err = e
+            if comm.max_scalar(1.0 if err is not None else 0.0) == 0.0:
+                eng.init_centroids()
+                eng.n_iter = start_iter
+                return eng
+            del eng, source
+            if dev.type == "cuda":
+                torch.cuda.empty_cache()
+            chunk = max(1024, (chunk or n_local) // 2)
+            if comm.is_root:
+                print(f"[kmeans] out of memory while building the engine "
+                      f"({type(err).__name__ if err else 'peer rank'}); retrying streamed with "
+                      f"chunk_rows={chunk}", flush=True)
+        raise err if err is not None else faults.oom_error("out of memory on a peer rank")
 
     def fit(self, x_local, init_centers_: Optional[np.ndarray] = None,
             n_global: Optional[int] = None, row_offset: Optional[int] = None) -> "KMeans":
@@ -237,20 +295,32 @@ class KMeans:
         n_local = int(x_local.n_rows if hasattr(x_local, "n_rows") else x_local.shape[0])
         if n_global is None or row_offset is None:
             n_global, row_offset = _shard_geometry(n_local, comm)
-        source, chunk_rows = self._make_source(x_local, dev, row_offset)
+        first = self._make_source(x_local, dev, row_offset)
         sync(dev)
         initialization_time = time.perf_counter() - t_init0
 
         t_setup0 = time.perf_counter()
-        eng = LloydEngine(source, cfg, comm, n_global, row_offset, init_centers_, chunk_rows)
+        ckpt = RunCheckpointer(cfg, comm, "distributedKMeans")
+        d = int(x_local.d if hasattr(x_local, "d") else x_local.shape[1])
+        resumed = ckpt.load_for_resume(cfg.n_clusters, d)
+        start_iter = 0
+        if resumed is not None:
+            init_centers_, start_iter = resumed.centers, resumed.n_iter
+            if comm.is_root:
+                print(f"[kmeans] resuming from {cfg.checkpoint_path} at iteration {start_iter}",
+                      flush=True)
+        eng = self._build_engine(first, x_local, dev, comm, n_global, row_offset, n_local,
+                                 init_centers_, start_iter)
+        del first
         sync(dev)
         setup_time = time.perf_counter() - t_setup0
 
         # ------------------------------------------------------------ timed loop
         history = []
+        centers_host = lambda: eng.C.double().cpu().numpy()
         timer = DeviceTimer(dev)
         timer.start()
-        for _ in range(cfg.max_iter):
+        for _ in range(max(0, cfg.max_iter - start_iter)):
             eng.step()
             n = eng.n_iter
             if eng.need_shift and (cfg.tol > 0 or n % cfg.log_every == 0):
@@ -260,7 +330,10 @@ class KMeans:
                     print(f"[kmeans] iter {n} max centroid shift^2 {sv:.3e}", flush=True)
                 if cfg.tol > 0 and sv <= cfg.tol:
                     break
+            ckpt.maybe_save(n, centers_host)
+            faults.maybe_fail(str(n), comm.rank)
         computation_time = timer.stop()
+        ckpt.maybe_save(eng.n_iter, centers_host, final=True)
 
         # ------------------------------------------- final label pass (untimed)
         inertia = eng.label_pass() if cfg.label_pass else None

@@ -27,6 +27,8 @@ from ..config import ClusterConfig
 from ..data.stream import ResidentSource
 from ..ops import acc_dtype_for, make_lloyd_ops
 from ..parallel.dist import Comm, local_comm
+from ..utils import faults
+from ..utils.checkpoint import RunCheckpointer
 from ..utils.timers import DeviceTimer, sync
 from .init import init_centers, init_centers_from_source
 from .kmeans import ClusterResult, _shard_geometry
@@ -45,7 +47,8 @@ class MiniBatchStepper:
         k = self.k = cfg.n_clusters
         if isinstance(source, torch.Tensor):
             dev = source.device
-            self.local = make_lloyd_ops(source, k, cfg.dtype, cfg.backend, cfg.empty_cluster)
+            self.local = make_lloyd_ops(source, k, cfg.dtype, cfg.backend, cfg.empty_cluster,
+                                        cfg.deterministic)
             self.source = ResidentSource(self.local.x, self.local.layout, row_offset)
             self.d = int(source.shape[1])
             self.c0 = init_centers(cfg.init, source, row_offset, n_global, k, comm, cfg.seed,
@@ -55,7 +58,7 @@ class MiniBatchStepper:
             self.source = source
             self.d = int(source.d)
             self.local = make_lloyd_ops(torch.zeros(1, self.d, device=dev), k, cfg.dtype,
-                                        cfg.backend, cfg.empty_cluster)
+                                        cfg.backend, cfg.empty_cluster, cfg.deterministic)
             self.c0 = init_centers_from_source(cfg.init, source, row_offset, n_global, k, comm,
                                                cfg.seed, given=init_centers_, d=self.d)
         self.device = dev
@@ -154,14 +157,28 @@ class MiniBatchKMeans:
         initialization_time = time.perf_counter() - t0
 
         t1 = time.perf_counter()
+        ckpt = RunCheckpointer(cfg, comm, "miniBatchKMeans")
+        d = int(x_local.d if hasattr(x_local, "d") else x_local.shape[1])
+        resumed = ckpt.load_for_resume(cfg.n_clusters, d)
+        if resumed is not None:
+            init_centers_ = resumed.centers
         eng = MiniBatchStepper(x_local, cfg, comm, n_global, row_offset, init_centers_)
+        if resumed is not None:
+            # per-center counts come back exactly; the batch sampler is re-seeded from the
+            # iteration count (statistically equivalent, not the uninterrupted stream)
+            eng.n_iter = resumed.n_iter
+            if "counts" in resumed.arrays:
+                eng.v = torch.as_tensor(resumed.arrays["counts"], dtype=torch.float64, device=dev)
+            eng.gen.manual_seed(cfg.seed * 1000003 + comm.rank + 7919 * resumed.n_iter)
         sync(dev)
         setup_time = time.perf_counter() - t1
 
         timer = DeviceTimer(dev)
         timer.start()
         history = []
-        for _ in range(cfg.max_iter):
+        centers_host = lambda: eng.C.double().cpu().numpy()
+        counts_host = lambda: {"counts": eng.v.cpu().numpy()}
+        for _ in range(max(0, cfg.max_iter - eng.n_iter)):
             eng.step()
             n = eng.n_iter
             if cfg.tol > 0 or (cfg.log_every and n % cfg.log_every == 0):
@@ -169,7 +186,10 @@ class MiniBatchKMeans:
                 history.append({"iter": n, "shift": sv})
                 if cfg.tol > 0 and sv <= cfg.tol:
                     break
+            ckpt.maybe_save(n, centers_host, counts_host)
+            faults.maybe_fail(str(n), comm.rank)
         computation_time = timer.stop()
+        ckpt.maybe_save(eng.n_iter, centers_host, counts_host, final=True)
 
         labels, inertia = eng.label_pass() if cfg.label_pass else (None, None)
         self.engine_ = eng

@@ -101,7 +101,12 @@ class NativeUpdate:
             self.work = torch.empty(int(ops.update_sorted_workspace(n, k)), dtype=torch.int32,
                                     device=device)
 
+    deterministic = False
+
     def __call__(self, x, labels, sums, counts):
+        if self.deterministic:
+            deterministic_update(x, labels, sums, counts)
+            return
         if self.kind == "lds":
             self.ops.update(x, labels, sums, counts)
         else:
@@ -109,6 +114,22 @@ class NativeUpdate:
                 self.work = torch.empty(int(self.ops.update_sorted_workspace(x.shape[0], sums.shape[0])),
                                         dtype=torch.int32, device=x.device)
             self.ops.update_sorted(x, labels, sums, counts, self.work)
+
+
+def deterministic_update(x, labels, sums, counts):
+    """Run-to-run bitwise reproducible partial sums (SURVEY.md §5.2 ``--deterministic``):
+    PyTorch's sort-based ``index_put_(accumulate=True)`` under deterministic algorithms
+    instead of the float atomics of the HIP update kernels."""
+    prev = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    try:
+        idx = (labels[: x.shape[0]].long(),)
+        d = sums.shape[1]
+        sums.index_put_(idx, x[:, :d].to(sums.dtype), accumulate=True)
+        counts.index_put_(idx, torch.ones(x.shape[0], dtype=counts.dtype, device=x.device),
+                          accumulate=True)
+    finally:
+        torch.use_deterministic_algorithms(prev)
 
 
 class _LocalOpsBase:
@@ -409,8 +430,15 @@ class HipGemmLloyd(_HipExactBase):
 
 
 def make_lloyd_ops(x: torch.Tensor, k: int, dtype: str = "bf16", backend: str = "auto",
-                   empty_cluster: str = "keep"):
+                   empty_cluster: str = "keep", deterministic: bool = False):
     """Pick the fastest local implementation for (device, dtype, K, D)."""
+    ops = _make_lloyd_ops(x, k, dtype, backend, empty_cluster, deterministic)
+    if deterministic and isinstance(getattr(ops, "update", None), NativeUpdate):
+        ops.update.deterministic = True
+    return ops
+
+
+def _make_lloyd_ops(x, k, dtype, backend, empty_cluster, deterministic):
     d = x.shape[1]
     if not use_native(x.device, backend):
         return TorchLloyd(x, k, dtype if dtype in ("fp64", "fp32") else "fp32", empty_cluster)
@@ -426,7 +454,7 @@ def make_lloyd_ops(x: torch.Tensor, k: int, dtype: str = "bf16", backend: str = 
         return HipGemmLloyd(x, k, "fp32", empty_cluster)
     tdt = TORCH_DTYPES[dtype]
     ops = _native.require()
-    if ops.lloyd_small_supported(tdt, k, d):
+    if ops.lloyd_small_supported(tdt, k, d) and not deterministic:
         return HipSmallLloyd(x, k, dtype, empty_cluster)
     if d <= (64 if dtype == "fp32" else 32):
         return HipSimtLloyd(x, k, dtype, empty_cluster)

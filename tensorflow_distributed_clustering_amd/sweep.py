@@ -73,6 +73,24 @@ def command(run: Run, args) -> List[str]:
     return cli
 
 
+def completed_runs(log_file: str) -> set:
+    """(method, GPUs, K, n_obs, n_dim) of rows with a numeric computation_time: the
+    sweep-level resume (the reference always re-ran every config)."""
+    import csv
+    done = set()
+    if not os.path.exists(log_file):
+        return done
+    with open(log_file, newline="") as f:
+        for row in csv.DictReader(f):
+            try:
+                float(row["computation_time"])
+            except (KeyError, TypeError, ValueError):
+                continue
+            done.add((row["method_name"], int(row["num_GPUs"]), int(row["K"]),
+                      int(row["n_obs"]), int(row["n_dim"])))
+    return done
+
+
 def make_dataset(path: str, n_obs: int, n_dim: int, seed: int, kind: str) -> None:
     from .data.synth import make_data
     make_data(path, n_obs, n_dim, seed, kind=kind)
@@ -97,6 +115,8 @@ def build_parser(default_grid: str = "reference") -> argparse.ArgumentParser:
     ap.add_argument("--skip_unavailable", action="store_true",
                     help="skip GPU counts above what this node has (the CLI would reject them)")
     ap.add_argument("--dry_run", action="store_true", help="print the commands only")
+    ap.add_argument("--skip_done", action="store_true",
+                    help="skip configs that already have a successful row in --log_file")
     ap.add_argument("--timeout", type=float, default=0, help="per-run timeout in seconds")
     ap.add_argument("cli_extra", nargs="*", help="extra flags for the CLI (after --)")
     return ap
@@ -111,6 +131,9 @@ def main(argv: Optional[Sequence[str]] = None, default_grid: str = "reference") 
         import torch
         avail = torch.cuda.device_count() or 1
         runs = [r for r in runs if r.n_gpus <= avail]
+    if args.skip_done:
+        done = completed_runs(args.log_file)
+        runs = [r for r in runs if (r.method, r.n_gpus, r.k, r.n_obs, r.n_dim) not in done]
     t0 = time.time()
     current_data = None
     worst = 0

@@ -1,0 +1,176 @@
+"""Checkpoint / resume, fault injection, OOM-adaptive retry, deterministic update
+(the reference had only an OOM retry that clustered batches
+independently, and no checkpointing at all)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import tensorflow_distributed_clustering_amd as tdc
+from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs
+from tensorflow_distributed_clustering_amd.ops import deterministic_update
+from tensorflow_distributed_clustering_amd.ops import reference as ref
+from tensorflow_distributed_clustering_amd.utils import checkpoint as ck
+from tensorflow_distributed_clustering_amd.utils import faults
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(autouse=True)
+def _clean_faults(monkeypatch):
+    monkeypatch.delenv("TDC_FAULT", raising=False)
+    faults._FIRED.clear()
+    yield
+    faults._FIRED.clear()
+
+
+def test_checkpoint_roundtrip_no_pickle(tmp_path):
+    p = str(tmp_path / "c.npz")
+    c = np.random.default_rng(0).normal(size=(7, 3))
+    ck.save(p, ck.Checkpoint("distributedKMeans", 5, c, meta={"x": 1}, arrays={"counts": np.arange(7)}))
+    got = ck.load(p)
+    assert got.n_iter == 5 and got.method == "distributedKMeans" and got.meta["x"] == 1
+    np.testing.assert_array_equal(got.centers, c)
+    np.testing.assert_array_equal(got.arrays["counts"], np.arange(7))
+    with np.load(p, allow_pickle=False) as z:  # loadable without pickle
+        assert set(z.files) >= {"centers", "meta_json", "arr_counts"}
+
+
+@pytest.mark.parametrize("model", ["kmeans", "fcm"])
+def test_crash_then_resume_matches_uninterrupted(tmp_path, monkeypatch, model):
+    x = gaussian_blobs(4000, 3, 5, seed=3, dtype=torch.float64)
+    cls = tdc.KMeans if model == "kmeans" else tdc.FuzzyCMeans
+    base = tdc.ClusterConfig(n_clusters=5, max_iter=8, dtype="fp64", seed=2, fuzzifier=2.0)
+    full = cls(base).fit(x).result_
+    path = str(tmp_path / "run.npz")
+    cfg = base.replace(checkpoint_path=path, checkpoint_every=1)
+    monkeypatch.setenv("TDC_FAULT", "crash@3")
+    with pytest.raises(faults.InjectedFault):
+        cls(cfg).fit(x)
+    assert ck.load(path).n_iter == 3
+    monkeypatch.delenv("TDC_FAULT")
+    res = cls(cfg.replace(resume=True)).fit(x).result_
+    assert res.n_iter == 8
+    np.testing.assert_allclose(res.centers, full.centers, rtol=1e-12, atol=1e-12)
+    assert ck.load(path).n_iter == 8  # final checkpoint
+
+
+def test_resume_rejects_mismatched_checkpoint(tmp_path):
+    path = str(tmp_path / "run.npz")
+    ck.save(path, ck.Checkpoint("distributedKMeans", 2, np.zeros((4, 3))))
+    x = gaussian_blobs(500, 3, 5, seed=1, dtype=torch.float64)
+    with pytest.raises(ValueError):
+        tdc.KMeans(tdc.ClusterConfig(n_clusters=5, dtype="fp64", checkpoint_path=path,
+                                     resume=True)).fit(x)
+
+
+def test_minibatch_checkpoint_restores_counts(tmp_path, monkeypatch):
+    x = gaussian_blobs(20000, 2, 4, seed=5, dtype=torch.float64)
+    path = str(tmp_path / "mb.npz")
+    cfg = tdc.ClusterConfig(n_clusters=4, max_iter=20, dtype="fp64", batch_size=500, seed=1,
+                            checkpoint_path=path, checkpoint_every=5)
+    monkeypatch.setenv("TDC_FAULT", "crash@10")
+    with pytest.raises(faults.InjectedFault):
+        tdc.MiniBatchKMeans(cfg).fit(x)
+    saved = ck.load(path)
+    assert saved.n_iter == 10 and saved.arrays["counts"].sum() == 10 * 500
+    monkeypatch.delenv("TDC_FAULT")
+    mb = tdc.MiniBatchKMeans(cfg.replace(resume=True)).fit(x)
+    assert mb.result_.n_iter == 20
+    assert mb.result_.counts.sum() == 20 * 500
+
+
+def test_setup_oom_retries_streamed(monkeypatch, capsys):
+    x = gaussian_blobs(5000, 4, 6, seed=7, dtype=torch.float64)
+    cfg = tdc.ClusterConfig(n_clusters=6, max_iter=6, dtype="fp64", seed=4)
+    ref_run = tdc.KMeans(cfg).fit(x).result_
+    monkeypatch.setenv("TDC_FAULT", "oom@setup")
+    res = tdc.KMeans(cfg).fit(x).result_
+    assert res.streamed  # the retry streams the shard in halved chunks
+    assert "retrying streamed with chunk_rows=2500" in capsys.readouterr().out
+    np.testing.assert_allclose(res.centers, ref_run.centers, rtol=1e-12, atol=1e-12)
+
+
+def test_setup_oom_gives_up_after_retries(monkeypatch):
+    x = gaussian_blobs(500, 2, 3, seed=7, dtype=torch.float64)
+    monkeypatch.setenv("TDC_FAULT", "oom@setup")
+    # zero retries allowed -> the injected OOM surfaces
+    with pytest.raises(Exception) as ei:
+        tdc.KMeans(tdc.ClusterConfig(n_clusters=3, dtype="fp64", max_oom_retries=0)).fit(x)
+    assert faults.is_oom(ei.value)
+
+
+def test_deterministic_update_matches_reference():
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(3000, 7, generator=g, dtype=torch.float64)
+    lab = torch.randint(0, 9, (3000,), generator=g, dtype=torch.int32)
+    sums = torch.zeros(9, 7, dtype=torch.float64)
+    counts = torch.zeros(9, dtype=torch.float64)
+    deterministic_update(x, lab, sums, counts)
+    rs, rc = ref.cluster_sums(x, lab, 9, acc_dtype=torch.float64)
+    torch.testing.assert_close(sums, rs)
+    torch.testing.assert_close(counts, rc)
+
+
+def test_cli_checkpoint_resume(tmp_path):
+    data = tmp_path / "d.npz"
+    X = gaussian_blobs(3000, 3, 4, seed=9, dtype=torch.float64).numpy()
+    np.savez(data, X=X, Y=np.zeros(3000))
+    log = tmp_path / "log.csv"
+    ckp = tmp_path / "c.npz"
+    cen = tmp_path / "cent.csv"
+    cmd = [sys.executable, os.path.join(ROOT, "scripts", "distribuitedClustering.py"),
+           "--n_obs=3000", "--n_dim=3", "--K=4", "--n_GPUs=1", "--n_max_iters=6", "--seed=3",
+           f"--log_file={log}", "--method_name=distributedKMeans", f"--data_file={data}",
+           "--device=cpu", f"--checkpoint={ckp}", "--checkpoint_every=2", f"--centroids_out={cen}"]
+    env = dict(os.environ, TDC_FAULT="crash@4")
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=300)
+    assert "InjectedFault" in (r.stdout + r.stderr)
+    assert ck.load(str(ckp)).n_iter == 4
+    env.pop("TDC_FAULT")
+    r = subprocess.run(cmd + ["--resume"], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "resuming from" in r.stdout
+    rows = open(log).read().strip().splitlines()
+    assert rows[1].split(",")[6] == "InjectedFault" and rows[2].split(",")[-1] == "6"
+
+
+def _oom_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank), TDC_FAULT="oom@setup:1")
+    torch.set_num_threads(1)
+    import tensorflow_distributed_clustering_amd as tdc
+    from tensorflow_distributed_clustering_amd.parallel import dist as D
+    D._COMM = None
+    comm = D.init_comm("cpu")
+    s, e = comm.shard(4001)
+    x = gaussian_blobs(e - s, 3, 5, seed=2, row_offset=s, dtype=torch.float64)
+    cfg = tdc.ClusterConfig(n_clusters=5, max_iter=5, dtype="fp64", seed=1)
+    r = tdc.KMeans(cfg, comm).fit(x, n_global=4001, row_offset=s).result_
+    if rank == 0:
+        q.put((r.centers, r.streamed))
+    D.destroy_comm()
+
+
+def test_oom_on_one_rank_retries_on_all_ranks():
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_oom_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    centers, streamed = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert streamed  # rank 0 did not OOM itself but followed the collective retry
+    x = gaussian_blobs(4001, 3, 5, seed=2, dtype=torch.float64)
+    single = tdc.KMeans(tdc.ClusterConfig(n_clusters=5, max_iter=5, dtype="fp64", seed=1)).fit(x)
+    np.testing.assert_allclose(centers, single.result_.centers, rtol=1e-10, atol=1e-10)

@@ -98,3 +98,16 @@ def test_sweep_runs_cli_on_cpu(tmp_path):
     assert len(rows) == 3 and rows[0][0] == "method_name"
     assert {rows[1][0], rows[2][0]} == {"distributedKMeans", "distributedFuzzyCMeans"}
     assert all(float(r[rows[0].index("computation_time")]) > 0 for r in rows[1:])
+
+
+def test_sweep_skip_done(tmp_path):
+    log = tmp_path / "exec.csv"
+    log.write_text("method_name,seed,num_GPUs,K,n_obs,n_dim,setup_time,initialization_time,"
+                   "computation_time,n_iter\n"
+                   "distributedKMeans,1,1,3,1000,5,0.1,0.1,0.5,20\n"
+                   "distributedFuzzyCMeans,1,1,3,1000,5,InternalError,InternalError,InternalError,20\n")
+    assert sweep.completed_runs(str(log)) == {("distributedKMeans", 1, 3, 1000, 5)}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "new_experiment.py"),
+                        "--n_obs", "1000", "--K", "3", "--gpus", "1", "--dry_run", "--skip_done",
+                        "--log_file", str(log)], capture_output=True, text=True, timeout=120)
+    assert "distributedFuzzyCMeans" in r.stdout and "method_name=distributedKMeans" not in r.stdout
