@@ -139,6 +139,12 @@ def build_parser():
                         help="continue from --checkpoint if it exists")
     parser.add_argument("--hbm_budget_gb", type=float, default=0.0,
                         help="per-GPU memory budget for the stream planner (0: free HBM)")
+    parser.add_argument("--log_device_placement", action="store_true",
+                        help="print rank -> device / shard / kernel backend (the reference's "
+                             "tf.ConfigProto(log_device_placement=True))")
+    parser.add_argument("--plot_out", default=None,
+                        help="SVG scatter of the first 10k points of rank 0 with initial and "
+                             "final centers")
     parser.add_argument("--deterministic", action="store_true",
                         help="run-to-run bitwise reproducible centroid update")
     return parser
@@ -206,6 +212,17 @@ def run(args) -> int:
             model = MiniBatchKMeans(cfg, comm)
         model.fit(xt, n_global=n_global, row_offset=row_off)
         result = model.result_
+        if args.log_device_placement:
+            name = (torch.cuda.get_device_name(comm.device) if comm.device.type == "cuda"
+                    else "host")
+            print(f"[placement] rank {comm.rank}/{comm.world_size} local_rank {comm.local_rank} "
+                  f"device {comm.device} ({name}) rows [{row_off}, {row_off + x.shape[0]}) "
+                  f"backend {result.backend} dtype {dtype}", flush=True)
+        if args.plot_out and comm.is_root:
+            from .utils.plots import scatter_svg
+            scatter_svg(args.plot_out, x, None if result.labels is None else
+                        result.labels.cpu().numpy(), result.init_centers, result.centers,
+                        title=f"{args.method_name} K={args.K}")
     except Exception:
         exc_type, exc_value, exc_tb = sys.exc_info()
         traceback.print_exc()
