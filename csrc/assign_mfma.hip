@@ -44,6 +44,32 @@ int tdc_assign_mfma_bf16(const void* X, int64_t N, int64_t ldx, int DP, const vo
   // LDS-DMA ring, 4 waves x P x 32 points per workgroup, 64-centroid stages.
   // TDC_ASSIGN_RING=1 selects the first ring variant (kept for A/B timing).
   static const int ring = getenv("TDC_ASSIGN_RING") ? atoi(getenv("TDC_ASSIGN_RING")) : 2;
+  static const int abl = getenv("TDC_ASSIGN_ABL") ? atoi(getenv("TDC_ASSIGN_ABL")) : 0;
+  static const int r2cfg = getenv("TDC_RING2_CFG") ? atoi(getenv("TDC_RING2_CFG")) : 0;
+  if (DP == 128 && ring == 2 && r2cfg != 0) {  // schedule experiments: QT*10 + NST
+    dim3 grid((unsigned)((N + 255) / 256));
+#define TDC_R2(QTV, NSTV)                                                                          \
+  if (r2cfg == QTV * 10 + NSTV) {                                                                  \
+    if (Kp % (32 * QTV) != 0) return (int)hipErrorInvalidValue;                                    \
+    hipLaunchKernelGGL((assign_mfma_bf16_ring2_kernel<128, 2, NSTV, 4, QTV>), grid, dim3(256), 0,  \
+                       stream, x, N, ldx, c, cnorm, Kp / (32 * QTV), labels, mind);                \
+  }
+    TDC_R2(2, 4) TDC_R2(1, 4) TDC_R2(1, 5) TDC_R2(1, 6) TDC_R2(1, 3)
+#undef TDC_R2
+    TDC_CHECK_LAUNCH();
+    return 0;
+  }
+  if (DP == 128 && ring == 2 && abl != 0) {  // timing ablations (tools only; results invalid)
+    dim3 grid((unsigned)((N + 255) / 256));
+#define TDC_ABL(A)                                                                                \
+  if (abl == A)                                                                                   \
+    hipLaunchKernelGGL((assign_mfma_bf16_ring2_kernel<128, 2, 3, 4, 2, A>), grid, dim3(256), 0,   \
+                       stream, x, N, ldx, c, cnorm, ntiles, labels, mind);
+    TDC_ABL(1) TDC_ABL(2) TDC_ABL(4) TDC_ABL(7)
+#undef TDC_ABL
+    TDC_CHECK_LAUNCH();
+    return 0;
+  }
   switch (DP) {
 #define TDC_CASE(DPV, PV, NSTV)                                                              \
   case DPV: {                                                                                \

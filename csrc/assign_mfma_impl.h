@@ -1,6 +1,8 @@
 // Implementation of the bf16 MFMA distance + argmin kernel (see assign_mfma.hip for the
 // design notes).  Shared by the library build and the ablation tool.
 #pragma once
+#include <type_traits>
+
 #include "tdc_common.h"
 
 namespace tdc {
@@ -381,7 +383,8 @@ void assign_mfma_bf16_ring_kernel(const __bf16* __restrict__ X, int64_t N, int64
 //    that also forced a vmcnt(0) at their use.
 // A fragments are prefetched two k-steps ahead.
 // ------------------------------------------------------------------------------------
-template <int DP, int P, int NST, int WAVES, int QT>
+// ABL (timing ablations only): 1 = no refill, 2 = no barrier, 4 = no epilogue
+template <int DP, int P, int NST, int WAVES, int QT, int ABL = 0>
 __global__ __launch_bounds__(WAVES * 64, (WAVES % 4 == 0 ? (WAVES / 4 > 1 ? WAVES / 4 : 3) : 2))
 void assign_mfma_bf16_ring2_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
                                    const __bf16* __restrict__ Cm2, const float* __restrict__ cnorm,
@@ -465,26 +468,32 @@ void assign_mfma_bf16_ring2_kernel(const __bf16* __restrict__ X, int64_t N, int6
     bt[p] = 0;
   }
 
-  for (int t = 0; t < ntiles; ++t) {
-    const int slot = t % NST;
-    {
+  // LDS read addresses: lane part precomputed once; slot / phase / norm offsets are
+  // immediates (the ring loop is unrolled by NST so the slot is a compile-time constant)
+  unsigned aoff[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) aoff[kk] = lds0 + r * (DP * 2) + swz<DP>(r, h * (CPR / 2) + kk) * 16;
+  const unsigned noff = lds0 + TILE_B + 16 * h;
+
+  auto stage = [&](int t, auto slot_c) __attribute__((always_inline)) {
+    constexpr int slot = decltype(slot_c)::value;
+    if constexpr (!(ABL & 1)) {
       const int tn = t + NST - 1;
-      issue(tn < ntiles ? tn : ntiles - 1, (t + NST - 1) % NST);
+      issue(tn < ntiles ? tn : ntiles - 1, (slot + NST - 1) % NST);
     }
-    const unsigned sbase = lds0 + slot * STAGE_B;
 #pragma unroll
     for (int q = 0; q < QT; ++q) {
-      const int row = q * 32 + r;
-      const unsigned abase = sbase + row * (DP * 2);
       auto afrag = [&](int kk) __attribute__((always_inline)) {
         bf16x8 a;
-        asm volatile("ds_read_b128 %0, %1" : "=v"(a) : "v"(abase + swz<DP>(row, h * (CPR / 2) + kk) * 16));
+        asm volatile("ds_read_b128 %0, %1 offset:%2"
+                     : "=v"(a) : "v"(aoff[kk]), "i"(slot * STAGE_B + q * 32 * DP * 2));
         return a;
       };
       f32x4 n4[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        asm volatile("ds_read_b128 %0, %1" : "=v"(n4[j]) : "v"(sbase + TILE_B + (q * 32 + 8 * j + 4 * h) * 4));
+        asm volatile("ds_read_b128 %0, %1 offset:%2"
+                     : "=v"(n4[j]) : "v"(noff), "i"(slot * STAGE_B + (q * 32 + 8 * j) * 4));
       bf16x8 a0 = afrag(0);
       bf16x8 a1 = afrag(KS > 1 ? 1 : 0);
       f32x16 acc[P];
@@ -518,21 +527,38 @@ void assign_mfma_bf16_ring2_kernel(const __bf16* __restrict__ X, int64_t N, int6
         a0 = a1;
         a1 = a2;
       }
+      if constexpr (ABL & 4) {
 #pragma unroll
-      for (int p = 0; p < P; ++p) {
-        float m = INFINITY;
+        for (int p = 0; p < P; ++p)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float v = __uint_as_float((__float_as_uint(acc[p][i]) & ~EMB) | (unsigned)(q * 16 + i));
-          m = __builtin_fminf(m, v);
+          for (int i = 0; i < 16; ++i) asm volatile("" ::"v"(acc[p][i]));
+      } else {
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+          float m = INFINITY;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float v = __uint_as_float((__float_as_uint(acc[p][i]) & ~EMB) | (unsigned)(q * 16 + i));
+            m = __builtin_fminf(m, v);
+          }
+          const bool up = m < best[p];
+          best[p] = up ? m : best[p];
+          bt[p] = up ? t : bt[p];
         }
-        const bool up = m < best[p];
-        best[p] = up ? m : best[p];
-        bt[p] = up ? t : bt[p];
       }
     }
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * VPS) : "memory");  // stage t+1 landed
-    __builtin_amdgcn_s_barrier();  // ... for every wave's pieces
+    if constexpr (ABL & 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * VPS) : "memory");  // stage t+1 landed
+    if constexpr (!(ABL & 2)) __builtin_amdgcn_s_barrier();  // ... for every wave's pieces
+  };
+
+  for (int t0 = 0; t0 < ntiles; t0 += NST) {
+    stage(t0, std::integral_constant<int, 0>{});
+    if constexpr (NST > 1) if (t0 + 1 < ntiles) stage(t0 + 1, std::integral_constant<int, 1>{});
+    if constexpr (NST > 2) if (t0 + 2 < ntiles) stage(t0 + 2, std::integral_constant<int, 2 % NST>{});
+    if constexpr (NST > 3) if (t0 + 3 < ntiles) stage(t0 + 3, std::integral_constant<int, 3 % NST>{});
+    if constexpr (NST > 4) if (t0 + 4 < ntiles) stage(t0 + 4, std::integral_constant<int, 4 % NST>{});
+    if constexpr (NST > 5) if (t0 + 5 < ntiles) stage(t0 + 5, std::integral_constant<int, 5 % NST>{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 

@@ -117,7 +117,7 @@ def build_parser():
                         help="Unable to find data file !!!")
     # ---- extensions (all optional) ----
     parser.add_argument("--dtype", default="auto", choices=["auto", "fp64", "fp32", "bf16", "fp8"])
-    parser.add_argument("--init", default="kmeans++", choices=["kmeans++", "first_k", "random"])
+    parser.add_argument("--init", default="kmeans++", choices=["kmeans++", "kmeans||", "first_k", "random"])
     parser.add_argument("--fuzzifier", type=float, default=None,
                         help="FCM m (default: the data dimension, as the reference)")
     parser.add_argument("--empty_cluster", default="keep", choices=["keep", "nan", "zero", "reseed"])

@@ -14,7 +14,7 @@ from typing import Optional
 
 METHODS = ("distributedKMeans", "distributedFuzzyCMeans", "miniBatchKMeans")
 DTYPES = ("fp64", "fp32", "bf16", "fp8")
-INITS = ("random", "first_k", "kmeans++", "given")
+INITS = ("random", "first_k", "kmeans++", "kmeans||", "given")
 EMPTY_POLICIES = ("keep", "nan", "reseed", "zero")
 BACKENDS = ("auto", "hip", "torch")
 

@@ -5,6 +5,7 @@ Reference variants:
   (`scripts/distribuitedClustering.py:82,191`);
 * first-K rows ``X[0:K]`` (`:325`; the CSV-era revision, see SURVEY §2.6);
 * K random rows without replacement (`ckpt/Testing Images-checkpoint.ipynb:290-291`).
+* (new) k-means|| (Bahmani et al. 2012): O(5) data sweeps instead of K, for large K.
 
 Here every method is *world-size invariant*: the chosen global row indices depend only
 on ``seed`` and ``N``, and each rank contributes the rows it owns to one SUM all-reduce,
@@ -130,6 +131,115 @@ def init_kmeanspp(x_local, row_offset, n_global, k, comm: Comm, seed,
     return centers
 
 
+# ------------------------------------------------------------------ k-means|| (Bahmani 2012)
+def _hash_uniform(rows: torch.Tensor, seed: int, rnd: int) -> torch.Tensor:
+    """Counter-based U[0,1) per GLOBAL row index: the sampling decision of a row does not
+    depend on which rank owns it (world-size invariant)."""
+    from ..data.synth import _mix32
+    s = (int(seed) * 0x9E3779B1 + (rnd + 1) * 0x85EBCA6B) & 0xFFFFFFFF
+    h = _mix32((rows * 0x27D4EB2F + s) & 0xFFFFFFFF)
+    h2 = _mix32((h ^ 0x5BD1E995) & 0xFFFFFFFF)
+    return ((h >> 8).double() * (1.0 / (1 << 24)) + (h2 >> 8).double() * (1.0 / (1 << 48)))
+
+
+def _min_sqdist(x: torch.Tensor, c: torch.Tensor, chunk: int = 1 << 16):
+    """(min_j ||x_i - c_j||^2, argmin) over a candidate set via chunked GEMM (fp32/fp64)."""
+    wd = torch.float64 if (x.dtype == torch.float64 or x.device.type == "cpu") else torch.float32
+    cw = c.to(wd)
+    cc = (cw * cw).sum(1)[None, :]
+    md = torch.empty(x.shape[0], dtype=wd, device=x.device)
+    lab = torch.empty(x.shape[0], dtype=torch.int64, device=x.device)
+    step = max(1, min(chunk, (1 << 28) // max(1, c.shape[0])))
+    for s0 in range(0, x.shape[0], step):
+        xs = x[s0:s0 + step].to(wd)
+        d = torch.addmm(cc, xs, cw.t(), alpha=-2.0).add_((xs * xs).sum(1)[:, None])
+        m, a = d.min(1)
+        md[s0:s0 + step] = m.clamp_min_(0)
+        lab[s0:s0 + step] = a
+    return md, lab
+
+
+def _gather_varlen(comm: Comm, local: torch.Tensor) -> torch.Tensor:
+    """Concatenate every rank's 1-D int64 tensor (rank order), replicated."""
+    sizes = comm.all_gather_sizes(int(local.numel()))
+    total = int(sum(sizes))
+    out = torch.zeros(total, dtype=torch.int64, device=comm.device)
+    off = int(sum(sizes[: comm.rank]))
+    out[off:off + local.numel()] = local.to(comm.device)
+    comm.allreduce_(out)
+    return out
+
+
+def weighted_kmeanspp(c: torch.Tensor, w: torch.Tensor, k: int, seed: int,
+                      lloyd_iters: int = 10) -> torch.Tensor:
+    """k-means++ on a small weighted point set, then a few weighted Lloyd steps
+    (the recluster step of k-means||; Spark MLlib's LocalKMeans does the same)."""
+    rng = np.random.default_rng(seed)
+    m = c.shape[0]
+    c = c.double()
+    w = w.double()
+    trials = 2 + int(math.log(k))
+    centers = torch.empty(k, c.shape[1], dtype=torch.float64, device=c.device)
+    p0 = (w / w.sum()).cpu().numpy()
+    first = int(rng.choice(m, p=p0))
+    centers[0] = c[first]
+    closest = ((c - c[first]) ** 2).sum(1)
+    for j in range(1, k):
+        pot = (w * closest)
+        tot = float(pot.sum())
+        if tot <= 0:
+            cand = rng.integers(0, m, size=trials)
+        else:
+            cum = torch.cumsum(pot, 0).cpu().numpy()
+            cand = np.searchsorted(cum, rng.random(trials) * tot, side="right").clip(0, m - 1)
+        cd = torch.cdist(c, c[torch.as_tensor(cand, device=c.device)]) ** 2  # [m, T]
+        nd = torch.minimum(cd, closest[:, None])
+        best = int((w[:, None] * nd).sum(0).argmin())
+        centers[j] = c[int(cand[best])]
+        closest = nd[:, best]
+    for _ in range(lloyd_iters):
+        lab = torch.cdist(c, centers).argmin(1)
+        s = torch.zeros_like(centers).index_add_(0, lab, c * w[:, None])
+        n = torch.zeros(k, dtype=torch.float64, device=c.device).index_add_(0, lab, w)
+        nz = n > 0
+        centers[nz] = s[nz] / n[nz, None]
+    return centers
+
+
+def init_kmeans_parallel(x_local, row_offset, n_global, k, comm: Comm, seed,
+                         rounds: int = 5, oversample: float = 2.0):
+    """Scalable k-means++ ("k-means||"): ``rounds`` passes that each keep every point
+    with probability min(1, l d^2 / phi) (l = oversample*K), then weighted k-means++ on
+    the ~l*rounds candidates.  O(rounds) sweeps over the data instead of K, and each pass
+    is one chunked GEMM + one all-reduce -- the seeding that scales to K=65536."""
+    dev = x_local.device
+    n_local = x_local.shape[0]
+    rows = torch.arange(row_offset, row_offset + n_local, dtype=torch.int64, device=dev)
+    l = oversample * k
+    C = gather_global_rows(x_local, row_offset, floyd_sample(n_global, 1, seed), comm)
+    md, _ = _min_sqdist(x_local, C)
+    for rnd in range(rounds):
+        phi = comm.sum_scalar(float(md.double().sum()))
+        if phi <= 0:
+            break
+        u = _hash_uniform(rows, seed, rnd)
+        pick = rows[u < (l * md.double() / phi)]
+        idx = _gather_varlen(comm, pick)
+        if idx.numel() == 0:
+            continue
+        newc = gather_global_rows(x_local, row_offset, idx.tolist(), comm)
+        C = torch.cat([C, newc])
+        nd, _ = _min_sqdist(x_local, newc)
+        md = torch.minimum(md, nd)
+    if C.shape[0] <= k:
+        extra = floyd_sample(n_global, k, seed + 17)[: k - C.shape[0]]
+        return torch.cat([C, gather_global_rows(x_local, row_offset, extra, comm)])
+    _, lab = _min_sqdist(x_local, C)
+    w = torch.bincount(lab, minlength=C.shape[0]).double()
+    comm.allreduce_(w)
+    return weighted_kmeanspp(C, w, k, seed)
+
+
 def init_centers(method: str, x_local: torch.Tensor, row_offset: int, n_global: int, k: int,
                  comm: Comm, seed: int = 0, given: Optional[torch.Tensor] = None) -> torch.Tensor:
     """[K, D] float64 on the shard's device, identical on every rank."""
@@ -148,6 +258,8 @@ def init_centers(method: str, x_local: torch.Tensor, row_offset: int, n_global: 
         return init_first_k(x_local, row_offset, n_global, k, comm, seed)
     if method == "kmeans++":
         return init_kmeanspp(x_local, row_offset, n_global, k, comm, seed)
+    if method == "kmeans||":
+        return init_kmeans_parallel(x_local, row_offset, n_global, k, comm, seed)
     raise ValueError(f"unknown init {method!r}")
 
 
@@ -207,10 +319,11 @@ def init_centers_from_source(method: str, source, row_offset: int, n_global: int
         return gather_rows_from_source(source, row_offset, floyd_sample(n_global, k, seed), comm, d)
     if method == "first_k":
         return gather_rows_from_source(source, row_offset, range(k), comm, d)
-    if method == "kmeans++":
+    if method in ("kmeans++", "kmeans||"):
         m = min(n_global, max(50_000, 256 * k))
         sample = gather_rows_from_source(source, row_offset, floyd_sample(n_global, m, seed + 1),
                                          comm, d)
         from ..parallel.dist import local_comm
-        return init_kmeanspp(sample, 0, m, k, local_comm(sample.device), seed)
+        fn = init_kmeanspp if method == "kmeans++" else init_kmeans_parallel
+        return fn(sample, 0, m, k, local_comm(sample.device), seed)
     raise ValueError(f"unknown init {method!r}")

@@ -66,6 +66,13 @@ def test_kmeans_dp_equals_single(world, init):
     assert itw == it1
 
 
+def test_kmeans_parallel_init_world_invariant():
+    c1, l1, in1, it1, i1 = run_world(1, init="kmeans||", k=8)
+    c2, l2, in2, it2, i2 = run_world(2, init="kmeans||", k=8)
+    np.testing.assert_allclose(i2, i1, rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(c2, c1, rtol=1e-10, atol=1e-10)
+
+
 def test_fcm_dp_equals_single():
     c1, l1, *_ = run_world(1, method="fcm", init="first_k", d=4, k=3)
     c4, l4, *_ = run_world(4, method="fcm", init="first_k", d=4, k=3)

@@ -118,3 +118,13 @@ def test_config_validation():
         tdc.ClusterConfig(n_clusters=3, dtype="fp16")
     with pytest.raises(ValueError):
         tdc.ClusterConfig(n_clusters=3, init="bogus")
+
+
+def test_kmeans_parallel_init_quality():
+    from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs as gb
+    x = gb(30000, 3, 20, seed=4, dtype=torch.float64)
+    res = {}
+    for init in ("kmeans||", "random"):
+        res[init] = tdc.KMeans(tdc.ClusterConfig(n_clusters=20, max_iter=0, dtype="fp64",
+                                                 init=init, seed=2)).fit(x).result_.inertia
+    assert res["kmeans||"] < 0.6 * res["random"]
