@@ -65,7 +65,7 @@ int tdc_assign_mfma_bf16(const void* X, int64_t N, int64_t ldx, int DP, const vo
   if (abl == A)                                                                                   \
     hipLaunchKernelGGL((assign_mfma_bf16_ring2_kernel<128, 2, 3, 4, 2, A>), grid, dim3(256), 0,   \
                        stream, x, N, ldx, c, cnorm, ntiles, labels, mind);
-    TDC_ABL(1) TDC_ABL(2) TDC_ABL(4) TDC_ABL(7)
+    TDC_ABL(1) TDC_ABL(2) TDC_ABL(4) TDC_ABL(7) TDC_ABL(8)
 #undef TDC_ABL
     TDC_CHECK_LAUNCH();
     return 0;

@@ -383,7 +383,8 @@ void assign_mfma_bf16_ring_kernel(const __bf16* __restrict__ X, int64_t N, int64
 //    that also forced a vmcnt(0) at their use.
 // A fragments are prefetched two k-steps ahead.
 // ------------------------------------------------------------------------------------
-// ABL (timing ablations only): 1 = no refill, 2 = no barrier, 4 = no epilogue
+// ABL (timing ablations only): 1 = no refill, 2 = no barrier, 4 = no epilogue,
+// 8 = let the scheduler move work across the MFMA steps (valid results)
 template <int DP, int P, int NST, int WAVES, int QT, int ABL = 0>
 __global__ __launch_bounds__(WAVES * 64, (WAVES % 4 == 0 ? (WAVES / 4 > 1 ? WAVES / 4 : 3) : 2))
 void assign_mfma_bf16_ring2_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
@@ -523,7 +524,7 @@ void assign_mfma_bf16_ring2_kernel(const __bf16* __restrict__ X, int64_t N, int6
           for (int p = 0; p < P; ++p)
             acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq[p][kk], acc[p], 0, 0, 0);
         }
-        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!(ABL & 8)) __builtin_amdgcn_sched_barrier(0);
         a0 = a1;
         a1 = a2;
       }
