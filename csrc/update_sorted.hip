@@ -167,6 +167,31 @@ template <> struct RowLoad<double, 2> {
     a[0] += t.x; a[1] += t.y;
   }
 };
+// split load / accumulate (so a batch of row loads can be in flight before any add)
+template <typename XT, int VEC> struct RowRaw;
+template <> struct RowRaw<__bf16, 8> {
+  typedef uint4 raw_t;
+  __device__ static raw_t load(const __bf16* p) { return *reinterpret_cast<const uint4*>(p); }
+  __device__ static void add(const raw_t& t, float (&a)[8]) {
+    a[0] += __uint_as_float(t.x << 16); a[1] += __uint_as_float(t.x & 0xffff0000u);
+    a[2] += __uint_as_float(t.y << 16); a[3] += __uint_as_float(t.y & 0xffff0000u);
+    a[4] += __uint_as_float(t.z << 16); a[5] += __uint_as_float(t.z & 0xffff0000u);
+    a[6] += __uint_as_float(t.w << 16); a[7] += __uint_as_float(t.w & 0xffff0000u);
+  }
+};
+template <> struct RowRaw<float, 4> {
+  typedef float4 raw_t;
+  __device__ static raw_t load(const float* p) { return *reinterpret_cast<const float4*>(p); }
+  __device__ static void add(const raw_t& t, float (&a)[4]) {
+    a[0] += t.x; a[1] += t.y; a[2] += t.z; a[3] += t.w;
+  }
+};
+template <> struct RowRaw<double, 2> {
+  typedef double2 raw_t;
+  __device__ static raw_t load(const double* p) { return *reinterpret_cast<const double2*>(p); }
+  __device__ static void add(const raw_t& t, double (&a)[2]) { a[0] += t.x; a[1] += t.y; }
+};
+
 template <typename XT> struct RowLoad1 {
   typedef typename std::conditional<sizeof(XT) == 8, double, float>::type acc_t;
   __device__ static void add(const XT* p, acc_t (&a)[1]) { a[0] += (acc_t)p[0]; }
@@ -182,7 +207,7 @@ __global__ __launch_bounds__(256) void segsum_kernel(const XT* __restrict__ X, i
                                                      int64_t rows_per_wave) {
   typedef typename RowLoad1<XT>::acc_t AT;  // fp64 data -> fp64 partials, else fp32
   constexpr int G = 64 / TPR;
-  constexpr int U = 4;  // rows per group in flight
+  constexpr int U = 8;  // rows per group in flight
   const int lane = threadIdx.x & 63;
   const int g = lane / TPR, t = lane % TPR;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -212,32 +237,72 @@ __global__ __launch_bounds__(256) void segsum_kernel(const XT* __restrict__ X, i
     _Pragma("unroll") for (int e = 0; e < VEC; ++e) acc[e] = 0;                       \
   } while (0)
     int64_t j = a + g;
-    // fast path: U rows of this group all inside the current segment
-    while (j < b) {
-      if (j + (U - 1) * G < min(b, kend)) {
-        int32_t idx[U];
+    if constexpr (VEC > 1) {
+      // fast path, software pipelined: the permutation entries of batch i+1 are loaded
+      // while the U row gathers of batch i are in flight (one round trip per batch
+      // instead of two)
+      typedef typename RowRaw<XT, VEC>::raw_t raw_t;
+      int32_t nidx[U];
+      bool nfast = j + (U - 1) * G < min(b, kend);
+      if (nfast) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) idx[u] = perm[j + u * G];
-        if (colok) {
+        for (int u = 0; u < U; ++u) nidx[u] = perm[j + u * G];
+      }
+      while (j < b) {
+        if (nfast) {
+          raw_t xv[U];
+          if (colok) {
 #pragma unroll
-          for (int u = 0; u < U; ++u) {
-            if constexpr (VEC == 1) RowLoad1<XT>::add(X + (int64_t)idx[u] * ldx + col, acc);
-            else RowLoad<XT, VEC>::add(X + (int64_t)idx[u] * ldx + col, acc);
+            for (int u = 0; u < U; ++u) xv[u] = RowRaw<XT, VEC>::load(X + (int64_t)nidx[u] * ldx + col);
+          }
+          j += U * G;
+          nfast = j + (U - 1) * G < min(b, kend);
+          if (nfast) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) nidx[u] = perm[j + u * G];
+          }
+          if (colok) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) RowRaw<XT, VEC>::add(xv[u], acc);
+          }
+        } else {
+          while (j >= kend) {  // crossed into a later segment
+            TDC_FLUSH(k);
+            ++k;
+            kend = offsets[k + 1];
+          }
+          const int32_t idx = perm[j];
+          if (colok) RowLoad<XT, VEC>::add(X + (int64_t)idx * ldx + col, acc);
+          j += G;
+          nfast = j + (U - 1) * G < min(b, kend);
+          if (nfast) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) nidx[u] = perm[j + u * G];
           }
         }
-        j += U * G;
-      } else {
-        while (j >= kend) {  // crossed into a later segment
-          TDC_FLUSH(k);
-          ++k;
-          kend = offsets[k + 1];
+      }
+    } else {
+      // fast path: U rows of this group all inside the current segment
+      while (j < b) {
+        if (j + (U - 1) * G < min(b, kend)) {
+          int32_t idx[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) idx[u] = perm[j + u * G];
+          if (colok) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) RowLoad1<XT>::add(X + (int64_t)idx[u] * ldx + col, acc);
+          }
+          j += U * G;
+        } else {
+          while (j >= kend) {
+            TDC_FLUSH(k);
+            ++k;
+            kend = offsets[k + 1];
+          }
+          const int32_t idx = perm[j];
+          if (colok) RowLoad1<XT>::add(X + (int64_t)idx * ldx + col, acc);
+          j += G;
         }
-        const int32_t idx = perm[j];
-        if (colok) {
-          if constexpr (VEC == 1) RowLoad1<XT>::add(X + (int64_t)idx * ldx + col, acc);
-          else RowLoad<XT, VEC>::add(X + (int64_t)idx * ldx + col, acc);
-        }
-        j += G;
       }
     }
     TDC_FLUSH(k);
