@@ -8,14 +8,17 @@
 //                 atomic per non-empty bin per block)
 //   2. scan     : exclusive prefix sum -> segment offsets; counts also added (acc dtype)
 //                 straight into the all-reduce buffer
-//   3. scatter  : counting-sort the point indices by label (block-aggregated cursor
-//                 reservation: one returning global atomic per bin per block)
+//   3. scatter  : counting-sort the point indices by label: one pass per block over its
+//                 whole range (LDS histogram, one returning atomic per bin to reserve the
+//                 block's sub-range, LDS cursors); K > 16384: global cursor atomics
 //   4. segsum   : each wave walks a contiguous range of the sorted index, gathers whole
 //                 rows (16 B per lane, a row per 16/32/64 lanes), accumulates in fp32
 //                 registers and flushes with global atomics only at segment boundaries
 //                 (~1-3 flushes per wave instead of one atomic per element).
 //
 // X is read exactly once (as whole-row gathers); labels twice; the permutation once.
+#include <algorithm>
+
 #include "tdc_common.h"
 #include "kernels.h"
 
@@ -139,6 +142,54 @@ __global__ __launch_bounds__(256) void scatter_kernel(const int32_t* __restrict_
       }
     }
     if (agg) __syncthreads();
+  }
+}
+
+// ---- one-pass block scatter for K <= LDS_HIST_MAX_K ----
+// Each block takes a contiguous label range: LDS histogram of the range, ONE returning
+// global atomic per non-empty bin to reserve the block's sub-range of that segment, then
+// the scatter with LDS cursors.  (The per-4096-label passes of scatter_kernel reserved
+// once per bin per pass: ~5x more global atomics at N=10M, K=1024.)
+__global__ __launch_bounds__(256) void bscatter_kernel(const int32_t* __restrict__ labels, int64_t N,
+                                                       int K, int* __restrict__ cursor,
+                                                       int32_t* __restrict__ perm, int64_t per_block) {
+  extern __shared__ int s_mem[];
+  int* s_cnt = s_mem;
+  int* s_cur = s_mem + K;
+  const int tid = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * per_block;
+  const int64_t r1 = min(N, r0 + per_block);
+  for (int k = tid; k < K; k += 256) s_cnt[k] = 0;
+  __syncthreads();
+  int64_t i = r0 + tid;
+  for (; i + 3 * 256 < r1; i += 4 * 256) {
+    const int a0 = labels[i], a1 = labels[i + 256], a2 = labels[i + 512], a3 = labels[i + 768];
+    if ((unsigned)a0 < (unsigned)K) atomicAdd(s_cnt + a0, 1);
+    if ((unsigned)a1 < (unsigned)K) atomicAdd(s_cnt + a1, 1);
+    if ((unsigned)a2 < (unsigned)K) atomicAdd(s_cnt + a2, 1);
+    if ((unsigned)a3 < (unsigned)K) atomicAdd(s_cnt + a3, 1);
+  }
+  for (; i < r1; i += 256) {
+    const int a0 = labels[i];
+    if ((unsigned)a0 < (unsigned)K) atomicAdd(s_cnt + a0, 1);
+  }
+  __syncthreads();
+  for (int k = tid; k < K; k += 256) {
+    const int c = s_cnt[k];
+    s_cur[k] = c ? atomicAdd(cursor + k, c) : 0;
+  }
+  __syncthreads();
+  i = r0 + tid;
+  for (; i + 3 * 256 < r1; i += 4 * 256) {
+    const int a0 = labels[i], a1 = labels[i + 256], a2 = labels[i + 512], a3 = labels[i + 768];
+    if ((unsigned)a0 < (unsigned)K) perm[atomicAdd(s_cur + a0, 1)] = (int32_t)i;
+    if ((unsigned)a1 < (unsigned)K) perm[atomicAdd(s_cur + a1, 1)] = (int32_t)(i + 256);
+    if ((unsigned)a2 < (unsigned)K) perm[atomicAdd(s_cur + a2, 1)] = (int32_t)(i + 512);
+    if ((unsigned)a3 < (unsigned)K) perm[atomicAdd(s_cur + a3, 1)] = (int32_t)(i + 768);
+  }
+  for (; i < r1; i += 256) {
+    const int a0 = labels[i];
+    if ((unsigned)a0 < (unsigned)K) perm[atomicAdd(s_cur + a0, 1)] = (int32_t)i;
   }
 }
 
@@ -389,13 +440,20 @@ int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int6
     hipLaunchKernelGGL(scan_kernel<float>, dim3(1), dim3(1024), 0, s, cnt, K, offsets, cursor,
                        (float*)counts);
   TDC_CHECK_LAUNCH();
-  {
+  if (K <= LDS_HIST_MAX_K) {
+    int64_t blocks = (int64_t)num_cus * 2;
+    int64_t per = (N + blocks - 1) / blocks;
+    if (per < 4096) per = 4096;
+    blocks = (N + per - 1) / per;
+    hipLaunchKernelGGL(bscatter_kernel, dim3((unsigned)blocks), dim3(256), 2 * sizeof(int) * (size_t)K,
+                       s, labels, N, K, cursor, perm, per);
+    TDC_CHECK_LAUNCH();
+  } else {
     int64_t blocks = (int64_t)num_cus * 4;
     int64_t per = (N + blocks - 1) / blocks;
     per = ((per + 4095) / 4096) * 4096;
     blocks = (N + per - 1) / per;
-    const size_t lds = K <= 4096 ? 2 * sizeof(int) * (size_t)K : 0;
-    hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)blocks), dim3(256), lds, s, labels, N, K,
+    hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)blocks), dim3(256), 0, s, labels, N, K,
                        cursor, perm, per);
     TDC_CHECK_LAUNCH();
   }

@@ -97,7 +97,8 @@ def test_update_lds(gpu, xdt, n, d, k):
 
 @pytest.mark.parametrize("xdt", [torch.bfloat16, torch.float32, torch.float64])
 @pytest.mark.parametrize("n,d,k", [(10000, 5, 3), (50000, 128, 1024), (5000, 33, 70),
-                                   (3000, 300, 40), (20000, 64, 5000), (4000, 768, 20000)])
+                                   (3000, 300, 40), (20000, 64, 5000), (4000, 768, 20000),
+                                   (300000, 16, 16384), (777, 8, 4)])
 def test_update_sorted(gpu, xdt, n, d, k):
     from tensorflow_distributed_clustering_amd import _native
     ops = _native.require()
