@@ -51,6 +51,8 @@ def parse(argv=None):
                          "dp100m (N=100M total), minibatch1b (mini-batch N=1B D=64 K=4096), "
                          "embed50m_fp8 (N=50M D=768 K=65536, fp8 block-scaled MFMA)")
     ap.add_argument("--batch-size", type=int, default=0, help="mini-batch rows per rank")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step from a captured HIP graph (1 GPU; RCCL capture for N>1)")
     ap.add_argument("--profile-steps", action="store_true",
                     help="print a per-phase breakdown after the timed region")
     a = ap.parse_args(argv)
@@ -100,6 +102,8 @@ def main(argv=None):
     else:
         eng = LloydEngine(x, cfg, comm, n_global, s)
         points_per_step = n_global
+        if a.graph and dev.type == "cuda":
+            eng.capture(include_collectives=world > 1)
 
     for _ in range(a.warmup):
         eng.step()

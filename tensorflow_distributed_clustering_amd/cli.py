@@ -145,6 +145,8 @@ def build_parser():
     parser.add_argument("--plot_out", default=None,
                         help="SVG scatter of the first 10k points of rank 0 with initial and "
                              "final centers")
+    parser.add_argument("--graph", action="store_true",
+                        help="replay each iteration from a captured HIP graph (1 GPU)")
     parser.add_argument("--deterministic", action="store_true",
                         help="run-to-run bitwise reproducible centroid update")
     return parser
@@ -201,7 +203,8 @@ def run(args) -> int:
                             chunk_rows=args.chunk_rows, batch_size=args.batch_size,
                             checkpoint_path=args.checkpoint or "",
                             checkpoint_every=args.checkpoint_every, resume=args.resume,
-                            hbm_budget_gb=args.hbm_budget_gb, deterministic=args.deterministic)
+                            hbm_budget_gb=args.hbm_budget_gb, deterministic=args.deterministic,
+                            graph=args.graph)
         xt = torch.from_numpy(np.asarray(x))
         if args.method_name == "distributedKMeans":
             model = KMeans(cfg, comm)

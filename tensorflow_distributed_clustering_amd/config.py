@@ -62,6 +62,7 @@ class ClusterConfig:
     checkpoint_every: int = 0   # iterations between checkpoints (0: final only)
     resume: bool = False        # continue from checkpoint_path if it exists
     max_oom_retries: int = 4    # setup OOM -> halve the streamed chunk and retry
+    graph: bool = False         # replay each Lloyd step from a captured hipGraph
 
     def __post_init__(self):
         if self.n_clusters <= 0:

@@ -146,6 +146,14 @@ class LloydEngine:
         return self.source.chunks(self.chunk_rows)
 
     def step(self):
+        g = getattr(self, "_graph", None)
+        if g is not None:
+            g.replay()
+            self.n_iter += 1
+            return
+        self._eager_step()
+
+    def _eager_step(self):
         self.buf.zero_()
         if not self.streamed:
             self.local.step(self.C, self.labels, None, self.sums, self.counts)
@@ -161,6 +169,41 @@ class LloydEngine:
         if self.cfg.empty_cluster == "reseed":
             self._reseed()
         self.n_iter += 1
+
+    # ------------------------------------------------------------ HIP graph replay
+    def graphable(self) -> bool:
+        """A step is capturable when it is device-only: resident shard (streamed chunks
+        loop over host work), no host-side reseed, a CUDA device.  Collectives are
+        captured only on request (RCCL graph capture), so by default world_size == 1."""
+        return (self.device.type == "cuda" and not self.streamed
+                and self.cfg.empty_cluster != "reseed")
+
+    def capture(self, include_collectives: bool = False):
+        """Capture one step into a hipGraph (torch.cuda.CUDAGraph); ``step()`` replays it.
+
+        The step is launch-bound for small N (6-8 kernels + an all-reduce per iteration);
+        replay removes the per-launch host cost.  Warm-up runs on a side stream first, as
+        graph capture requires."""
+        if not self.graphable():
+            raise RuntimeError("this engine configuration cannot be captured")
+        if self.comm.world_size > 1 and not include_collectives:
+            raise RuntimeError("capture with world_size > 1 needs include_collectives=True")
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        snapshot = (self.C.clone(), self.n_iter)
+        with torch.cuda.stream(s):
+            self._eager_step()          # warm-up (allocations, kernel attributes, RCCL comms)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self.C.copy_(snapshot[0])
+        self.local.prepare(self.C)
+        self.n_iter = snapshot[1]
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._eager_step()
+        # capture does not execute: restore the iteration count, keep C untouched
+        self.n_iter = snapshot[1]
+        self._graph = g
+        return self
 
     def _reseed(self):
         empty = torch.nonzero(self.counts == 0).flatten().cpu().tolist()
@@ -312,6 +355,8 @@ class KMeans:
         eng = self._build_engine(first, x_local, dev, comm, n_global, row_offset, n_local,
                                  init_centers_, start_iter)
         del first
+        if cfg.graph and eng.graphable() and comm.world_size == 1:
+            eng.capture()
         sync(dev)
         setup_time = time.perf_counter() - t_setup0
 

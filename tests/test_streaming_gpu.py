@@ -57,3 +57,14 @@ def test_minibatch_gpu_bf16(gpu):
                                         init="kmeans++"), device=gpu).fit(x)
     assert mb.result_.backend == "hip_bf16_mfma"
     assert mb.result_.inertia <= 1.10 * full.result_.inertia
+
+
+@pytest.mark.parametrize("dtype,d,k", [("bf16", 128, 256), ("fp64", 5, 3), ("fp8", 256, 96)])
+def test_graph_replay_matches_eager(gpu, dtype, d, k):
+    x = gaussian_blobs(100_000, d, k, seed=2, dtype=torch.float32, device=gpu)
+    cfg = tdc.ClusterConfig(n_clusters=k, max_iter=7, dtype=dtype, seed=4)
+    eager = tdc.KMeans(cfg, device=gpu).fit(x).result_
+    graph = tdc.KMeans(cfg.replace(graph=True), device=gpu).fit(x).result_
+    assert graph.n_iter == eager.n_iter == 7
+    np.testing.assert_allclose(graph.centers, eager.centers, rtol=1e-5, atol=1e-5)
+    assert (graph.labels == eager.labels).float().mean().item() > 0.999
