@@ -120,7 +120,8 @@ def build_parser():
     parser.add_argument("--init", default="kmeans++", choices=["kmeans++", "kmeans||", "first_k", "random"])
     parser.add_argument("--fuzzifier", type=float, default=None,
                         help="FCM m (default: the data dimension, as the reference)")
-    parser.add_argument("--empty_cluster", default="keep", choices=["keep", "nan", "zero", "reseed"])
+    parser.add_argument("--empty_cluster", default="keep",
+                        choices=["keep", "nan", "nan_any", "zero", "reseed"])
     parser.add_argument("--tol", type=float, default=0.0)
     parser.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
     parser.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
@@ -196,7 +197,7 @@ def run(args) -> int:
                   file=sys.stderr)
         dtype = resolve_dtype(args.dtype, args.K, d)
         init = "first_k" if args.compat else args.init
-        empty = "nan" if args.compat else args.empty_cluster
+        empty = "nan_any" if args.compat else args.empty_cluster
         cfg = ClusterConfig(n_clusters=args.K, max_iter=args.n_max_iters, tol=args.tol,
                             dtype=dtype, init=init, seed=args.seed, fuzzifier=args.fuzzifier,
                             empty_cluster=empty, backend=args.backend,

@@ -15,7 +15,7 @@ from typing import Optional
 METHODS = ("distributedKMeans", "distributedFuzzyCMeans", "miniBatchKMeans")
 DTYPES = ("fp64", "fp32", "bf16", "fp8")
 INITS = ("random", "first_k", "kmeans++", "kmeans||", "given")
-EMPTY_POLICIES = ("keep", "nan", "reseed", "zero")
+EMPTY_POLICIES = ("keep", "nan", "nan_any", "reseed", "zero")
 BACKENDS = ("auto", "hip", "torch")
 
 
@@ -33,7 +33,9 @@ class ClusterConfig:
     fuzzifier       FCM m. ``None`` = compat value D (`:121,129`).
     fcm_nan_to_zero compat: membership NaN (point on a centroid) -> 0 (`:125-126`);
                     False gives the correct one-hot membership.
-    empty_cluster   'keep' (default) | 'nan' (reference) | 'reseed' | 'zero'
+    empty_cluster   'keep' (default) | 'nan' (globally empty -> NaN, the segment-sum
+                    notebook) | 'nan_any' (empty on ANY rank -> NaN, the script's
+                    reduce_mean poisoning) | 'reseed' | 'zero'
     backend         'hip' native kernels, 'torch' reference ops, 'auto'
     deterministic   ordered per-block reduction instead of float atomics
     chunk_rows      rows per streamed chunk (0 = whole shard resident)

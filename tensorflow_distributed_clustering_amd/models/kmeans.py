@@ -112,9 +112,15 @@ class LloydEngine:
         self._init_given = init_centers_
         self.C = torch.zeros(k, self.d, dtype=self.local.c_dtype, device=dev)
         acc = acc_dtype_for(cfg.dtype, k, self.d)
-        self.buf = torch.zeros(k * self.d + k, dtype=acc, device=dev)
+        # 'nan_any' (script compat): K extra "empty on this rank" flags ride in the same
+        # all-reduce; a cluster empty on ANY rank becomes NaN everywhere, like the
+        # reference's per-GPU reduce_mean of an empty gather (`distribuitedClustering.py:240,248`)
+        self.nan_any = cfg.empty_cluster == "nan_any"
+        extra = k if self.nan_any else 0
+        self.buf = torch.zeros(k * self.d + k + extra, dtype=acc, device=dev)
         self.sums = self.buf[: k * self.d].view(k, self.d)
-        self.counts = self.buf[k * self.d:]
+        self.counts = self.buf[k * self.d: k * self.d + k]
+        self.empty_flags = self.buf[k * self.d + k:] if self.nan_any else None
         self.labels = torch.zeros(self.n_local, dtype=torch.int32, device=dev)
         mdt = torch.float64 if self.local.c_dtype == torch.float64 else torch.float32
         self.mind = torch.zeros(self.n_local, dtype=mdt, device=dev) if cfg.compute_inertia else None
@@ -162,7 +168,11 @@ class LloydEngine:
                 s = start - self.source.row_offset  # chunk starts are source-global
                 self.local.bind(chunk).step(self.C, self.labels[s:s + chunk.shape[0]], None,
                                             self.sums, self.counts)
+        if self.nan_any:
+            self.empty_flags.copy_((self.counts == 0).to(self.buf.dtype))
         self.comm.allreduce_bucketed_(self.buf, self.bucket_bytes)
+        if self.nan_any:
+            self.counts.masked_fill_(self.empty_flags > 0, 0)
         if self.shift is not None:
             self.shift.zero_()
         self.local.finalize(self.sums, self.counts, self.C, self.shift)

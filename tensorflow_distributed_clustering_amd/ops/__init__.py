@@ -29,7 +29,7 @@ import torch
 from .. import _native
 from . import reference as ref
 
-POLICY_CODES = {"keep": 0, "reseed": 0, "nan": 1, "zero": 2}
+POLICY_CODES = {"keep": 0, "reseed": 0, "nan": 1, "nan_any": 1, "zero": 2}
 TORCH_DTYPES = {"fp64": torch.float64, "fp32": torch.float32, "bf16": torch.bfloat16,
                 "fp8": torch.bfloat16}
 MFMA_DIMS = (32, 64, 128, 256)

@@ -84,7 +84,7 @@ def finalize(sums: torch.Tensor, counts: torch.Tensor, old: torch.Tensor,
             new[empty] = old[empty].to(new.dtype)
         elif empty_cluster == "zero":
             new[empty] = 0
-        else:  # 'nan': the reference's 0/0 (`distribuitedClustering.py:262`)
+        else:  # 'nan' / 'nan_any': the reference's 0/0 (`distribuitedClustering.py:262`)
             new[empty] = float("nan")
     return new.to(old.dtype)
 

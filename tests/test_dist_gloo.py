@@ -85,3 +85,45 @@ def test_dp_tolerance_stop_consistent():
     c2, _, _, it2, _ = run_world(2, iters=200, extra={"tol": 1e-10})
     assert it1 == it2 and it1 < 200
     np.testing.assert_allclose(c2, c1, rtol=1e-12, atol=1e-12)
+
+
+def _split_worker(rank, world, port, policy, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    import tensorflow_distributed_clustering_amd as tdc
+    from tensorflow_distributed_clustering_amd.parallel import dist as D
+    D._COMM = None
+    comm = D.init_comm("cpu")
+    # rank 0 owns only points near (0,0), rank 1 only points near (10,10)
+    g = torch.Generator().manual_seed(rank)
+    x = torch.randn(500, 2, generator=g, dtype=torch.float64) * 0.1 + 10.0 * rank
+    cfg = tdc.ClusterConfig(n_clusters=2, max_iter=1, dtype="fp64", empty_cluster=policy)
+    r = tdc.KMeans(cfg, comm).fit(x, init_centers_=np.array([[0.0, 0.0], [10.0, 10.0]]),
+                                  n_global=1000, row_offset=500 * rank).result_
+    if rank == 0:
+        q.put(r.centers)
+    D.destroy_comm()
+
+
+def _run_split(policy):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_split_worker, args=(r, 2, port, policy, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return out
+
+
+def test_nan_any_poisons_cluster_empty_on_one_rank():
+    # each cluster is empty on one of the two ranks: the script's per-GPU reduce_mean
+    # poisons both centroids ('nan_any'); the globally-empty rule ('nan') does not
+    assert np.isnan(_run_split("nan_any")).all()
+    c = _run_split("nan")
+    assert not np.isnan(c).any()
+    np.testing.assert_allclose(c, [[0, 0], [10, 10]], atol=0.05)
