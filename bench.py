@@ -22,7 +22,8 @@ import os
 import sys
 import time
 
-BASELINE_POINTS_PER_SEC = 177.7e6
+BASELINE_POINTS_PER_SEC = 177.7e6       # K-Means, scripts/executions_log.csv:320
+BASELINE_FCM_POINTS_PER_SEC = 325.8e6   # FCM, scripts/executions_log.csv:321
 
 # BASELINE.json configs (the default is the headline metric/config)
 PRESETS = {
@@ -30,6 +31,11 @@ PRESETS = {
     "dp100m": dict(n_per_gpu=100_000_000, dim=128, k=1024, scaling="strong", mode="lloyd"),
     "minibatch1b": dict(n_per_gpu=1_000_000_000, dim=64, k=4096, scaling="strong",
                         mode="minibatch", batch_size=1 << 20),
+    # the reference's published configs (scripts/executions_log.csv): N=25M, D=5, fp64
+    "ref25m_kmeans": dict(n_per_gpu=25_000_000, dim=5, k=3, scaling="strong", mode="lloyd",
+                          dtype="fp64"),
+    "ref25m_fcm": dict(n_per_gpu=25_000_000, dim=5, k=3, scaling="strong", mode="lloyd",
+                       dtype="fp64", method="fcm"),
     "embed50m_fp8": dict(n_per_gpu=50_000_000, dim=768, k=65536, scaling="strong", mode="lloyd",
                          dtype="fp8"),
 }
@@ -49,8 +55,11 @@ def parse(argv=None):
     ap.add_argument("--preset", default="headline", choices=sorted(PRESETS),
                     help="BASELINE config: headline (N=10M/GPU D=128 K=1024, default), "
                          "dp100m (N=100M total), minibatch1b (mini-batch N=1B D=64 K=4096), "
-                         "embed50m_fp8 (N=50M D=768 K=65536, fp8 block-scaled MFMA)")
+                         "embed50m_fp8 (N=50M D=768 K=65536, fp8 block-scaled MFMA), "
+                         "ref25m_kmeans / ref25m_fcm (the reference's own N=25M D=5 K=3 fp64)")
     ap.add_argument("--batch-size", type=int, default=0, help="mini-batch rows per rank")
+    ap.add_argument("--method", default="kmeans", choices=["kmeans", "fcm"],
+                    help="fcm: distributed Fuzzy C-Means step (fuzzifier m = D, as the reference)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step from a captured HIP graph (1 GPU; RCCL capture for N>1)")
     ap.add_argument("--profile-steps", action="store_true",
@@ -99,6 +108,10 @@ def main(argv=None):
         eng = MiniBatchStepper(x, cfg.replace(batch_size=a.batch_size or (1 << 20)), comm,
                                n_global, s)
         points_per_step = eng.batch_rows * world
+    elif a.method == "fcm":
+        from tensorflow_distributed_clustering_amd.models.fcm import FcmEngine
+        eng = FcmEngine(x, cfg, comm, n_global, s)
+        points_per_step = n_global
     else:
         eng = LloydEngine(x, cfg, comm, n_global, s)
         points_per_step = n_global
@@ -121,7 +134,7 @@ def main(argv=None):
     ms = elapsed / max(1, a.steps) * 1e3
     pps = points_per_step * a.steps / elapsed
     breakdown = None
-    if a.profile_steps and dev.type == "cuda" and a.mode == "lloyd":
+    if a.profile_steps and dev.type == "cuda" and a.mode == "lloyd" and a.method == "kmeans":
         breakdown = phase_breakdown(eng, torch, dev)
     if rank == 0:
         out = {
@@ -134,13 +147,15 @@ def main(argv=None):
             "ms_per_step": ms,
             "higher_is_better": True,
             "scaling": a.scaling,
-            "vs_baseline": pps / BASELINE_POINTS_PER_SEC,
+            "vs_baseline": pps / (BASELINE_FCM_POINTS_PER_SEC if a.method == "fcm"
+                                  else BASELINE_POINTS_PER_SEC),
             "dtype": a.dtype,
             "data": "synthetic gaussian blobs (on-device, counter-based), random-row init",
             "preset": a.preset,
             "iters_per_sec": 1e3 / ms,
             "backend": eng.local.name,
-            "config": {"model": "kmeans-minibatch" if a.mode == "minibatch" else "kmeans-lloyd",
+            "config": {"model": ("kmeans-minibatch" if a.mode == "minibatch" else
+                                 "fuzzy-cmeans" if a.method == "fcm" else "kmeans-lloyd"),
                        "global_batch": points_per_step, "seq_len": a.dim, "N": n_global,
                        "K": a.k, "D": a.dim, "points_per_gpu": e - s,
                        "parallelism": f"dp{world}"},

@@ -27,6 +27,43 @@ from .init import init_centers
 from .kmeans import ClusterResult, _shard_geometry
 
 
+class FcmEngine:
+    """Resident state of one distributed FCM run; ``step()`` = one iteration (fused tower
+    kernel, one packed all-reduce of [sum W X | sum W], the N3 divide).  Timed by bench.py."""
+
+    def __init__(self, x_local, cfg: ClusterConfig, comm: Comm, n_global: int, row_offset: int,
+                 init_centers_=None, m: Optional[float] = None):
+        self.cfg, self.comm = cfg, comm
+        k, d = cfg.n_clusters, int(x_local.shape[1])
+        self.k, self.d = k, d
+        self.m = float(m) if m is not None else (float(cfg.fuzzifier) if cfg.fuzzifier is not None
+                                                 else float(d))
+        dev = x_local.device
+        self.device = dev
+        self.local = make_fcm_ops(x_local, k, cfg.dtype, self.m, cfg.fcm_nan_to_zero, cfg.backend)
+        self.c0 = init_centers(cfg.init, x_local, row_offset, n_global, k, comm, cfg.seed,
+                               given=init_centers_)
+        self.C = self.c0.to(self.local.c_dtype).clone().contiguous()
+        self.buf = torch.zeros(k * d + k, dtype=torch.float64, device=dev)
+        self.wx = self.buf[: k * d].view(k, d)
+        self.ws = self.buf[k * d:]
+        self.labels = torch.zeros(self.local.n, dtype=torch.int32, device=dev)
+        self.shift = torch.zeros(1, dtype=torch.float32, device=dev) if cfg.tol > 0 else None
+        self.n_iter = 0
+
+    def step(self):
+        self.buf.zero_()
+        self.local.step(self.C, self.labels, self.wx, self.ws)
+        self.comm.allreduce_(self.buf)
+        if self.shift is not None:
+            self.shift.zero_()
+        self.local.finalize(self.wx, self.ws, self.C, self.shift)
+        self.n_iter += 1
+
+    def label_pass(self):
+        self.local.assign(self.C, self.labels)
+
+
 class FuzzyCMeans:
     def __init__(self, cfg: ClusterConfig, comm: Optional[Comm] = None, device=None):
         self.cfg = cfg
@@ -51,8 +88,6 @@ class FuzzyCMeans:
         if n_global is None or row_offset is None:
             n_global, row_offset = _shard_geometry(int(x_local.shape[0]), comm)
         k, d = cfg.n_clusters, int(x_local.shape[1])
-        m = self.fuzzifier(d)
-        local = make_fcm_ops(x_local, k, cfg.dtype, m, cfg.fcm_nan_to_zero, cfg.backend)
         sync(dev)
         initialization_time = time.perf_counter() - t0
 
@@ -62,48 +97,37 @@ class FuzzyCMeans:
         start_iter = 0
         if resumed is not None:
             init_centers_, start_iter = resumed.centers, resumed.n_iter
-        c0 = init_centers(cfg.init, x_local, row_offset, n_global, k, comm, cfg.seed,
-                          given=init_centers_)
-        C = c0.to(local.c_dtype).clone().contiguous()
-        buf = torch.zeros(k * d + k, dtype=torch.float64, device=dev)
-        wx = buf[: k * d].view(k, d)
-        ws = buf[k * d:]
-        labels = torch.zeros(local.n, dtype=torch.int32, device=dev)
-        need_shift = cfg.tol > 0
-        shift = torch.zeros(1, dtype=torch.float32, device=dev) if need_shift else None
+        eng = FcmEngine(x_local, cfg, comm, n_global, row_offset, init_centers_, self.fuzzifier(d))
+        eng.n_iter = start_iter
         sync(dev)
         setup_time = time.perf_counter() - t1
 
         timer = DeviceTimer(dev)
         timer.start()
-        n_iter = start_iter
         history = []
-        centers_host = lambda: C.double().cpu().numpy()
-        for it in range(start_iter, cfg.max_iter):
-            buf.zero_()
-            local.step(C, labels, wx, ws)
-            comm.allreduce_(buf)
-            if shift is not None:
-                shift.zero_()
-            local.finalize(wx, ws, C, shift)
-            n_iter = it + 1
-            if need_shift:
-                sv = float(shift.item())
+        centers_host = lambda: eng.C.double().cpu().numpy()
+        for _ in range(start_iter, cfg.max_iter):
+            eng.step()
+            n_iter = eng.n_iter
+            if eng.shift is not None:
+                sv = float(eng.shift.item())
                 history.append({"iter": n_iter, "shift": sv})
                 if sv <= cfg.tol:
                     break
             ckpt.maybe_save(n_iter, centers_host)
             faults.maybe_fail(str(n_iter), comm.rank)
         computation_time = timer.stop()
+        n_iter = eng.n_iter
         ckpt.maybe_save(n_iter, centers_host, final=True)
 
         if cfg.label_pass:
-            local.assign(C, labels)
+            eng.label_pass()
+        self.engine_ = eng
         self.result_ = ClusterResult(
-            centers=C.double().cpu().numpy(), init_centers=c0.cpu().numpy(), labels=labels,
-            counts=ws.double().cpu().numpy(), n_iter=n_iter, inertia=None,
+            centers=eng.C.double().cpu().numpy(), init_centers=eng.c0.cpu().numpy(),
+            labels=eng.labels, counts=eng.ws.double().cpu().numpy(), n_iter=n_iter, inertia=None,
             setup_time=setup_time, initialization_time=initialization_time,
-            computation_time=computation_time, backend=local.name, history=history,
+            computation_time=computation_time, backend=eng.local.name, history=history,
             n_global=n_global)
         return self
 
