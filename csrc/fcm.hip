@@ -8,8 +8,9 @@
 //   MatMul(W, X) [K,D], Sum(W, 1) [K]           (+ CPU argmax label pass :141)
 // Here ONE kernel reads each point once and keeps sum_i w_ki x_i and sum_i w_ki in
 // VGPRs (static register tiles), then reduces wave -> LDS -> one global atomic per
-// output per block.  d^(-2/(m-1)) is computed as exp2(log2(d^2) * -1/(m-1)) so no
-// sqrt is needed; the argmax label comes for free.
+// output per block.  d^(-2/(m-1)) = (d^2)^(-1/(m-1)) and u^m use transcendental-free
+// forms for the common fuzzifiers (m = 2, 3, 5; integer m by binary powering) and
+// exp2/log2 otherwise; the argmax label comes for free.
 //
 // nan_to_zero = 1 reproduces the reference guard (a point ON a centroid gets zero
 // membership everywhere, :125-126); 0 gives the correct one-hot membership.
@@ -23,11 +24,39 @@ __device__ __forceinline__ double tdc_exp2(double v) { return exp2(v); }
 __device__ __forceinline__ float tdc_log2(float v) { return log2f(v); }
 __device__ __forceinline__ double tdc_log2(double v) { return log2(v); }
 
+// t = (d^2)^expo, expo = -1/(m-1).  pmode picks a transcendental-free form for the common
+// fuzzifiers: 1: m=2 (1/d2), 2: m=3 (1/sqrt d2), 3: m=5 (the reference's m = D = 5:
+// 1/sqrt(sqrt d2)); 0: exp2(expo * log2 d2).
+template <typename T>
+__device__ __forceinline__ T fcm_t(T dd, T expo, int pmode) {
+  switch (pmode) {
+    case 1: return (T)1 / dd;
+    case 2: return (T)1 / sqrt(dd);
+    case 3: return (T)1 / sqrt(sqrt(dd));
+    default: return tdc_exp2(tdc_log2(dd) * expo);
+  }
+}
+// w = u^m: binary powering for integer m in [1, 16] (mint), else exp2(m log2 u)
+template <typename T>
+__device__ __forceinline__ T fcm_w(T u, T m, int mint) {
+  if (mint > 0) {
+    T r = (mint & 1) ? u : (T)1;
+    T b = u;
+#pragma unroll
+    for (int e = mint >> 1; e > 0; e >>= 1) {
+      b = b * b;
+      if (e & 1) r = r * b;
+    }
+    return r;
+  }
+  return u > (T)0 ? tdc_exp2(m * tdc_log2(u)) : (T)0;
+}
+
 template <typename T, typename ACC, int KMAX, int DMAX>
 __global__ __launch_bounds__(256) void fcm_small_kernel(
     const T* __restrict__ X, int64_t N, int64_t ldx, int D, const T* __restrict__ C, int K,
-    T expo, T m, int nan_to_zero, int32_t* __restrict__ labels, ACC* __restrict__ wx,
-    ACC* __restrict__ ws) {
+    T expo, T m, int pmode, int mint, int nan_to_zero, int32_t* __restrict__ labels,
+    ACC* __restrict__ wx, ACC* __restrict__ ws) {
   __shared__ T s_c[KMAX * DMAX];
   __shared__ T s_red[4][KMAX * (DMAX + 1)];
   const int tid = threadIdx.x;
@@ -63,18 +92,19 @@ __global__ __launch_bounds__(256) void fcm_small_kernel(
         dd = fma(df, df, dd);
       }
       const bool on = (k < K);
-      t[k] = !on ? (T)0 : (dd == (T)0 ? inf : tdc_exp2(tdc_log2(dd) * expo));
+      t[k] = !on ? (T)0 : (dd == (T)0 ? inf : fcm_t(dd, expo, pmode));
       nzero += (on && dd == (T)0);
       tsum += t[k];
     }
     // memberships u_k, argmax label, weights w_k = u_k^m (all in t[])
     int best = 0;
     T bu = (T)-1;
+    const T inv = (T)1 / tsum;
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
       T u;
       if (nzero == 0) {
-        u = t[k] / tsum;
+        u = t[k] * inv;
       } else if (nan_to_zero) {
         u = (T)0;  // inf/inf = NaN -> 0 and finite/inf = 0  (reference guard)
       } else {
@@ -84,7 +114,7 @@ __global__ __launch_bounds__(256) void fcm_small_kernel(
         bu = u;
         best = k;
       }
-      t[k] = (u > (T)0) ? tdc_exp2(m * tdc_log2(u)) : (T)0;
+      t[k] = (u > (T)0) ? fcm_w(u, m, mint) : (T)0;
     }
     labels[i] = best;
 #pragma unroll
@@ -123,9 +153,11 @@ int launch_fcm(const void* X, int64_t N, int64_t ldx, int D, const void* C, int 
   if (g < 1) g = 1;
   if (g > 2048) g = 2048;
   const T expo = (T)(-1.0 / (m - 1.0));
+  const int pmode = m == 2.0 ? 1 : (m == 3.0 ? 2 : (m == 5.0 ? 3 : 0));
+  const int mint = (m == (double)(int)m && m >= 1.0 && m <= 16.0) ? (int)m : 0;
   hipLaunchKernelGGL((fcm_small_kernel<T, ACC, KMAX, DMAX>), dim3((unsigned)g), dim3(256), 0, s,
-                     (const T*)X, N, ldx, D, (const T*)C, K, expo, (T)m, nan_to_zero, labels,
-                     (ACC*)wx, (ACC*)ws);
+                     (const T*)X, N, ldx, D, (const T*)C, K, expo, (T)m, pmode, mint, nan_to_zero,
+                     labels, (ACC*)wx, (ACC*)ws);
   TDC_CHECK_LAUNCH();
   return 0;
 }
