@@ -481,8 +481,11 @@ class TorchFCM(_LocalOpsBase):
         labels.copy_(lab)
 
     def assign(self, C, labels):
-        u = ref.fcm_memberships(self.x, C.to(self.x.dtype), self.m, self.nan_to_zero)
-        labels.copy_(u.argmax(1).to(torch.int32))
+        c = C.to(self.x.dtype)
+        step = max(1, (1 << 26) // max(1, self.k))  # bound the [rows, K] membership block
+        for s in range(0, self.n, step):
+            u = ref.fcm_memberships(self.x[s:s + step], c, self.m, self.nan_to_zero)
+            labels[s:s + step] = u.argmax(1).to(torch.int32)
 
 
 class HipSmallFCM(_LocalOpsBase):
