@@ -1,0 +1,41 @@
+"""bench.py contract (driver-facing): one JSON line from rank 0, whole-job value, torchrun
+launch with one rank per device (gloo ranks on CPU here)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+        "scaling", "vs_baseline", "dtype", "data", "config"}
+
+
+def _run(args, timeout=600):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args,
+                       capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_bench_json_contract(gpus):
+    d = _run(["--gpus", str(gpus), "--steps", "3", "--warmup", "1", "--n-per-gpu", "20000",
+              "--k", "16", "--dim", "8", "--dtype", "fp32"])
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == gpus and d["steps"] == 3 and d["warmup"] == 1
+    assert d["config"]["global_batch"] == 20000 * gpus and d["config"]["parallelism"] == f"dp{gpus}"
+    assert d["scaling"] == "weak" and d["higher_is_better"] is True
+    # whole-job value = global points per step / step time
+    assert d["value"] == pytest.approx(20000 * gpus / (d["ms_per_step"] / 1e3), rel=1e-6)
+
+
+def test_bench_fcm_and_minibatch_presets():
+    d = _run(["--preset", "ref25m_fcm", "--n-per-gpu", "30000", "--steps", "2", "--warmup", "1"])
+    assert d["config"]["model"] == "fuzzy-cmeans" and d["dtype"] == "fp64"
+    d = _run(["--preset", "minibatch1b", "--n-per-gpu", "50000", "--k", "32", "--batch-size", "4096",
+              "--steps", "2", "--warmup", "1", "--dtype", "fp32"])
+    assert d["config"]["model"] == "kmeans-minibatch" and d["config"]["global_batch"] == 4096
