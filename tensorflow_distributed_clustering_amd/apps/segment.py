@@ -27,6 +27,7 @@ import numpy as np
 import torch
 
 from ..config import ClusterConfig
+from ..models.fcm import FuzzyCMeans
 from ..models.kmeans import KMeans
 
 
@@ -108,22 +109,45 @@ class Segmentation:
 
 def segment(img: np.ndarray, k: int, max_iter: int = 20, dtype: str = "fp32",
             init: str = "kmeans++", seed: int = 0, device: Optional[str] = None,
-            tol: float = 0.0) -> Segmentation:
+            tol: float = 0.0, method: str = "kmeans", fuzzifier: Optional[float] = None) -> Segmentation:
+    """Segment one frame.  method 'fcm' runs Fuzzy C-Means (hard labels = argmax membership;
+    the notebook's FCM used m = D = 3 for RGB)."""
     h, w = img.shape[:2]
     dev = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
     px = torch.from_numpy(to_pixels(img)).to(dev)
     cfg = ClusterConfig(n_clusters=k, max_iter=max_iter, dtype=dtype, init=init, seed=seed,
-                        tol=tol)
+                        tol=tol, fuzzifier=fuzzifier)
     t0 = time.perf_counter()
-    km = KMeans(cfg, device=dev).fit(px)
+    model = FuzzyCMeans if method == "fcm" else KMeans
+    km = model(cfg, device=dev).fit(px)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     secs = time.perf_counter() - t0
     r = km.result_
     lab = r.labels.long().cpu().numpy()
-    seg = np.clip(np.rint(r.centers[lab]), 0, 255).astype(np.uint8).reshape(h, w, -1)
-    return Segmentation(seg, lab.reshape(h, w), r.centers, float(r.inertia or 0.0), secs,
+    seg = np.clip(np.rint(np.nan_to_num(r.centers)[lab]), 0, 255).astype(np.uint8).reshape(h, w, -1)
+    inertia = r.inertia
+    if inertia is None:  # FCM: report the hard-assignment SSE
+        inertia = float(((to_pixels(img) - r.centers[lab]) ** 2).sum())
+    return Segmentation(seg, lab.reshape(h, w), r.centers, float(inertia), secs,
                         has_nan_centers(r.centers))
+
+
+def benchmark_frames(n_frames: int = 10, h: int = 640, w: int = 640, k: int = 3,
+                     max_iter: int = 20, dtype: str = "fp64", method: str = "kmeans",
+                     device: Optional[str] = None) -> dict:
+    """The notebook's per-frame protocol (`Testing Images.ipynb`): 409,600-px RGB frames,
+    K=3, 20 iterations, fp64; mean seconds per frame (fit incl. setup; first frame =
+    warm-up, excluded)."""
+    times = []
+    for f in range(n_frames + 1):
+        img, _ = synthetic_image(h, w, k=max(k, 3), seed=100 + f)
+        s = segment(img, k, max_iter, dtype, "random", seed=f, device=device, method=method)
+        if f:
+            times.append(s.seconds)
+    return {"frames": n_frames, "pixels": h * w, "K": k, "iters": max_iter, "dtype": dtype,
+            "method": method, "mean_seconds_per_frame": float(np.mean(times)),
+            "points_iter_per_sec": h * w * max_iter / float(np.mean(times))}
 
 
 def main(argv=None) -> int:
@@ -138,9 +162,16 @@ def main(argv=None) -> int:
     ap.add_argument("--out", default=None, help="write the segmented image here")
     ap.add_argument("--compare", action="store_true",
                     help="cross-check against the cv2.kmeans-style best-of-10 baseline")
+    ap.add_argument("--method", default="kmeans", choices=["kmeans", "fcm"])
+    ap.add_argument("--bench_frames", type=int, default=0,
+                    help="run the notebook's per-frame benchmark on N synthetic 640x640 frames")
     a = ap.parse_args(argv)
+    if a.bench_frames:
+        print(json.dumps(benchmark_frames(a.bench_frames, k=a.K, max_iter=a.n_max_iters,
+                                          dtype=a.dtype, method=a.method, device=a.device)))
+        return 0
     img = load_image(a.image) if a.image else synthetic_image(seed=a.seed)[0]
-    s = segment(img, a.K, a.n_max_iters, a.dtype, a.init, a.seed, a.device)
+    s = segment(img, a.K, a.n_max_iters, a.dtype, a.init, a.seed, a.device, method=a.method)
     out = {"pixels": int(img.shape[0] * img.shape[1]), "K": a.K, "seconds": s.seconds,
            "inertia": s.inertia, "nan_centers": s.has_nan}
     if a.compare:

@@ -66,3 +66,11 @@ def test_cli_placement_and_plot(tmp_path):
     assert r.returncode == 0, r.stderr
     assert "[placement] rank 0/1" in r.stdout and "rows [0, 2000)" in r.stdout
     assert svg.exists()
+
+
+def test_fcm_segmentation_and_frame_bench():
+    img, region = seg.synthetic_image(96, 96, k=3, seed=5)
+    s = seg.segment(img, 3, max_iter=10, dtype="fp64", device="cpu", method="fcm", seed=1)
+    assert s.image.shape == img.shape and s.inertia > 0
+    b = seg.benchmark_frames(n_frames=1, h=64, w=64, k=3, max_iter=3, device="cpu")
+    assert b["pixels"] == 4096 and b["mean_seconds_per_frame"] > 0
