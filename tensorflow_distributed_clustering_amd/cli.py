@@ -146,6 +146,14 @@ def build_parser():
     parser.add_argument("--plot_out", default=None,
                         help="SVG scatter of the first 10k points of rank 0 with initial and "
                              "final centers")
+    parser.add_argument("--log_every", type=int, default=0,
+                        help="every N iterations print (and record in --extended_log) the max "
+                             "centroid shift and the inertia of that iteration")
+    parser.add_argument("--torch_profile", default=None, metavar="DIR",
+                        help="record the fit with torch.profiler (ROCm/roctracer) and write a "
+                             "chrome trace + kernel table to DIR")
+    parser.add_argument("--collective_timeout", type=float, default=600.0,
+                        help="seconds before a stuck collective raises (init_process_group)")
     parser.add_argument("--graph", action="store_true",
                         help="replay each iteration from a captured HIP graph (1 GPU)")
     parser.add_argument("--deterministic", action="store_true",
@@ -185,7 +193,7 @@ def run(args) -> int:
     device = args.device
     if device == "auto":
         device = "cuda" if torch.cuda.device_count() > 0 else "cpu"
-    comm = init_comm(device)
+    comm = init_comm(device, timeout_s=args.collective_timeout)
     status = 0
     result = None
     exc_name = None
@@ -205,7 +213,7 @@ def run(args) -> int:
                             checkpoint_path=args.checkpoint or "",
                             checkpoint_every=args.checkpoint_every, resume=args.resume,
                             hbm_budget_gb=args.hbm_budget_gb, deterministic=args.deterministic,
-                            graph=args.graph)
+                            graph=args.graph, log_every=args.log_every)
         xt = torch.from_numpy(np.asarray(x))
         if args.method_name == "distributedKMeans":
             model = KMeans(cfg, comm)
@@ -214,7 +222,12 @@ def run(args) -> int:
         else:
             from .models.minibatch import MiniBatchKMeans
             model = MiniBatchKMeans(cfg, comm)
-        model.fit(xt, n_global=n_global, row_offset=row_off)
+        if args.torch_profile:
+            from .utils.timers import profiled
+            with profiled(args.torch_profile, comm.rank):
+                model.fit(xt, n_global=n_global, row_offset=row_off)
+        else:
+            model.fit(xt, n_global=n_global, row_offset=row_off)
         result = model.result_
         if args.log_device_placement:
             name = (torch.cuda.get_device_name(comm.device) if comm.device.type == "cuda"
@@ -264,7 +277,7 @@ def run(args) -> int:
                         "n_iter": n_iter, "computation_time": comp, "backend": result.backend,
                         "points_per_sec": result.n_global * n_iter / comp if comp > 0 else None,
                         "iters_per_sec": n_iter / comp if comp > 0 else None,
-                        "inertia": result.inertia}) + "\n")
+                        "inertia": result.inertia, "history": result.history}) + "\n")
         print("log_file =", args.log_file)
     return status
 

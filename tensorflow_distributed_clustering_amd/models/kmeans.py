@@ -151,23 +151,30 @@ class LloydEngine:
     def _chunks(self):
         return self.source.chunks(self.chunk_rows)
 
-    def step(self):
+    def step(self, with_inertia: bool = False) -> Optional[float]:
+        """One Lloyd iteration.  ``with_inertia``: also return the global inertia of this
+        iteration's assignment (the fused distance epilogue writes min distances; costs one
+        scalar all-reduce + host sync, so it is only requested at log points)."""
         g = getattr(self, "_graph", None)
-        if g is not None:
+        if g is not None and not with_inertia:
             g.replay()
             self.n_iter += 1
-            return
-        self._eager_step()
+            return None
+        return self._eager_step(with_inertia)
 
-    def _eager_step(self):
+    def _eager_step(self, with_inertia: bool = False) -> Optional[float]:
         self.buf.zero_()
+        mind = self.mind if (with_inertia and self.mind is not None) else None
         if not self.streamed:
-            self.local.step(self.C, self.labels, None, self.sums, self.counts)
+            self.local.step(self.C, self.labels, mind, self.sums, self.counts)
         else:
             for start, chunk in self._chunks():
                 s = start - self.source.row_offset  # chunk starts are source-global
-                self.local.bind(chunk).step(self.C, self.labels[s:s + chunk.shape[0]], None,
+                e = s + chunk.shape[0]
+                self.local.bind(chunk).step(self.C, self.labels[s:e],
+                                            None if mind is None else mind[s:e],
                                             self.sums, self.counts)
+        inertia = self.comm.sum_scalar(float(mind.double().sum())) if mind is not None else None
         if self.nan_any:
             self.empty_flags.copy_((self.counts == 0).to(self.buf.dtype))
         self.comm.allreduce_bucketed_(self.buf, self.bucket_bytes)
@@ -179,6 +186,7 @@ class LloydEngine:
         if self.cfg.empty_cluster == "reseed":
             self._reseed()
         self.n_iter += 1
+        return inertia
 
     # ------------------------------------------------------------ HIP graph replay
     def graphable(self) -> bool:
@@ -376,13 +384,18 @@ class KMeans:
         timer = DeviceTimer(dev)
         timer.start()
         for _ in range(max(0, cfg.max_iter - start_iter)):
-            eng.step()
+            log_pt = cfg.log_every > 0 and (eng.n_iter + 1) % cfg.log_every == 0
+            inertia_it = eng.step(with_inertia=log_pt and cfg.compute_inertia)
             n = eng.n_iter
-            if eng.need_shift and (cfg.tol > 0 or n % cfg.log_every == 0):
+            if eng.need_shift and (cfg.tol > 0 or log_pt):
                 sv = float(eng.shift.item())
-                history.append({"iter": n, "shift": sv})
-                if cfg.log_every and comm.is_root and n % cfg.log_every == 0:
-                    print(f"[kmeans] iter {n} max centroid shift^2 {sv:.3e}", flush=True)
+                rec = {"iter": n, "shift": sv}
+                if inertia_it is not None:
+                    rec["inertia"] = inertia_it  # of this iteration's assignment (pre-update)
+                history.append(rec)
+                if log_pt and comm.is_root:
+                    extra = f" inertia {inertia_it:.6e}" if inertia_it is not None else ""
+                    print(f"[kmeans] iter {n} max centroid shift^2 {sv:.3e}{extra}", flush=True)
                 if cfg.tol > 0 and sv <= cfg.tol:
                     break
             ckpt.maybe_save(n, centers_host)

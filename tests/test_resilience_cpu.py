@@ -174,3 +174,23 @@ def test_oom_on_one_rank_retries_on_all_ranks():
     x = gaussian_blobs(4001, 3, 5, seed=2, dtype=torch.float64)
     single = tdc.KMeans(tdc.ClusterConfig(n_clusters=5, max_iter=5, dtype="fp64", seed=1)).fit(x)
     np.testing.assert_allclose(centers, single.result_.centers, rtol=1e-10, atol=1e-10)
+
+
+def test_cli_log_every_profile_and_timeout_flags(tmp_path):
+    data = tmp_path / "d.npz"
+    X = gaussian_blobs(3000, 3, 4, seed=9, dtype=torch.float64).numpy()
+    np.savez(data, X=X, Y=np.zeros(3000))
+    ext, prof = tmp_path / "e.jsonl", tmp_path / "prof"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "distribuitedClustering.py"),
+                        "--n_obs=3000", "--n_dim=3", "--K=4", "--n_GPUs=1", "--n_max_iters=6",
+                        "--seed=3", f"--log_file={tmp_path / 'l.csv'}",
+                        "--method_name=distributedKMeans", f"--data_file={data}", "--device=cpu",
+                        "--log_every=3", f"--extended_log={ext}", f"--torch_profile={prof}",
+                        "--collective_timeout=120"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "[kmeans] iter 3 max centroid shift^2" in r.stdout and "inertia" in r.stdout
+    import json
+    hist = json.loads(ext.read_text().strip())["history"]
+    assert [h["iter"] for h in hist] == [3, 6] and all(h["inertia"] > 0 for h in hist)
+    assert (prof / "trace_rank0.json").exists() and (prof / "kernels_rank0.txt").exists()

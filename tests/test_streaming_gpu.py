@@ -68,3 +68,20 @@ def test_graph_replay_matches_eager(gpu, dtype, d, k):
     assert graph.n_iter == eager.n_iter == 7
     np.testing.assert_allclose(graph.centers, eager.centers, rtol=1e-5, atol=1e-5)
     assert (graph.labels == eager.labels).float().mean().item() > 0.999
+
+
+def test_deterministic_mode_bitwise_reproducible(gpu):
+    x = gaussian_blobs(300_000, 64, 512, seed=8, dtype=torch.bfloat16, device=gpu)
+    cfg = tdc.ClusterConfig(n_clusters=512, max_iter=5, dtype="bf16", seed=1, deterministic=True)
+    a = tdc.KMeans(cfg, device=gpu).fit(x).result_
+    b = tdc.KMeans(cfg, device=gpu).fit(x).result_
+    assert np.array_equal(a.centers, b.centers)
+    assert torch.equal(a.labels, b.labels)
+
+
+def test_per_iteration_inertia_on_gpu(gpu):
+    x = gaussian_blobs(200_000, 32, 64, seed=3, dtype=torch.bfloat16, device=gpu)
+    r = tdc.KMeans(tdc.ClusterConfig(n_clusters=64, max_iter=6, dtype="bf16", log_every=1,
+                                     seed=2), device=gpu).fit(x).result_
+    inert = [h["inertia"] for h in r.history]
+    assert len(inert) == 6 and all(b <= a * 1.0001 for a, b in zip(inert, inert[1:]))
