@@ -306,6 +306,24 @@ void quant_fp8(const at::Tensor& X, int64_t valid, int64_t neg2, at::Tensor& Q, 
         "quant_fp8");
 }
 
+void kpp_step(const at::Tensor& X, const at::Tensor& cand, at::Tensor& closest, int64_t mode,
+              at::Tensor& pots) {
+  check_cuda(X, "X");
+  check_rows(X, "X");
+  TORCH_CHECK(cand.is_contiguous() && cand.dim() == 2 && cand.size(1) == X.size(1),
+              "tdc.kpp_step: cand [T, D]");
+  TORCH_CHECK(closest.scalar_type() == cand.scalar_type() && closest.is_contiguous() &&
+                  closest.numel() >= X.size(0), "tdc.kpp_step: closest [N] in the candidate dtype");
+  TORCH_CHECK(pots.scalar_type() == at::kDouble && pots.is_contiguous() && pots.numel() >= cand.size(0),
+              "tdc.kpp_step: pots fp64 [T]");
+  const DevGuard guard(X.device());
+  check(tdc_kpp_step(dcode(X.scalar_type()), dcode(cand.scalar_type()), X.data_ptr(), X.size(0),
+                     X.stride(0), (int)X.size(1), cand.data_ptr(), (int)cand.size(0),
+                     closest.data_ptr(), (int)mode, pots.data_ptr<double>(),
+                     num_cus(X.device().index()), cur_stream()),
+        "kpp_step");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(tdc, m) {
@@ -321,6 +339,7 @@ TORCH_LIBRARY(tdc, m) {
   m.def("assign_bigd_supported(ScalarType dtype, int DP) -> bool", &assign_bigd_supported);
   m.def("assign_bigd(Tensor X, Tensor? Xs, Tensor xnorm, Tensor Cm2, Tensor? Cs, Tensor cnorm, int kg_tiles, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!)? keys) -> ()");
   m.def("quant_fp8(Tensor X, int valid, int neg2, Tensor(a!) Q, Tensor(b!) S, Tensor(c!)? norm) -> ()");
+  m.def("kpp_step(Tensor X, Tensor cand, Tensor(a!) closest, int mode, Tensor(b!) pots) -> ()");
   m.def("finalize(Tensor? sums, Tensor? counts, Tensor(a!) C, int policy, Tensor(b!)? shift, Tensor(c!)? Cm2, Tensor(d!)? cnorm) -> ()");
 }
 
@@ -334,4 +353,5 @@ TORCH_LIBRARY_IMPL(tdc, CUDA, m) {
   m.impl("finalize", &finalize);
   m.impl("assign_bigd", &assign_bigd);
   m.impl("quant_fp8", &quant_fp8);
+  m.impl("kpp_step", &kpp_step);
 }

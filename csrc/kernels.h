@@ -71,3 +71,11 @@ int tdc_assign_bigd_supported(int dtype, int DP);
 // neg2 != 0: centroid operand (-2c; norm of +c).  Rows >= valid are padding.
 int tdc_quant_fp8(int src_dtype, const void* X, int64_t rows, int64_t valid, int d, int64_t ldx,
                   int DP, int neg2, void* Q, void* S, float* norm, hipStream_t stream);
+
+// N7 k-means++ step (kmeanspp.hip).  cand [T, D] (d_dtype, T <= 16), closest [N] (d_dtype).
+// mode 0: pots[t] += sum_i min(closest_i, ||x_i - cand_t||^2) for every candidate;
+// mode 1 (T == 1): closest_i = min(closest_i, ||x_i - cand_0||^2), pots[0] += sum closest.
+// pots is fp64 and accumulated (caller zeroes it).
+int tdc_kpp_step(int x_dtype, int d_dtype, const void* X, int64_t N, int64_t ldx, int D,
+                 const void* cand, int T, void* closest, int mode, double* pots, int num_cus,
+                 hipStream_t s);

@@ -80,25 +80,47 @@ def _sqdist_to(x: torch.Tensor, c: torch.Tensor, chunk: int = 1 << 22) -> torch.
     return out
 
 
+def _native_kpp(x_local, wd, trials):
+    """The N7 kernel applies to GPU shards (bf16/fp32/fp64 rows, candidates fit LDS)."""
+    if x_local.device.type != "cuda" or trials > 16:
+        return None
+    if x_local.dtype not in (torch.bfloat16, torch.float32, torch.float64) or x_local.stride(1) != 1:
+        return None
+    if trials * x_local.shape[1] * (8 if wd == torch.float64 else 4) > 64 * 1024:
+        return None
+    from .. import _native
+    return _native.require()
+
+
 def init_kmeanspp(x_local, row_offset, n_global, k, comm: Comm, seed,
                   n_local_trials: Optional[int] = None, work_dtype=None):
-    """Distributed greedy k-means++ (sklearn's variant: 2 + ln K trials per step)."""
+    """Distributed greedy k-means++ (sklearn's variant: 2 + ln K trials per step).
+
+    On a GPU shard each step is two passes of the N7 kernel (`csrc/kmeanspp.hip`): score
+    all candidates in one sweep, then apply the winner; elsewhere the same step in torch."""
     if n_local_trials is None:
         n_local_trials = 2 + int(math.log(k))
     dev = x_local.device
     wd = work_dtype or (torch.float64 if x_local.dtype == torch.float64 or dev.type == "cpu"
                         else torch.float32)
+    ops = _native_kpp(x_local, wd, n_local_trials)
     rng = np.random.default_rng(seed)
     n_local = x_local.shape[0]
-    sizes = comm.all_gather_sizes(n_local)
-    offsets = np.concatenate([[0], np.cumsum(sizes)])
     centers = torch.empty(k, x_local.shape[1], dtype=torch.float64, device=dev)
     first = int(rng.integers(0, n_global))
     centers[0] = gather_global_rows(x_local, row_offset, [first], comm)[0]
-    closest = _sqdist_to(x_local, centers[:1].to(wd))[0]
+    pots_buf = torch.zeros(max(16, n_local_trials), dtype=torch.float64, device=dev)
+    if ops is not None:
+        closest = torch.full((n_local,), float("inf"), dtype=wd, device=dev)
+        pots_buf.zero_()
+        ops.kpp_step(x_local, centers[:1].to(wd).contiguous(), closest, 1, pots_buf)
+        local_pot = pots_buf[:1].clone()
+    else:
+        closest = _sqdist_to(x_local, centers[:1].to(wd))[0]
+        local_pot = closest.sum().double().reshape(1)
     for c in range(1, k):
         pots = torch.zeros(comm.world_size, dtype=torch.float64, device=dev)
-        pots[comm.rank] = closest.sum().double()
+        pots[comm.rank] = local_pot[0]
         comm.allreduce_(pots)
         pots_h = pots.cpu().numpy()
         total = float(pots_h.sum())
@@ -122,11 +144,23 @@ def init_kmeanspp(x_local, row_offset, n_global, k, comm: Comm, seed,
             comm.allreduce_(ci)  # only the owner wrote a non-zero (owners differ per trial)
             cand_idx = [int(v) for v in ci.tolist()]
         cand = gather_global_rows(x_local, row_offset, cand_idx, comm)
-        dist = torch.minimum(_sqdist_to(x_local, cand.to(wd)), closest[None, :])
-        tp = dist.double().sum(1)
-        comm.allreduce_(tp)
-        best = int(torch.argmin(tp).item())
-        closest = dist[best].contiguous()
+        if ops is not None:
+            tp = pots_buf[: len(cand_idx)]
+            tp.zero_()
+            ops.kpp_step(x_local, cand.to(wd).contiguous(), closest, 0, tp)
+            tp = tp.clone()
+            comm.allreduce_(tp)
+            best = int(torch.argmin(tp).item())
+            pots_buf.zero_()
+            ops.kpp_step(x_local, cand[best:best + 1].to(wd).contiguous(), closest, 1, pots_buf)
+            local_pot = pots_buf[:1].clone()
+        else:
+            dist = torch.minimum(_sqdist_to(x_local, cand.to(wd)), closest[None, :])
+            tp = dist.double().sum(1)
+            comm.allreduce_(tp)
+            best = int(torch.argmin(tp).item())
+            closest = dist[best].contiguous()
+            local_pot = closest.sum().double().reshape(1)
         centers[c] = cand[best]
     return centers
 

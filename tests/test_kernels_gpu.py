@@ -222,3 +222,38 @@ def test_finalize_and_prep(gpu, policy):
     if policy == "keep":
         dd = ((C.double() - old.double()) ** 2).sum(1).max()
         torch.testing.assert_close(shift.double()[0], dd, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("xdt,ddt", [(torch.bfloat16, torch.float32), (torch.float32, torch.float32),
+                                     (torch.float64, torch.float64), (torch.float32, torch.float64)])
+@pytest.mark.parametrize("n,d,t", [(20000, 5, 8), (5000, 128, 10), (3001, 33, 1), (7000, 300, 12)])
+def test_kpp_step(gpu, xdt, ddt, n, d, t):
+    from tensorflow_distributed_clustering_amd import _native
+    ops = _native.require()
+    g = torch.Generator().manual_seed(n + d)
+    x = torch.randn(n, d, generator=g).to(xdt).to(gpu)
+    cand = torch.randn(t, d, generator=g, dtype=torch.float64).to(ddt).to(gpu)
+    closest = (torch.rand(n, generator=g, dtype=torch.float64) * 2 * d).to(ddt).to(gpu)
+    d2 = ((x.double()[None] - cand.double()[:, None]) ** 2).sum(-1)  # [t, n]
+    pots = torch.zeros(16, dtype=torch.float64, device=gpu)
+    ops.kpp_step(x, cand, closest, 0, pots)
+    ref_pots = torch.minimum(d2, closest.double()[None]).sum(1)
+    torch.testing.assert_close(pots[:t], ref_pots, rtol=1e-5, atol=1e-3)
+    pots.zero_()
+    c1 = closest.clone()
+    ops.kpp_step(x, cand[:1].contiguous(), c1, 1, pots)
+    ref_c = torch.minimum(d2[0], closest.double())
+    torch.testing.assert_close(c1.double(), ref_c, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(pots[0], ref_c.sum(), rtol=1e-5, atol=1e-3)
+
+
+def test_native_kmeanspp_matches_torch_path(gpu):
+    import tensorflow_distributed_clustering_amd as tdc
+    from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs
+    from tensorflow_distributed_clustering_amd.models.init import init_kmeanspp
+    from tensorflow_distributed_clustering_amd.parallel.dist import local_comm
+    x = gaussian_blobs(50000, 8, 16, seed=1, dtype=torch.float64, device=gpu)
+    comm = local_comm(gpu)
+    native = init_kmeanspp(x, 0, 50000, 16, comm, 3)
+    torch_path = init_kmeanspp(x.cpu(), 0, 50000, 16, local_comm(torch.device("cpu")), 3)
+    torch.testing.assert_close(native.cpu(), torch_path, rtol=0, atol=0)
