@@ -90,7 +90,7 @@ def finalize(sums: torch.Tensor, counts: torch.Tensor, old: torch.Tensor,
 
 
 def fcm_memberships(x: torch.Tensor, c: torch.Tensor, m: float,
-                    nan_to_zero: bool = True) -> torch.Tensor:
+                    nan_to_zero: bool = True, exact: Optional[bool] = None) -> torch.Tensor:
     """u[n, K]; u_ik = d_ik^(-2/(m-1)) / sum_k' d_ik'^(-2/(m-1)).
 
     nan_to_zero=True is the reference guard (`distribuitedClustering.py:125-126`):
@@ -99,7 +99,9 @@ def fcm_memberships(x: torch.Tensor, c: torch.Tensor, m: float,
     """
     if m <= 1.0:
         raise ValueError(f"FCM fuzzifier must be > 1, got {m} (reference uses m := D; D=1 divides by zero)")
-    d = pairwise_sqdist(x, c, exact=True).sqrt()
+    if exact is None:  # difference form (the reference's) for small D; GEMM form above
+        exact = x.shape[1] <= 16
+    d = pairwise_sqdist(x, c, exact=exact).sqrt()
     t = d.pow(-2.0 / (m - 1.0))
     u = t / t.sum(1, keepdim=True)
     bad = torch.isnan(u)
@@ -122,7 +124,7 @@ def fcm_partial(x: torch.Tensor, c: torch.Tensor, m: float, nan_to_zero: bool = 
     wx = torch.zeros(k, x.shape[1], dtype=acc_dtype, device=x.device)
     ws = torch.zeros(k, dtype=acc_dtype, device=x.device)
     labels = torch.empty(n, dtype=torch.int32, device=x.device)
-    step = _chunk_rows(n, k, max(1, chunk_elems // max(1, x.shape[1])))
+    step = _chunk_rows(n, k, max(1, chunk_elems // max(1, x.shape[1] if x.shape[1] <= 16 else 4)))
     for s in range(0, n, step):
         xs = x[s:s + step]
         u = fcm_memberships(xs, c, m, nan_to_zero)
