@@ -86,7 +86,7 @@ class HostSource:
     """Host-resident shard streamed through pinned memory by the native RowStreamer."""
 
     def __init__(self, x_host: np.ndarray, layout: Layout, device, row_offset: int = 0,
-                 n_pinned: int = 3, n_threads: int = 8):
+                 n_pinned: int = 3, n_threads: int = 8, resident_rows: int = 0):
         if x_host.dtype not in (np.float64, np.float32):
             x_host = np.ascontiguousarray(x_host, dtype=np.float32)
         if x_host.strides[1] != x_host.itemsize:
@@ -105,6 +105,10 @@ class HostSource:
         self.streamer = torch.classes.tdc.RowStreamer(
             int(x_host.ctypes.data), 0 if x_host.dtype == np.float64 else 1, self.n_rows, self.d,
             ld, dst_type, layout[1], n_threads)
+        # hybrid residency: the first resident_rows rows are uploaded once and stay in HBM;
+        # only the remainder streams every pass (data 1.5x HBM -> 1/3 of it crosses PCIe)
+        self.resident_rows = int(min(max(0, resident_rows), self.n_rows)) if self.device.type == "cuda" else 0
+        self._resident = None
 
     def chunks(self, chunk_rows: int) -> Iterator[Tuple[int, torch.Tensor]]:
         chunk_rows = min(chunk_rows or self.n_rows, self.n_rows)
@@ -120,10 +124,22 @@ class HostSource:
                 self.streamer.wait(self.streamer.submit(slot, s, rows))
                 yield self.row_offset + s, slot[:rows]
             return
+        R = self.resident_rows
+        if R and self._resident is None:
+            self._resident = torch.empty(R, width, dtype=dt, device=self.device)
+            for s0 in range(0, R, chunk_rows):  # one-time upload through the same converter
+                rows = min(chunk_rows, R - s0)
+                self.streamer.wait(self.streamer.submit(pinned[0], s0, rows))
+                self._resident[s0:s0 + rows].copy_(pinned[0][:rows])
+            torch.cuda.current_stream(self.device).synchronize()
+        for s0 in range(0, R, chunk_rows):
+            yield self.row_offset + s0, self._resident[s0:min(R, s0 + chunk_rows)]
+        if R >= self.n_rows:
+            return
         devbuf = [torch.empty(chunk_rows, width, dtype=dt, device=self.device) for _ in range(2)]
         copy_stream = torch.cuda.Stream(device=self.device)
         compute = torch.cuda.current_stream(self.device)
-        starts = list(range(0, self.n_rows, chunk_rows))
+        starts = list(range(R, self.n_rows, chunk_rows))
         tickets = {}
         h2d_done = [None] * self.n_pinned
         slot_free = [None, None]
@@ -182,3 +198,20 @@ def plan_chunk_rows(n_rows: int, row_bytes: int, k: int, d: int, device,
         return 0
     rows = int((budget - fixed) // (2 * per_row + row_bytes))  # 2 device slots + staging
     return max(1 << 16, (rows // 4096) * 4096)
+
+
+def plan_resident_rows(n_rows: int, row_bytes: int, chunk_rows: int, k: int, d: int, device,
+                       budget_gb: float = 0.0, reserve_frac: float = 0.15,
+                       per_row_extra: int = 16) -> int:
+    """Rows of a streamed shard that can stay resident in HBM next to the streaming
+    buffers (2 device slots of chunk_rows) and the per-row work buffers of all rows."""
+    device = torch.device(device)
+    if device.type != "cuda":
+        return 0
+    if budget_gb > 0:
+        budget = budget_gb * (1 << 30)
+    else:
+        budget, _ = torch.cuda.mem_get_info(device)
+    budget *= (1.0 - reserve_frac)
+    fixed = k * d * 16 + (64 << 20) + 2 * chunk_rows * row_bytes + n_rows * per_row_extra
+    return int(max(0, min(n_rows, (budget - fixed) // row_bytes)))

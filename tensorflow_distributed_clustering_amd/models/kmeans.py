@@ -31,7 +31,7 @@ import numpy as np
 import torch
 
 from ..config import ClusterConfig
-from ..data.stream import HostSource, ResidentSource, plan_chunk_rows
+from ..data.stream import HostSource, ResidentSource, plan_chunk_rows, plan_resident_rows
 from ..ops import acc_dtype_for, make_lloyd_ops, padded_dim
 from ..parallel.dist import Comm, local_comm
 from ..utils import faults
@@ -304,7 +304,11 @@ class KMeans:
                                                 cfg.hbm_budget_gb)
                 if chunk:
                     layout = (torch.bfloat16 if cfg.dtype == "bf16" else torch.float32, width)
-                    return HostSource(xn, layout, dev, row_offset), chunk
+                    resident = 0
+                    if not want:  # planner-driven streaming: keep what fits in HBM resident
+                        resident = plan_resident_rows(xn.shape[0], width * es, chunk,
+                                                      cfg.n_clusters, d, dev, cfg.hbm_budget_gb)
+                    return HostSource(xn, layout, dev, row_offset, resident_rows=resident), chunk
         return torch.as_tensor(xn).to(dev), want
 
     def _build_engine(self, first, x_local, dev, comm, n_global, row_offset, n_local,

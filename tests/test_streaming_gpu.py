@@ -85,3 +85,16 @@ def test_per_iteration_inertia_on_gpu(gpu):
                                      seed=2), device=gpu).fit(x).result_
     inert = [h["inertia"] for h in r.history]
     assert len(inert) == 6 and all(b <= a * 1.0001 for a, b in zip(inert, inert[1:]))
+
+
+def test_hybrid_resident_host_stream(gpu):
+    xh = gaussian_blobs(150_000, 32, 16, seed=3, dtype=torch.float32).numpy()
+    hs = HostSource(xh, (torch.bfloat16, 32), gpu, resident_rows=70_000)
+    for _ in range(2):  # second pass reuses the resident prefix
+        got = torch.cat([c.clone() for _, c in hs.chunks(25_000)]).cpu()
+        assert torch.equal(got, torch.from_numpy(xh).to(torch.bfloat16))
+    cfg = tdc.ClusterConfig(n_clusters=16, max_iter=5, dtype="bf16", seed=5, hbm_budget_gb=0.02)
+    a = tdc.KMeans(cfg, device=gpu).fit(xh)  # tiny budget -> planner streams + keeps a prefix
+    b = tdc.KMeans(cfg.replace(hbm_budget_gb=0.0), device=gpu).fit(torch.from_numpy(xh).to(gpu))
+    assert a.result_.streamed
+    np.testing.assert_allclose(a.result_.centers, b.result_.centers, rtol=1e-4, atol=1e-4)
