@@ -44,18 +44,6 @@ int tdc_assign_mfma_bf16(const void* X, int64_t N, int64_t ldx, int DP, const vo
   // LDS-DMA ring, 4 waves x P x 32 points per workgroup, 64-centroid stages.
   // TDC_ASSIGN_RING=1 selects the first ring variant (kept for A/B timing).
   static const int ring = getenv("TDC_ASSIGN_RING") ? atoi(getenv("TDC_ASSIGN_RING")) : 2;
-  if (ring == 4 && DP == 128) {  // experimental ring4 (P=4 points tiles per wave, 1 wave/SIMD)
-    static const int nst4 = getenv("TDC_RING4_NST") ? atoi(getenv("TDC_RING4_NST")) : 4;
-    dim3 grid((unsigned)((N + 511) / 512));
-    if (nst4 == 3)
-      hipLaunchKernelGGL((assign_mfma_bf16_ring4_kernel<128, 4, 3, 2>), grid, dim3(256), 0, stream,
-                         x, N, ldx, c, cnorm, ntiles, labels, mind);
-    else
-      hipLaunchKernelGGL((assign_mfma_bf16_ring4_kernel<128, 4, 4, 2>), grid, dim3(256), 0, stream,
-                         x, N, ldx, c, cnorm, ntiles, labels, mind);
-    TDC_CHECK_LAUNCH();
-    return 0;
-  }
   static const int abl = getenv("TDC_ASSIGN_ABL") ? atoi(getenv("TDC_ASSIGN_ABL")) : 0;
   static const int r2cfg = getenv("TDC_RING2_CFG") ? atoi(getenv("TDC_RING2_CFG")) : 0;
   if (DP == 128 && ring == 2 && r2cfg != 0) {  // schedule experiments: QT*10 + NST

@@ -581,202 +581,4 @@ void assign_mfma_bf16_ring2_kernel(const __bf16* __restrict__ X, int64_t N, int6
   }
 }
 
-// ------------------------------------------------------------------------------------
-// Variant 4 ("ring4", experimental, TDC_ASSIGN_RING=4): one wave per SIMD holding P=4
-// point tiles (512 points per workgroup, half the centroid traffic per point of ring2),
-// two accumulator sets so phase q's MFMAs are interleaved with phase q-1's argmin
-// epilogue (sched_group_barrier: ~3 VALU + 1/4 LDS read per MFMA gap), the ring refill
-// issued by inline asm (invisible to the compiler, so its LDS reads are tracked exactly).
-// ------------------------------------------------------------------------------------
-template <int DP, int P, int NST, int QT>
-__global__ __launch_bounds__(256, 1)
-void assign_mfma_bf16_ring4_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
-                                   const __bf16* __restrict__ Cm2, const float* __restrict__ cnorm,
-                                   int ntiles, int32_t* __restrict__ labels,
-                                   float* __restrict__ mind) {
-  constexpr int WAVES = 4;
-  constexpr int BNL = 32 * QT;
-  constexpr int CPR = DP / 8;
-  constexpr int KS = DP / 16;
-  constexpr int HALF = DP / 2;
-  constexpr int TILE_B = BNL * DP * 2;
-  constexpr int NORM_B = BNL * 4;
-  constexpr int STAGE_B = TILE_B + NORM_B;
-  constexpr int PIECES = TILE_B / 1024;
-  constexpr int PPW = PIECES / WAVES;
-  constexpr int NCH = NORM_B / 16;
-  constexpr int NPW = NCH / WAVES;
-  constexpr int VPS = PPW + 1;
-  static_assert(PIECES % WAVES == 0 && NCH % WAVES == 0 && NPW >= 1, "stage split");
-  static_assert(QT % 2 == 0, "phases ping-pong between two accumulator sets");
-  constexpr unsigned EMB = QT * 16 <= 32 ? 31u : 63u;
-  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE_B];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int w = tid >> 6;
-  const int r = lane & 31;
-  const int h = lane >> 5;
-  const int64_t pbase = (int64_t)blockIdx.x * (WAVES * P * 32) + (int64_t)w * (P * 32);
-  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-
-  bf16x8 bq[P][KS];
-#pragma unroll
-  for (int p = 0; p < P; ++p) {
-    int64_t row = pbase + p * 32 + r;
-    if (row >= N) row = N - 1;
-    const bf16x8* src = reinterpret_cast<const bf16x8*>(X + row * ldx + h * HALF);
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk) bq[p][kk] = src[kk];
-  }
-#pragma unroll
-  for (int p = 0; p < P; ++p)
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk) asm volatile("" ::"v"(bq[p][kk]));
-
-  auto issue = [&](int t, int slot) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      const int piece = w * PPW + i;
-      const int L = piece * 64 + lane;
-      const int row = L / CPR, cp = L % CPR;
-      const __bf16* src = Cm2 + ((int64_t)t * BNL + row) * DP + swz<DP>(row, cp) * 8;
-      const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + slot * STAGE_B + piece * 1024);
-      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(dst), "v"(src)
-                   : "memory");
-    }
-    const float* nsrc = cnorm + (int64_t)t * BNL + (w * NPW + (lane < NPW ? lane : 0)) * 4;
-    const unsigned ndst = __builtin_amdgcn_readfirstlane(lds0 + slot * STAGE_B + TILE_B + w * NPW * 16);
-    if (lane < NPW)
-      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(ndst), "v"(nsrc)
-                   : "memory");
-  };
-
-#pragma unroll
-  for (int t = 0; t < NST - 1; ++t) issue(t < ntiles ? t : ntiles - 1, t);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * VPS) : "memory");
-  __builtin_amdgcn_s_barrier();
-
-  float best[P];
-  int bt[P];
-#pragma unroll
-  for (int p = 0; p < P; ++p) {
-    best[p] = INFINITY;
-    bt[p] = 0;
-  }
-  f32x16 accA[P], accB[P];
-#pragma unroll
-  for (int p = 0; p < P; ++p)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) accB[p][i] = accA[p][i] = 3.0e38f;
-
-  auto epilogue = [&](f32x16 (&acc)[P], int q, int t) __attribute__((always_inline)) {
-#pragma unroll
-    for (int p = 0; p < P; ++p) {
-      float m = INFINITY;
-#pragma unroll
-      for (int i = 0; i < 16; ++i)
-        m = __builtin_fminf(m, __uint_as_float((__float_as_uint(acc[p][i]) & ~EMB) | (unsigned)(q * 16 + i)));
-      const bool up = m < best[p];
-      best[p] = up ? m : best[p];
-      bt[p] = up ? t : bt[p];
-    }
-  };
-
-  auto phase = [&](const char* sp, int q, f32x16 (&acc_cur)[P], f32x16 (&acc_prev)[P],
-                   int prev_q, int prev_t) __attribute__((always_inline)) {
-    const char* arow = sp + (q * 32 + r) * (DP * 2);
-    f32x4 n4[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      n4[j] = *reinterpret_cast<const f32x4*>(sp + TILE_B + (q * 32 + 8 * j + 4 * h) * 4);
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk) {
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(arow + swz<DP>(q * 32 + r, h * (CPR / 2) + kk) * 16);
-#pragma unroll
-      for (int p = 0; p < P; ++p) {
-        if (kk == 0) {
-          f32x16 init;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            init[4 * j + 0] = n4[j][0];
-            init[4 * j + 1] = n4[j][1];
-            init[4 * j + 2] = n4[j][2];
-            init[4 * j + 3] = n4[j][3];
-          }
-          acc_cur[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bq[p][0], init, 0, 0, 0);
-        } else {
-          acc_cur[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bq[p][kk], acc_cur[p], 0, 0, 0);
-        }
-      }
-    }
-    epilogue(acc_prev, prev_q, prev_t);
-    // schedule: norms + fragments 0,1 first; per k-step P MFMAs, each followed by ~3
-    // epilogue VALU; the read of fragment kk+2 after the k-step
-    __builtin_amdgcn_sched_group_barrier(0x100, KS > 1 ? 6 : 5, 0);
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk) {
-#pragma unroll
-      for (int p = 0; p < P; ++p) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-      }
-      if (kk + 2 < KS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    }
-  };
-
-  int prev_t = 0;
-  auto stage = [&](int t, auto slot_c) __attribute__((always_inline)) {
-    constexpr int slot = decltype(slot_c)::value;
-    {
-      const int tn = t + NST - 1;
-      issue(tn < ntiles ? tn : ntiles - 1, (slot + NST - 1) % NST);
-    }
-    const char* sp = smem + slot * STAGE_B;
-#pragma unroll
-    for (int q = 0; q < QT; q += 2) {
-      phase(sp, q, accA, accB, QT - 1, q == 0 ? prev_t : t);
-      phase(sp, q + 1, accB, accA, q, t);
-    }
-    prev_t = t;
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * VPS) : "memory");
-    __builtin_amdgcn_s_barrier();
-  };
-
-  for (int t0 = 0; t0 < ntiles; t0 += NST) {
-    stage(t0, std::integral_constant<int, 0>{});
-    if constexpr (NST > 1) if (t0 + 1 < ntiles) stage(t0 + 1, std::integral_constant<int, 1>{});
-    if constexpr (NST > 2) if (t0 + 2 < ntiles) stage(t0 + 2, std::integral_constant<int, 2 % NST>{});
-    if constexpr (NST > 3) if (t0 + 3 < ntiles) stage(t0 + 3, std::integral_constant<int, 3 % NST>{});
-  }
-  epilogue(accB, QT - 1, prev_t);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-#pragma unroll
-  for (int p = 0; p < P; ++p) {
-    float s = 0.f;
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float f = (float)bq[p][kk][j];
-        s = fmaf(f, f, s);
-      }
-    const float xn = s + __shfl_xor(s, 32, 64);
-    const float ob = __shfl_xor(best[p], 32, 64);
-    const int obt = __shfl_xor(bt[p], 32, 64);
-    const unsigned e0 = __float_as_uint(best[p]) & EMB, e1 = __float_as_uint(ob) & EMB;
-    const int l0 = bt[p] * BNL + (int)(e0 >> 4) * 32 + (int)(e0 & 3) + 8 * (int)((e0 & 15) >> 2) + 4 * h;
-    const int l1 = obt * BNL + (int)(e1 >> 4) * 32 + (int)(e1 & 3) + 8 * (int)((e1 & 15) >> 2) + 4 * (1 - h);
-    const float v0 = __uint_as_float(__float_as_uint(best[p]) & ~EMB);
-    const float v1 = __uint_as_float(__float_as_uint(ob) & ~EMB);
-    const bool other = (v1 < v0) || (v1 == v0 && l1 < l0);
-    const int64_t row = pbase + p * 32 + r;
-    if (h == 0 && row < N) {
-      labels[row] = other ? l1 : l0;
-      if (mind) mind[row] = fmaxf((other ? v1 : v0) + xn, 0.f);
-    }
-  }
-}
-
 }  // namespace tdc
