@@ -194,3 +194,58 @@ def test_cli_log_every_profile_and_timeout_flags(tmp_path):
     hist = json.loads(ext.read_text().strip())["history"]
     assert [h["iter"] for h in hist] == [3, 6] and all(h["inertia"] > 0 for h in hist)
     assert (prof / "trace_rank0.json").exists() and (prof / "kernels_rank0.txt").exists()
+
+
+def _resume_worker(rank, world, port, path, crash, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    if crash:
+        os.environ["TDC_FAULT"] = "crash@3"
+    else:
+        os.environ.pop("TDC_FAULT", None)
+    torch.set_num_threads(1)
+    import tensorflow_distributed_clustering_amd as tdc
+    from tensorflow_distributed_clustering_amd.parallel import dist as D
+    from tensorflow_distributed_clustering_amd.utils import faults as F
+    D._COMM = None
+    comm = D.init_comm("cpu")
+    s, e = comm.shard(6001)
+    x = gaussian_blobs(e - s, 3, 5, seed=4, row_offset=s, dtype=torch.float64)
+    cfg = tdc.ClusterConfig(n_clusters=5, max_iter=8, dtype="fp64", seed=2,
+                            checkpoint_path=path, checkpoint_every=1, resume=not crash)
+    try:
+        r = tdc.KMeans(cfg, comm).fit(x, n_global=6001, row_offset=s).result_
+        if rank == 0:
+            q.put(("ok", r.centers))
+    except F.InjectedFault:
+        if rank == 0:
+            q.put(("crashed", None))
+    D.destroy_comm()
+
+
+def _world2(path, crash):
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_resume_worker, args=(r, 2, port, path, crash, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+    return out
+
+
+def test_distributed_crash_and_resume(tmp_path):
+    path = str(tmp_path / "dist.npz")
+    status, _ = _world2(path, crash=True)
+    assert status == "crashed" and ck.load(path).n_iter == 3
+    status, centers = _world2(path, crash=False)
+    assert status == "ok"
+    x = gaussian_blobs(6001, 3, 5, seed=4, dtype=torch.float64)
+    full = tdc.KMeans(tdc.ClusterConfig(n_clusters=5, max_iter=8, dtype="fp64", seed=2)).fit(x)
+    np.testing.assert_allclose(centers, full.result_.centers, rtol=1e-10, atol=1e-10)
