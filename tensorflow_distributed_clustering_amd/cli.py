@@ -26,7 +26,6 @@ import json
 import os
 import subprocess
 import sys
-import time
 import traceback
 
 LOG_HEADER = ["method_name", "seed", "num_GPUs", "K", "n_obs", "n_dim", "setup_time",

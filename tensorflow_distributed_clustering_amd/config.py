@@ -9,7 +9,7 @@ semantics and whose ``compat`` value reproduces the reference behaviour.
 from __future__ import annotations
 
 import dataclasses
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Optional
 
 METHODS = ("distributedKMeans", "distributedFuzzyCMeans", "miniBatchKMeans")

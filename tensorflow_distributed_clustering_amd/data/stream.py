@@ -15,7 +15,6 @@ already in the kernel layout (``layout = (torch dtype, padded width)``):
 """
 from __future__ import annotations
 
-import math
 from typing import Iterator, Optional, Tuple
 
 import numpy as np

@@ -14,7 +14,6 @@ from __future__ import annotations
 import time
 from typing import Optional
 
-import numpy as np
 import torch
 
 from ..config import ClusterConfig

@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import datetime
 import os
-from typing import List, Optional, Sequence, Tuple
+from typing import List, Optional, Tuple
 
 import torch
 import torch.distributed as dist

@@ -4,8 +4,6 @@ label with the initial and final centers overlaid.  Written as self-contained SV
 plotting dependency); the first two feature columns are plotted."""
 from __future__ import annotations
 
-from typing import Optional
-
 import numpy as np
 
 PALETTE = ["#1f77b4", "#ff7f0e", "#2ca02c", "#d62728", "#9467bd", "#8c564b", "#e377c2",
