@@ -157,6 +157,8 @@ def build_parser():
                         help="replay each iteration from a captured HIP graph (1 GPU)")
     parser.add_argument("--deterministic", action="store_true",
                         help="run-to-run bitwise reproducible centroid update")
+    parser.add_argument("--spherical", action="store_true",
+                        help="cosine (spherical) K-Means: unit-normalised rows and centroids")
     return parser
 
 
@@ -212,7 +214,8 @@ def run(args) -> int:
                             checkpoint_path=args.checkpoint or "",
                             checkpoint_every=args.checkpoint_every, resume=args.resume,
                             hbm_budget_gb=args.hbm_budget_gb, deterministic=args.deterministic,
-                            graph=args.graph, log_every=args.log_every)
+                            graph=args.graph, log_every=args.log_every,
+                            spherical=args.spherical)
         xt = torch.from_numpy(np.asarray(x))
         if args.method_name == "distributedKMeans":
             model = KMeans(cfg, comm)

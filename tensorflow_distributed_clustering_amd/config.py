@@ -65,6 +65,7 @@ class ClusterConfig:
     resume: bool = False        # continue from checkpoint_path if it exists
     max_oom_retries: int = 4    # setup OOM -> halve the streamed chunk and retry
     graph: bool = False         # replay each Lloyd step from a captured hipGraph
+    spherical: bool = False     # cosine / spherical K-Means: unit rows, unit centroids
 
     def __post_init__(self):
         if self.n_clusters <= 0:

@@ -75,6 +75,8 @@ class FuzzyCMeans:
 
     def fit(self, x_local, init_centers_=None, n_global=None, row_offset=None) -> "FuzzyCMeans":
         cfg = self.cfg
+        if cfg.spherical:
+            raise ValueError("spherical=True is implemented for KMeans (Lloyd) only")
         t0 = time.perf_counter()
         x_local = torch.as_tensor(x_local)
         dev = torch.device(self.device) if self.device is not None else (

@@ -86,6 +86,11 @@ class LloydEngine:
         k = cfg.n_clusters
         self.k = k
         if isinstance(source, torch.Tensor):
+            if cfg.spherical:
+                # cosine K-Means: on unit vectors ||x - c||^2 = 2 - 2 cos(x, c) for unit c,
+                # so the L2 kernels rank by cosine once rows and centroids are normalised
+                n = source.float().norm(dim=1, keepdim=True).clamp_min_(1e-30)
+                source = (source.float() / n).to(source.dtype)
             x0 = source
             self.local = make_lloyd_ops(source, k, cfg.dtype, cfg.backend, cfg.empty_cluster,
                                         cfg.deterministic)
@@ -95,6 +100,8 @@ class LloydEngine:
             self.d = int(source.shape[1])
             self.n_local = int(source.shape[0])
         else:
+            if cfg.spherical:
+                raise ValueError("spherical K-Means needs a resident shard (normalised once)")
             self.source = source
             self.device = torch.device(getattr(source, "device", comm.device))
             self.d = int(source.d)
@@ -142,6 +149,8 @@ class LloydEngine:
         else:
             c0 = init_centers_from_source(cfg.init, self.source, self.row_offset, self.n_global,
                                           k, comm, cfg.seed, given=self._init_given, d=self.d)
+        if cfg.spherical:
+            c0 = c0 / c0.norm(dim=1, keepdim=True).clamp_min(1e-30)
         self.c0 = c0
         self.C.copy_(c0.to(self.local.c_dtype))  # never alias c0
         self.local.prepare(self.C)
@@ -183,6 +192,9 @@ class LloydEngine:
         if self.shift is not None:
             self.shift.zero_()
         self.local.finalize(self.sums, self.counts, self.C, self.shift)
+        if self.cfg.spherical:  # project the means back to the sphere
+            self.C.div_(self.C.norm(dim=1, keepdim=True).clamp_min_(1e-30))
+            self.local.prepare(self.C)
         if self.cfg.empty_cluster == "reseed":
             self._reseed()
         self.n_iter += 1

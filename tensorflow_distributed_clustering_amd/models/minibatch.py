@@ -138,6 +138,8 @@ class MiniBatchKMeans:
 
     def fit(self, x_local, init_centers_=None, n_global=None, row_offset=None) -> "MiniBatchKMeans":
         cfg = self.cfg
+        if cfg.spherical:
+            raise ValueError("spherical=True is implemented for KMeans (Lloyd) only")
         t0 = time.perf_counter()
         if hasattr(x_local, "chunks"):
             dev = torch.device(getattr(x_local, "device", "cpu"))

@@ -128,3 +128,19 @@ def test_kmeans_parallel_init_quality():
         res[init] = tdc.KMeans(tdc.ClusterConfig(n_clusters=20, max_iter=0, dtype="fp64",
                                                  init=init, seed=2)).fit(x).result_.inertia
     assert res["kmeans||"] < 0.6 * res["random"]
+
+
+def test_spherical_kmeans_matches_cosine_reference():
+    g = torch.Generator().manual_seed(0)
+    dirs = torch.nn.functional.normalize(torch.randn(6, 16, generator=g, dtype=torch.float64), dim=1)
+    lab = torch.randint(0, 6, (6000,), generator=g)
+    scale = torch.rand(6000, 1, generator=g, dtype=torch.float64) * 10 + 0.1  # norms must not matter
+    x = (dirs[lab] + 0.05 * torch.randn(6000, 16, generator=g, dtype=torch.float64)) * scale
+    r = tdc.KMeans(tdc.ClusterConfig(n_clusters=6, max_iter=15, dtype="fp64", spherical=True,
+                                     init="kmeans++", seed=1)).fit(x).result_
+    c = torch.as_tensor(r.centers)
+    torch.testing.assert_close(c.norm(dim=1), torch.ones(6, dtype=torch.float64))
+    cos = torch.nn.functional.normalize(x, dim=1) @ c.t()
+    assert torch.equal(cos.argmax(1).to(torch.int32), r.labels)
+    # every true direction is recovered by some centroid
+    assert (dirs @ c.t()).max(1).values.min() > 0.99

@@ -98,3 +98,16 @@ def test_hybrid_resident_host_stream(gpu):
     b = tdc.KMeans(cfg.replace(hbm_budget_gb=0.0), device=gpu).fit(torch.from_numpy(xh).to(gpu))
     assert a.result_.streamed
     np.testing.assert_allclose(a.result_.centers, b.result_.centers, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_spherical_kmeans_gpu_bf16(gpu):
+    g = torch.Generator().manual_seed(3)
+    dirs = torch.nn.functional.normalize(torch.randn(32, 128, generator=g), dim=1)
+    lab = torch.randint(0, 32, (200_000,), generator=g)
+    x = (dirs[lab] + 0.02 * torch.randn(200_000, 128, generator=g)) * (1 + 5 * torch.rand(200_000, 1, generator=g))
+    r = tdc.KMeans(tdc.ClusterConfig(n_clusters=32, max_iter=10, dtype="bf16", spherical=True,
+                                     init="kmeans++", seed=0)).fit(x.cuda()).result_
+    c = torch.as_tensor(r.centers).float().cpu()
+    torch.testing.assert_close(c.norm(dim=1), torch.ones(32), atol=1e-2, rtol=0)
+    assert (dirs @ c.t()).max(1).values.min() > 0.98
