@@ -17,6 +17,8 @@
 //                 (~1-3 flushes per wave instead of one atomic per element).
 //
 // X is read exactly once (as whole-row gathers); labels twice; the permutation once.
+#include <stdlib.h>
+
 #include <algorithm>
 
 #include "tdc_common.h"
@@ -150,7 +152,8 @@ __global__ __launch_bounds__(256) void scatter_kernel(const int32_t* __restrict_
 // global atomic per non-empty bin to reserve the block's sub-range of that segment, then
 // the scatter with LDS cursors.  (The per-4096-label passes of scatter_kernel reserved
 // once per bin per pass: ~5x more global atomics at N=10M, K=1024.)
-__global__ __launch_bounds__(256) void bscatter_kernel(const int32_t* __restrict__ labels, int64_t N,
+template <int NT>
+__global__ __launch_bounds__(NT) void bscatter_kernel(const int32_t* __restrict__ labels, int64_t N,
                                                        int K, int* __restrict__ cursor,
                                                        int32_t* __restrict__ perm, int64_t per_block) {
   extern __shared__ int s_mem[];
@@ -159,35 +162,35 @@ __global__ __launch_bounds__(256) void bscatter_kernel(const int32_t* __restrict
   const int tid = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.x * per_block;
   const int64_t r1 = min(N, r0 + per_block);
-  for (int k = tid; k < K; k += 256) s_cnt[k] = 0;
+  for (int k = tid; k < K; k += NT) s_cnt[k] = 0;
   __syncthreads();
   int64_t i = r0 + tid;
-  for (; i + 3 * 256 < r1; i += 4 * 256) {
-    const int a0 = labels[i], a1 = labels[i + 256], a2 = labels[i + 512], a3 = labels[i + 768];
+  for (; i + 3 * NT < r1; i += 4 * NT) {
+    const int a0 = labels[i], a1 = labels[i + NT], a2 = labels[i + 2 * NT], a3 = labels[i + 3 * NT];
     if ((unsigned)a0 < (unsigned)K) atomicAdd(s_cnt + a0, 1);
     if ((unsigned)a1 < (unsigned)K) atomicAdd(s_cnt + a1, 1);
     if ((unsigned)a2 < (unsigned)K) atomicAdd(s_cnt + a2, 1);
     if ((unsigned)a3 < (unsigned)K) atomicAdd(s_cnt + a3, 1);
   }
-  for (; i < r1; i += 256) {
+  for (; i < r1; i += NT) {
     const int a0 = labels[i];
     if ((unsigned)a0 < (unsigned)K) atomicAdd(s_cnt + a0, 1);
   }
   __syncthreads();
-  for (int k = tid; k < K; k += 256) {
+  for (int k = tid; k < K; k += NT) {
     const int c = s_cnt[k];
     s_cur[k] = c ? atomicAdd(cursor + k, c) : 0;
   }
   __syncthreads();
   i = r0 + tid;
-  for (; i + 3 * 256 < r1; i += 4 * 256) {
-    const int a0 = labels[i], a1 = labels[i + 256], a2 = labels[i + 512], a3 = labels[i + 768];
+  for (; i + 3 * NT < r1; i += 4 * NT) {
+    const int a0 = labels[i], a1 = labels[i + NT], a2 = labels[i + 2 * NT], a3 = labels[i + 3 * NT];
     if ((unsigned)a0 < (unsigned)K) perm[atomicAdd(s_cur + a0, 1)] = (int32_t)i;
-    if ((unsigned)a1 < (unsigned)K) perm[atomicAdd(s_cur + a1, 1)] = (int32_t)(i + 256);
-    if ((unsigned)a2 < (unsigned)K) perm[atomicAdd(s_cur + a2, 1)] = (int32_t)(i + 512);
-    if ((unsigned)a3 < (unsigned)K) perm[atomicAdd(s_cur + a3, 1)] = (int32_t)(i + 768);
+    if ((unsigned)a1 < (unsigned)K) perm[atomicAdd(s_cur + a1, 1)] = (int32_t)(i + NT);
+    if ((unsigned)a2 < (unsigned)K) perm[atomicAdd(s_cur + a2, 1)] = (int32_t)(i + 2 * NT);
+    if ((unsigned)a3 < (unsigned)K) perm[atomicAdd(s_cur + a3, 1)] = (int32_t)(i + 3 * NT);
   }
-  for (; i < r1; i += 256) {
+  for (; i < r1; i += NT) {
     const int a0 = labels[i];
     if ((unsigned)a0 < (unsigned)K) perm[atomicAdd(s_cur + a0, 1)] = (int32_t)i;
   }
@@ -222,7 +225,11 @@ template <> struct RowLoad<double, 2> {
 template <typename XT, int VEC> struct RowRaw;
 template <> struct RowRaw<__bf16, 8> {
   typedef uint4 raw_t;
-  __device__ static raw_t load(const __bf16* p) { return *reinterpret_cast<const uint4*>(p); }
+  __device__ static raw_t load(const __bf16* p) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
   __device__ static void add(const raw_t& t, float (&a)[8]) {
     a[0] += __uint_as_float(t.x << 16); a[1] += __uint_as_float(t.x & 0xffff0000u);
     a[2] += __uint_as_float(t.y << 16); a[3] += __uint_as_float(t.y & 0xffff0000u);
@@ -441,12 +448,23 @@ int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int6
                        (float*)counts);
   TDC_CHECK_LAUNCH();
   if (K <= LDS_HIST_MAX_K) {
-    int64_t blocks = (int64_t)num_cus * 2;
+    // one 1024-thread block per CU: 16 waves keep the LDS-rank -> store chains in flight
+    // (2 x 256-thread blocks per CU measured 122 us at N=10M, K=1024); still one
+    // reservation atomic per non-empty bin per block
+    static const int nt = [] {
+      const char* e = getenv("TDC_BSCATTER_THREADS");
+      return (e && atoi(e) == 256) ? 256 : 1024;
+    }();
+    int64_t blocks = nt == 1024 ? (int64_t)num_cus : (int64_t)num_cus * 2;
     int64_t per = (N + blocks - 1) / blocks;
     if (per < 4096) per = 4096;
     blocks = (N + per - 1) / per;
-    hipLaunchKernelGGL(bscatter_kernel, dim3((unsigned)blocks), dim3(256), 2 * sizeof(int) * (size_t)K,
-                       s, labels, N, K, cursor, perm, per);
+    if (nt == 1024)
+      hipLaunchKernelGGL(bscatter_kernel<1024>, dim3((unsigned)blocks), dim3(1024),
+                         2 * sizeof(int) * (size_t)K, s, labels, N, K, cursor, perm, per);
+    else
+      hipLaunchKernelGGL(bscatter_kernel<256>, dim3((unsigned)blocks), dim3(256),
+                         2 * sizeof(int) * (size_t)K, s, labels, N, K, cursor, perm, per);
     TDC_CHECK_LAUNCH();
   } else {
     int64_t blocks = (int64_t)num_cus * 4;
