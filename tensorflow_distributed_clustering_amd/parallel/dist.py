@@ -39,8 +39,9 @@ class Comm:
     """Thin handle over the default process group (or a single-process no-op)."""
 
     def __init__(self, device: torch.device, rank: int = 0, world_size: int = 1,
-                 local_rank: int = 0, group=None):
+                 local_rank: int = 0, group=None, backend: str = ""):
         self.device = device
+        self.backend = backend
         self.rank = rank
         self.world_size = world_size
         self.local_rank = local_rank
@@ -95,7 +96,7 @@ class Comm:
 
     def barrier(self):
         if self.world_size > 1:
-            if self.device.type == "cuda":
+            if self.device.type == "cuda" and self.backend == "nccl":
                 dist.barrier(group=self.group, device_ids=[self.device.index])
             else:
                 dist.barrier(group=self.group)
@@ -128,8 +129,10 @@ class Comm:
             return local
         sizes = self.all_gather_sizes(local.shape[0])
         mx = max(sizes)
-        buf = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=self.device)
-        buf[: local.shape[0]] = local
+        # gloo gathers host tensors only (GPU ranks over gloo: TDC_DIST_BACKEND=gloo)
+        dev = torch.device("cpu") if self.backend == "gloo" else self.device
+        buf = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=dev)
+        buf[: local.shape[0]] = local.to(dev)
         if self.rank == 0:
             bufs = [torch.empty_like(buf) for _ in range(self.world_size)]
             dist.gather(buf, gather_list=bufs, dst=0, group=self.group)
@@ -162,15 +165,19 @@ def init_comm(device_type: Optional[str] = None, timeout_s: float = 600.0) -> Co
     else:
         device = torch.device("cpu")
     group = None
+    # TDC_DIST_BACKEND=gloo runs GPU ranks over gloo (host-staged collectives): rehearses the
+    # multi-rank GPU path with several ranks on ONE GPU, which RCCL does not allow
+    backend = os.environ.get("TDC_DIST_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if device_type == "cuda" else "gloo"
         kw = dict(backend=backend, init_method="env://", world_size=world, rank=rank,
                   timeout=datetime.timedelta(seconds=timeout_s))
-        if device_type == "cuda":
+        if device_type == "cuda" and backend == "nccl":
             kw["device_id"] = device
         dist.init_process_group(**kw)
-    _COMM = Comm(device, rank, world, local_rank, group)
+    if dist.is_initialized():
+        backend = str(dist.get_backend())
+    _COMM = Comm(device, rank, world, local_rank, group, backend if world > 1 else "")
     return _COMM
 
 

@@ -1,0 +1,79 @@
+"""Multi-rank GPU path on ONE MI355X: ranks share cuda:0 and talk over gloo
+(``TDC_DIST_BACKEND=gloo``; RCCL refuses two ranks on one device).  Everything but the
+transport is the production path: on-device shard generation, world-size-invariant
+init, the HIP kernels, the packed all-reduce of [sums | counts] and the replicated
+finalize.  World 2 must reproduce world 1 (up to float-atomic summation order).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q, dtype, n, d, k, iters, method):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank), TDC_DIST_BACKEND="gloo")
+    import tensorflow_distributed_clustering_amd as tdc
+    from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs
+    from tensorflow_distributed_clustering_amd.parallel import dist as D
+    D._COMM = None
+    comm = D.init_comm("cuda")
+    s, e = comm.shard(n)
+    tdt = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp64": torch.float64}[dtype]
+    x = gaussian_blobs(e - s, d, k, seed=3, row_offset=s, dtype=tdt, device=comm.device)
+    cfg = tdc.ClusterConfig(n_clusters=k, max_iter=iters, dtype=dtype, init="random", seed=3)
+    model = (tdc.KMeans if method == "kmeans" else tdc.FuzzyCMeans)(cfg, comm)
+    model.fit(x, n_global=n, row_offset=s)
+    r = model.result_
+    labels = comm.gather_rows_to_root(torch.as_tensor(r.labels, device=comm.device))
+    if rank == 0:
+        q.put((np.asarray(r.centers), labels.cpu().numpy(), r.backend))
+    D.destroy_comm()
+
+
+def _run(world, dtype, n, d, k, iters=4, method="kmeans"):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, dtype, n, d, k, iters, method))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=100)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return out
+
+
+def test_bf16_mfma_two_ranks_match_one(gpu):
+    c1, l1, b1 = _run(1, "bf16", 200_003, 128, 256)
+    c2, l2, b2 = _run(2, "bf16", 200_003, 128, 256)
+    assert b1 == b2 == "hip_bf16_mfma"
+    np.testing.assert_allclose(c2, c1, rtol=1e-3, atol=1e-3)
+    assert (l1 == l2).mean() > 0.999
+
+
+def test_fp64_fused_two_ranks_match_one(gpu):
+    c1, l1, _ = _run(1, "fp64", 100_001, 5, 3)
+    c2, l2, _ = _run(2, "fp64", 100_001, 5, 3)
+    np.testing.assert_allclose(c2, c1, rtol=1e-10, atol=1e-10)
+    np.testing.assert_array_equal(l2, l1)
+
+
+def test_fcm_two_ranks_match_one(gpu):
+    c1, l1, _ = _run(1, "fp64", 50_000, 5, 4, method="fcm")
+    c2, l2, _ = _run(2, "fp64", 50_000, 5, 4, method="fcm")
+    np.testing.assert_allclose(c2, c1, rtol=1e-9, atol=1e-9)
+    np.testing.assert_array_equal(l2, l1)
