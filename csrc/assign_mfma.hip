@@ -43,7 +43,7 @@ int tdc_assign_mfma_bf16(const void* X, int64_t N, int64_t ldx, int DP, const vo
   const __bf16* c = (const __bf16*)Cm2;
   // LDS-DMA ring, 4 waves x P x 32 points per workgroup, 64-centroid stages.
   // TDC_ASSIGN_RING=1 selects the first ring variant (kept for A/B timing).
-  static const int ring = getenv("TDC_ASSIGN_RING") ? atoi(getenv("TDC_ASSIGN_RING")) : 2;
+  static const int ring = getenv("TDC_ASSIGN_RING") ? atoi(getenv("TDC_ASSIGN_RING")) : 3;
   static const int abl = getenv("TDC_ASSIGN_ABL") ? atoi(getenv("TDC_ASSIGN_ABL")) : 0;
   static const int r2cfg = getenv("TDC_RING2_CFG") ? atoi(getenv("TDC_RING2_CFG")) : 0;
   if (DP == 128 && ring == 2 && r2cfg != 0) {  // schedule experiments: QT*10 + NST
@@ -67,6 +67,37 @@ int tdc_assign_mfma_bf16(const void* X, int64_t N, int64_t ldx, int DP, const vo
                        stream, x, N, ldx, c, cnorm, ntiles, labels, mind);
     TDC_ABL(1) TDC_ABL(2) TDC_ABL(4) TDC_ABL(7) TDC_ABL(8)
 #undef TDC_ABL
+    TDC_CHECK_LAUNCH();
+    return 0;
+  }
+  static const int r3cfg = getenv("TDC_RING3_CFG") ? atoi(getenv("TDC_RING3_CFG")) : 0;
+  if (ring == 3 && DP == 128 && r3cfg != 0) {  // schedule experiments: WAVES*1000+P*100+QT*10+NST
+#define TDC_R3(WV, PV, QTV, NSTV)                                                                  \
+  if (r3cfg == WV * 1000 + PV * 100 + QTV * 10 + NSTV) {                                           \
+    if (Kp % (16 * QTV) != 0) return (int)hipErrorInvalidValue;                                    \
+    const int64_t per = WV * PV * 16;                                                              \
+    hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<128, PV, NSTV, WV, QTV>),                    \
+                       dim3((unsigned)((N + per - 1) / per)), dim3(WV * 64), 0, stream, x, N, ldx, \
+                       c, cnorm, Kp / (16 * QTV), labels, mind);                                   \
+  }
+    TDC_R3(4, 4, 2, 3) TDC_R3(4, 4, 8, 2) TDC_R3(4, 2, 4, 3) TDC_R3(4, 8, 4, 3)
+    TDC_R3(8, 4, 4, 3) TDC_R3(4, 4, 4, 2) TDC_R3(4, 4, 2, 4)
+#undef TDC_R3
+    TDC_CHECK_LAUNCH();
+    return 0;
+  }
+  if (ring == 3 && (DP == 64 || DP == 128 || DP == 256)) {  // 16x16x32 MFMA variant
+    const int64_t per = 4 * 4 * 16;
+    dim3 grid((unsigned)((N + per - 1) / per));
+    if (DP == 64)
+      hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<64, 4, 3, 4, 4>), grid, dim3(256), 0,
+                         stream, x, N, ldx, c, cnorm, Kp / 64, labels, mind);
+    else if (DP == 128)
+      hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<128, 4, 3, 4, 4>), grid, dim3(256), 0,
+                         stream, x, N, ldx, c, cnorm, Kp / 64, labels, mind);
+    else
+      hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<256, 4, 2, 4, 4>), grid, dim3(256), 0,
+                         stream, x, N, ldx, c, cnorm, Kp / 64, labels, mind);
     TDC_CHECK_LAUNCH();
     return 0;
   }

@@ -581,4 +581,202 @@ void assign_mfma_bf16_ring2_kernel(const __bf16* __restrict__ X, int64_t N, int6
   }
 }
 
+
+// ------------------------------------------------------------------------------------
+// Variant 4 ("ring3"): ring2's pipeline on v_mfma_f32_16x16x32_bf16 instead of 32x32x16.
+// Same FLOP per cycle and the same A-fragment LDS traffic per FLOP (each A fragment is
+// shared by P=4 point tiles of 16), but MI355X holds a higher clock under the 16x16
+// shape on random data (MI355X_MICROARCH.md "DVFS give-back" item 7: ~1.12-1.15x FLOP/s
+// at equal cycles per FLOP).  C layout: lane l holds rows 4*(l>>4)+i (centroids) of
+// column l&15 (its point); the 4 lane groups are combined once at the end.
+// ------------------------------------------------------------------------------------
+template <int DP, int P, int NST, int WAVES, int QT>
+__global__ __launch_bounds__(WAVES * 64, (WAVES % 4 == 0 ? (WAVES / 4 > 1 ? WAVES / 4 : 3) : 2))
+void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
+                                   const __bf16* __restrict__ Cm2, const float* __restrict__ cnorm,
+                                   int ntiles, int32_t* __restrict__ labels,
+                                   float* __restrict__ mind) {
+  constexpr int BNL = 16 * QT;                     // centroids per stage
+  constexpr int CPR = DP / 8;
+  constexpr int KS = DP / 32;                      // 32-deep k-steps
+  constexpr int TILE_B = BNL * DP * 2;
+  constexpr int NORM_B = BNL * 4;
+  constexpr int STAGE_B = TILE_B + NORM_B;
+  constexpr int PIECES = TILE_B / 1024;
+  constexpr int PPW = PIECES / WAVES;
+  constexpr int NCH = NORM_B / 16;
+  constexpr int NPW = NCH / WAVES;
+  constexpr int VPS = PPW + 1;
+  static_assert(PIECES % WAVES == 0 && NCH % WAVES == 0 && NPW >= 1, "stage split");
+  static_assert(KS >= 1, "DP >= 32");
+  constexpr unsigned EMB = QT * 4 <= 16 ? 15u : 31u;  // (q, reg) id bits in the mantissa
+  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE_B];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = tid >> 6;
+  const int r = lane & 15;   // point column of the tile / centroid row of the A fragment
+  const int g = lane >> 4;   // k-group of the operands / row group of the accumulator
+  const int64_t pbase = (int64_t)blockIdx.x * (WAVES * P * 16) + (int64_t)w * (P * 16);
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+
+  bf16x8 bq[P][KS];
+  float xn[P] = {};
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    int64_t row = pbase + p * 16 + r;
+    if (row >= N) row = N - 1;
+    const __bf16* src = X + row * ldx + g * 8;
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) bq[p][kk] = *reinterpret_cast<const bf16x8*>(src + kk * 32);
+  }
+  // ||x||^2 only feeds the optional min-distance output: skip its ~5 VALU per element
+  // when the caller does not ask for it (uniform branch)
+  if (mind) {
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      float s = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = (float)bq[p][kk][j];
+          s = fmaf(f, f, s);
+        }
+      s += __shfl_xor(s, 16, 64);
+      xn[p] = s + __shfl_xor(s, 32, 64);
+    }
+  }
+
+  auto issue = [&](int t, int slot) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int piece = w * PPW + i;
+      const int L = piece * 64 + lane;
+      const int row = L / CPR, cp = L % CPR;
+      const int csrc = swz<DP>(row, cp);
+      const __bf16* src = Cm2 + ((int64_t)t * BNL + row) * DP + csrc * 8;
+      __builtin_amdgcn_global_load_lds(
+          (const void*)src,
+          (__attribute__((address_space(3))) void*)(smem + slot * STAGE_B + piece * 1024), 16, 0, 0);
+    }
+    if (lane < NPW) {
+      const float* src = cnorm + (int64_t)t * BNL + (w * NPW + lane) * 4;
+      __builtin_amdgcn_global_load_lds(
+          (const void*)src,
+          (__attribute__((address_space(3))) void*)(smem + slot * STAGE_B + TILE_B + w * NPW * 16),
+          16, 0, 0);
+    }
+  };
+
+#pragma unroll
+  for (int t = 0; t < NST - 1; ++t) issue(t < ntiles ? t : ntiles - 1, t);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * VPS) : "memory");
+  __builtin_amdgcn_s_barrier();
+
+  float best[P];
+  int bt[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    best[p] = INFINITY;
+    bt[p] = 0;
+  }
+
+  // A fragment of k-step kk: row q*16 + r of the stage, 16-B chunk kk*4 + g (the XOR
+  // swizzle depends on r only, so the phase is an immediate offset)
+  unsigned aoff[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) aoff[kk] = lds0 + r * (DP * 2) + swz<DP>(r, kk * 4 + g) * 16;
+  const unsigned noff = lds0 + TILE_B + 16 * g;  // norms of rows q*16 + 4g .. +3
+
+  auto stage = [&](int t, auto slot_c) __attribute__((always_inline)) {
+    constexpr int slot = decltype(slot_c)::value;
+    {
+      const int tn = t + NST - 1;
+      issue(tn < ntiles ? tn : ntiles - 1, (slot + NST - 1) % NST);
+    }
+    // running key minimum of the whole stage (all QT phases): one compare/select per
+    // point tile per stage instead of per phase
+    float m[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) m[p] = INFINITY;
+#pragma unroll
+    for (int q = 0; q < QT; ++q) {
+      auto afrag = [&](int kk) __attribute__((always_inline)) {
+        bf16x8 a;
+        asm volatile("ds_read_b128 %0, %1 offset:%2"
+                     : "=v"(a) : "v"(aoff[kk]), "i"(slot * STAGE_B + q * 16 * DP * 2));
+        return a;
+      };
+      f32x4 n4;
+      asm volatile("ds_read_b128 %0, %1 offset:%2"
+                   : "=v"(n4) : "v"(noff), "i"(slot * STAGE_B + q * 16 * 4));
+      bf16x8 a0 = afrag(0);
+      bf16x8 a1 = afrag(KS > 1 ? 1 : 0);
+      f32x4 acc[P];
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        bf16x8 a2 = a1;
+        if (kk + 2 < KS) a2 = afrag(kk + 2);
+        if (kk + 2 < KS) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+        else if (kk + 1 < KS) asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int p = 0; p < P; ++p)
+          acc[p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bq[p][kk], kk == 0 ? n4 : acc[p],
+                                                            0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        a0 = a1;
+        a1 = a2;
+      }
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float v = __uint_as_float((__float_as_uint(acc[p][i]) & ~EMB) | (unsigned)(q * 4 + i));
+          m[p] = __builtin_fminf(m[p], v);
+        }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const bool up = m[p] < best[p];
+      best[p] = up ? m[p] : best[p];
+      bt[p] = up ? t : bt[p];
+    }
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * VPS) : "memory");  // stage t+1 landed
+    __builtin_amdgcn_s_barrier();  // ... for every wave's pieces
+  };
+
+  for (int t0 = 0; t0 < ntiles; t0 += NST) {
+    stage(t0, std::integral_constant<int, 0>{});
+    if constexpr (NST > 1) if (t0 + 1 < ntiles) stage(t0 + 1, std::integral_constant<int, 1>{});
+    if constexpr (NST > 2) if (t0 + 2 < ntiles) stage(t0 + 2, std::integral_constant<int, 2 % NST>{});
+    if constexpr (NST > 3) if (t0 + 3 < ntiles) stage(t0 + 3, std::integral_constant<int, 3 % NST>{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // ---- combine the 4 lane groups (same point, disjoint centroid rows) ----
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const unsigned e = __float_as_uint(best[p]) & EMB;
+    int lab = bt[p] * BNL + (int)(e >> 2) * 16 + 4 * g + (int)(e & 3);
+    float v = __uint_as_float(__float_as_uint(best[p]) & ~EMB);
+#pragma unroll
+    for (int o = 16; o <= 32; o <<= 1) {
+      const float ov = __shfl_xor(v, o, 64);
+      const int ol = __shfl_xor(lab, o, 64);
+      const bool other = (ov < v) || (ov == v && ol < lab);
+      v = other ? ov : v;
+      lab = other ? ol : lab;
+    }
+    const int64_t row = pbase + p * 16 + r;
+    if (g == 0 && row < N) {
+      labels[row] = lab;
+      if (mind) mind[row] = fmaxf(v + xn[p], 0.f);
+    }
+  }
+}
+
 }  // namespace tdc
