@@ -125,3 +125,27 @@ int tdc_assign_mfma_bf16(const void* X, int64_t N, int64_t ldx, int DP, const vo
   TDC_CHECK_LAUNCH();
   return 0;
 }
+
+// Indexed rows (mini-batches): point i is row rowidx[i] of X; always the ring3 schedule.
+int tdc_assign_mfma_bf16_indexed(const void* X, const int32_t* rowidx, int64_t N, int64_t ldx,
+                                 int DP, const void* Cm2, const float* cnorm, int Kp,
+                                 int32_t* labels, float* mind, hipStream_t stream) {
+  if (N <= 0) return 0;
+  if (Kp % 64 != 0 || rowidx == nullptr) return (int)hipErrorInvalidValue;
+  const __bf16* x = (const __bf16*)X;
+  const __bf16* c = (const __bf16*)Cm2;
+  const dim3 grid((unsigned)((N + 255) / 256));
+  if (DP == 64)
+    hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<64, 4, 3, 4, 4>), grid, dim3(256), 0, stream,
+                       x, N, ldx, c, cnorm, Kp / 64, labels, mind, rowidx);
+  else if (DP == 128)
+    hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<128, 4, 3, 4, 4>), grid, dim3(256), 0,
+                       stream, x, N, ldx, c, cnorm, Kp / 64, labels, mind, rowidx);
+  else if (DP == 256)
+    hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<256, 4, 2, 4, 4>), grid, dim3(256), 0,
+                       stream, x, N, ldx, c, cnorm, Kp / 64, labels, mind, rowidx);
+  else
+    return (int)hipErrorInvalidValue;
+  TDC_CHECK_LAUNCH();
+  return 0;
+}

@@ -595,7 +595,8 @@ __global__ __launch_bounds__(WAVES * 64, (WAVES % 4 == 0 ? (WAVES / 4 > 1 ? WAVE
 void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
                                    const __bf16* __restrict__ Cm2, const float* __restrict__ cnorm,
                                    int ntiles, int32_t* __restrict__ labels,
-                                   float* __restrict__ mind) {
+                                   float* __restrict__ mind,
+                                   const int32_t* __restrict__ rowidx = nullptr) {
   constexpr int BNL = 16 * QT;                     // centroids per stage
   constexpr int CPR = DP / 8;
   constexpr int KS = DP / 32;                      // 32-deep k-steps
@@ -626,6 +627,9 @@ void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int6
   for (int p = 0; p < P; ++p) {
     int64_t row = pbase + p * 16 + r;
     if (row >= N) row = N - 1;
+    // indexed mode (mini-batches): point i of this launch is shard row rowidx[i], so a
+    // sampled batch is never materialised
+    if (rowidx) row = rowidx[row];
     const __bf16* src = X + row * ldx + g * 8;
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) bq[p][kk] = *reinterpret_cast<const bf16x8*>(src + kk * 32);

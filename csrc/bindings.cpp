@@ -218,6 +218,107 @@ void finalize(const std::optional<at::Tensor>& sums, const std::optional<at::Ten
         "finalize");
 }
 
+// rows of a mini-batch by index: point i of the launch is row rowidx[i] of X
+void check_rowidx(const at::Tensor& X, const at::Tensor& rowidx, int64_t n, const char* op) {
+  TORCH_CHECK(rowidx.scalar_type() == at::kInt && rowidx.is_contiguous() && rowidx.dim() == 1,
+              "tdc.", op, ": rowidx must be contiguous int32 [B]");
+  TORCH_CHECK(rowidx.numel() == n, "tdc.", op, ": rowidx/labels length mismatch");
+  TORCH_CHECK(rowidx.device() == X.device(), "tdc.", op, ": rowidx on another device");
+  TORCH_CHECK(X.size(0) < ((int64_t)1 << 31), "tdc.", op, ": X has >= 2^31 rows");
+}
+
+void assign_bf16_indexed(const at::Tensor& X, const at::Tensor& rowidx, const at::Tensor& Cm2,
+                         const at::Tensor& cnorm, at::Tensor& labels,
+                         const std::optional<at::Tensor>& mind) {
+  check_cuda(X, "X");
+  check_rows(X, "X");
+  TORCH_CHECK(X.scalar_type() == at::kBFloat16 && Cm2.scalar_type() == at::kBFloat16,
+              "tdc.assign_bf16_indexed: X and Cm2 must be bfloat16");
+  TORCH_CHECK(cnorm.scalar_type() == at::kFloat && labels.scalar_type() == at::kInt,
+              "tdc.assign_bf16_indexed: cnorm fp32, labels int32");
+  TORCH_CHECK(Cm2.is_contiguous() && cnorm.is_contiguous() && labels.is_contiguous(),
+              "tdc.assign_bf16_indexed: Cm2/cnorm/labels must be contiguous");
+  const int64_t B = rowidx.numel();
+  check_rowidx(X, rowidx, B, "assign_bf16_indexed");
+  const int DP = (int)Cm2.size(1);
+  const int Kp = (int)Cm2.size(0);
+  TORCH_CHECK(DP == 64 || DP == 128 || DP == 256,
+              "tdc.assign_bf16_indexed: padded dim must be 64/128/256, got ", DP);
+  TORCH_CHECK(X.size(1) >= DP, "tdc.assign_bf16_indexed: X has fewer columns than Cm2");
+  TORCH_CHECK(X.stride(0) % 8 == 0 && (reinterpret_cast<uintptr_t>(X.data_ptr()) % 16) == 0,
+              "tdc.assign_bf16_indexed: X rows must be 16-byte aligned");
+  TORCH_CHECK(Kp % 64 == 0 && cnorm.numel() >= Kp, "tdc.assign_bf16_indexed: Kp % 64");
+  TORCH_CHECK(labels.numel() >= B, "tdc.assign_bf16_indexed: labels too small");
+  float* md = nullptr;
+  if (mind.has_value() && mind->defined()) {
+    TORCH_CHECK(mind->scalar_type() == at::kFloat && mind->numel() >= B && mind->is_contiguous(),
+                "tdc.assign_bf16_indexed: mind must be fp32 [B]");
+    md = mind->data_ptr<float>();
+  }
+  const DevGuard guard(X.device());
+  check(tdc_assign_mfma_bf16_indexed(X.data_ptr(), rowidx.data_ptr<int32_t>(), B, X.stride(0), DP,
+                                     Cm2.data_ptr(), cnorm.data_ptr<float>(), Kp,
+                                     labels.data_ptr<int32_t>(), md, cur_stream()),
+        "assign_bf16_indexed");
+}
+
+void update_sorted_indexed(const at::Tensor& X, const at::Tensor& rowidx, const at::Tensor& labels,
+                           at::Tensor& sums, at::Tensor& counts, at::Tensor& work) {
+  check_cuda(X, "X");
+  check_rows(X, "X");
+  const int64_t B = labels.numel();
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous(),
+              "tdc.update_sorted_indexed: labels int32 [B]");
+  check_rowidx(X, rowidx, B, "update_sorted_indexed");
+  TORCH_CHECK(sums.dim() == 2 && sums.is_contiguous() && counts.is_contiguous(),
+              "tdc.update_sorted_indexed: sums");
+  TORCH_CHECK(sums.scalar_type() == counts.scalar_type() && counts.numel() >= sums.size(0),
+              "tdc.update_sorted_indexed: counts");
+  TORCH_CHECK(X.size(1) >= sums.size(1), "tdc.update_sorted_indexed: X narrower than sums");
+  TORCH_CHECK(work.scalar_type() == at::kInt && work.is_contiguous() &&
+                  work.numel() >= tdc_update_sorted_workspace(B, (int)sums.size(0)),
+              "tdc.update_sorted_indexed: workspace too small");
+  const DevGuard guard(X.device());
+  check(tdc_update_sorted(dcode(X.scalar_type()), dcode(sums.scalar_type()), X.data_ptr(), B,
+                          X.stride(0), (int)sums.size(1), labels.data_ptr<int32_t>(),
+                          (int)sums.size(0), sums.data_ptr(), counts.data_ptr(),
+                          work.data_ptr<int>(), num_cus(X.device().index()), cur_stream(),
+                          rowidx.data_ptr<int32_t>()),
+        "update_sorted_indexed");
+}
+
+void sculley_update(const at::Tensor& sums, const at::Tensor& counts, at::Tensor& C, at::Tensor& v,
+                    const std::optional<at::Tensor>& shift, const std::optional<at::Tensor>& Cm2,
+                    const std::optional<at::Tensor>& cnorm) {
+  check_cuda(C, "C");
+  TORCH_CHECK(C.is_contiguous() && C.dim() == 2, "tdc.sculley_update: C");
+  const int K = (int)C.size(0), D = (int)C.size(1);
+  TORCH_CHECK(sums.is_contiguous() && sums.numel() == (int64_t)K * D, "tdc.sculley_update: sums");
+  TORCH_CHECK(counts.scalar_type() == sums.scalar_type() && counts.numel() >= K,
+              "tdc.sculley_update: counts");
+  TORCH_CHECK(v.scalar_type() == at::kDouble && v.is_contiguous() && v.numel() >= K,
+              "tdc.sculley_update: v must be fp64 [K]");
+  int Kp = K, DP = D;
+  if (Cm2.has_value() && Cm2->defined()) {
+    TORCH_CHECK(Cm2->scalar_type() == at::kBFloat16 && Cm2->is_contiguous(), "tdc.sculley_update: Cm2");
+    TORCH_CHECK(cnorm.has_value() && cnorm->defined(), "tdc.sculley_update: cnorm required with Cm2");
+    Kp = (int)Cm2->size(0);
+    DP = (int)Cm2->size(1);
+    TORCH_CHECK(Kp >= K && DP >= D, "tdc.sculley_update: Cm2 smaller than C");
+  }
+  float* sh = nullptr;
+  if (shift.has_value() && shift->defined()) {
+    TORCH_CHECK(shift->scalar_type() == at::kFloat, "tdc.sculley_update: shift fp32");
+    sh = shift->data_ptr<float>();
+  }
+  const DevGuard guard(C.device());
+  check(tdc_sculley_update(dcode(sums.scalar_type()), dcode(C.scalar_type()), sums.data_ptr(),
+                           counts.data_ptr(), K, D, C.data_ptr(), v.data_ptr<double>(), sh,
+                           opt_ptr(Cm2), static_cast<float*>(opt_ptr(cnorm)), Kp, DP,
+                           cur_stream()),
+        "sculley_update");
+}
+
 bool assign_bigd_supported(at::ScalarType dtype, int64_t DP) {
   const int code = dtype == at::kFloat8_e4m3fn ? TDC_FP8 : (dtype == at::kBFloat16 ? TDC_BF16 : -1);
   return code >= 0 && tdc_assign_bigd_supported(code, (int)DP) != 0;
@@ -341,6 +442,9 @@ TORCH_LIBRARY(tdc, m) {
   m.def("quant_fp8(Tensor X, int valid, int neg2, Tensor(a!) Q, Tensor(b!) S, Tensor(c!)? norm) -> ()");
   m.def("kpp_step(Tensor X, Tensor cand, Tensor(a!) closest, int mode, Tensor(b!) pots) -> ()");
   m.def("finalize(Tensor? sums, Tensor? counts, Tensor(a!) C, int policy, Tensor(b!)? shift, Tensor(c!)? Cm2, Tensor(d!)? cnorm) -> ()");
+  m.def("assign_bf16_indexed(Tensor X, Tensor rowidx, Tensor Cm2, Tensor cnorm, Tensor(a!) labels, Tensor(b!)? mind) -> ()");
+  m.def("update_sorted_indexed(Tensor X, Tensor rowidx, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work) -> ()");
+  m.def("sculley_update(Tensor sums, Tensor counts, Tensor(a!) C, Tensor(b!) v, Tensor(c!)? shift, Tensor(d!)? Cm2, Tensor(e!)? cnorm) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(tdc, CUDA, m) {
@@ -354,4 +458,7 @@ TORCH_LIBRARY_IMPL(tdc, CUDA, m) {
   m.impl("assign_bigd", &assign_bigd);
   m.impl("quant_fp8", &quant_fp8);
   m.impl("kpp_step", &kpp_step);
+  m.impl("assign_bf16_indexed", &assign_bf16_indexed);
+  m.impl("update_sorted_indexed", &update_sorted_indexed);
+  m.impl("sculley_update", &sculley_update);
 }

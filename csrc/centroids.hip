@@ -79,9 +79,91 @@ int launch_finalize(const void* sums, const void* counts, int K, int D, void* C,
   return 0;
 }
 
+// Mini-batch (Sculley) centre update, one wave per centroid row:
+//   n_k > 0:  c_k <- (v_k c_k + S_k) / (v_k + n_k),  v_k <- v_k + n_k   (fp64 arithmetic)
+//   n_k = 0:  c_k unchanged
+// shift = max over updated k of ||c_k - c_k_old||^2, plus the bf16 operand prep of the
+// next assignment -- one launch instead of ~15 small fp64 elementwise kernels.
+template <typename ACC, typename CT>
+__global__ __launch_bounds__(256) void sculley_kernel(const ACC* __restrict__ sums,
+                                                      const ACC* __restrict__ counts, int K, int D,
+                                                      CT* __restrict__ C, double* __restrict__ v,
+                                                      float* __restrict__ shift,
+                                                      __bf16* __restrict__ Cm2,
+                                                      float* __restrict__ cnorm, int Kp, int DP) {
+  const int lane = threadIdx.x & 63;
+  const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k >= Kp) return;
+  if (k >= K) {
+    if (Cm2)
+      for (int d = lane; d < DP; d += 64) Cm2[(int64_t)k * DP + d] = (__bf16)0.f;
+    if (cnorm && lane == 0) cnorm[k] = 3.0e38f;
+    return;
+  }
+  const double n = (double)counts[k];
+  const double vk = v[k];
+  const double inv = n > 0.0 ? 1.0 / (vk + n) : 0.0;
+  float sh = 0.f, nrm = 0.f;
+  const int dend = Cm2 ? (DP > D ? DP : D) : D;
+  for (int d = lane; d < dend; d += 64) {
+    if (d < D) {
+      const CT old = C[(int64_t)k * D + d];
+      CT nw = old;
+      if (n > 0.0) {
+        nw = (CT)((vk * (double)old + (double)sums[(int64_t)k * D + d]) * inv);
+        C[(int64_t)k * D + d] = nw;
+        const float df = (float)nw - (float)old;
+        sh += df * df;
+      }
+      if (Cm2) {
+        const __bf16 b = (__bf16)(float)nw;
+        const float bf = (float)b;
+        Cm2[(int64_t)k * DP + d] = (__bf16)(-2.f * bf);
+        nrm = fmaf(bf, bf, nrm);
+      }
+    } else if (Cm2 && d < DP) {
+      Cm2[(int64_t)k * DP + d] = (__bf16)0.f;
+    }
+  }
+  if (shift) {
+    sh = wave_sum(sh);
+    if (lane == 0) atomicMax(reinterpret_cast<unsigned*>(shift), __float_as_uint(sh));
+  }
+  if (cnorm) {
+    nrm = wave_sum(nrm);
+    if (lane == 0) cnorm[k] = nrm;
+  }
+  if (lane == 0) v[k] = vk + n;  // every lane read v[k] above (wave lockstep)
+}
+
+template <typename ACC, typename CT>
+int launch_sculley(const void* sums, const void* counts, int K, int D, void* C, double* v,
+                   float* shift, void* Cm2, float* cnorm, int Kp, int DP, hipStream_t s) {
+  const int rows = Cm2 ? (Kp > K ? Kp : K) : K;
+  hipLaunchKernelGGL((sculley_kernel<ACC, CT>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s,
+                     (const ACC*)sums, (const ACC*)counts, K, D, (CT*)C, v, shift, (__bf16*)Cm2,
+                     cnorm, Kp, DP);
+  TDC_CHECK_LAUNCH();
+  return 0;
+}
+
 }  // namespace tdc
 
 using namespace tdc;
+
+int tdc_sculley_update(int acc_dtype, int c_dtype, const void* sums, const void* counts, int K,
+                       int D, void* C, double* v, float* shift, void* Cm2, float* cnorm, int Kp,
+                       int DP, hipStream_t s) {
+  if (acc_dtype == TDC_F64 && c_dtype == TDC_F32)
+    return launch_sculley<double, float>(sums, counts, K, D, C, v, shift, Cm2, cnorm, Kp, DP, s);
+  if (acc_dtype == TDC_F32 && c_dtype == TDC_F32)
+    return launch_sculley<float, float>(sums, counts, K, D, C, v, shift, Cm2, cnorm, Kp, DP, s);
+  if (acc_dtype == TDC_F64 && c_dtype == TDC_F64)
+    return launch_sculley<double, double>(sums, counts, K, D, C, v, shift, Cm2, cnorm, Kp, DP, s);
+  if (acc_dtype == TDC_F32 && c_dtype == TDC_F64)
+    return launch_sculley<float, double>(sums, counts, K, D, C, v, shift, Cm2, cnorm, Kp, DP, s);
+  return (int)hipErrorInvalidValue;
+}
 
 int tdc_finalize(int acc_dtype, int c_dtype, const void* sums, const void* counts, int K, int D,
                  void* C, int policy, float* shift, void* Cm2, float* cnorm, int Kp, int DP,

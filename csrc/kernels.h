@@ -14,6 +14,10 @@ enum TdcDtype { TDC_F32 = 0, TDC_F64 = 1, TDC_BF16 = 2, TDC_FP8 = 3 };
 int tdc_assign_mfma_bf16(const void* X, int64_t N, int64_t ldx, int DP, const void* Cm2,
                          const float* cnorm, int Kp, int32_t* labels, float* mind,
                          hipStream_t stream);
+// Same, point i = row rowidx[i] of X (mini-batches without a gathered copy); DP 64/128/256.
+int tdc_assign_mfma_bf16_indexed(const void* X, const int32_t* rowidx, int64_t N, int64_t ldx,
+                                 int DP, const void* Cm2, const float* cnorm, int Kp,
+                                 int32_t* labels, float* mind, hipStream_t stream);
 
 // N1 (exact)  SIMT difference-form assignment for fp32/fp64, any K, D <= 64.
 int tdc_assign_simt(int dtype, const void* X, int64_t N, int64_t ldx, int D, const void* C,
@@ -35,9 +39,10 @@ int tdc_update_lds(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t
 // N2 (large K x D): counting sort by label + segmented row gather-sum.  work: int32
 // workspace of tdc_update_sorted_workspace(N, K) elements.  sums/counts are accumulated
 // (caller zeroes them once per pass).
+// rowidx (nullable): labels[i] belongs to row rowidx[i] of X (N = number of labels).
 int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
                       const int32_t* labels, int K, void* sums, void* counts, int* work,
-                      int num_cus, hipStream_t stream);
+                      int num_cus, hipStream_t stream, const int32_t* rowidx = nullptr);
 int64_t tdc_update_sorted_workspace(int64_t N, int K);
 
 // N4/N5  fused small-K Fuzzy C-Means tower: sum_i w_ki x_i, sum_i w_ki, argmax labels.
@@ -53,6 +58,13 @@ int tdc_fcm_small_supported(int dtype, int K, int D);
 int tdc_finalize(int acc_dtype, int c_dtype, const void* sums, const void* counts, int K,
                  int D, void* C, int policy, float* shift, void* Cm2, float* cnorm, int Kp,
                  int DP, hipStream_t stream);
+
+// Mini-batch (Sculley) update: n = counts[k] > 0 -> C[k] = (v[k] C[k] + sums[k]) / (v[k] + n),
+// v[k] += n (v fp64 [K]); shift (nullable, zeroed by the caller) = max ||dC_k||^2 over the
+// updated k; optional bf16 prep of the next assignment as in tdc_finalize.
+int tdc_sculley_update(int acc_dtype, int c_dtype, const void* sums, const void* counts, int K,
+                       int D, void* C, double* v, float* shift, void* Cm2, float* cnorm, int Kp,
+                       int DP, hipStream_t stream);
 
 // N1 wide-D / fp8 (assign_bigd.hip).  dtype TDC_BF16: X bf16 rows (ldx elements), Cm2
 // bf16 [Kp, DP] = -2c, DP in {384,512}.  dtype TDC_FP8: X e4m3 bytes (ldx bytes),

@@ -102,7 +102,8 @@ __global__ __launch_bounds__(1024) void scan_kernel(const int* __restrict__ cnt,
 __global__ __launch_bounds__(256) void scatter_kernel(const int32_t* __restrict__ labels, int64_t N,
                                                       int K, int* __restrict__ cursor,
                                                       int32_t* __restrict__ perm,
-                                                      int64_t per_block) {
+                                                      int64_t per_block,
+                                                      const int32_t* __restrict__ rowidx) {
   constexpr int R = 16;  // labels per thread per pass (4096 per block pass)
   extern __shared__ int s_mem[];
   int* s_cnt = s_mem;
@@ -140,7 +141,8 @@ __global__ __launch_bounds__(256) void scatter_kernel(const int32_t* __restrict_
     for (int j = 0; j < R; ++j) {
       if (rank[j] >= 0) {
         const int pos = agg ? s_base[lab[j]] + rank[j] : rank[j];
-        perm[pos] = (int32_t)(p0 + j * 256 + tid);
+        const int64_t i = p0 + j * 256 + tid;
+        perm[pos] = rowidx ? rowidx[i] : (int32_t)i;
       }
     }
     if (agg) __syncthreads();
@@ -155,7 +157,10 @@ __global__ __launch_bounds__(256) void scatter_kernel(const int32_t* __restrict_
 template <int NT>
 __global__ __launch_bounds__(NT) void bscatter_kernel(const int32_t* __restrict__ labels, int64_t N,
                                                        int K, int* __restrict__ cursor,
-                                                       int32_t* __restrict__ perm, int64_t per_block) {
+                                                       int32_t* __restrict__ perm, int64_t per_block,
+                                                       const int32_t* __restrict__ rowidx) {
+  // perm holds X row numbers: i itself, or rowidx[i] for an indexed (mini-batch) pass
+#define TDC_ROW(ii) (rowidx ? rowidx[ii] : (int32_t)(ii))
   extern __shared__ int s_mem[];
   int* s_cnt = s_mem;
   int* s_cur = s_mem + K;
@@ -185,15 +190,16 @@ __global__ __launch_bounds__(NT) void bscatter_kernel(const int32_t* __restrict_
   i = r0 + tid;
   for (; i + 3 * NT < r1; i += 4 * NT) {
     const int a0 = labels[i], a1 = labels[i + NT], a2 = labels[i + 2 * NT], a3 = labels[i + 3 * NT];
-    if ((unsigned)a0 < (unsigned)K) perm[atomicAdd(s_cur + a0, 1)] = (int32_t)i;
-    if ((unsigned)a1 < (unsigned)K) perm[atomicAdd(s_cur + a1, 1)] = (int32_t)(i + NT);
-    if ((unsigned)a2 < (unsigned)K) perm[atomicAdd(s_cur + a2, 1)] = (int32_t)(i + 2 * NT);
-    if ((unsigned)a3 < (unsigned)K) perm[atomicAdd(s_cur + a3, 1)] = (int32_t)(i + 3 * NT);
+    if ((unsigned)a0 < (unsigned)K) perm[atomicAdd(s_cur + a0, 1)] = TDC_ROW(i);
+    if ((unsigned)a1 < (unsigned)K) perm[atomicAdd(s_cur + a1, 1)] = TDC_ROW(i + NT);
+    if ((unsigned)a2 < (unsigned)K) perm[atomicAdd(s_cur + a2, 1)] = TDC_ROW(i + 2 * NT);
+    if ((unsigned)a3 < (unsigned)K) perm[atomicAdd(s_cur + a3, 1)] = TDC_ROW(i + 3 * NT);
   }
   for (; i < r1; i += NT) {
     const int a0 = labels[i];
-    if ((unsigned)a0 < (unsigned)K) perm[atomicAdd(s_cur + a0, 1)] = (int32_t)i;
+    if ((unsigned)a0 < (unsigned)K) perm[atomicAdd(s_cur + a0, 1)] = TDC_ROW(i);
   }
+#undef TDC_ROW
 }
 
 template <typename XT, int VEC> struct RowLoad;
@@ -296,49 +302,79 @@ __global__ __launch_bounds__(256) void segsum_kernel(const XT* __restrict__ X, i
   } while (0)
     int64_t j = a + g;
     if constexpr (VEC > 1) {
-      // fast path, software pipelined: the permutation entries of batch i+1 are loaded
-      // while the U row gathers of batch i are in flight (one round trip per batch
-      // instead of two)
+      // One software-pipelined loop over wave-uniform batches [p, pe): a batch never
+      // straddles a segment boundary, all U row gathers of a batch are in flight at once
+      // and the permutation entries of the next batch load while they are.  When a batch
+      // closes a segment the G row-groups of the wave are summed with cross-lane
+      // shuffles and only group 0 issues the atomics: short segments (mini-batches,
+      // large K) used to flush from every group into the same addresses, a G-way
+      // same-address conflict inside each atomic instruction.
       typedef typename RowRaw<XT, VEC>::raw_t raw_t;
+      int64_t p = a;
+      int64_t knext = k + 1 < K ? offsets[k + 2] : N;
+      int64_t pe = min(min(b, kend), p + U * G);
       int32_t nidx[U];
-      bool nfast = j + (U - 1) * G < min(b, kend);
-      if (nfast) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) nidx[u] = perm[j + u * G];
+      for (int u = 0; u < U; ++u) {
+        const int64_t r = p + g + u * G;
+        nidx[u] = r < pe ? perm[r] : 0;
       }
-      while (j < b) {
-        if (nfast) {
-          raw_t xv[U];
-          if (colok) {
+      while (p < b) {
+        raw_t xv[U];
+        if (colok) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) xv[u] = RowRaw<XT, VEC>::load(X + (int64_t)nidx[u] * ldx + col);
-          }
-          j += U * G;
-          nfast = j + (U - 1) * G < min(b, kend);
-          if (nfast) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) nidx[u] = perm[j + u * G];
-          }
-          if (colok) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) RowRaw<XT, VEC>::add(xv[u], acc);
-          }
-        } else {
-          while (j >= kend) {  // crossed into a later segment
-            TDC_FLUSH(k);
-            ++k;
-            kend = offsets[k + 1];
-          }
-          const int32_t idx = perm[j];
-          if (colok) RowLoad<XT, VEC>::add(X + (int64_t)idx * ldx + col, acc);
-          j += G;
-          nfast = j + (U - 1) * G < min(b, kend);
-          if (nfast) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) nidx[u] = perm[j + u * G];
-          }
+          for (int u = 0; u < U; ++u)
+            if (p + g + u * G < pe) xv[u] = RowRaw<XT, VEC>::load(X + (int64_t)nidx[u] * ldx + col);
         }
+        const bool closes = pe == kend || pe == b;  // wave-uniform
+        int kn = k;
+        int64_t kendn = kend, knextn = knext;
+        if (pe == kend) {
+          do {  // next non-empty segment (the boundary after it is prefetched)
+            ++kn;
+            kendn = knextn;
+            knextn = kn + 1 < K ? offsets[kn + 2] : N;
+          } while (kendn <= pe && kn + 1 < K);
+        }
+        const int64_t pn = pe;
+        const int64_t pen = min(min(b, kendn), pn + U * G);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t r = pn + g + u * G;
+          nidx[u] = r < pen ? perm[r] : 0;
+        }
+        if (colok) {
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            if (p + g + u * G < pe) RowRaw<XT, VEC>::add(xv[u], acc);
+        }
+        if (closes) {
+#pragma unroll
+          for (int off = TPR; off < 64; off <<= 1)
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) acc[e] += __shfl_xor(acc[e], off, 64);
+          // every group now holds the segment's sums: group g adds elements e0 + g, so
+          // each atomic wave-instruction covers up to 64 distinct columns (Guideline 12:
+          // few, wide atomic instructions) instead of VEC instructions of TPR lanes
+#pragma unroll
+          for (int e0 = 0; e0 < VEC; e0 += G) {
+            const int e = e0 + g;
+            AT v = 0;
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) v = (q == e) ? acc[q] : v;
+            if (colok && e < VEC && col + e < D && v != (AT)0)
+              atomic_add(&sums[(int64_t)k * D + col + e], (ACC)v);
+          }
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) acc[e] = 0;
+        }
+        k = kn;
+        kend = kendn;
+        knext = knextn;
+        p = pn;
+        pe = pen;
       }
+      (void)j;
     } else {
       // fast path: U rows of this group all inside the current segment
       while (j < b) {
@@ -422,7 +458,7 @@ int dispatch_segsum(int x_dtype, const void* X, int64_t ldx, int D, const int32_
 
 int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
                       const int32_t* labels, int K, void* sums, void* counts, int* work,
-                      int num_cus, hipStream_t s) {
+                      int num_cus, hipStream_t s, const int32_t* rowidx) {
   if (N <= 0) return 0;
   if (N >= (int64_t)1 << 31) return (int)hipErrorInvalidValue;
   // workspace layout (ints): cnt[K] | offsets[K+1] | cursor[K] | perm[N]
@@ -461,10 +497,10 @@ int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int6
     blocks = (N + per - 1) / per;
     if (nt == 1024)
       hipLaunchKernelGGL(bscatter_kernel<1024>, dim3((unsigned)blocks), dim3(1024),
-                         2 * sizeof(int) * (size_t)K, s, labels, N, K, cursor, perm, per);
+                         2 * sizeof(int) * (size_t)K, s, labels, N, K, cursor, perm, per, rowidx);
     else
       hipLaunchKernelGGL(bscatter_kernel<256>, dim3((unsigned)blocks), dim3(256),
-                         2 * sizeof(int) * (size_t)K, s, labels, N, K, cursor, perm, per);
+                         2 * sizeof(int) * (size_t)K, s, labels, N, K, cursor, perm, per, rowidx);
     TDC_CHECK_LAUNCH();
   } else {
     int64_t blocks = (int64_t)num_cus * 4;
@@ -472,7 +508,7 @@ int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int6
     per = ((per + 4095) / 4096) * 4096;
     blocks = (N + per - 1) / per;
     hipLaunchKernelGGL(scatter_kernel, dim3((unsigned)blocks), dim3(256), 0, s, labels, N, K,
-                       cursor, perm, per);
+                       cursor, perm, per, rowidx);
     TDC_CHECK_LAUNCH();
   }
   if (acc_dtype == TDC_F64)

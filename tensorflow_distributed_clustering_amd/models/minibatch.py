@@ -74,6 +74,7 @@ class MiniBatchStepper:
         self.gen = torch.Generator(device=dev).manual_seed(cfg.seed * 1000003 + comm.rank)
         self._stream_iter = None
         self.shift = None
+        self._shift_buf = None
         self.n_iter = 0
 
     @property
@@ -94,12 +95,31 @@ class MiniBatchStepper:
                 self._stream_iter = None  # next epoch over the shard
         raise RuntimeError("empty source")
 
+    def _indexed(self) -> bool:
+        """Resident shard on the bf16 MFMA path: sample row *indices* and let the kernels
+        read the rows in place (no [B, D] gather copy per step)."""
+        sup = getattr(self.local, "supports_indexed", None)
+        return self.resident and self.device.type == "cuda" and sup is not None and sup()
+
     def step(self):
-        batch = self.next_batch()
         self.buf.zero_()
-        self.local.bind(batch).step(self.C, self.blabels[: batch.shape[0]], None, self.sums,
-                                    self.counts)
+        if self._indexed():
+            idx = torch.randint(self.n_local, (self.batch_rows,), generator=self.gen,
+                                device=self.device, dtype=torch.int32)
+            self.local.step_indexed(self.C, idx, self.blabels, None, self.sums, self.counts)
+        else:
+            batch = self.next_batch()
+            self.local.bind(batch).step(self.C, self.blabels[: batch.shape[0]], None, self.sums,
+                                        self.counts)
         self.comm.allreduce_bucketed_(self.buf, 64 << 20)
+        if hasattr(self.local, "sculley"):
+            if self._shift_buf is None:
+                self._shift_buf = torch.zeros(1, dtype=torch.float32, device=self.device)
+            self._shift_buf.zero_()
+            self.local.sculley(self.sums, self.counts, self.C, self.v, self._shift_buf)
+            self.shift = self._shift_buf
+            self.n_iter += 1
+            return
         C64 = self.C.double()
         cnt = self.counts.double()
         nv = self.v + cnt

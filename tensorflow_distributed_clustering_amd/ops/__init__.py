@@ -37,6 +37,11 @@ WIDE_BF16_DIMS = (384, 512)
 FP8_DIMS = (256, 512, 768, 1024)
 # centroid bytes one K-group may occupy (an XCD's L2 is 4 MiB; leave room for X/labels)
 KGROUP_BYTES = int(__import__("os").environ.get("TDC_KGROUP_BYTES", 3 << 20))
+# assign/update overlap: the resident bf16 step runs in this many row slices; slice i's
+# (memory-bound) update runs on a side stream while slice i+1's (MFMA-bound) assign runs
+OVERLAP_SLICES = int(__import__("os").environ.get("TDC_OVERLAP_SLICES", 1))
+OVERLAP_PRIO = int(__import__("os").environ.get("TDC_OVERLAP_PRIO", 0))  # side stream
+OVERLAP_MIN_ROWS = 1 << 20  # per slice: below this the assign grid no longer fills 256 CUs
 
 
 def acc_dtype_for(dtype: str, k: int, d: int) -> torch.dtype:
@@ -114,6 +119,17 @@ class NativeUpdate:
                 self.work = torch.empty(int(self.ops.update_sorted_workspace(x.shape[0], sums.shape[0])),
                                         dtype=torch.int32, device=x.device)
             self.ops.update_sorted(x, labels, sums, counts, self.work)
+
+
+    def supports_indexed(self) -> bool:
+        return self.kind == "sorted" and not self.deterministic
+
+    def indexed(self, x, rowidx, labels, sums, counts):
+        """Partials of the rows ``x[rowidx]`` without gathering them (mini-batches)."""
+        need = int(self.ops.update_sorted_workspace(rowidx.shape[0], sums.shape[0]))
+        if self.work is None or self.work.numel() < need:
+            self.work = torch.empty(need, dtype=torch.int32, device=x.device)
+        self.ops.update_sorted_indexed(x, rowidx, labels, sums, counts, self.work)
 
 
 def deterministic_update(x, labels, sums, counts):
@@ -222,15 +238,58 @@ class HipBf16Lloyd(_LocalOpsBase):
     def prepare(self, C):
         self.ops.finalize(None, None, C, 0, None, self.cm2, self.cnorm)
 
+    def _slices(self):
+        n = self.n
+        s = max(1, min(OVERLAP_SLICES, n // OVERLAP_MIN_ROWS))
+        if s <= 1 or self.update.kind != "sorted" or self.update.deterministic:
+            return None
+        b = [(n * i // s) // 256 * 256 for i in range(s)] + [n]
+        return list(zip(b[:-1], b[1:]))
+
     def step(self, C, labels, mind, sums, counts):
-        self.ops.assign_bf16(self.x, self.cm2, self.cnorm, labels, mind)
-        self.update(self.x, labels, sums, counts)
+        sl = self._slices()
+        if sl is None:
+            self.ops.assign_bf16(self.x, self.cm2, self.cnorm, labels, mind)
+            self.update(self.x, labels, sums, counts)
+            return
+        # fork/join over a side stream (also valid under hipGraph capture): the update of
+        # slice i (gather-bound, ~5 TB/s) overlaps the assign of slice i+1 (MFMA-bound).
+        # Updates stay ordered on the side stream, so one workspace and the accumulating
+        # sums/counts are safe.
+        main = torch.cuda.current_stream(self.device)
+        side = getattr(self, "_side", None)
+        if side is None:
+            side = self._side = torch.cuda.Stream(device=self.device, priority=OVERLAP_PRIO)
+        side.wait_stream(main)
+        for s, e in sl:
+            self.ops.assign_bf16(self.x[s:e], self.cm2, self.cnorm, labels[s:e],
+                                 None if mind is None else mind[s:e])
+            ev = torch.cuda.Event()
+            ev.record(main)
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                self.update(self.x[s:e], labels[s:e], sums, counts)
+        main.wait_stream(side)
 
     def assign(self, C, labels, mind):
         self.ops.assign_bf16(self.x, self.cm2, self.cnorm, labels, mind)
 
     def finalize(self, sums, counts, C, shift):
         self.ops.finalize(sums, counts, C, self.policy, shift, self.cm2, self.cnorm)
+
+    # -------------------------------------------------- mini-batches by row index
+    def supports_indexed(self) -> bool:
+        return self.dp in (64, 128, 256) and self.update.supports_indexed()
+
+    def step_indexed(self, C, rowidx, labels, mind, sums, counts):
+        """Assign + partials of the shard rows ``rowidx`` (int32 [B]); the batch is never
+        copied out of the shard (the kernels load row rowidx[i] for point i)."""
+        self.ops.assign_bf16_indexed(self.x, rowidx, self.cm2, self.cnorm, labels, mind)
+        self.update.indexed(self.x, rowidx, labels, sums, counts)
+
+    def sculley(self, sums, counts, C, v, shift):
+        """Native mini-batch centre update + next-assignment operand prep (one launch)."""
+        self.ops.sculley_update(sums, counts, C, v, shift, self.cm2, self.cnorm)
 
 
 class _GroupedAssign:

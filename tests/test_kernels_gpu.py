@@ -257,3 +257,117 @@ def test_native_kmeanspp_matches_torch_path(gpu):
     native = init_kmeanspp(x, 0, 50000, 16, comm, 3)
     torch_path = init_kmeanspp(x.cpu(), 0, 50000, 16, local_comm(torch.device("cpu")), 3)
     torch.testing.assert_close(native.cpu(), torch_path, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("slices", [2, 4])
+def test_bf16_step_sliced_overlap(gpu, slices, monkeypatch):
+    """The resident bf16 step split into row slices, with each slice's update on a side
+    stream overlapping the next slice's assign, gives the same labels / counts / sums as
+    the unsliced step (and the fp64 oracle), eagerly and under hipGraph capture."""
+    import tensorflow_distributed_clustering_amd.ops as ops_mod
+    n, d, k = 2_100_000 + 77, 128, 1024
+    monkeypatch.setattr(ops_mod, "OVERLAP_MIN_ROWS", 1 << 18)
+    x, c = _bf16_case(n, d, k, gpu, seed=5)
+    lo = ops_mod.make_lloyd_ops(x, k, "bf16", "hip")
+    assert isinstance(lo, ops_mod.HipBf16Lloyd) and lo.update.kind == "sorted"
+    C = c.float().contiguous()
+    lo.prepare(C)
+    outs = []
+    for s in (1, slices):
+        monkeypatch.setattr(ops_mod, "OVERLAP_SLICES", s)
+        assert (lo._slices() is None) == (s == 1)
+        lab = torch.zeros(n, dtype=torch.int32, device=gpu)
+        sums = torch.zeros(k, d, dtype=torch.float32, device=gpu)
+        cnt = torch.zeros(k, dtype=torch.float32, device=gpu)
+        lo.step(C, lab, None, sums, cnt)
+        torch.cuda.synchronize()
+        outs.append((lab, sums, cnt))
+    (l1, s1, c1), (l2, s2, c2) = outs
+    assert torch.equal(l1, l2)
+    assert torch.equal(c1, c2) and int(c1.sum()) == n
+    torch.testing.assert_close(s2, s1, rtol=1e-4, atol=1e-2)
+    s_ref, c_ref = ref.cluster_sums(x.double(), l1, k, acc_dtype=torch.float64)
+    assert torch.equal(c1.double(), c_ref)
+    torch.testing.assert_close(s2.double(), s_ref, rtol=1e-4, atol=1e-2)
+    # the same sliced step captured into a hipGraph and replayed
+    lab = torch.zeros(n, dtype=torch.int32, device=gpu)
+    sums = torch.zeros(k, d, dtype=torch.float32, device=gpu)
+    cnt = torch.zeros(k, dtype=torch.float32, device=gpu)
+    side = torch.cuda.Stream(device=gpu)
+    side.wait_stream(torch.cuda.current_stream(gpu))
+    with torch.cuda.stream(side):
+        lo.step(C, lab, None, sums, cnt)  # warm-up outside capture
+    torch.cuda.current_stream(gpu).wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        sums.zero_()
+        cnt.zero_()
+        lo.step(C, lab, None, sums, cnt)
+    lab.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(lab, l1) and torch.equal(cnt, c1)
+    torch.testing.assert_close(sums, s1, rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("n,b,d,k", [(50000, 20000, 128, 1024), (30000, 7777, 64, 4096),
+                                     (20000, 5000, 256, 300)])
+def test_indexed_assign_and_update(gpu, n, b, d, k):
+    """Mini-batch kernels that read rows in place by index == the same kernels on the
+    gathered batch (labels bitwise, counts exactly, sums to fp32 atomic-order tolerance)."""
+    import tensorflow_distributed_clustering_amd.ops as ops_mod
+    from tensorflow_distributed_clustering_amd import _native
+    ops = _native.require()
+    x, c = _bf16_case(n, d, k, gpu, seed=n + b)
+    lo = ops_mod.make_lloyd_ops(x, k, "bf16", "hip")
+    C = c.float().contiguous()
+    lo.prepare(C)
+    g = torch.Generator(device=gpu).manual_seed(7)
+    idx = torch.randint(n, (b,), generator=g, device=gpu, dtype=torch.int32)
+    lab_i = torch.full((b,), -1, dtype=torch.int32, device=gpu)
+    md_i = torch.zeros(b, dtype=torch.float32, device=gpu)
+    ops.assign_bf16_indexed(lo.x, idx, lo.cm2, lo.cnorm, lab_i, md_i)
+    xb = lo.x.index_select(0, idx.long()).contiguous()
+    lab_g = torch.full((b,), -1, dtype=torch.int32, device=gpu)
+    md_g = torch.zeros(b, dtype=torch.float32, device=gpu)
+    ops.assign_bf16(xb, lo.cm2, lo.cnorm, lab_g, md_g)
+    assert torch.equal(lab_i, lab_g)
+    assert torch.equal(md_i, md_g)
+    work = torch.empty(int(ops.update_sorted_workspace(b, k)), dtype=torch.int32, device=gpu)
+    s_i = torch.zeros(k, d, dtype=torch.float32, device=gpu)
+    c_i = torch.zeros(k, dtype=torch.float32, device=gpu)
+    ops.update_sorted_indexed(lo.x, idx, lab_i, s_i, c_i, work)
+    s_ref, c_ref = ref.cluster_sums(xb[:, :d].double(), lab_g, k, acc_dtype=torch.float64)
+    assert torch.equal(c_i.double(), c_ref)
+    torch.testing.assert_close(s_i.double(), s_ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("cdt", [torch.float32, torch.float64])
+def test_sculley_update(gpu, cdt):
+    from tensorflow_distributed_clustering_amd import _native
+    ops = _native.require()
+    k, d, kp, dp = 300, 100, 320, 128
+    g = torch.Generator().manual_seed(11)
+    C = torch.randn(k, d, generator=g, dtype=torch.float64)
+    v = torch.randint(0, 50, (k,), generator=g).double()
+    cnt = torch.randint(0, 5, (k,), generator=g).float()
+    sums = torch.randn(k, d, generator=g).float() * cnt[:, None]
+    nv = v + cnt.double()
+    upd = cnt > 0
+    want = torch.where(upd[:, None], (v[:, None] * C.to(cdt).double() + sums.double())
+                       / nv.clamp_min(1)[:, None], C.to(cdt).double())
+    want_shift = ((want - C.to(cdt).double()) ** 2).sum(1).max()
+    Cg, vg = C.to(cdt).to(gpu), v.to(gpu)
+    shift = torch.zeros(1, dtype=torch.float32, device=gpu)
+    cm2 = torch.full((kp, dp), 7.0, dtype=torch.bfloat16, device=gpu)
+    cnorm = torch.zeros(kp, dtype=torch.float32, device=gpu)
+    ops.sculley_update(sums.to(gpu), cnt.to(gpu), Cg, vg, shift, cm2, cnorm)
+    tol = 1e-6 if cdt == torch.float32 else 1e-12
+    torch.testing.assert_close(Cg.double().cpu(), want, rtol=tol, atol=tol)
+    assert torch.equal(vg.cpu(), nv)
+    assert abs(float(shift) - float(want_shift)) <= 1e-4 * float(want_shift)
+    cb = Cg.float().to(torch.bfloat16).float()
+    torch.testing.assert_close(cm2[:k, :d].float(), -2 * cb)
+    assert (cm2[:k, d:] == 0).all() and (cm2[k:] == 0).all()
+    torch.testing.assert_close(cnorm[:k], (cb * cb).sum(1), rtol=1e-5, atol=1e-4)
+    assert (cnorm[k:] == 3e38).all()

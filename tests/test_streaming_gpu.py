@@ -59,6 +59,20 @@ def test_minibatch_gpu_bf16(gpu):
     assert mb.result_.inertia <= 1.10 * full.result_.inertia
 
 
+def test_minibatch_gpu_indexed_path(gpu):
+    """K x D past the LDS update: the mini-batch step samples row indices and the kernels
+    read the rows in place (+ the native Sculley update); quality vs full-batch Lloyd."""
+    n, d, k = 600_000, 128, 1024
+    x = gaussian_blobs(n, d, 256, seed=6, dtype=torch.bfloat16, device=gpu)
+    cfg = tdc.ClusterConfig(n_clusters=k, max_iter=40, dtype="bf16", seed=3, batch_size=65536)
+    mb = tdc.MiniBatchKMeans(cfg, device=gpu).fit(x)
+    assert mb.engine_._indexed() and mb.result_.backend == "hip_bf16_mfma"
+    assert int(mb.result_.counts.sum()) == 40 * 65536
+    full = tdc.KMeans(tdc.ClusterConfig(n_clusters=k, max_iter=10, dtype="bf16", seed=3),
+                      device=gpu).fit(x)
+    assert mb.result_.inertia <= 1.15 * full.result_.inertia
+
+
 @pytest.mark.parametrize("dtype,d,k", [("bf16", 128, 256), ("fp64", 5, 3), ("fp8", 256, 96)])
 def test_graph_replay_matches_eager(gpu, dtype, d, k):
     x = gaussian_blobs(100_000, d, k, seed=2, dtype=torch.float32, device=gpu)
