@@ -8,10 +8,31 @@
 // and, for the bf16 MFMA assignment, writes its operands in the same pass:
 //   Cm2[k] = -2 * bf16(c_k)   (exact scaling), cnorm[k] = ||bf16(c_k)||^2 (fp32),
 //   pad rows k >= K: Cm2 = 0, cnorm = 3e38 (never selected).
+#include <algorithm>
+
 #include "tdc_common.h"
 #include "kernels.h"
 
 namespace tdc {
+
+// One wave per centroid row, rows strided over a grid of at most MAX_BLOCKS blocks; the
+// shift max is reduced per block (LDS) so the single-address atomicMax runs once per
+// block instead of once per row (4096 same-address atomics cost ~40 us).
+constexpr int MAX_BLOCKS = 256;
+
+// shift values are >= 0 or NaN: as unsigned bit patterns every NaN orders above every
+// finite value, so an integer max keeps a NaN shift NaN (a float fmax would drop it)
+__device__ __forceinline__ void block_max_shift(unsigned sh, float* shift) {
+  __shared__ unsigned s_sh[4];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sh = max(sh, (unsigned)__shfl_xor((int)sh, o, 64));
+  if ((threadIdx.x & 63) == 0) s_sh[threadIdx.x >> 6] = sh;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned m = max(max(s_sh[0], s_sh[1]), max(s_sh[2], s_sh[3]));
+    if (m != 0u) atomicMax(reinterpret_cast<unsigned*>(shift), m);
+  }
+}
 
 template <typename ACC, typename CT>
 __global__ __launch_bounds__(256) void finalize_kernel(const ACC* __restrict__ sums,
@@ -21,58 +42,59 @@ __global__ __launch_bounds__(256) void finalize_kernel(const ACC* __restrict__ s
                                                        __bf16* __restrict__ Cm2,
                                                        float* __restrict__ cnorm, int Kp, int DP) {
   const int lane = threadIdx.x & 63;
-  const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (k >= Kp) return;
-  if (k >= K) {
-    if (Cm2)
-      for (int d = lane; d < DP; d += 64) Cm2[(int64_t)k * DP + d] = (__bf16)0.f;
-    if (cnorm && lane == 0) cnorm[k] = 3.0e38f;
-    return;
-  }
-  float sh = 0.f, nrm = 0.f;
-  ACC cnt = sums ? counts[k] : (ACC)1;
-  const int dend = Cm2 ? (DP > D ? DP : D) : D;
-  for (int d = lane; d < dend; d += 64) {
-    if (d < D) {
-      const CT old = C[(int64_t)k * D + d];
-      CT nw = old;
-      if (sums) {
-        if (cnt > (ACC)0) {
-          nw = (CT)(sums[(int64_t)k * D + d] / cnt);
-        } else if (policy == 1) {
-          nw = (CT)NAN;
-        } else if (policy == 2) {
-          nw = (CT)0;
+  const int rows = Cm2 ? (Kp > K ? Kp : K) : K;
+  unsigned shmax = 0u;
+  for (int k = blockIdx.x * 4 + (threadIdx.x >> 6); k < rows; k += gridDim.x * 4) {
+    if (k >= K) {
+      if (Cm2)
+        for (int d = lane; d < DP; d += 64) Cm2[(int64_t)k * DP + d] = (__bf16)0.f;
+      if (cnorm && lane == 0) cnorm[k] = 3.0e38f;
+      continue;
+    }
+    float sh = 0.f, nrm = 0.f;
+    ACC cnt = sums ? counts[k] : (ACC)1;
+    const int dend = Cm2 ? (DP > D ? DP : D) : D;
+    for (int d = lane; d < dend; d += 64) {
+      if (d < D) {
+        const CT old = C[(int64_t)k * D + d];
+        CT nw = old;
+        if (sums) {
+          if (cnt > (ACC)0) {
+            nw = (CT)(sums[(int64_t)k * D + d] / cnt);
+          } else if (policy == 1) {
+            nw = (CT)NAN;
+          } else if (policy == 2) {
+            nw = (CT)0;
+          }
+          C[(int64_t)k * D + d] = nw;
+          const float df = (float)nw - (float)old;
+          sh += df * df;
         }
-        C[(int64_t)k * D + d] = nw;
-        const float df = (float)nw - (float)old;
-        sh += df * df;
+        if (Cm2) {
+          const __bf16 b = (__bf16)(float)nw;
+          const float bf = (float)b;
+          Cm2[(int64_t)k * DP + d] = (__bf16)(-2.f * bf);
+          nrm = fmaf(bf, bf, nrm);
+        }
+      } else if (Cm2 && d < DP) {
+        Cm2[(int64_t)k * DP + d] = (__bf16)0.f;
       }
-      if (Cm2) {
-        const __bf16 b = (__bf16)(float)nw;
-        const float bf = (float)b;
-        Cm2[(int64_t)k * DP + d] = (__bf16)(-2.f * bf);
-        nrm = fmaf(bf, bf, nrm);
-      }
-    } else if (Cm2 && d < DP) {
-      Cm2[(int64_t)k * DP + d] = (__bf16)0.f;
+    }
+    if (sums && shift) shmax = max(shmax, __float_as_uint(wave_sum(sh)));
+    if (cnorm) {
+      nrm = wave_sum(nrm);
+      if (lane == 0) cnorm[k] = nrm;
     }
   }
-  if (sums && shift) {
-    sh = wave_sum(sh);
-    if (lane == 0) atomicMax(reinterpret_cast<unsigned*>(shift), __float_as_uint(sh));
-  }
-  if (cnorm) {
-    nrm = wave_sum(nrm);
-    if (lane == 0) cnorm[k] = nrm;
-  }
+  if (sums && shift) block_max_shift(shmax, shift);
 }
 
 template <typename ACC, typename CT>
 int launch_finalize(const void* sums, const void* counts, int K, int D, void* C, int policy,
                     float* shift, void* Cm2, float* cnorm, int Kp, int DP, hipStream_t s) {
   const int rows = Cm2 ? (Kp > K ? Kp : K) : K;
-  hipLaunchKernelGGL((finalize_kernel<ACC, CT>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0,
+  const int blocks = std::min((rows + 3) / 4, MAX_BLOCKS);
+  hipLaunchKernelGGL((finalize_kernel<ACC, CT>), dim3((unsigned)blocks), dim3(256), 0,
                      s, (const ACC*)sums, (const ACC*)counts, K, D, (CT*)C, policy, shift,
                      (__bf16*)Cm2, cnorm, Kp, DP);
   TDC_CHECK_LAUNCH();
@@ -92,55 +114,56 @@ __global__ __launch_bounds__(256) void sculley_kernel(const ACC* __restrict__ su
                                                       __bf16* __restrict__ Cm2,
                                                       float* __restrict__ cnorm, int Kp, int DP) {
   const int lane = threadIdx.x & 63;
-  const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (k >= Kp) return;
-  if (k >= K) {
-    if (Cm2)
-      for (int d = lane; d < DP; d += 64) Cm2[(int64_t)k * DP + d] = (__bf16)0.f;
-    if (cnorm && lane == 0) cnorm[k] = 3.0e38f;
-    return;
-  }
-  const double n = (double)counts[k];
-  const double vk = v[k];
-  const double inv = n > 0.0 ? 1.0 / (vk + n) : 0.0;
-  float sh = 0.f, nrm = 0.f;
-  const int dend = Cm2 ? (DP > D ? DP : D) : D;
-  for (int d = lane; d < dend; d += 64) {
-    if (d < D) {
-      const CT old = C[(int64_t)k * D + d];
-      CT nw = old;
-      if (n > 0.0) {
-        nw = (CT)((vk * (double)old + (double)sums[(int64_t)k * D + d]) * inv);
-        C[(int64_t)k * D + d] = nw;
-        const float df = (float)nw - (float)old;
-        sh += df * df;
-      }
-      if (Cm2) {
-        const __bf16 b = (__bf16)(float)nw;
-        const float bf = (float)b;
-        Cm2[(int64_t)k * DP + d] = (__bf16)(-2.f * bf);
-        nrm = fmaf(bf, bf, nrm);
-      }
-    } else if (Cm2 && d < DP) {
-      Cm2[(int64_t)k * DP + d] = (__bf16)0.f;
+  const int rows = Cm2 ? (Kp > K ? Kp : K) : K;
+  unsigned shmax = 0u;
+  for (int k = blockIdx.x * 4 + (threadIdx.x >> 6); k < rows; k += gridDim.x * 4) {
+    if (k >= K) {
+      if (Cm2)
+        for (int d = lane; d < DP; d += 64) Cm2[(int64_t)k * DP + d] = (__bf16)0.f;
+      if (cnorm && lane == 0) cnorm[k] = 3.0e38f;
+      continue;
     }
+    const double n = (double)counts[k];
+    const double vk = v[k];
+    const double inv = n > 0.0 ? 1.0 / (vk + n) : 0.0;
+    float sh = 0.f, nrm = 0.f;
+    const int dend = Cm2 ? (DP > D ? DP : D) : D;
+    for (int d = lane; d < dend; d += 64) {
+      if (d < D) {
+        const CT old = C[(int64_t)k * D + d];
+        CT nw = old;
+        if (n > 0.0) {
+          nw = (CT)((vk * (double)old + (double)sums[(int64_t)k * D + d]) * inv);
+          C[(int64_t)k * D + d] = nw;
+          const float df = (float)nw - (float)old;
+          sh += df * df;
+        }
+        if (Cm2) {
+          const __bf16 b = (__bf16)(float)nw;
+          const float bf = (float)b;
+          Cm2[(int64_t)k * DP + d] = (__bf16)(-2.f * bf);
+          nrm = fmaf(bf, bf, nrm);
+        }
+      } else if (Cm2 && d < DP) {
+        Cm2[(int64_t)k * DP + d] = (__bf16)0.f;
+      }
+    }
+    if (shift) shmax = max(shmax, __float_as_uint(wave_sum(sh)));
+    if (cnorm) {
+      nrm = wave_sum(nrm);
+      if (lane == 0) cnorm[k] = nrm;
+    }
+    if (lane == 0) v[k] = vk + n;  // every lane read v[k] above (wave lockstep)
   }
-  if (shift) {
-    sh = wave_sum(sh);
-    if (lane == 0) atomicMax(reinterpret_cast<unsigned*>(shift), __float_as_uint(sh));
-  }
-  if (cnorm) {
-    nrm = wave_sum(nrm);
-    if (lane == 0) cnorm[k] = nrm;
-  }
-  if (lane == 0) v[k] = vk + n;  // every lane read v[k] above (wave lockstep)
+  if (shift) block_max_shift(shmax, shift);
 }
 
 template <typename ACC, typename CT>
 int launch_sculley(const void* sums, const void* counts, int K, int D, void* C, double* v,
                    float* shift, void* Cm2, float* cnorm, int Kp, int DP, hipStream_t s) {
   const int rows = Cm2 ? (Kp > K ? Kp : K) : K;
-  hipLaunchKernelGGL((sculley_kernel<ACC, CT>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s,
+  const int blocks = std::min((rows + 3) / 4, MAX_BLOCKS);
+  hipLaunchKernelGGL((sculley_kernel<ACC, CT>), dim3((unsigned)blocks), dim3(256), 0, s,
                      (const ACC*)sums, (const ACC*)counts, K, D, (CT*)C, v, shift, (__bf16*)Cm2,
                      cnorm, Kp, DP);
   TDC_CHECK_LAUNCH();
