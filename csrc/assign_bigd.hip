@@ -90,7 +90,9 @@ __device__ __forceinline__ f32x16 mma(const typename OP::frag& a, const typename
 // D: padded feature count.  X rows: ldx BYTES apart.  Xs/Cs: E8M0 scales [rows, D/32].
 // ABL (timing ablations, 0 in production; results are invalid otherwise):
 //   1 = no ring refill after the prologue, 2 = no per-stage barrier, 4 = no epilogue
-template <class OP, int D, int WAVES, int NST, int ABL = 0>
+// QH: 32-centroid row tiles per ring stage (QH=2 halves the per-stage barrier / refill /
+// norm-load overhead per MFMA; the stage index t then counts QH-tile stages).
+template <class OP, int D, int WAVES, int NST, int ABL = 0, int QH = 1>
 __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
     const uint8_t* __restrict__ X, const uint8_t* __restrict__ Xs, int64_t N, int64_t ldx,
     const uint8_t* __restrict__ Cm2, const uint8_t* Cs,
@@ -102,11 +104,20 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
   constexpr int NK = HALFB / OP::FB;    // MFMAs per 32x32 tile
   constexpr int CPR = RB / 16;
   constexpr int UPF = OP::FB / 16;      // 16-B LDS reads per fragment
-  constexpr int TILE_B = 32 * RB;
+  constexpr int TILE_B = QH * 32 * RB;
   constexpr int PIECES = TILE_B / 1024;
   constexpr int PPW = PIECES / WAVES;
   constexpr int SB = D / 32;            // scale bytes per row
   constexpr int NSW = OP::SCALED ? NK / 2 : 1;  // scale dwords per lane (= the row's)
+  // per-stage side region, DMA'd with the tile: ||c||^2 of the QH*32 rows, then (fp8)
+  // their E8M0 scale rows; every wave issues exactly ONE extra LDS-DMA for it (LPW lanes)
+  constexpr int NRM_B = QH * 32 * 4;
+  constexpr int EXB = NRM_B + (OP::SCALED ? QH * 32 * SB : 0);
+  constexpr int EXC = EXB / 16;
+  constexpr int LPW = (EXC + WAVES - 1) / WAVES;
+  constexpr int STAGE_B = TILE_B + WAVES * LPW * 16;
+  constexpr int VPS = PPW + 1;          // vector-memory ops per wave per stage
+  static_assert(EXB % 16 == 0 && LPW <= 64, "side region");
   static_assert(RB % 256 == 0, "row bytes must be a multiple of 256");
   static_assert(PIECES % WAVES == 0, "stage must split evenly over the waves");
   static_assert(!OP::SCALED || NK % 2 == 0, "fp8: D must be a multiple of 128");
@@ -163,53 +174,59 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
       const int piece = w * PPW + i;
       const int L = piece * 64 + lane;  // 16-B chunk index inside the stage
       const int row = L / CPR, cp = L % CPR;
-      const uint8_t* src = Cm2 + ((int64_t)t * 32 + row) * RB + swz<RB>(row, cp) * 16;
+      const uint8_t* src = Cm2 + ((int64_t)t * (32 * QH) + row) * RB + swz<RB>(row, cp) * 16;
       __builtin_amdgcn_global_load_lds(
           (const void*)src,
-          (__attribute__((address_space(3))) void*)(smem + slot * TILE_B + piece * 1024), 16, 0, 0);
+          (__attribute__((address_space(3))) void*)(smem + slot * STAGE_B + piece * 1024), 16, 0, 0);
+    }
+    if (lane < LPW) {
+      const int c = w * LPW + lane;  // 16-B chunk of the side region
+      const uint8_t* src = reinterpret_cast<const uint8_t*>(cnorm);  // (pad chunks: dummy)
+      if (c < NRM_B / 16)
+        src = reinterpret_cast<const uint8_t*>(cnorm + (int64_t)t * (QH * 32)) + c * 16;
+      else if (OP::SCALED && c < EXC)
+        src = Cs + (int64_t)t * (QH * 32) * SB + (c - NRM_B / 16) * 16;
+      __builtin_amdgcn_global_load_lds(
+          (const void*)src,
+          (__attribute__((address_space(3))) void*)(smem + slot * STAGE_B + TILE_B + w * LPW * 16),
+          16, 0, 0);
     }
   };
-  // per-tile operands that do not go through LDS: ||c||^2 rows of this lane, A scales.
-  // Issued with inline asm so the compiler does not track them: its waitcnt pass puts a
-  // conservative vmcnt(0) before their first use inside the ring loop (= waiting for the
-  // refill DMAs just issued).  They are issued before the stage's refill and consumed one
-  // stage later, after the counted end-of-stage vmcnt wait has retired them.
-  auto load_norm = [&](int t, f32x16& init, int* sa) __attribute__((always_inline)) {
-    const float* ns = cnorm + (int64_t)t * 32 + 4 * h;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      f32x4 v;
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(ns + 8 * q) : "memory");
-      init[4 * q + 0] = v[0];
-      init[4 * q + 1] = v[1];
-      init[4 * q + 2] = v[2];
-      init[4 * q + 3] = v[3];
-    }
-    if constexpr (OP::SCALED) {
-      const int* s = reinterpret_cast<const int*>(Cs + ((int64_t)t * 32 + r) * SB);
-#pragma unroll
-      for (int i = 0; i < NSW; ++i)
-        asm volatile("global_load_dword %0, %1, off" : "=v"(sa[i]) : "v"(s + i) : "memory");
-    }
-  };
-
   float best = INFINITY;
   int bt = 0;
-  // one ring stage; cur/nxt are distinct register sets (the loop is unrolled by two and
-  // swaps them), so consuming the prefetched norms never needs a copy -- a copy would
-  // force a vmcnt wait on the freshly issued ring DMAs.
-  auto stage = [&](int i, const f32x16& init_cur, const int* sa_cur, f32x16& init_nxt,
-                   int* sa_nxt) __attribute__((always_inline)) {
+  // one ring stage: the tile, its norms and its scales all arrived by LDS-DMA NST-1
+  // stages ago, so the only vmcnt wait per stage is the counted one on the ring
+  auto stage = [&](int i) __attribute__((always_inline)) {
     const int t = t0 + i;
     const int slot = i % NST;
-    load_norm(i + 1 < nt ? t + 1 : t, init_nxt, sa_nxt);
-    asm volatile("" ::: "memory");  // keep these loads older than the refill (vmcnt order)
     if constexpr (!(ABL & 1)) {
       const int in = i + NST - 1;
       issue(t0 + (in < nt ? in : nt - 1), in % NST);
     }
+#pragma unroll 1
+    for (int qh = 0; qh < QH; ++qh) {
     // LDS byte address of this lane's row in the slot
-    const unsigned rbase = lds_base + slot * TILE_B + r * RB;
+    const unsigned rbase = lds_base + slot * STAGE_B + (qh * 32 + r) * RB;
+    const unsigned xbase = lds_base + slot * STAGE_B + TILE_B;
+    // accumulator init = ||c||^2 of rows qh*32 + 8j + 4h + [0,4) (32x32 C layout) and the
+    // scale row of centroid row qh*32 + r; issued before the fragments, so the first
+    // counted lgkmcnt wait below also covers them
+    f32x16 acc;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f32x4 v;
+      asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(xbase + (qh * 32 + 8 * j + 4 * h) * 4));
+      acc[4 * j + 0] = v[0];
+      acc[4 * j + 1] = v[1];
+      acc[4 * j + 2] = v[2];
+      acc[4 * j + 3] = v[3];
+    }
+    int sa_row[NSW];
+    if constexpr (OP::SCALED) {
+#pragma unroll
+      for (int j = 0; j < NSW; ++j)
+        asm volatile("ds_read_b32 %0, %1" : "=v"(sa_row[j]) : "v"(xbase + NRM_B + (qh * 32 + r) * SB + 4 * j));
+    }
     // A fragments via inline-asm ds_read_b128: the compiler cannot prove they do not
     // alias the in-flight LDS-DMA ring refill, so compiler-visible LDS reads get a
     // vmcnt(0) in front of them (= waiting for the refill just issued, every stage).
@@ -227,7 +244,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
       }
       return a;
     };
-    f32x16 acc = init_cur;
     typename OP::frag a0 = lds_frag(0);
     typename OP::frag a1 = lds_frag(NK > 1 ? 1 : 0);
 #pragma unroll
@@ -242,7 +258,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
       __builtin_amdgcn_sched_barrier(0);
       int sa = 0, sb = 0;
       if constexpr (OP::SCALED) {  // block 2kk+h: dword kk>>1, byte 2(kk&1)+h
-        sa = (sa_cur[kk >> 1] >> (16 * (kk & 1) + hsh)) & 0xff;
+        sa = (sa_row[kk >> 1] >> (16 * (kk & 1) + hsh)) & 0xff;
         sb = (xs[kk >> 1] >> (16 * (kk & 1) + hsh)) & 0xff;
       }
       acc = mma<OP>(a0, bq[kk], acc, sa, sb);
@@ -260,30 +276,24 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
         m = __builtin_fminf(m, __uint_as_float((__float_as_uint(acc[j]) & ~EMB) | (unsigned)j));
       const bool up = m < best;
       best = up ? m : best;
-      bt = up ? t : bt;
+      bt = up ? t * QH + qh : bt;  // 32-row tile index
     }
+    }  // qh
     if constexpr (ABL & 1) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * PPW) : "memory");  // stage i+1 landed
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * VPS) : "memory");  // stage i+1 landed
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if constexpr (!(ABL & 2)) __builtin_amdgcn_s_barrier();  // ... for every wave's pieces
   };
 
-  f32x16 init_a, init_b;
-  int sa_a[NSW], sa_b[NSW];
-  load_norm(t0, init_a, sa_a);
-  asm volatile("" ::: "memory");
 #pragma unroll
   for (int s = 0; s < NST - 1; ++s) issue(t0 + (s < nt ? s : nt - 1), s);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * PPW) : "memory");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * VPS) : "memory");
   __builtin_amdgcn_s_barrier();
 
-  for (int i = 0; i < nt; i += 2) {
-    stage(i, init_a, sa_a, init_b, sa_b);
-    if (i + 1 < nt) stage(i + 1, init_b, sa_b, init_a, sa_a);
-  }
+  for (int i = 0; i < nt; ++i) stage(i);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   const float ob = __shfl_xor(best, 32, 64);
@@ -393,13 +403,16 @@ __global__ __launch_bounds__(256) void quant_fp8_kernel(const T* __restrict__ X,
 using namespace tdc::bigd;
 
 namespace {
-template <class OP, int D, int WAVES, int NST, int ABL = 0>
+template <class OP, int D, int WAVES, int NST, int ABL = 0, int QH = 1>
 int launch_bigd(const void* X, const void* Xs, int64_t N, int64_t ldx_bytes, const void* Cm2,
                 const void* Cs, const float* cnorm, int Kp, int kg_tiles, const float* xnorm,
                 int32_t* labels, float* mind, unsigned long long* keys, hipStream_t stream) {
-  constexpr int TILE_B = 32 * D * OP::ES;
-  const size_t lds = (size_t)NST * TILE_B;
-  auto kern = assign_bigd_kernel<OP, D, WAVES, NST, ABL>;
+  // = the kernel's STAGE_B: tile + one 16-B side chunk per lane of LPW lanes per wave
+  constexpr int TILE_B = QH * 32 * D * OP::ES;
+  constexpr int EXB = QH * 32 * 4 + (OP::SCALED ? QH * 32 * (D / 32) : 0);
+  constexpr int LPW = (EXB / 16 + WAVES - 1) / WAVES;
+  const size_t lds = (size_t)NST * (TILE_B + WAVES * LPW * 16);
+  auto kern = assign_bigd_kernel<OP, D, WAVES, NST, ABL, QH>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -407,7 +420,11 @@ int launch_bigd(const void* X, const void* Xs, int64_t N, int64_t ldx_bytes, con
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  const int ntiles = Kp / 32;
+  // stages of QH 32-row tiles (the caller checked Kp % (32*QH) == 0); a K-group is a
+  // whole number of stages (the group size is an L2-residency tunable, labels do not
+  // depend on it)
+  const int ntiles = Kp / (32 * QH);
+  if (kg_tiles > 0) kg_tiles = kg_tiles / QH > 0 ? kg_tiles / QH : 1;
   if (kg_tiles <= 0 || kg_tiles > ntiles) kg_tiles = ntiles;
   const int ngroups = (ntiles + kg_tiles - 1) / kg_tiles;
   if (ngroups > 1 && keys == nullptr) return (int)hipErrorInvalidValue;
@@ -449,6 +466,10 @@ int tdc_assign_bigd(int dtype, const void* X, const void* Xs, int64_t N, int64_t
       case 512: return launch_bigd<OpFp8, 512, 8, 4>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
       case 768: {
         static const int abl = getenv("TDC_BIGD_ABL") ? atoi(getenv("TDC_BIGD_ABL")) : 0;
+        // 64-row stages: 206.5 vs 211.8 ms (grouped), 197.3 vs 200.8 ms (one group) at N=5M
+        static const int qh = getenv("TDC_BIGD_QH") ? atoi(getenv("TDC_BIGD_QH")) : 2;
+        if (abl == 0 && qh == 2 && Kp % 64 == 0)  // 64-row stages
+          return launch_bigd<OpFp8, 768, 8, 3, 0, 2>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
         switch (abl) {  // timing ablations (tools only)
           case 1: return launch_bigd<OpFp8, 768, 8, 4, 1>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
           case 2: return launch_bigd<OpFp8, 768, 8, 4, 2>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);

@@ -35,8 +35,11 @@ TORCH_DTYPES = {"fp64": torch.float64, "fp32": torch.float32, "bf16": torch.bflo
 MFMA_DIMS = (32, 64, 128, 256)
 WIDE_BF16_DIMS = (384, 512)
 FP8_DIMS = (256, 512, 768, 1024)
-# centroid bytes one K-group may occupy (an XCD's L2 is 4 MiB; leave room for X/labels)
-KGROUP_BYTES = int(__import__("os").environ.get("TDC_KGROUP_BYTES", 3 << 20))
+# centroid bytes one K-group may occupy (0 = one group over all of K).  Grouping keeps a
+# group L2-resident per XCD, but measured slower than one group (the 256 MiB MALL serves
+# the 48 MiB fp8 table): N=5M D=768 K=65536 fp8, 3 MiB groups 206.5 ms vs one group
+# 197.3 ms (docs/PERF_NOTES.md).  Kept as a tunable (TDC_KGROUP_BYTES).
+KGROUP_BYTES = int(__import__("os").environ.get("TDC_KGROUP_BYTES", 0))
 # assign/update overlap: the resident bf16 step runs in this many row slices; slice i's
 # (memory-bound) update runs on a side stream while slice i+1's (MFMA-bound) assign runs
 OVERLAP_SLICES = int(__import__("os").environ.get("TDC_OVERLAP_SLICES", 1))
@@ -78,6 +81,8 @@ def fp8_dim(d: int) -> Optional[int]:
 
 def kgroup_tiles(row_bytes: int, kp: int) -> int:
     """Centroid tiles (of 32) per K-group so a group stays L2-resident (0 = one group)."""
+    if KGROUP_BYTES <= 0:
+        return 0
     tiles = max(1, KGROUP_BYTES // (32 * row_bytes))
     return 0 if tiles * 32 >= kp else int(tiles)
 
