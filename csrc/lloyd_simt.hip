@@ -42,11 +42,26 @@ __global__ __launch_bounds__(256) void lloyd_small_kernel(
     for (int d = 0; d < DMAX; ++d) acc[k][d] = 0;
   }
 
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + tid; i < N; i += stride) {
+  // KMAX >= 16 (K up to 16, e.g. the reference's K=15): the register tiles leave ~2 waves
+  // per SIMD, too few to cover the 8-B row loads, so contiguous 256-row tiles are staged
+  // through LDS with 16-B loads (K=15 D=5 fp64: 26.3 -> 32.5 G points/s; slower at
+  // small KMAX, where occupancy already hides the loads: docs/PERF_NOTES.md)
+  constexpr bool STAGE = KMAX >= 16;
+  __shared__ __attribute__((aligned(16))) T s_x[STAGE ? 256 * DMAX : 1];
+  const bool tiled = STAGE && ldx == D && ((uintptr_t)X % 16) == 0;
+  const int64_t ntile = (N + 255) / 256;
+  for (int64_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+    const int64_t i = tile * 256 + tid;
+    if (tiled) {
+      __syncthreads();  // previous tile consumed
+      stage_rows_lds(X, N, D, tile * 256, s_x);
+      __syncthreads();
+    }
+    if (i >= N) continue;
     T x[DMAX];
 #pragma unroll
-    for (int d = 0; d < DMAX; ++d) x[d] = (d < D) ? X[i * ldx + d] : (T)0;
+    for (int d = 0; d < DMAX; ++d)
+      x[d] = (d < D) ? (tiled ? s_x[tid * D + d] : X[i * ldx + d]) : (T)0;
     T bd = (T)INFINITY;  // NaN distances (poisoned centroid, empty_cluster='nan') never win
     int best = 0;
 #pragma unroll

@@ -45,4 +45,22 @@ template <typename T, typename A> __device__ __forceinline__ A to_acc(T v) { ret
 __device__ __forceinline__ void atomic_add(float* p, float v) { atomicAdd(p, v); }
 __device__ __forceinline__ void atomic_add(double* p, double v) { atomicAdd(p, v); }
 
+// Stage rows [r0, r0 + 256) of a CONTIGUOUS row-major X (ldx == D, 16-B aligned base)
+// into LDS with 16-byte loads.  Returns the number of valid rows; the caller syncs before
+// reading s_x[row * D + d].
+template <typename T>
+__device__ __forceinline__ int stage_rows_lds(const T* __restrict__ X, int64_t N, int D,
+                                              int64_t r0, T* s_x) {
+  const int rows = (int)((N - r0) < 256 ? (N - r0) : 256);
+  const T* src = X + r0 * D;
+  if (rows == 256) {
+    const int nch = 256 * D * (int)sizeof(T) / 16;
+    for (int c = threadIdx.x; c < nch; c += 256)
+      reinterpret_cast<uint4*>(s_x)[c] = reinterpret_cast<const uint4*>(src)[c];
+  } else {
+    for (int e = threadIdx.x; e < rows * D; e += 256) s_x[e] = src[e];
+  }
+  return rows;
+}
+
 }  // namespace tdc
