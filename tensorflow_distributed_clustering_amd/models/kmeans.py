@@ -433,13 +433,27 @@ class KMeans:
             n_global=n_global, streamed=eng.streamed)
         return self
 
+    def predictor(self, device=None):
+        """A :class:`..serving.ClusterPredictor` on the fitted centroids (cached per device)."""
+        from ..serving import ClusterPredictor
+        if self.result_ is None:
+            raise RuntimeError("fit() first")
+        dev = torch.device(device) if device is not None else torch.device(
+            self.result_.labels.device if self.result_.labels is not None else "cpu")
+        cache = self.__dict__.setdefault("_predictors", {})
+        key = (str(dev), id(self.result_))
+        if key not in cache:
+            cache.clear()
+            cache[key] = ClusterPredictor(self.result_.centers, self.cfg.dtype, dev,
+                                          self.cfg.backend)
+        return cache[key]
+
     def predict(self, x: torch.Tensor) -> torch.Tensor:
         """Labels of new points against the fitted centroids (local, no collectives)."""
         x = torch.as_tensor(x)
-        cfg = self.cfg
-        local = make_lloyd_ops(x, cfg.n_clusters, cfg.dtype, cfg.backend, cfg.empty_cluster)
-        C = torch.as_tensor(self.result_.centers).to(x.device, local.c_dtype).contiguous()
-        local.prepare(C)
-        labels = torch.empty(local.n, dtype=torch.int32, device=x.device)
-        local.assign(C, labels, None)
-        return labels
+        return self.predictor(x.device).predict(x)
+
+    def score(self, x: torch.Tensor) -> float:
+        """Negative inertia of ``x`` (sklearn convention)."""
+        x = torch.as_tensor(x)
+        return self.predictor(x.device).score(x)

@@ -111,6 +111,25 @@ class MiniBatchStepper:
             batch = self.next_batch()
             self.local.bind(batch).step(self.C, self.blabels[: batch.shape[0]], None, self.sums,
                                         self.counts)
+        self._apply()
+
+    def step_on(self, batch: torch.Tensor):
+        """One mini-batch update on rows the caller supplies (``partial_fit``; online /
+        streaming clustering).  Collective: every rank calls it with its own batch."""
+        dt, width = self.local.layout
+        if not (batch.dtype == dt and batch.shape[1] == width and batch.is_contiguous()):
+            xb = torch.zeros(batch.shape[0], width, dtype=dt, device=self.device)
+            xb[:, : min(width, batch.shape[1])] = batch[:, :width]
+            batch = xb
+        if self.blabels.numel() < batch.shape[0]:
+            self.blabels = torch.zeros(batch.shape[0], dtype=torch.int32, device=self.device)
+        self.buf.zero_()
+        self.local.bind(batch).step(self.C, self.blabels[: batch.shape[0]], None, self.sums,
+                                    self.counts)
+        self._apply()
+
+    def _apply(self):
+        """All-reduce the batch partials and move the centres (Sculley)."""
         self.comm.allreduce_bucketed_(self.buf, 64 << 20)
         if hasattr(self.local, "sculley"):
             if self._shift_buf is None:
@@ -154,7 +173,38 @@ class MiniBatchKMeans:
 
     @property
     def cluster_centers_(self):
+        if self.result_ is None and getattr(self, "engine_", None) is not None:
+            return self.engine_.C.double().cpu().numpy()  # partial_fit state
         return self.result_.centers
+
+    def partial_fit(self, x_batch, init_centers_=None) -> "MiniBatchKMeans":
+        """Online update from one batch of rows (sklearn ``partial_fit``): the first call
+        initialises the centres from that batch (``cfg.init``; it needs >= K rows), every
+        call then applies one Sculley update with the batch.  Multi-rank: every rank calls
+        it with its own batch (one all-reduce per call)."""
+        cfg = self.cfg
+        x = torch.as_tensor(x_batch)
+        dev = torch.device(self.device) if self.device is not None else (
+            self.comm.device if self.comm is not None else x.device)
+        x = x.to(dev)
+        if self.comm is None:
+            self.comm = local_comm(dev)
+        eng = getattr(self, "engine_", None)
+        if eng is None:
+            n_global, row_offset = _shard_geometry(int(x.shape[0]), self.comm)
+            eng = self.engine_ = MiniBatchStepper(x, cfg.replace(batch_size=int(x.shape[0])),
+                                                  self.comm, n_global, row_offset,
+                                                  init_centers_)
+        eng.step_on(x)
+        self.result_ = None  # centres moved: cluster_centers_ reads the live state
+        return self
+
+    def predict(self, x):
+        """Labels of new rows against the current centres."""
+        from ..serving import ClusterPredictor
+        x = torch.as_tensor(x)
+        return ClusterPredictor(self.cluster_centers_, self.cfg.dtype, x.device,
+                                self.cfg.backend).predict(x)
 
     def fit(self, x_local, init_centers_=None, n_global=None, row_offset=None) -> "MiniBatchKMeans":
         cfg = self.cfg

@@ -79,12 +79,32 @@ def fp8_dim(d: int) -> Optional[int]:
     return None
 
 
-def kgroup_tiles(row_bytes: int, kp: int) -> int:
-    """Centroid tiles (of 32) per K-group so a group stays L2-resident (0 = one group)."""
-    if KGROUP_BYTES <= 0:
+# work items (point block x K-group) the wide-D kernel needs to fill 256 CUs
+KGROUP_MIN_ITEMS = 2048
+
+
+def kgroup_tiles(row_bytes: int, kp: int, n: Optional[int] = None) -> int:
+    """Centroid tiles (of 32) per K-group (0 = one group over all of K).
+
+    With ``TDC_KGROUP_BYTES`` > 0: groups of that many centroid bytes (L2 residency).
+    Otherwise one group, unless the point count is too small to fill the chip (serving
+    requests, small chunks): then K is split so that (N/256 point blocks) x groups reaches
+    KGROUP_MIN_ITEMS work items (1024 rows x K=65536 fp8: 4 items -> 2.2 ms; the groups'
+    winners merge through the 64-bit key atomics).  Groups are a whole number of 64-row
+    stages."""
+    ntiles = kp // 32
+    if KGROUP_BYTES > 0:
+        tiles = max(1, KGROUP_BYTES // (32 * row_bytes))
+        return 0 if tiles * 32 >= kp else int(tiles)
+    if n is None:
         return 0
-    tiles = max(1, KGROUP_BYTES // (32 * row_bytes))
-    return 0 if tiles * 32 >= kp else int(tiles)
+    npb = max(1, (n + 255) // 256)
+    if npb >= KGROUP_MIN_ITEMS or ntiles < 4:
+        return 0
+    groups = min(-(-KGROUP_MIN_ITEMS // npb), ntiles // 2)
+    tiles = -(-ntiles // groups)
+    tiles += tiles & 1
+    return 0 if tiles >= ntiles else int(tiles)
 
 
 def use_native(device: torch.device, backend: str) -> bool:
@@ -301,8 +321,14 @@ class _GroupedAssign:
     """Shared state of the K-grouped wide-D kernels: point norms + merge keys."""
 
     def _init_grouped(self, row_bytes: int):
+        self._row_bytes = row_bytes
         self.kg = kgroup_tiles(row_bytes, self.kp)
         self._keys = None
+
+    def _kg_for(self, n: int) -> int:
+        """K-group size for an n-row launch (splits K when n alone cannot fill the chip)."""
+        self.kg = kgroup_tiles(self._row_bytes, self.kp, n)
+        return self.kg
 
     def _keys_for(self, n):
         if self.kg == 0:
@@ -346,17 +372,18 @@ class HipWideBf16Lloyd(_GroupedAssign, _LocalOpsBase):
         return (torch.bfloat16, self.dp)
 
     def bind(self, x):
-        if x is not self.x:
-            if x.dtype != torch.bfloat16 or x.shape[1] != self.dp:
-                raise ValueError(f"chunk layout {(x.dtype, x.shape[1])} != {self.layout}")
-            self._set_x(x)
+        # always re-derive the row norms: the caller may have refilled the same buffer
+        if x.dtype != torch.bfloat16 or x.shape[1] != self.dp:
+            raise ValueError(f"chunk layout {(x.dtype, x.shape[1])} != {self.layout}")
+        self._set_x(x)
         return self
 
     def prepare(self, C):
         self.ops.finalize(None, None, C, 0, None, self.cm2, self.cnorm)
 
     def assign(self, C, labels, mind):
-        self.ops.assign_bigd(self.x, None, self.xnorm, self.cm2, None, self.cnorm, self.kg,
+        self.ops.assign_bigd(self.x, None, self.xnorm, self.cm2, None, self.cnorm,
+                             self._kg_for(self.x.shape[0]),
                              labels, mind, self._keys_for(self.n))
 
     def step(self, C, labels, mind, sums, counts):
@@ -412,10 +439,11 @@ class HipFp8Lloyd(_GroupedAssign, _LocalOpsBase):
         return (self.x.dtype, self.x.shape[1])
 
     def bind(self, x):
-        if x is not self.x:
-            if x.shape[1] != self.x.shape[1]:
-                raise ValueError(f"chunk layout {(x.dtype, x.shape[1])} != {self.layout}")
-            self._set_x(x)
+        # always re-quantise: the caller may have refilled the same buffer in place (a
+        # serving layout buffer, a streaming ring slot), so identity says nothing
+        if x.shape[1] != self.x.shape[1]:
+            raise ValueError(f"chunk layout {(x.dtype, x.shape[1])} != {self.layout}")
+        self._set_x(x)
         return self
 
     def prepare(self, C):
@@ -423,8 +451,9 @@ class HipFp8Lloyd(_GroupedAssign, _LocalOpsBase):
 
     def assign(self, C, labels, mind):
         n = self.n
+        kg = self._kg_for(n)
         self.ops.assign_bigd(self.x8[:n], self.xs[:n], self.xnorm[:n], self.cm2, self.cs,
-                             self.cnorm, self.kg, labels, None, self._keys_for(n))
+                             self.cnorm, kg, labels, None, self._keys_for(n))
         if mind is not None:
             # inertia from the full-precision shard (the fp8 distances include the
             # quantisation noise of both operands; they only pick the winner)
