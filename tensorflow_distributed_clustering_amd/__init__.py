@@ -10,8 +10,9 @@ from .models.kmeans import KMeans, ClusterResult
 from .models.fcm import FuzzyCMeans
 from .models.minibatch import MiniBatchKMeans
 from .parallel.dist import Comm, init_comm, local_comm, shard_bounds
+from .serving import ClusterPredictor
 
 __version__ = "0.1.0"
 
-__all__ = ["ClusterConfig", "KMeans", "FuzzyCMeans", "MiniBatchKMeans", "ClusterResult", "Comm", "init_comm",
-           "local_comm", "shard_bounds", "__version__"]
+__all__ = ["ClusterConfig", "KMeans", "FuzzyCMeans", "MiniBatchKMeans", "ClusterResult",
+           "ClusterPredictor", "Comm", "init_comm", "local_comm", "shard_bounds", "__version__"]
