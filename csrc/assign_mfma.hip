@@ -89,10 +89,18 @@ int tdc_assign_mfma_bf16(const void* X, int64_t N, int64_t ldx, int DP, const vo
   if (ring == 3 && (DP == 64 || DP == 128 || DP == 256)) {  // 16x16x32 MFMA variant
     const int64_t per = 4 * 4 * 16;
     dim3 grid((unsigned)((N + per - 1) / per));
-    if (DP == 64)
-      hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<64, 4, 3, 4, 4>), grid, dim3(256), 0,
-                         stream, x, N, ldx, c, cnorm, Kp / 64, labels, mind);
-    else if (DP == 128)
+    if (DP == 64) {
+      // D=64: P=8 point tiles per wave (the register footprint of D=128's P=4) and 128-row
+      // stages: 1.74 -> 1.60 ms at N=4M, K=4096 (TDC_RING3_D64 sweep)
+      const int64_t per8 = 4 * 8 * 16;
+      const dim3 grid8((unsigned)((N + per8 - 1) / per8));
+      if (Kp % 128 == 0)
+        hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<64, 8, 3, 4, 8>), grid8, dim3(256), 0,
+                           stream, x, N, ldx, c, cnorm, Kp / 128, labels, mind);
+      else
+        hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<64, 8, 3, 4, 4>), grid8, dim3(256), 0,
+                           stream, x, N, ldx, c, cnorm, Kp / 64, labels, mind);
+    } else if (DP == 128)
       hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<128, 4, 3, 4, 4>), grid, dim3(256), 0,
                          stream, x, N, ldx, c, cnorm, Kp / 64, labels, mind);
     else
@@ -135,9 +143,13 @@ int tdc_assign_mfma_bf16_indexed(const void* X, const int32_t* rowidx, int64_t N
   const __bf16* x = (const __bf16*)X;
   const __bf16* c = (const __bf16*)Cm2;
   const dim3 grid((unsigned)((N + 255) / 256));
-  if (DP == 64)
-    hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<64, 4, 3, 4, 4>), grid, dim3(256), 0, stream,
-                       x, N, ldx, c, cnorm, Kp / 64, labels, mind, rowidx);
+  const dim3 grid8((unsigned)((N + 511) / 512));
+  if (DP == 64 && Kp % 128 == 0)  // as in tdc_assign_mfma_bf16
+    hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<64, 8, 3, 4, 8>), grid8, dim3(256), 0,
+                       stream, x, N, ldx, c, cnorm, Kp / 128, labels, mind, rowidx);
+  else if (DP == 64)
+    hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<64, 8, 3, 4, 4>), grid8, dim3(256), 0,
+                       stream, x, N, ldx, c, cnorm, Kp / 64, labels, mind, rowidx);
   else if (DP == 128)
     hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<128, 4, 3, 4, 4>), grid, dim3(256), 0,
                        stream, x, N, ldx, c, cnorm, Kp / 64, labels, mind, rowidx);
