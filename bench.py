@@ -60,6 +60,9 @@ def parse(argv=None):
     ap.add_argument("--batch-size", type=int, default=0, help="mini-batch rows per rank")
     ap.add_argument("--method", default="kmeans", choices=["kmeans", "fcm"],
                     help="fcm: distributed Fuzzy C-Means step (fuzzifier m = D, as the reference)")
+    ap.add_argument("--algorithm", default="lloyd", choices=["lloyd", "bounded"],
+                    help="bounded: Lloyd with Hamerly bounds (not the headline metric's "
+                         "algorithm; reported in config.algorithm)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step from a captured HIP graph (1 GPU; RCCL capture for N>1)")
     ap.add_argument("--profile-steps", action="store_true",
@@ -102,7 +105,7 @@ def main(argv=None):
           "fp64": torch.float64}[a.dtype]
     x = gaussian_blobs(e - s, a.dim, a.k, seed=a.seed, row_offset=s, dtype=dt, device=dev)
     cfg = tdc.ClusterConfig(n_clusters=a.k, max_iter=a.steps, dtype=a.dtype, init="random",
-                            seed=a.seed, compute_inertia=False)
+                            seed=a.seed, compute_inertia=False, algorithm=a.algorithm)
     if a.mode == "minibatch":
         from tensorflow_distributed_clustering_amd.models.minibatch import MiniBatchStepper
         eng = MiniBatchStepper(x, cfg.replace(batch_size=a.batch_size or (1 << 20)), comm,
@@ -111,6 +114,10 @@ def main(argv=None):
     elif a.method == "fcm":
         from tensorflow_distributed_clustering_amd.models.fcm import FcmEngine
         eng = FcmEngine(x, cfg, comm, n_global, s)
+        points_per_step = n_global
+    elif a.algorithm == "bounded":
+        from tensorflow_distributed_clustering_amd.models.bounded import BoundedLloydEngine
+        eng = BoundedLloydEngine(x, cfg, comm, n_global, s)
         points_per_step = n_global
     else:
         eng = LloydEngine(x, cfg, comm, n_global, s)
@@ -162,6 +169,9 @@ def main(argv=None):
         }
         if breakdown:
             out["phase_ms"] = breakdown
+        if a.algorithm != "lloyd":
+            out["config"]["algorithm"] = a.algorithm
+            out["active_frac_last_step"] = getattr(eng, "active_frac", None)
         print(json.dumps(out), flush=True)
 
 

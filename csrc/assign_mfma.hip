@@ -161,3 +161,29 @@ int tdc_assign_mfma_bf16_indexed(const void* X, const int32_t* rowidx, int64_t N
   TDC_CHECK_LAUNCH();
   return 0;
 }
+
+// Top-2 distances (labels, d1 = min squared distance, d2 = second smallest); rowidx
+// nullable (indexed rows as above).  Feeds the bounds of models/bounded.py.
+int tdc_assign_mfma_bf16_top2(const void* X, const int32_t* rowidx, int64_t N, int64_t ldx,
+                              int DP, const void* Cm2, const float* cnorm, int Kp,
+                              int32_t* labels, float* mind, float* mind2, hipStream_t stream) {
+  if (N <= 0) return 0;
+  if (Kp % 64 != 0 || mind == nullptr || mind2 == nullptr) return (int)hipErrorInvalidValue;
+  const __bf16* x = (const __bf16*)X;
+  const __bf16* c = (const __bf16*)Cm2;
+  const dim3 grid((unsigned)((N + 255) / 256));
+  const dim3 grid8((unsigned)((N + 511) / 512));
+  if (DP == 64)
+    hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<64, 8, 3, 4, 4, true>), grid8, dim3(256), 0,
+                       stream, x, N, ldx, c, cnorm, Kp / 64, labels, mind, rowidx, mind2);
+  else if (DP == 128)
+    hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<128, 4, 3, 4, 4, true>), grid, dim3(256), 0,
+                       stream, x, N, ldx, c, cnorm, Kp / 64, labels, mind, rowidx, mind2);
+  else if (DP == 256)
+    hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<256, 4, 2, 4, 4, true>), grid, dim3(256), 0,
+                       stream, x, N, ldx, c, cnorm, Kp / 64, labels, mind, rowidx, mind2);
+  else
+    return (int)hipErrorInvalidValue;
+  TDC_CHECK_LAUNCH();
+  return 0;
+}

@@ -590,13 +590,16 @@ void assign_mfma_bf16_ring2_kernel(const __bf16* __restrict__ X, int64_t N, int6
 // at equal cycles per FLOP).  C layout: lane l holds rows 4*(l>>4)+i (centroids) of
 // column l&15 (its point); the 4 lane groups are combined once at the end.
 // ------------------------------------------------------------------------------------
-template <int DP, int P, int NST, int WAVES, int QT>
+// TOP2: also track the second-smallest distance (mind2): one v_med3 + one v_min per
+// score instead of half a v_min3 (bounds-based pruning, models/bounded.py).
+template <int DP, int P, int NST, int WAVES, int QT, bool TOP2 = false>
 __global__ __launch_bounds__(WAVES * 64, (WAVES % 4 == 0 ? (WAVES / 4 > 1 ? WAVES / 4 : 3) : 2))
 void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
                                    const __bf16* __restrict__ Cm2, const float* __restrict__ cnorm,
                                    int ntiles, int32_t* __restrict__ labels,
                                    float* __restrict__ mind,
-                                   const int32_t* __restrict__ rowidx = nullptr) {
+                                   const int32_t* __restrict__ rowidx = nullptr,
+                                   float* __restrict__ mind2 = nullptr) {
   constexpr int BNL = 16 * QT;                     // centroids per stage
   constexpr int CPR = DP / 8;
   constexpr int KS = DP / 32;                      // 32-deep k-steps
@@ -636,7 +639,7 @@ void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int6
   }
   // ||x||^2 only feeds the optional min-distance output: skip its ~5 VALU per element
   // when the caller does not ask for it (uniform branch)
-  if (mind) {
+  if (mind || mind2) {
 #pragma unroll
     for (int p = 0; p < P; ++p) {
       float s = 0.f;
@@ -678,11 +681,12 @@ void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int6
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * VPS) : "memory");
   __builtin_amdgcn_s_barrier();
 
-  float best[P];
+  float best[P], best2[P];
   int bt[P];
 #pragma unroll
   for (int p = 0; p < P; ++p) {
     best[p] = INFINITY;
+    best2[p] = INFINITY;
     bt[p] = 0;
   }
 
@@ -701,9 +705,9 @@ void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int6
     }
     // running key minimum of the whole stage (all QT phases): one compare/select per
     // point tile per stage instead of per phase
-    float m[P];
+    float m[P], m2[P];
 #pragma unroll
-    for (int p = 0; p < P; ++p) m[p] = INFINITY;
+    for (int p = 0; p < P; ++p) m[p] = m2[p] = INFINITY;
 #pragma unroll
     for (int q = 0; q < QT; ++q) {
       auto afrag = [&](int kk) __attribute__((always_inline)) {
@@ -739,12 +743,15 @@ void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int6
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float v = __uint_as_float((__float_as_uint(acc[p][i]) & ~EMB) | (unsigned)(q * 4 + i));
+          if constexpr (TOP2) m2[p] = __builtin_amdgcn_fmed3f(m[p], m2[p], v);  // m <= m2 kept
           m[p] = __builtin_fminf(m[p], v);
         }
       }
     }
 #pragma unroll
     for (int p = 0; p < P; ++p) {
+      if constexpr (TOP2)  // 2nd of the union of {best, best2} and {m, m2}
+        best2[p] = __builtin_fminf(__builtin_fminf(best2[p], m2[p]), __builtin_fmaxf(best[p], m[p]));
       const bool up = m[p] < best[p];
       best[p] = up ? m[p] : best[p];
       bt[p] = up ? t : bt[p];
@@ -767,10 +774,15 @@ void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int6
     const unsigned e = __float_as_uint(best[p]) & EMB;
     int lab = bt[p] * BNL + (int)(e >> 2) * 16 + 4 * g + (int)(e & 3);
     float v = __uint_as_float(__float_as_uint(best[p]) & ~EMB);
+    float v2 = __uint_as_float(__float_as_uint(best2[p]) & ~EMB);
 #pragma unroll
     for (int o = 16; o <= 32; o <<= 1) {
       const float ov = __shfl_xor(v, o, 64);
       const int ol = __shfl_xor(lab, o, 64);
+      if constexpr (TOP2) {
+        const float ov2 = __shfl_xor(v2, o, 64);
+        v2 = fminf(fminf(v2, ov2), fmaxf(v, ov));
+      }
       const bool other = (ov < v) || (ov == v && ol < lab);
       v = other ? ov : v;
       lab = other ? ol : lab;
@@ -779,6 +791,7 @@ void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int6
     if (g == 0 && row < N) {
       labels[row] = lab;
       if (mind) mind[row] = fmaxf(v + xn[p], 0.f);
+      if (TOP2 && mind2) mind2[row] = fmaxf(v2 + xn[p], 0.f);
     }
   }
 }

@@ -319,6 +319,79 @@ void sculley_update(const at::Tensor& sums, const at::Tensor& counts, at::Tensor
         "sculley_update");
 }
 
+void assign_bf16_top2(const at::Tensor& X, const std::optional<at::Tensor>& rowidx,
+                      const at::Tensor& Cm2, const at::Tensor& cnorm, at::Tensor& labels,
+                      at::Tensor& mind, at::Tensor& mind2) {
+  check_cuda(X, "X");
+  check_rows(X, "X");
+  TORCH_CHECK(X.scalar_type() == at::kBFloat16 && Cm2.scalar_type() == at::kBFloat16,
+              "tdc.assign_bf16_top2: X and Cm2 must be bfloat16");
+  TORCH_CHECK(cnorm.scalar_type() == at::kFloat && labels.scalar_type() == at::kInt,
+              "tdc.assign_bf16_top2: cnorm fp32, labels int32");
+  TORCH_CHECK(Cm2.is_contiguous() && cnorm.is_contiguous() && labels.is_contiguous(),
+              "tdc.assign_bf16_top2: Cm2/cnorm/labels must be contiguous");
+  const bool idx = rowidx.has_value() && rowidx->defined();
+  const int64_t B = idx ? rowidx->numel() : X.size(0);
+  if (idx) check_rowidx(X, *rowidx, B, "assign_bf16_top2");
+  const int DP = (int)Cm2.size(1);
+  const int Kp = (int)Cm2.size(0);
+  TORCH_CHECK(DP == 64 || DP == 128 || DP == 256, "tdc.assign_bf16_top2: DP must be 64/128/256");
+  TORCH_CHECK(X.size(1) >= DP, "tdc.assign_bf16_top2: X has fewer columns than Cm2");
+  TORCH_CHECK(X.stride(0) % 8 == 0 && (reinterpret_cast<uintptr_t>(X.data_ptr()) % 16) == 0,
+              "tdc.assign_bf16_top2: X rows must be 16-byte aligned");
+  TORCH_CHECK(Kp % 64 == 0 && cnorm.numel() >= Kp, "tdc.assign_bf16_top2: Kp % 64");
+  TORCH_CHECK(labels.numel() >= B, "tdc.assign_bf16_top2: labels too small");
+  for (const at::Tensor* m : {&mind, &mind2})
+    TORCH_CHECK(m->scalar_type() == at::kFloat && m->numel() >= B && m->is_contiguous(),
+                "tdc.assign_bf16_top2: mind/mind2 must be fp32 [B]");
+  const DevGuard guard(X.device());
+  check(tdc_assign_mfma_bf16_top2(X.data_ptr(), idx ? rowidx->data_ptr<int32_t>() : nullptr, B,
+                                  X.stride(0), DP, Cm2.data_ptr(), cnorm.data_ptr<float>(), Kp,
+                                  labels.data_ptr<int32_t>(), mind.data_ptr<float>(),
+                                  mind2.data_ptr<float>(), cur_stream()),
+        "assign_bf16_top2");
+}
+
+void bounds_filter(const at::Tensor& labels, at::Tensor& ub, at::Tensor& lb, const at::Tensor& drift,
+                   const at::Tensor& maxdrift, double slack, at::Tensor& active, at::Tensor& count) {
+  check_cuda(labels, "labels");
+  const int64_t N = labels.numel();
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous(), "tdc.bounds_filter: labels");
+  for (const at::Tensor* t : {&ub, &lb})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == N,
+                "tdc.bounds_filter: ub/lb fp32 [N]");
+  TORCH_CHECK(drift.scalar_type() == at::kFloat && drift.is_contiguous(), "tdc.bounds_filter: drift");
+  TORCH_CHECK(maxdrift.scalar_type() == at::kFloat && maxdrift.numel() >= 1, "tdc.bounds_filter: maxdrift");
+  TORCH_CHECK(active.scalar_type() == at::kInt && active.numel() >= N && active.is_contiguous(),
+              "tdc.bounds_filter: active int32 [N]");
+  TORCH_CHECK(count.scalar_type() == at::kInt && count.numel() >= 1, "tdc.bounds_filter: count");
+  const DevGuard guard(labels.device());
+  check(tdc_bounds_filter(labels.data_ptr<int32_t>(), N, ub.data_ptr<float>(), lb.data_ptr<float>(),
+                          drift.data_ptr<float>(), maxdrift.data_ptr<float>(), (float)slack,
+                          active.data_ptr<int32_t>(), count.data_ptr<int>(), cur_stream()),
+        "bounds_filter");
+}
+
+void bounds_scatter(const at::Tensor& active, const at::Tensor& count, const at::Tensor& blab,
+                    const at::Tensor& d1, const at::Tensor& d2, at::Tensor& labels, at::Tensor& ub,
+                    at::Tensor& lb, at::Tensor& moved_idx, at::Tensor& moved_old,
+                    at::Tensor& moved_new, at::Tensor& mcount) {
+  check_cuda(labels, "labels");
+  const int64_t cap = active.numel();
+  TORCH_CHECK(blab.numel() >= cap && d1.numel() >= cap && d2.numel() >= cap,
+              "tdc.bounds_scatter: per-active arrays shorter than active");
+  TORCH_CHECK(moved_idx.numel() >= cap && moved_old.numel() >= cap && moved_new.numel() >= cap,
+              "tdc.bounds_scatter: moved arrays shorter than active");
+  TORCH_CHECK(ub.numel() == labels.numel() && lb.numel() == labels.numel(), "tdc.bounds_scatter: ub/lb");
+  const DevGuard guard(labels.device());
+  check(tdc_bounds_scatter(active.data_ptr<int32_t>(), count.data_ptr<int>(), cap,
+                           blab.data_ptr<int32_t>(), d1.data_ptr<float>(), d2.data_ptr<float>(),
+                           labels.data_ptr<int32_t>(), ub.data_ptr<float>(), lb.data_ptr<float>(),
+                           moved_idx.data_ptr<int32_t>(), moved_old.data_ptr<int32_t>(),
+                           moved_new.data_ptr<int32_t>(), mcount.data_ptr<int>(), cur_stream()),
+        "bounds_scatter");
+}
+
 bool assign_bigd_supported(at::ScalarType dtype, int64_t DP) {
   const int code = dtype == at::kFloat8_e4m3fn ? TDC_FP8 : (dtype == at::kBFloat16 ? TDC_BF16 : -1);
   return code >= 0 && tdc_assign_bigd_supported(code, (int)DP) != 0;
@@ -444,6 +517,9 @@ TORCH_LIBRARY(tdc, m) {
   m.def("finalize(Tensor? sums, Tensor? counts, Tensor(a!) C, int policy, Tensor(b!)? shift, Tensor(c!)? Cm2, Tensor(d!)? cnorm) -> ()");
   m.def("assign_bf16_indexed(Tensor X, Tensor rowidx, Tensor Cm2, Tensor cnorm, Tensor(a!) labels, Tensor(b!)? mind) -> ()");
   m.def("update_sorted_indexed(Tensor X, Tensor rowidx, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work) -> ()");
+  m.def("assign_bf16_top2(Tensor X, Tensor? rowidx, Tensor Cm2, Tensor cnorm, Tensor(a!) labels, Tensor(b!) mind, Tensor(c!) mind2) -> ()");
+  m.def("bounds_filter(Tensor labels, Tensor(a!) ub, Tensor(b!) lb, Tensor drift, Tensor maxdrift, float slack, Tensor(c!) active, Tensor(d!) count) -> ()");
+  m.def("bounds_scatter(Tensor active, Tensor count, Tensor blab, Tensor d1, Tensor d2, Tensor(a!) labels, Tensor(b!) ub, Tensor(c!) lb, Tensor(d!) moved_idx, Tensor(e!) moved_old, Tensor(f!) moved_new, Tensor(g!) mcount) -> ()");
   m.def("sculley_update(Tensor sums, Tensor counts, Tensor(a!) C, Tensor(b!) v, Tensor(c!)? shift, Tensor(d!)? Cm2, Tensor(e!)? cnorm) -> ()");
 }
 
@@ -461,4 +537,7 @@ TORCH_LIBRARY_IMPL(tdc, CUDA, m) {
   m.impl("assign_bf16_indexed", &assign_bf16_indexed);
   m.impl("update_sorted_indexed", &update_sorted_indexed);
   m.impl("sculley_update", &sculley_update);
+  m.impl("assign_bf16_top2", &assign_bf16_top2);
+  m.impl("bounds_filter", &bounds_filter);
+  m.impl("bounds_scatter", &bounds_scatter);
 }

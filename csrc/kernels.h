@@ -19,6 +19,26 @@ int tdc_assign_mfma_bf16_indexed(const void* X, const int32_t* rowidx, int64_t N
                                  int DP, const void* Cm2, const float* cnorm, int Kp,
                                  int32_t* labels, float* mind, hipStream_t stream);
 
+// Same, with the second-smallest squared distance too (mind, mind2 required); rowidx
+// nullable.  DP 64/128/256.
+int tdc_assign_mfma_bf16_top2(const void* X, const int32_t* rowidx, int64_t N, int64_t ldx,
+                              int DP, const void* Cm2, const float* cnorm, int Kp,
+                              int32_t* labels, float* mind, float* mind2, hipStream_t stream);
+
+// Bounds-based pruning (bounds.hip).  filter: ub[i] += drift[labels[i]], lb[i] -= maxdrift
+// (device scalar); rows that may change label (ub * (1 + slack) >= lb) are appended to
+// active (int32) with count (device int, zeroed by the caller).
+int tdc_bounds_filter(const int32_t* labels, int64_t N, float* ub, float* lb, const float* drift,
+                      const float* maxdrift, float slack, int32_t* active, int* count,
+                      hipStream_t stream);
+// scatter: for the M active rows (M read from count on the device, up to cap): new label
+// blab[j], bounds from the top-2 squared distances d1/d2; rows whose label changed are
+// appended to moved_idx / moved_old / moved_new with mcount (zeroed by the caller).
+int tdc_bounds_scatter(const int32_t* active, const int* count, int64_t cap,
+                       const int32_t* blab, const float* d1, const float* d2, int32_t* labels,
+                       float* ub, float* lb, int32_t* moved_idx, int32_t* moved_old,
+                       int32_t* moved_new, int* mcount, hipStream_t stream);
+
 // N1 (exact)  SIMT difference-form assignment for fp32/fp64, any K, D <= 64.
 int tdc_assign_simt(int dtype, const void* X, int64_t N, int64_t ldx, int D, const void* C,
                     int K, int32_t* labels, void* mind, hipStream_t stream);

@@ -159,6 +159,9 @@ def build_parser():
                         help="run-to-run bitwise reproducible centroid update")
     parser.add_argument("--spherical", action="store_true",
                         help="cosine (spherical) K-Means: unit-normalised rows and centroids")
+    parser.add_argument("--algorithm", default="lloyd", choices=["lloyd", "bounded"],
+                        help="bounded: exact Lloyd that re-assigns only the rows its Hamerly "
+                             "bounds cannot settle (resident bf16 MFMA path)")
     return parser
 
 
@@ -215,7 +218,7 @@ def run(args) -> int:
                             checkpoint_every=args.checkpoint_every, resume=args.resume,
                             hbm_budget_gb=args.hbm_budget_gb, deterministic=args.deterministic,
                             graph=args.graph, log_every=args.log_every,
-                            spherical=args.spherical)
+                            spherical=args.spherical, algorithm=args.algorithm)
         xt = torch.from_numpy(np.asarray(x))
         if args.method_name == "distributedKMeans":
             model = KMeans(cfg, comm)

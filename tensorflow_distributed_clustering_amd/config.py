@@ -17,6 +17,7 @@ DTYPES = ("fp64", "fp32", "bf16", "fp8")
 INITS = ("random", "first_k", "kmeans++", "kmeans||", "given")
 EMPTY_POLICIES = ("keep", "nan", "nan_any", "reseed", "zero")
 BACKENDS = ("auto", "hip", "torch")
+ALGORITHMS = ("lloyd", "bounded")
 
 
 @dataclass(frozen=True)
@@ -41,6 +42,8 @@ class ClusterConfig:
     chunk_rows      rows per streamed chunk (0 = whole shard resident)
     hbm_budget_gb   planner budget per GPU (MI355X has 288 GB)
     checkpoint_*    periodic centroid checkpoints / resume (reference: none)
+    algorithm       'lloyd' | 'bounded' (exact Lloyd that re-assigns only the rows its
+                    Hamerly bounds cannot settle; resident bf16 MFMA path, else Lloyd)
     """
 
     n_clusters: int
@@ -66,6 +69,7 @@ class ClusterConfig:
     max_oom_retries: int = 4    # setup OOM -> halve the streamed chunk and retry
     graph: bool = False         # replay each Lloyd step from a captured hipGraph
     spherical: bool = False     # cosine / spherical K-Means: unit rows, unit centroids
+    algorithm: str = "lloyd"    # 'bounded': Lloyd with Hamerly bounds (models/bounded.py)
 
     def __post_init__(self):
         if self.n_clusters <= 0:
@@ -80,6 +84,8 @@ class ClusterConfig:
             raise ValueError(f"empty_cluster must be one of {EMPTY_POLICIES}")
         if self.backend not in BACKENDS:
             raise ValueError(f"backend must be one of {BACKENDS}")
+        if self.algorithm not in ALGORITHMS:
+            raise ValueError(f"algorithm must be one of {ALGORITHMS}")
 
     def replace(self, **kw) -> "ClusterConfig":
         return dataclasses.replace(self, **kw)

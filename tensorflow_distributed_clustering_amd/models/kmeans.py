@@ -341,8 +341,11 @@ class KMeans:
                     source, chunk_rows = self._make_source(x_local, dev, row_offset, chunk)
                 first = None
                 faults.maybe_fail("setup", comm.rank)
-                eng = LloydEngine(source, cfg, comm, n_global, row_offset, init_centers_,
-                                  chunk_rows, defer_init=True)
+                cls = LloydEngine
+                if cfg.algorithm == "bounded":
+                    from .bounded import BoundedLloydEngine as cls
+                eng = cls(source, cfg, comm, n_global, row_offset, init_centers_,
+                          chunk_rows, defer_init=True)
             except Exception as e:  # noqa: BLE001 - filtered right below
                 if not faults.is_oom(e):
                     raise

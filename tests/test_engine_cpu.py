@@ -144,3 +144,14 @@ def test_spherical_kmeans_matches_cosine_reference():
     assert torch.equal(cos.argmax(1).to(torch.int32), r.labels)
     # every true direction is recovered by some centroid
     assert (dirs @ c.t()).max(1).values.min() > 0.99
+
+
+def test_bounded_algorithm_falls_back_to_lloyd_on_cpu():
+    x = gaussian_blobs(3000, 3, 5, seed=2, dtype=torch.float64)
+    cfg = tdc.ClusterConfig(n_clusters=5, max_iter=8, dtype="fp64", seed=1)
+    a = tdc.KMeans(cfg).fit(x).result_
+    km = tdc.KMeans(cfg.replace(algorithm="bounded")).fit(x)
+    assert not km.engine_.enabled
+    np.testing.assert_array_equal(km.result_.centers, a.centers)
+    with pytest.raises(ValueError):
+        tdc.ClusterConfig(n_clusters=2, algorithm="elkan")

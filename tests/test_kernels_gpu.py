@@ -371,3 +371,79 @@ def test_sculley_update(gpu, cdt):
     assert (cm2[:k, d:] == 0).all() and (cm2[k:] == 0).all()
     torch.testing.assert_close(cnorm[:k], (cb * cb).sum(1), rtol=1e-5, atol=1e-4)
     assert (cnorm[k:] == 3e38).all()
+
+
+@pytest.mark.parametrize("n,d,k", [(30000, 128, 1024), (20000, 64, 4096), (9000, 256, 200),
+                                   (777, 128, 70)])
+def test_assign_bf16_top2(gpu, n, d, k):
+    """Top-2 epilogue: same labels as the plain kernel, d1 = its min distance, d2 = the
+    second-smallest distance (fp64 oracle on the bf16 operands, bf16-level tolerance);
+    the indexed form equals the gathered rows."""
+    import tensorflow_distributed_clustering_amd.ops as ops_mod
+    from tensorflow_distributed_clustering_amd import _native
+    ops = _native.require()
+    x, c = _bf16_case(n, d, k, gpu, seed=d + k)
+    lo = ops_mod.make_lloyd_ops(x, k, "bf16", "hip")
+    C = c.float().contiguous()
+    lo.prepare(C)
+    lab = torch.empty(n, dtype=torch.int32, device=gpu)
+    d1 = torch.empty(n, dtype=torch.float32, device=gpu)
+    d2 = torch.empty(n, dtype=torch.float32, device=gpu)
+    ops.assign_bf16_top2(lo.x, None, lo.cm2, lo.cnorm, lab, d1, d2)
+    lab0 = torch.empty_like(lab)
+    md0 = torch.empty_like(d1)
+    ops.assign_bf16(lo.x, lo.cm2, lo.cnorm, lab0, md0)
+    assert torch.equal(lab, lab0)
+    # equal up to the centroid-id bits embedded in the score mantissa (QT may differ)
+    torch.testing.assert_close(d1, md0, rtol=1e-4, atol=1e-3)
+    cb = C.to(torch.bfloat16).double()
+    dd = ref.pairwise_sqdist(lo.x[:, :d].double(), cb, exact=True)
+    top = dd.topk(2, largest=False).values
+    scale = (lo.x[:, :d].double() ** 2).sum(1) + (cb * cb).sum(1).max()
+    assert ((d2.double() - top[:, 1]).abs() <= 1e-5 * scale + 1e-3).all()
+    assert (d2 >= d1).all()
+    g = torch.Generator(device=gpu).manual_seed(3)
+    idx = torch.randint(n, (n // 3,), generator=g, device=gpu, dtype=torch.int32)
+    li = torch.empty(n // 3, dtype=torch.int32, device=gpu)
+    e1 = torch.empty(n // 3, dtype=torch.float32, device=gpu)
+    e2 = torch.empty(n // 3, dtype=torch.float32, device=gpu)
+    ops.assign_bf16_top2(lo.x, idx, lo.cm2, lo.cnorm, li, e1, e2)
+    assert torch.equal(li, lab[idx.long()]) and torch.equal(e2, d2[idx.long()])
+
+
+def test_bounds_filter_and_scatter(gpu):
+    from tensorflow_distributed_clustering_amd import _native
+    ops = _native.require()
+    n, k = 100_003, 50
+    g = torch.Generator(device=gpu).manual_seed(0)
+    labels = torch.randint(k, (n,), generator=g, device=gpu, dtype=torch.int32)
+    ub = torch.rand(n, generator=g, device=gpu)
+    lb = ub + torch.rand(n, generator=g, device=gpu) * 0.5
+    drift = torch.rand(k, generator=g, device=gpu) * 0.1
+    maxd = drift.max().reshape(1)
+    ub2, lb2 = ub + drift[labels.long()], lb - maxd
+    want = (~(ub2 * 1.001 < lb2)).nonzero().flatten()
+    active = torch.empty(n, dtype=torch.int32, device=gpu)
+    cnt = torch.zeros(2, dtype=torch.int32, device=gpu)
+    ops.bounds_filter(labels, ub, lb, drift, maxd, 1e-3, active, cnt[0:1])
+    m = int(cnt[0])
+    assert m == want.numel() and torch.equal(active[:m].sort().values.long(), want)
+    torch.testing.assert_close(ub, ub2)
+    torch.testing.assert_close(lb, lb2)
+    act = active[:m]
+    blab = torch.where(act % 3 == 0, (labels[act.long()] + 1) % k, labels[act.long()])
+    d1 = torch.rand(m, generator=g, device=gpu)
+    d2 = d1 + 1
+    moved = torch.empty(3, m, dtype=torch.int32, device=gpu)
+    old = labels.clone()
+    ops.bounds_scatter(act, cnt[0:1], blab, d1, d2, labels, ub, lb, moved[0], moved[1], moved[2],
+                       cnt[1:2])
+    mv = int(cnt[1])
+    chg = act[(blab != old[act.long()])]
+    assert mv == chg.numel()
+    order = moved[0, :mv].sort()
+    assert torch.equal(order.values, chg.sort().values)
+    assert torch.equal(moved[1, :mv], old[moved[0, :mv].long()])
+    assert torch.equal(moved[2, :mv], labels[moved[0, :mv].long()])
+    assert torch.equal(labels[act.long()], blab)
+    torch.testing.assert_close(ub[act.long()], d1.sqrt())
