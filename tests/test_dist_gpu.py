@@ -21,7 +21,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q, dtype, n, d, k, iters, method):
+def _worker(rank, world, port, q, dtype, n, d, k, iters, method, algorithm="lloyd"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
                       RANK=str(rank), LOCAL_RANK=str(rank), TDC_DIST_BACKEND="gloo")
     import tensorflow_distributed_clustering_amd as tdc
@@ -32,7 +32,8 @@ def _worker(rank, world, port, q, dtype, n, d, k, iters, method):
     s, e = comm.shard(n)
     tdt = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp64": torch.float64}[dtype]
     x = gaussian_blobs(e - s, d, k, seed=3, row_offset=s, dtype=tdt, device=comm.device)
-    cfg = tdc.ClusterConfig(n_clusters=k, max_iter=iters, dtype=dtype, init="random", seed=3)
+    cfg = tdc.ClusterConfig(n_clusters=k, max_iter=iters, dtype=dtype, init="random", seed=3,
+                            algorithm=algorithm)
     model = (tdc.KMeans if method == "kmeans" else tdc.FuzzyCMeans)(cfg, comm)
     model.fit(x, n_global=n, row_offset=s)
     r = model.result_
@@ -42,11 +43,12 @@ def _worker(rank, world, port, q, dtype, n, d, k, iters, method):
     D.destroy_comm()
 
 
-def _run(world, dtype, n, d, k, iters=4, method="kmeans"):
+def _run(world, dtype, n, d, k, iters=4, method="kmeans", algorithm="lloyd"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, dtype, n, d, k, iters, method))
+    procs = [ctx.Process(target=_worker,
+                         args=(r, world, port, q, dtype, n, d, k, iters, method, algorithm))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -77,3 +79,13 @@ def test_fcm_two_ranks_match_one(gpu):
     c2, l2, _ = _run(2, "fp64", 50_000, 5, 4, method="fcm")
     np.testing.assert_allclose(c2, c1, rtol=1e-9, atol=1e-9)
     np.testing.assert_array_equal(l2, l1)
+
+
+def test_bounded_two_ranks_match_lloyd(gpu):
+    """algorithm='bounded' on 2 ranks: per-rank pruning, one all-reduce of the deltas per
+    step, replicated fp64 totals -> the single-rank Lloyd result."""
+    c1, l1, _ = _run(1, "bf16", 200_003, 128, 1024, iters=12)
+    c2, l2, b2 = _run(2, "bf16", 200_003, 128, 1024, iters=12, algorithm="bounded")
+    assert b2 == "hip_bf16_mfma"
+    np.testing.assert_allclose(c2, c1, rtol=2e-3, atol=2e-3)
+    assert (l1 == l2).mean() > 0.999
