@@ -12,146 +12,46 @@
 #include <torch/custom_class.h>
 #include <torch/extension.h>
 
-#include <atomic>
-#include <condition_variable>
-#include <cstring>
-#include <deque>
-#include <functional>
-#include <mutex>
-#include <thread>
-#include <unordered_map>
-#include <vector>
+#include <memory>
+
+#include "row_streamer.h"
 
 namespace {
 
-inline uint16_t f32_to_bf16_rne(float f) {
-  uint32_t u;
-  std::memcpy(&u, &f, 4);
-  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
-
-enum SrcType { SRC_F64 = 0, SRC_F32 = 1 };
-enum DstType { DST_BF16 = 0, DST_F32 = 1 };
-
+// TorchScript custom class over tdc::RowStreamerCore (tensor checks live here)
 class RowStreamer : public torch::CustomClassHolder {
  public:
   RowStreamer(int64_t src_addr, int64_t src_type, int64_t n_rows, int64_t n_cols,
-              int64_t src_ld, int64_t dst_type, int64_t dp, int64_t n_threads)
-      : src_(reinterpret_cast<const char*>(src_addr)), src_type_(src_type), n_rows_(n_rows),
-        n_cols_(n_cols), src_ld_(src_ld), dst_type_(dst_type), dp_(dp) {
-    TORCH_CHECK(src_addr != 0, "RowStreamer: null source");
-    TORCH_CHECK(src_type == SRC_F64 || src_type == SRC_F32, "RowStreamer: src must be f64/f32");
-    TORCH_CHECK(dst_type == DST_BF16 || dst_type == DST_F32, "RowStreamer: dst must be bf16/f32");
-    TORCH_CHECK(dp >= n_cols, "RowStreamer: padded width smaller than the row");
-    const int64_t nt = n_threads > 0 ? n_threads : 4;
-    for (int64_t i = 0; i < nt; ++i) workers_.emplace_back([this] { loop(); });
-  }
-
-  ~RowStreamer() override {
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      stop_ = true;
+              int64_t src_ld, int64_t dst_type, int64_t dp, int64_t n_threads) {
+    try {
+      core_ = std::make_unique<tdc::RowStreamerCore>(reinterpret_cast<const void*>(src_addr),
+                                                     src_type, n_rows, n_cols, src_ld, dst_type,
+                                                     dp, n_threads);
+    } catch (const std::exception& e) {
+      TORCH_CHECK(false, e.what());
     }
-    cv_.notify_all();
-    for (auto& t : workers_) t.join();
   }
 
   // fill dst[0:rows, 0:dp] with source rows [start, start+rows); returns a ticket
   int64_t submit(at::Tensor dst, int64_t start, int64_t rows) {
     TORCH_CHECK(!dst.is_cuda(), "RowStreamer: destination must be host memory");
-    TORCH_CHECK(dst.is_contiguous() && dst.dim() == 2 && dst.size(1) == dp_, "RowStreamer: dst [rows, dp]");
+    TORCH_CHECK(dst.is_contiguous() && dst.dim() == 2 && dst.size(1) == core_->dp(),
+                "RowStreamer: dst [rows, dp]");
     TORCH_CHECK(dst.size(0) >= rows, "RowStreamer: dst too small");
-    TORCH_CHECK(start >= 0 && rows >= 0 && start + rows <= n_rows_, "RowStreamer: range out of bounds");
-    TORCH_CHECK((dst_type_ == DST_BF16 && dst.scalar_type() == at::kBFloat16) ||
-                    (dst_type_ == DST_F32 && dst.scalar_type() == at::kFloat),
+    TORCH_CHECK(start >= 0 && rows >= 0 && start + rows <= core_->rows(),
+                "RowStreamer: range out of bounds");
+    TORCH_CHECK((core_->dst_type() == tdc::DST_BF16 && dst.scalar_type() == at::kBFloat16) ||
+                    (core_->dst_type() == tdc::DST_F32 && dst.scalar_type() == at::kFloat),
                 "RowStreamer: dst dtype mismatch");
-    char* out = static_cast<char*>(dst.data_ptr());
-    const int64_t ticket = next_ticket_++;
-    const int64_t pieces = std::max<int64_t>(1, std::min<int64_t>((int64_t)workers_.size() * 2,
-                                                                  (rows + 4095) / 4096));
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      pending_[ticket] = pieces;
-      const int64_t per = (rows + pieces - 1) / pieces;
-      for (int64_t p = 0; p < pieces; ++p) {
-        const int64_t r0 = p * per, r1 = std::min(rows, r0 + per);
-        q_.push_back([=] { convert(out, start, r0, r1); finish(ticket); });
-      }
-    }
-    cv_.notify_all();
-    return ticket;
+    return core_->submit(dst.data_ptr(), start, rows);
   }
 
-  void wait(int64_t ticket) {
-    std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [&] { return pending_.find(ticket) == pending_.end(); });
-  }
-
-  int64_t rows() const { return n_rows_; }
-  int64_t cols() const { return n_cols_; }
+  void wait(int64_t ticket) { core_->wait(ticket); }
+  int64_t rows() const { return core_->rows(); }
+  int64_t cols() const { return core_->cols(); }
 
  private:
-  void convert(char* out, int64_t start, int64_t r0, int64_t r1) {
-    const size_t es = src_type_ == SRC_F64 ? 8 : 4;
-    for (int64_t r = r0; r < r1; ++r) {
-      const char* srow = src_ + (size_t)(start + r) * src_ld_ * es;
-      if (dst_type_ == DST_BF16) {
-        uint16_t* drow = reinterpret_cast<uint16_t*>(out) + (size_t)r * dp_;
-        if (src_type_ == SRC_F64) {
-          const double* s = reinterpret_cast<const double*>(srow);
-          for (int64_t c = 0; c < n_cols_; ++c) drow[c] = f32_to_bf16_rne((float)s[c]);
-        } else {
-          const float* s = reinterpret_cast<const float*>(srow);
-          for (int64_t c = 0; c < n_cols_; ++c) drow[c] = f32_to_bf16_rne(s[c]);
-        }
-        for (int64_t c = n_cols_; c < dp_; ++c) drow[c] = 0;
-      } else {
-        float* drow = reinterpret_cast<float*>(out) + (size_t)r * dp_;
-        if (src_type_ == SRC_F64) {
-          const double* s = reinterpret_cast<const double*>(srow);
-          for (int64_t c = 0; c < n_cols_; ++c) drow[c] = (float)s[c];
-        } else {
-          std::memcpy(drow, srow, (size_t)n_cols_ * 4);
-        }
-        for (int64_t c = n_cols_; c < dp_; ++c) drow[c] = 0.f;
-      }
-    }
-  }
-
-  void finish(int64_t ticket) {
-    std::lock_guard<std::mutex> g(mu_);
-    auto it = pending_.find(ticket);
-    if (it != pending_.end() && --(it->second) == 0) {
-      pending_.erase(it);
-      done_cv_.notify_all();
-    }
-  }
-
-  void loop() {
-    for (;;) {
-      std::function<void()> job;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
-        if (stop_ && q_.empty()) return;
-        job = std::move(q_.front());
-        q_.pop_front();
-      }
-      job();
-    }
-  }
-
-  const char* src_;
-  int64_t src_type_, n_rows_, n_cols_, src_ld_, dst_type_, dp_;
-  std::vector<std::thread> workers_;
-  std::mutex mu_;
-  std::condition_variable cv_, done_cv_;
-  std::deque<std::function<void()>> q_;
-  std::unordered_map<int64_t, int64_t> pending_;
-  std::atomic<int64_t> next_ticket_{0};
-  bool stop_ = false;
+  std::unique_ptr<tdc::RowStreamerCore> core_;
 };
 
 }  // namespace
