@@ -159,6 +159,9 @@ def build_parser():
                         help="run-to-run bitwise reproducible centroid update")
     parser.add_argument("--spherical", action="store_true",
                         help="cosine (spherical) K-Means: unit-normalised rows and centroids")
+    parser.add_argument("--dist_debug", action="store_true",
+                        help="check every collective for rank mismatches "
+                             "(TORCH_DISTRIBUTED_DEBUG=DETAIL)")
     parser.add_argument("--algorithm", default="lloyd", choices=["lloyd", "bounded"],
                         help="bounded: exact Lloyd that re-assigns only the rows its Hamerly "
                              "bounds cannot settle (resident bf16 MFMA path)")
@@ -197,7 +200,7 @@ def run(args) -> int:
     device = args.device
     if device == "auto":
         device = "cuda" if torch.cuda.device_count() > 0 else "cpu"
-    comm = init_comm(device, timeout_s=args.collective_timeout)
+    comm = init_comm(device, timeout_s=args.collective_timeout, debug=args.dist_debug)
     status = 0
     result = None
     exc_name = None

@@ -144,14 +144,24 @@ class Comm:
 _COMM: Optional[Comm] = None
 
 
-def init_comm(device_type: Optional[str] = None, timeout_s: float = 600.0) -> Comm:
+def init_comm(device_type: Optional[str] = None, timeout_s: float = 600.0,
+              debug: bool = False) -> Comm:
     """Initialise (once) from torchrun's env:// variables.
 
     device_type: 'cuda' | 'cpu' | None (auto: cuda if visible).
+    timeout_s:   collective timeout: a hung peer fails the run instead of blocking it.
+    debug:       collective-mismatch detection: ``TORCH_DISTRIBUTED_DEBUG=
+                 DETAIL`` wraps the process group so every collective first checks that
+                 all ranks issue the same op with the same shapes and dtypes (a rank that
+                 diverges raises instead of deadlocking or corrupting a reduction).  Costs
+                 an extra small collective per call: for tests and debugging runs.
     """
     global _COMM
     if _COMM is not None:
         return _COMM
+    if debug:
+        os.environ["TORCH_DISTRIBUTED_DEBUG"] = "DETAIL"
+        dist.set_debug_level(dist.DebugLevel.DETAIL)  # the env is read once, at import
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -127,3 +127,36 @@ def test_nan_any_poisons_cluster_empty_on_one_rank():
     c = _run_split("nan")
     assert not np.isnan(c).any()
     np.testing.assert_allclose(c, [[0, 0], [10, 10]], atol=0.05)
+
+
+def _mismatch_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from tensorflow_distributed_clustering_amd.parallel import dist as D
+    D._COMM = None
+    comm = D.init_comm("cpu", timeout_s=60, debug=True)
+    comm.allreduce_(torch.ones(4, dtype=torch.float64))  # consistent: passes
+    err = ""
+    try:  # rank 1 reduces a different shape (a diverged rank)
+        comm.allreduce_(torch.ones(4 if rank == 0 else 5, dtype=torch.float64))
+    except RuntimeError as e:
+        err = str(e)
+    q.put((rank, err))
+    D.destroy_comm()
+
+
+def test_dist_debug_detects_collective_mismatch():
+    """--dist_debug (TORCH_DISTRIBUTED_DEBUG=DETAIL): a rank issuing a mismatched
+    collective raises on every rank instead of hanging or reducing garbage."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mismatch_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(res[r] for r in (0, 1)), res
+    assert any("shape" in res[r].lower() or "mismatch" in res[r].lower() for r in (0, 1)), res
