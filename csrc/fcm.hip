@@ -31,8 +31,8 @@ template <typename T>
 __device__ __forceinline__ T fcm_t(T dd, T expo, int pmode) {
   switch (pmode) {
     case 1: return (T)1 / dd;
-    case 2: return (T)1 / sqrt(dd);
-    case 3: return (T)1 / sqrt(sqrt(dd));
+    case 2: return rsqrt(dd);          // one rsqrt instead of sqrt + divide
+    case 3: return rsqrt(sqrt(dd));
     default: return tdc_exp2(tdc_log2(dd) * expo);
   }
 }
