@@ -92,13 +92,16 @@ __device__ __forceinline__ f32x16 mma(const typename OP::frag& a, const typename
 //   1 = no ring refill after the prologue, 2 = no per-stage barrier, 4 = no epilogue
 // QH: 32-centroid row tiles per ring stage (QH=2 halves the per-stage barrier / refill /
 // norm-load overhead per MFMA; the stage index t then counts QH-tile stages).
-template <class OP, int D, int WAVES, int NST, int ABL = 0, int QH = 1>
+// TOP2: also the runner-up centroid (labels2) and both distances (mind/mind2), for the
+// exact re-check of near ties (recheck_top2_kernel); single K-group only.
+template <class OP, int D, int WAVES, int NST, int ABL = 0, int QH = 1, bool TOP2 = false>
 __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
     const uint8_t* __restrict__ X, const uint8_t* __restrict__ Xs, int64_t N, int64_t ldx,
     const uint8_t* __restrict__ Cm2, const uint8_t* Cs,
     const float* cnorm, int ntiles, int kg_tiles, int64_t npb, int64_t n_items,
     int64_t items_per_xcd, const float* __restrict__ xnorm, int32_t* __restrict__ labels,
-    float* __restrict__ mind, unsigned long long* __restrict__ keys) {
+    float* __restrict__ mind, unsigned long long* __restrict__ keys,
+    int32_t* __restrict__ labels2 = nullptr, float* __restrict__ mind2 = nullptr) {
   constexpr int RB = D * OP::ES;        // bytes per row
   constexpr int HALFB = RB / 2;         // lane half h covers bytes [h*HALFB, (h+1)*HALFB)
   constexpr int NK = HALFB / OP::FB;    // MFMAs per 32x32 tile
@@ -192,8 +195,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
           16, 0, 0);
     }
   };
-  float best = INFINITY;
-  int bt = 0;
+  float best = INFINITY, best2 = INFINITY;
+  int bt = 0, bt2 = 0;
   // one ring stage: the tile, its norms and its scales all arrived by LDS-DMA NST-1
   // stages ago, so the only vmcnt wait per stage is the counted one on the ring
   auto stage = [&](int i) __attribute__((always_inline)) {
@@ -270,13 +273,27 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
 #pragma unroll
       for (int j = 0; j < 16; ++j) asm volatile("" ::"v"(acc[j]));
     } else {
-      float m = INFINITY;
+      float m = INFINITY, m2 = INFINITY;
 #pragma unroll
-      for (int j = 0; j < 16; ++j)
-        m = __builtin_fminf(m, __uint_as_float((__float_as_uint(acc[j]) & ~EMB) | (unsigned)j));
+      for (int j = 0; j < 16; ++j) {
+        const float v = __uint_as_float((__float_as_uint(acc[j]) & ~EMB) | (unsigned)j);
+        if constexpr (TOP2) m2 = __builtin_amdgcn_fmed3f(m, m2, v);  // m <= m2 kept
+        m = __builtin_fminf(m, v);
+      }
+      const int tt = t * QH + qh;  // 32-row tile index
       const bool up = m < best;
+      if constexpr (TOP2) {  // runner-up of {best, best2} U {m, m2}, with its tile
+        const float c = up ? best : m;
+        const int ct = up ? bt : tt;
+        const bool s2 = m2 < c;
+        const float cand = s2 ? m2 : c;
+        const int candt = s2 ? tt : ct;
+        const bool up2 = cand < best2;
+        best2 = up2 ? cand : best2;
+        bt2 = up2 ? candt : bt2;
+      }
       best = up ? m : best;
-      bt = up ? t * QH + qh : bt;  // 32-row tile index
+      bt = up ? tt : bt;
     }
     }  // qh
     if constexpr (ABL & 1) {
@@ -304,6 +321,24 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
   const float v0 = __uint_as_float(__float_as_uint(best) & ~EMB);
   const float v1 = __uint_as_float(__float_as_uint(ob) & ~EMB);
   const bool other = (v1 < v0) || (v1 == v0 && l1 < l0);
+  if constexpr (TOP2) {  // merge the two lane halves' runner-ups
+    const float ob2 = __shfl_xor(best2, 32, 64);
+    const int obt2 = __shfl_xor(bt2, 32, 64);
+    const unsigned f0 = __float_as_uint(best2) & EMB, f1 = __float_as_uint(ob2) & EMB;
+    const int k0 = bt2 * 32 + (int)(f0 & 3) + 8 * (int)(f0 >> 2) + 4 * h;
+    const int k1 = obt2 * 32 + (int)(f1 & 3) + 8 * (int)(f1 >> 2) + 4 * (1 - h);
+    const float w0 = __uint_as_float(__float_as_uint(best2) & ~EMB);
+    const float w1 = __uint_as_float(__float_as_uint(ob2) & ~EMB);
+    // candidates: the loser of the two bests, and both runner-ups
+    float cv = other ? v0 : v1;
+    int cl = other ? l0 : l1;
+    if (w0 < cv) { cv = w0; cl = k0; }
+    if (w1 < cv) { cv = w1; cl = k1; }
+    if (h == 0 && prow < N && labels2) {
+      labels2[prow] = cl;
+      if (mind2) mind2[prow] = fmaxf(cv + xnorm[prow], 0.f);
+    }
+  }
   if (h == 0 && prow < N) {
     const int lab = other ? l1 : l0;
     const float v = other ? v1 : v0;
@@ -403,16 +438,17 @@ __global__ __launch_bounds__(256) void quant_fp8_kernel(const T* __restrict__ X,
 using namespace tdc::bigd;
 
 namespace {
-template <class OP, int D, int WAVES, int NST, int ABL = 0, int QH = 1>
+template <class OP, int D, int WAVES, int NST, int ABL = 0, int QH = 1, bool TOP2 = false>
 int launch_bigd(const void* X, const void* Xs, int64_t N, int64_t ldx_bytes, const void* Cm2,
                 const void* Cs, const float* cnorm, int Kp, int kg_tiles, const float* xnorm,
-                int32_t* labels, float* mind, unsigned long long* keys, hipStream_t stream) {
+                int32_t* labels, float* mind, unsigned long long* keys, hipStream_t stream,
+                int32_t* labels2 = nullptr, float* mind2 = nullptr) {
   // = the kernel's STAGE_B: tile + one 16-B side chunk per lane of LPW lanes per wave
   constexpr int TILE_B = QH * 32 * D * OP::ES;
   constexpr int EXB = QH * 32 * 4 + (OP::SCALED ? QH * 32 * (D / 32) : 0);
   constexpr int LPW = (EXB / 16 + WAVES - 1) / WAVES;
   const size_t lds = (size_t)NST * (TILE_B + WAVES * LPW * 16);
-  auto kern = assign_bigd_kernel<OP, D, WAVES, NST, ABL, QH>;
+  auto kern = assign_bigd_kernel<OP, D, WAVES, NST, ABL, QH, TOP2>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -428,6 +464,7 @@ int launch_bigd(const void* X, const void* Xs, int64_t N, int64_t ldx_bytes, con
   if (kg_tiles <= 0 || kg_tiles > ntiles) kg_tiles = ntiles;
   const int ngroups = (ntiles + kg_tiles - 1) / kg_tiles;
   if (ngroups > 1 && keys == nullptr) return (int)hipErrorInvalidValue;
+  if (TOP2 && ngroups > 1) return (int)hipErrorInvalidValue;  // runner-up: one K-group only
   const int64_t per = (int64_t)WAVES * 32;
   const int64_t npb = (N + per - 1) / per;
   const int64_t n_items = npb * ngroups;
@@ -436,7 +473,7 @@ int launch_bigd(const void* X, const void* Xs, int64_t N, int64_t ldx_bytes, con
   hipLaunchKernelGGL(kern, grid, dim3(WAVES * 64), lds, stream, (const uint8_t*)X,
                      (const uint8_t*)Xs, N, ldx_bytes, (const uint8_t*)Cm2, (const uint8_t*)Cs,
                      cnorm, ntiles, kg_tiles, npb, n_items, ipx, xnorm, labels, mind,
-                     ngroups > 1 ? keys : nullptr);
+                     ngroups > 1 ? keys : nullptr, labels2, mind2);
   TDC_CHECK_LAUNCH();
   if (ngroups > 1) {
     hipLaunchKernelGGL(keys_finalize_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0,
@@ -457,9 +494,22 @@ int tdc_assign_bigd_supported(int dtype, int DP) {
 int tdc_assign_bigd(int dtype, const void* X, const void* Xs, int64_t N, int64_t ldx, int DP,
                     const void* Cm2, const void* Cs, const float* cnorm, int Kp, int kg_tiles,
                     const float* xnorm, int32_t* labels, float* mind, unsigned long long* keys,
-                    hipStream_t stream) {
+                    hipStream_t stream, int32_t* labels2, float* mind2) {
   if (N <= 0) return 0;
   if (Kp % 32 != 0) return (int)hipErrorInvalidValue;
+  if (labels2 != nullptr) {  // fp8 with runner-up (near-tie re-check)
+    if (dtype != TDC_FP8) return (int)hipErrorInvalidValue;
+    switch (DP) {
+      case 256: return launch_bigd<OpFp8, 256, 8, 4, 0, 1, true>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream, labels2, mind2);
+      case 512: return launch_bigd<OpFp8, 512, 8, 4, 0, 1, true>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream, labels2, mind2);
+      case 768:
+        if (Kp % 64 == 0)
+          return launch_bigd<OpFp8, 768, 8, 3, 0, 2, true>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream, labels2, mind2);
+        return launch_bigd<OpFp8, 768, 8, 4, 0, 1, true>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream, labels2, mind2);
+      case 1024: return launch_bigd<OpFp8, 1024, 8, 4, 0, 1, true>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream, labels2, mind2);
+    }
+    return (int)hipErrorInvalidValue;
+  }
   if (dtype == TDC_FP8) {
     switch (DP) {
       case 256: return launch_bigd<OpFp8, 256, 8, 4>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
@@ -488,6 +538,62 @@ int tdc_assign_bigd(int dtype, const void* X, const void* Xs, int64_t N, int64_t
     }
   }
   return (int)hipErrorInvalidValue;
+}
+
+namespace {
+// Exact re-check of the fp8 winner against the runner-up: one wave per point whose fp8
+// margin d2 - d1 is within tau * d2 (the quantisation noise of both operands), distances
+// in fp32 difference form from the full-precision row and centroids.  Points with a
+// clear margin exit after reading two floats.
+template <typename XT>
+__global__ __launch_bounds__(256) void recheck_top2_kernel(const XT* __restrict__ X, int64_t ldx,
+                                                           int D, const float* __restrict__ C,
+                                                           int32_t* __restrict__ labels,
+                                                           const int32_t* __restrict__ labels2,
+                                                           const float* __restrict__ d1,
+                                                           const float* __restrict__ d2, float tau,
+                                                           int64_t N, int* __restrict__ flips) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= N) return;
+  const float a = d1[i], b = d2[i];
+  if (!(b - a <= tau * b)) return;  // clear margin (NaN-safe: NaN re-checks)
+  const int l1 = labels[i], l2 = labels2[i];
+  if (l1 == l2) return;
+  const XT* x = X + i * ldx;
+  const float* c1 = C + (int64_t)l1 * D;
+  const float* c2 = C + (int64_t)l2 * D;
+  float s1 = 0.f, s2 = 0.f;
+  for (int d = lane; d < D; d += 64) {
+    const float xv = (float)x[d];
+    const float e1 = xv - c1[d], e2 = xv - c2[d];
+    s1 = fmaf(e1, e1, s1);
+    s2 = fmaf(e2, e2, s2);
+  }
+  s1 = tdc::wave_sum(s1);
+  s2 = tdc::wave_sum(s2);
+  if (lane == 0 && (s2 < s1 || (s2 == s1 && l2 < l1))) {
+    labels[i] = l2;
+    if (flips) atomicAdd(flips, 1);
+  }
+}
+}  // namespace
+
+int tdc_recheck_top2(int x_dtype, const void* X, int64_t N, int64_t ldx, int D, const float* C,
+                     int32_t* labels, const int32_t* labels2, const float* d1, const float* d2,
+                     float tau, int* flips, hipStream_t stream) {
+  if (N <= 0) return 0;
+  const dim3 grid((unsigned)((N + 3) / 4));
+  if (x_dtype == TDC_BF16)
+    hipLaunchKernelGGL(recheck_top2_kernel<__bf16>, grid, dim3(256), 0, stream, (const __bf16*)X,
+                       ldx, D, C, labels, labels2, d1, d2, tau, N, flips);
+  else if (x_dtype == TDC_F32)
+    hipLaunchKernelGGL(recheck_top2_kernel<float>, grid, dim3(256), 0, stream, (const float*)X,
+                       ldx, D, C, labels, labels2, d1, d2, tau, N, flips);
+  else
+    return (int)hipErrorInvalidValue;
+  TDC_CHECK_LAUNCH();
+  return 0;
 }
 
 int tdc_quant_fp8(int src_dtype, const void* X, int64_t rows, int64_t valid, int d, int64_t ldx,

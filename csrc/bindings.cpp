@@ -401,7 +401,8 @@ bool assign_bigd_supported(at::ScalarType dtype, int64_t DP) {
 void assign_bigd(const at::Tensor& X, const std::optional<at::Tensor>& Xs, const at::Tensor& xnorm,
                  const at::Tensor& Cm2, const std::optional<at::Tensor>& Cs,
                  const at::Tensor& cnorm, int64_t kg_tiles, at::Tensor& labels,
-                 const std::optional<at::Tensor>& mind, const std::optional<at::Tensor>& keys) {
+                 const std::optional<at::Tensor>& mind, const std::optional<at::Tensor>& keys,
+                 const std::optional<at::Tensor>& labels2, const std::optional<at::Tensor>& mind2) {
   check_cuda(X, "X");
   check_rows(X, "X");
   const bool fp8 = X.scalar_type() == at::kFloat8_e4m3fn;
@@ -449,11 +450,49 @@ void assign_bigd(const at::Tensor& X, const std::optional<at::Tensor>& Xs, const
   const int ntiles = Kp / 32;
   const int kg = (kg_tiles <= 0 || kg_tiles > ntiles) ? ntiles : (int)kg_tiles;
   TORCH_CHECK(kg == ntiles || kp != nullptr, "tdc.assign_bigd: keys required with >1 centroid group");
+  int32_t* l2 = nullptr;
+  float* m2 = nullptr;
+  if (labels2.has_value() && labels2->defined()) {
+    TORCH_CHECK(fp8 && kg == ntiles, "tdc.assign_bigd: labels2 needs fp8 and one centroid group");
+    TORCH_CHECK(labels2->scalar_type() == at::kInt && labels2->numel() >= N && labels2->is_contiguous(),
+                "tdc.assign_bigd: labels2 int32 [N]");
+    TORCH_CHECK(mind2.has_value() && mind2->defined() && mind2->scalar_type() == at::kFloat &&
+                    mind2->numel() >= N && mind2->is_contiguous() && md != nullptr,
+                "tdc.assign_bigd: labels2 needs mind and mind2 fp32 [N]");
+    l2 = labels2->data_ptr<int32_t>();
+    m2 = mind2->data_ptr<float>();
+  }
   const DevGuard guard(X.device());
   check(tdc_assign_bigd(fp8 ? TDC_FP8 : TDC_BF16, X.data_ptr(), xs, N, X.stride(0), DP, Cm2.data_ptr(),
                         cs, cnorm.data_ptr<float>(), Kp, kg, xnorm.data_ptr<float>(),
-                        labels.data_ptr<int32_t>(), md, kp, cur_stream()),
+                        labels.data_ptr<int32_t>(), md, kp, cur_stream(), l2, m2),
         "assign_bigd");
+}
+
+int64_t recheck_top2(const at::Tensor& X, const at::Tensor& C, at::Tensor& labels,
+                     const at::Tensor& labels2, const at::Tensor& d1, const at::Tensor& d2,
+                     double tau) {
+  check_cuda(X, "X");
+  check_rows(X, "X");
+  TORCH_CHECK(X.scalar_type() == at::kBFloat16 || X.scalar_type() == at::kFloat,
+              "tdc.recheck_top2: X bf16 or fp32");
+  TORCH_CHECK(C.scalar_type() == at::kFloat && C.is_contiguous() && C.dim() == 2 &&
+                  X.size(1) >= C.size(1), "tdc.recheck_top2: C fp32 [K, D]");
+  const int64_t N = X.size(0);
+  for (const at::Tensor* t : {static_cast<const at::Tensor*>(&labels), &labels2})
+    TORCH_CHECK(t->scalar_type() == at::kInt && t->numel() >= N && t->is_contiguous(),
+                "tdc.recheck_top2: labels int32 [N]");
+  for (const at::Tensor* t : {&d1, &d2})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() >= N && t->is_contiguous(),
+                "tdc.recheck_top2: distances fp32 [N]");
+  const DevGuard guard(X.device());
+  auto flips = at::zeros({1}, labels.options());
+  check(tdc_recheck_top2(dcode(X.scalar_type()), X.data_ptr(), N, X.stride(0), (int)C.size(1),
+                         C.data_ptr<float>(), labels.data_ptr<int32_t>(),
+                         labels2.data_ptr<int32_t>(), d1.data_ptr<float>(), d2.data_ptr<float>(),
+                         (float)tau, flips.data_ptr<int>(), cur_stream()),
+        "recheck_top2");
+  return 0;  // the flip count stays on the device (no host sync in the iteration)
 }
 
 void quant_fp8(const at::Tensor& X, int64_t valid, int64_t neg2, at::Tensor& Q, at::Tensor& S,
@@ -511,7 +550,8 @@ TORCH_LIBRARY(tdc, m) {
   m.def("fcm_small_supported(ScalarType dtype, int K, int D) -> bool", &fcm_small_supported);
   m.def("fcm_small(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) wx, Tensor(c!) ws) -> ()");
   m.def("assign_bigd_supported(ScalarType dtype, int DP) -> bool", &assign_bigd_supported);
-  m.def("assign_bigd(Tensor X, Tensor? Xs, Tensor xnorm, Tensor Cm2, Tensor? Cs, Tensor cnorm, int kg_tiles, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!)? keys) -> ()");
+  m.def("assign_bigd(Tensor X, Tensor? Xs, Tensor xnorm, Tensor Cm2, Tensor? Cs, Tensor cnorm, int kg_tiles, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!)? keys, Tensor(d!)? labels2=None, Tensor(e!)? mind2=None) -> ()");
+  m.def("recheck_top2(Tensor X, Tensor C, Tensor(a!) labels, Tensor labels2, Tensor d1, Tensor d2, float tau) -> int");
   m.def("quant_fp8(Tensor X, int valid, int neg2, Tensor(a!) Q, Tensor(b!) S, Tensor(c!)? norm) -> ()");
   m.def("kpp_step(Tensor X, Tensor cand, Tensor(a!) closest, int mode, Tensor(b!) pots) -> ()");
   m.def("finalize(Tensor? sums, Tensor? counts, Tensor(a!) C, int policy, Tensor(b!)? shift, Tensor(c!)? Cm2, Tensor(d!)? cnorm) -> ()");
@@ -532,6 +572,7 @@ TORCH_LIBRARY_IMPL(tdc, CUDA, m) {
   m.impl("fcm_small", &fcm_small);
   m.impl("finalize", &finalize);
   m.impl("assign_bigd", &assign_bigd);
+  m.impl("recheck_top2", &recheck_top2);
   m.impl("quant_fp8", &quant_fp8);
   m.impl("kpp_step", &kpp_step);
   m.impl("assign_bf16_indexed", &assign_bf16_indexed);

@@ -92,10 +92,17 @@ int tdc_sculley_update(int acc_dtype, int c_dtype, const void* sums, const void*
 // cnorm [Kp] (pad 3e38), xnorm [N] (for mind).  Kp % 32 == 0.  The K loop is split into
 // groups of kg_tiles*32 centroids (0 = one group); with >1 group keys (uint64 [N], all
 // ones on entry; reset on exit) merges the group winners.
+// labels2 / mind2 (fp8, one K-group): also the runner-up centroid and its distance.
 int tdc_assign_bigd(int dtype, const void* X, const void* Xs, int64_t N, int64_t ldx, int DP,
                     const void* Cm2, const void* Cs, const float* cnorm, int Kp, int kg_tiles,
                     const float* xnorm, int32_t* labels, float* mind, unsigned long long* keys,
-                    hipStream_t stream);
+                    hipStream_t stream, int32_t* labels2 = nullptr, float* mind2 = nullptr);
+// Near-tie re-check of a top-2 assignment: where d2 - d1 <= tau * d2, recompute both
+// distances exactly (fp32, difference form) from X (bf16 / f32 rows) and C (fp32 [K, D])
+// and swap the label if the runner-up is closer.  flips (nullable) counts the swaps.
+int tdc_recheck_top2(int x_dtype, const void* X, int64_t N, int64_t ldx, int D, const float* C,
+                     int32_t* labels, const int32_t* labels2, const float* d1, const float* d2,
+                     float tau, int* flips, hipStream_t stream);
 int tdc_assign_bigd_supported(int dtype, int DP);
 
 // N8 fp8 quantiser: rows of X (f32/f64/bf16, d valid columns, ldx elements) -> Q e4m3

@@ -162,6 +162,9 @@ def build_parser():
     parser.add_argument("--dist_debug", action="store_true",
                         help="check every collective for rank mismatches "
                              "(TORCH_DISTRIBUTED_DEBUG=DETAIL)")
+    parser.add_argument("--fp8_recheck", type=float, default=0.0,
+                        help="fp8: re-check near ties (fp8 margin within this fraction of the "
+                             "runner-up distance) exactly in fp32; 0 = off")
     parser.add_argument("--algorithm", default="lloyd", choices=["lloyd", "bounded"],
                         help="bounded: exact Lloyd that re-assigns only the rows its Hamerly "
                              "bounds cannot settle (resident bf16 MFMA path)")
@@ -221,7 +224,8 @@ def run(args) -> int:
                             checkpoint_every=args.checkpoint_every, resume=args.resume,
                             hbm_budget_gb=args.hbm_budget_gb, deterministic=args.deterministic,
                             graph=args.graph, log_every=args.log_every,
-                            spherical=args.spherical, algorithm=args.algorithm)
+                            spherical=args.spherical, algorithm=args.algorithm,
+                            fp8_recheck=args.fp8_recheck)
         xt = torch.from_numpy(np.asarray(x))
         if args.method_name == "distributedKMeans":
             model = KMeans(cfg, comm)

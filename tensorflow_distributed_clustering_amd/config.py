@@ -70,6 +70,7 @@ class ClusterConfig:
     graph: bool = False         # replay each Lloyd step from a captured hipGraph
     spherical: bool = False     # cosine / spherical K-Means: unit rows, unit centroids
     algorithm: str = "lloyd"    # 'bounded': Lloyd with Hamerly bounds (models/bounded.py)
+    fp8_recheck: float = 0.0    # fp8: exact re-check of near ties (relative margin; 0 = off)
 
     def __post_init__(self):
         if self.n_clusters <= 0:

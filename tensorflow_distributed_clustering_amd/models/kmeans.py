@@ -94,6 +94,8 @@ class LloydEngine:
             x0 = source
             self.local = make_lloyd_ops(source, k, cfg.dtype, cfg.backend, cfg.empty_cluster,
                                         cfg.deterministic)
+            if cfg.fp8_recheck > 0 and hasattr(self.local, "RECHECK_TAU"):
+                self.local.RECHECK_TAU = cfg.fp8_recheck
             self.source = ResidentSource(self.local.x, self.local.layout, row_offset)
             self.local.x = self.source.x
             self.device = source.device

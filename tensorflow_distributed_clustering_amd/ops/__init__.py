@@ -449,11 +449,35 @@ class HipFp8Lloyd(_GroupedAssign, _LocalOpsBase):
     def prepare(self, C):
         self.ops.quant_fp8(C, self.k, 1, self.cm2, self.cs, self.cnorm)
 
+    # near-tie re-check (ClusterConfig.fp8_recheck): where the fp8 margin between the
+    # winner and the runner-up is within RECHECK_TAU of the runner-up's distance, both
+    # distances are recomputed in fp32 from the full-precision rows.
+    # Off by default: the top-2 epilogue costs ~8 % of the assignment (embed50m_fp8:
+    # 1.93 -> 2.14 s/iter) for labels that only differ on near ties.  Needs one K-group
+    # (N >= KGROUP_MIN_ITEMS * 256 rows per launch).
+    RECHECK_TAU = float(__import__("os").environ.get("TDC_FP8_RECHECK_TAU", 0.0))
+
+    def _top2_buffers(self, n):
+        b = getattr(self, "_t2", None)
+        if b is None or b[0].numel() < n:
+            dev = self.device
+            b = self._t2 = (torch.empty(n, dtype=torch.int32, device=dev),
+                            torch.empty(n, dtype=torch.float32, device=dev),
+                            torch.empty(n, dtype=torch.float32, device=dev))
+        return b[0][:n], b[1][:n], b[2][:n]
+
     def assign(self, C, labels, mind):
         n = self.n
         kg = self._kg_for(n)
-        self.ops.assign_bigd(self.x8[:n], self.xs[:n], self.xnorm[:n], self.cm2, self.cs,
-                             self.cnorm, kg, labels, None, self._keys_for(n))
+        if self.RECHECK_TAU > 0 and kg == 0:
+            l2, d1, d2 = self._top2_buffers(n)
+            self.ops.assign_bigd(self.x8[:n], self.xs[:n], self.xnorm[:n], self.cm2, self.cs,
+                                 self.cnorm, 0, labels, d1, None, l2, d2)
+            self.ops.recheck_top2(self.x, C.float().contiguous(), labels, l2, d1, d2,
+                                  self.RECHECK_TAU)
+        else:
+            self.ops.assign_bigd(self.x8[:n], self.xs[:n], self.xnorm[:n], self.cm2, self.cs,
+                                 self.cnorm, kg, labels, None, self._keys_for(n))
         if mind is not None:
             # inertia from the full-precision shard (the fp8 distances include the
             # quantisation noise of both operands; they only pick the winner)
