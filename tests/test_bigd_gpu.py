@@ -180,7 +180,10 @@ def test_fp8_near_tie_recheck(gpu):
     agree1 = (out[0.05] == want).float().mean().item()
     # tie-heavy data (4 centroids per blob): 0.88 -> 0.985 measured on MI355X
     assert agree1 >= 0.97 and agree1 > agree0 + 0.05, (agree0, agree1)
-    # a re-checked label is never farther (exact fp32 distances) than the fp8 winner
-    g0 = dd.gather(1, out[0.0].long()[:, None]).squeeze(1)
-    g1 = dd.gather(1, out[0.05].long()[:, None]).squeeze(1)
-    assert (g1 <= g0 * (1 + 1e-5) + 1e-3).all()
+    # a re-checked label is never farther than the fp8 winner (fp64 difference form:
+    # cdist's expanded form above is less exact than the re-check itself)
+    chg = (out[0.0] != out[0.05]).nonzero().flatten()
+    xs = x[chg].double()
+    g0 = ((xs - c.double()[out[0.0][chg].long()]) ** 2).sum(1)
+    g1 = ((xs - c.double()[out[0.05][chg].long()]) ** 2).sum(1)
+    assert chg.numel() > 0 and (g1 <= g0 * (1 + 1e-6)).all()
