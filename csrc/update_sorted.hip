@@ -28,21 +28,22 @@ namespace tdc {
 
 constexpr int LDS_HIST_MAX_K = 16384;
 
-__global__ __launch_bounds__(256) void hist_kernel(const int32_t* __restrict__ labels, int64_t N,
-                                                   int K, int* __restrict__ cnt,
-                                                   int64_t per_block) {
+template <int NT>
+__global__ __launch_bounds__(NT) void hist_kernel(const int32_t* __restrict__ labels, int64_t N,
+                                                  int K, int* __restrict__ cnt,
+                                                  int64_t per_block) {
   extern __shared__ int s_h[];
   const int tid = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.x * per_block;
   const int64_t r1 = min(N, r0 + per_block);
   const bool lds = K <= LDS_HIST_MAX_K;
   if (lds) {
-    for (int k = tid; k < K; k += 256) s_h[k] = 0;
+    for (int k = tid; k < K; k += NT) s_h[k] = 0;
     __syncthreads();
   }
   int64_t i = r0 + tid;
-  for (; i + 3 * 256 < r1; i += 4 * 256) {
-    const int a = labels[i], b = labels[i + 256], c = labels[i + 512], d = labels[i + 768];
+  for (; i + 3 * NT < r1; i += 4 * NT) {
+    const int a = labels[i], b = labels[i + NT], c = labels[i + 2 * NT], d = labels[i + 3 * NT];
     if (lds) {
       if ((unsigned)a < (unsigned)K) atomicAdd(s_h + a, 1);
       if ((unsigned)b < (unsigned)K) atomicAdd(s_h + b, 1);
@@ -55,13 +56,13 @@ __global__ __launch_bounds__(256) void hist_kernel(const int32_t* __restrict__ l
       if ((unsigned)d < (unsigned)K) atomicAdd(cnt + d, 1);
     }
   }
-  for (; i < r1; i += 256) {
+  for (; i < r1; i += NT) {
     const int a = labels[i];
     if ((unsigned)a < (unsigned)K) atomicAdd(lds ? s_h + a : cnt + a, 1);
   }
   if (lds) {
     __syncthreads();
-    for (int k = tid; k < K; k += 256)
+    for (int k = tid; k < K; k += NT)
       if (s_h[k]) atomicAdd(cnt + k, s_h[k]);
   }
 }
@@ -468,12 +469,20 @@ int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int6
   int32_t* perm = cursor + K;
   if (hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)K, s) != hipSuccess) return (int)hipErrorUnknown;
   {
-    int64_t blocks = (int64_t)num_cus * 4;
+    // one 1024-thread block per CU: a quarter of the global flush atomics of 4 x 256-thread
+    // blocks per CU (each block adds its whole LDS histogram into cnt)
+    static const int hnt = getenv("TDC_HIST_THREADS") ? atoi(getenv("TDC_HIST_THREADS")) : 1024;
+    int64_t blocks = hnt == 1024 ? (int64_t)num_cus : (int64_t)num_cus * 4;
     int64_t per = (N + blocks - 1) / blocks;
     if (per < 4096) per = 4096;
     blocks = (N + per - 1) / per;
     const size_t lds = K <= LDS_HIST_MAX_K ? sizeof(int) * (size_t)K : 0;
-    hipLaunchKernelGGL(hist_kernel, dim3((unsigned)blocks), dim3(256), lds, s, labels, N, K, cnt, per);
+    if (hnt == 1024)
+      hipLaunchKernelGGL(hist_kernel<1024>, dim3((unsigned)blocks), dim3(1024), lds, s, labels, N,
+                         K, cnt, per);
+    else
+      hipLaunchKernelGGL(hist_kernel<256>, dim3((unsigned)blocks), dim3(256), lds, s, labels, N, K,
+                         cnt, per);
     TDC_CHECK_LAUNCH();
   }
   if (acc_dtype == TDC_F64)
