@@ -14,7 +14,7 @@ ONE packed all-reduce, exactly like the Lloyd partials.
 The reference has only plain Lloyd (`scripts/distribuitedClustering.py:180-294`); this is
 an opt-in algorithm with the same fixed points.  Results equal Lloyd's up to bf16
 near-ties (``slack`` widens the bound test by that relative margin) and fp32 summation
-order; the totals are recomputed from scratch every ``refresh`` iterations.
+order; the totals are recomputed from scratch every ``refresh`` (64) iterations.
 
 Requirements: the resident bf16 MFMA path (D <= 256) with the sorted update (K x D past
 the LDS-privatised update); other configurations run plain Lloyd (``LloydEngine``).
@@ -39,7 +39,7 @@ class BoundedLloydEngine(LloydEngine):
     """LloydEngine whose ``step()`` re-assigns only the rows the bounds cannot settle."""
 
     slack = 1e-3     # relative margin on ub (bf16 distance arithmetic)
-    refresh = 16     # iterations between full recomputations of the totals
+    refresh = 64     # iterations between full recomputations of the totals
 
     def __init__(self, *a, **kw):
         super().__init__(*a, **kw)
