@@ -33,3 +33,9 @@ def test_out_of_core_npz(tmp_path):
     out = _run("out_of_core_npz.py", ["--data", str(tmp_path / "d.npz"), "--k", "5",
                                        "--dtype", "fp64", "--chunk_rows", "3000"], tmp_path)
     assert out["n"] == 20000 and out["streamed"] and out["n_iter"] == 10
+
+
+def test_online_serving(tmp_path):
+    out = _run("online_serving.py", ["--d", "8", "--k", "6", "--batches", "5", "--batch", "2000",
+                                     "--requests", "4", "--request_rows", "256"], tmp_path)
+    assert out["batches_seen"] == 5 and out["label_agreement"] > 0.999
