@@ -142,3 +142,16 @@ def test_bounded_lloyd_matches_lloyd(gpu, d, k, policy):
     assert agree > 0.999
     assert b.engine_.active_frac < 0.9  # data dependent; 8-12 % on the headline config
     np.testing.assert_allclose(b.result_.counts.sum(), 300_000)
+
+
+def test_bounded_lloyd_policies_and_spherical(gpu):
+    """bounded == Lloyd also with NaN-poisoned empty clusters (drift -> inf re-assigns
+    every row) and for spherical K-Means (centroids re-normalised after each update)."""
+    x = gaussian_blobs(200_000, 128, 300, seed=3, dtype=torch.bfloat16, device=gpu)
+    base = tdc.ClusterConfig(n_clusters=512, max_iter=12, dtype="bf16", seed=2, init="random")
+    for cfg in (base.replace(empty_cluster="nan"), base.replace(spherical=True)):
+        a = tdc.KMeans(cfg, device=gpu).fit(x).result_
+        b = tdc.KMeans(cfg.replace(algorithm="bounded"), device=gpu).fit(x).result_
+        agree = (a.labels == b.labels).float().mean().item()
+        assert agree > 0.999, (cfg.empty_cluster, cfg.spherical, agree)
+        np.testing.assert_array_equal(np.isnan(a.centers).any(1), np.isnan(b.centers).any(1))
