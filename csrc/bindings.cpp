@@ -188,7 +188,8 @@ void fcm_small(const at::Tensor& X, const at::Tensor& C, double m, bool nan_to_z
 
 void finalize(const std::optional<at::Tensor>& sums, const std::optional<at::Tensor>& counts,
               at::Tensor& C, int64_t policy, const std::optional<at::Tensor>& shift,
-              const std::optional<at::Tensor>& Cm2, const std::optional<at::Tensor>& cnorm) {
+              const std::optional<at::Tensor>& Cm2, const std::optional<at::Tensor>& cnorm,
+              const std::optional<at::Tensor>& drift, const std::optional<at::Tensor>& maxdrift) {
   check_cuda(C, "C");
   TORCH_CHECK(C.is_contiguous() && C.dim() == 2, "tdc.finalize: C");
   const int K = (int)C.size(0), D = (int)C.size(1);
@@ -211,10 +212,22 @@ void finalize(const std::optional<at::Tensor>& sums, const std::optional<at::Ten
     TORCH_CHECK(shift->scalar_type() == at::kFloat, "tdc.finalize: shift fp32");
     sh = shift->data_ptr<float>();
   }
+  float* dr = nullptr;
+  float* mdr = nullptr;
+  if (drift.has_value() && drift->defined()) {
+    TORCH_CHECK(sums.has_value() && sums->defined(), "tdc.finalize: drift needs sums");
+    TORCH_CHECK(drift->scalar_type() == at::kFloat && drift->numel() >= K && drift->is_contiguous(),
+                "tdc.finalize: drift fp32 [K]");
+    TORCH_CHECK(maxdrift.has_value() && maxdrift->defined() &&
+                    maxdrift->scalar_type() == at::kFloat && maxdrift->numel() >= 1,
+                "tdc.finalize: maxdrift fp32 [1] required with drift");
+    dr = drift->data_ptr<float>();
+    mdr = maxdrift->data_ptr<float>();
+  }
   const DevGuard guard(C.device());
   check(tdc_finalize(acc, dcode(C.scalar_type()), opt_ptr(sums), opt_ptr(counts), K, D,
                      C.data_ptr(), (int)policy, sh, opt_ptr(Cm2),
-                     static_cast<float*>(opt_ptr(cnorm)), Kp, DP, cur_stream()),
+                     static_cast<float*>(opt_ptr(cnorm)), Kp, DP, cur_stream(), dr, mdr),
         "finalize");
 }
 
@@ -554,7 +567,7 @@ TORCH_LIBRARY(tdc, m) {
   m.def("recheck_top2(Tensor X, Tensor C, Tensor(a!) labels, Tensor labels2, Tensor d1, Tensor d2, float tau) -> int");
   m.def("quant_fp8(Tensor X, int valid, int neg2, Tensor(a!) Q, Tensor(b!) S, Tensor(c!)? norm) -> ()");
   m.def("kpp_step(Tensor X, Tensor cand, Tensor(a!) closest, int mode, Tensor(b!) pots) -> ()");
-  m.def("finalize(Tensor? sums, Tensor? counts, Tensor(a!) C, int policy, Tensor(b!)? shift, Tensor(c!)? Cm2, Tensor(d!)? cnorm) -> ()");
+  m.def("finalize(Tensor? sums, Tensor? counts, Tensor(a!) C, int policy, Tensor(b!)? shift, Tensor(c!)? Cm2, Tensor(d!)? cnorm, Tensor(e!)? drift=None, Tensor(f!)? maxdrift=None) -> ()");
   m.def("assign_bf16_indexed(Tensor X, Tensor rowidx, Tensor Cm2, Tensor cnorm, Tensor(a!) labels, Tensor(b!)? mind) -> ()");
   m.def("update_sorted_indexed(Tensor X, Tensor rowidx, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work) -> ()");
   m.def("assign_bf16_top2(Tensor X, Tensor? rowidx, Tensor Cm2, Tensor cnorm, Tensor(a!) labels, Tensor(b!) mind, Tensor(c!) mind2) -> ()");

@@ -40,10 +40,12 @@ __global__ __launch_bounds__(256) void finalize_kernel(const ACC* __restrict__ s
                                                        int D, CT* __restrict__ C, int policy,
                                                        float* __restrict__ shift,
                                                        __bf16* __restrict__ Cm2,
-                                                       float* __restrict__ cnorm, int Kp, int DP) {
+                                                       float* __restrict__ cnorm, int Kp, int DP,
+                                                       float* __restrict__ drift,
+                                                       float* __restrict__ maxdrift) {
   const int lane = threadIdx.x & 63;
   const int rows = Cm2 ? (Kp > K ? Kp : K) : K;
-  unsigned shmax = 0u;
+  unsigned shmax = 0u, dmax = 0u;
   for (int k = blockIdx.x * 4 + (threadIdx.x >> 6); k < rows; k += gridDim.x * 4) {
     if (k >= K) {
       if (Cm2)
@@ -51,7 +53,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(const ACC* __restrict__ s
       if (cnorm && lane == 0) cnorm[k] = 3.0e38f;
       continue;
     }
-    float sh = 0.f, nrm = 0.f;
+    float sh = 0.f, nrm = 0.f, dsq = 0.f;
     ACC cnt = sums ? counts[k] : (ACC)1;
     const int dend = Cm2 ? (DP > D ? DP : D) : D;
     for (int d = lane; d < dend; d += 64) {
@@ -69,6 +71,10 @@ __global__ __launch_bounds__(256) void finalize_kernel(const ACC* __restrict__ s
           C[(int64_t)k * D + d] = nw;
           const float df = (float)nw - (float)old;
           sh += df * df;
+          if (drift) {  // movement in the assignment kernels' own (bf16) coordinates
+            const float e = (float)(__bf16)(float)nw - (float)(__bf16)(float)old;
+            dsq = fmaf(e, e, dsq);
+          }
         }
         if (Cm2) {
           const __bf16 b = (__bf16)(float)nw;
@@ -81,22 +87,32 @@ __global__ __launch_bounds__(256) void finalize_kernel(const ACC* __restrict__ s
       }
     }
     if (sums && shift) shmax = max(shmax, __float_as_uint(wave_sum(sh)));
+    if (sums && drift) {
+      const float dk = sqrtf(wave_sum(dsq));  // NaN (poisoned centroid) stays NaN
+      if (lane == 0) drift[k] = dk;
+      dmax = max(dmax, __float_as_uint(dk));
+    }
     if (cnorm) {
       nrm = wave_sum(nrm);
       if (lane == 0) cnorm[k] = nrm;
     }
   }
   if (sums && shift) block_max_shift(shmax, shift);
+  if (sums && maxdrift) {
+    __syncthreads();  // block_max_shift's LDS slots are reused
+    block_max_shift(dmax, maxdrift);
+  }
 }
 
 template <typename ACC, typename CT>
 int launch_finalize(const void* sums, const void* counts, int K, int D, void* C, int policy,
-                    float* shift, void* Cm2, float* cnorm, int Kp, int DP, hipStream_t s) {
+                    float* shift, void* Cm2, float* cnorm, int Kp, int DP, hipStream_t s,
+                    float* drift, float* maxdrift) {
   const int rows = Cm2 ? (Kp > K ? Kp : K) : K;
   const int blocks = std::min((rows + 3) / 4, MAX_BLOCKS);
   hipLaunchKernelGGL((finalize_kernel<ACC, CT>), dim3((unsigned)blocks), dim3(256), 0,
                      s, (const ACC*)sums, (const ACC*)counts, K, D, (CT*)C, policy, shift,
-                     (__bf16*)Cm2, cnorm, Kp, DP);
+                     (__bf16*)Cm2, cnorm, Kp, DP, drift, maxdrift);
   TDC_CHECK_LAUNCH();
   return 0;
 }
@@ -190,14 +206,18 @@ int tdc_sculley_update(int acc_dtype, int c_dtype, const void* sums, const void*
 
 int tdc_finalize(int acc_dtype, int c_dtype, const void* sums, const void* counts, int K, int D,
                  void* C, int policy, float* shift, void* Cm2, float* cnorm, int Kp, int DP,
-                 hipStream_t s) {
+                 hipStream_t s, float* drift, float* maxdrift) {
   if (acc_dtype == TDC_F64 && c_dtype == TDC_F32)
-    return launch_finalize<double, float>(sums, counts, K, D, C, policy, shift, Cm2, cnorm, Kp, DP, s);
+    return launch_finalize<double, float>(sums, counts, K, D, C, policy, shift, Cm2, cnorm, Kp, DP, s,
+                                         drift, maxdrift);
   if (acc_dtype == TDC_F32 && c_dtype == TDC_F32)
-    return launch_finalize<float, float>(sums, counts, K, D, C, policy, shift, Cm2, cnorm, Kp, DP, s);
+    return launch_finalize<float, float>(sums, counts, K, D, C, policy, shift, Cm2, cnorm, Kp, DP, s,
+                                         drift, maxdrift);
   if (acc_dtype == TDC_F64 && c_dtype == TDC_F64)
-    return launch_finalize<double, double>(sums, counts, K, D, C, policy, shift, Cm2, cnorm, Kp, DP, s);
+    return launch_finalize<double, double>(sums, counts, K, D, C, policy, shift, Cm2, cnorm, Kp, DP, s,
+                                         drift, maxdrift);
   if (acc_dtype == TDC_F32 && c_dtype == TDC_F64)
-    return launch_finalize<float, double>(sums, counts, K, D, C, policy, shift, Cm2, cnorm, Kp, DP, s);
+    return launch_finalize<float, double>(sums, counts, K, D, C, policy, shift, Cm2, cnorm, Kp, DP, s,
+                                         drift, maxdrift);
   return (int)hipErrorInvalidValue;
 }

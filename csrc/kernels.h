@@ -75,9 +75,11 @@ int tdc_fcm_small_supported(int dtype, int K, int D);
 // optional bf16 prep of the next assignment (Cm2 [Kp, DP] = -2*bf16(c), cnorm [Kp]).
 // sums == nullptr: prep only (C unchanged).
 // policy: 0 keep, 1 nan, 2 zero.
+// drift (nullable, [K]) = ||bf16(c_new) - bf16(c_old)|| per centroid, maxdrift (nullable,
+// zeroed by the caller) = its max: the centroid movement the bounds of bounded Lloyd need.
 int tdc_finalize(int acc_dtype, int c_dtype, const void* sums, const void* counts, int K,
                  int D, void* C, int policy, float* shift, void* Cm2, float* cnorm, int Kp,
-                 int DP, hipStream_t stream);
+                 int DP, hipStream_t stream, float* drift = nullptr, float* maxdrift = nullptr);
 
 // Mini-batch (Sculley) update: n = counts[k] > 0 -> C[k] = (v[k] C[k] + sums[k]) / (v[k] + n),
 // v[k] += n (v fp64 [K]); shift (nullable, zeroed by the caller) = max ||dC_k||^2 over the

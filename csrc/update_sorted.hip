@@ -417,7 +417,7 @@ int launch_segsum(const void* X, int64_t ldx, int D, const int32_t* perm, const 
   const int lanes_needed = (D + VEC - 1) / VEC;
   int64_t waves = (int64_t)num_cus * 32;  // ~8 resident 256-thread blocks per CU
   int64_t rpw = (N + waves - 1) / waves;
-  if (rpw < 256) rpw = 256;
+  if (rpw < 64) rpw = 64;  // small N (mini-batches, moved rows): keep ~8K waves in flight
   waves = (N + rpw - 1) / rpw;
   const dim3 grid((unsigned)((waves + 3) / 4));
 #define TDC_SEG(TPRV)                                                                       \

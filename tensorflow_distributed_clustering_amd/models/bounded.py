@@ -72,7 +72,8 @@ class BoundedLloydEngine(LloydEngine):
         if not self.enabled:
             return super()._eager_step(with_inertia)
         lo, ops, x = self.local, self.local.ops, self.local.x
-        C_prev = self.C.clone()
+        C_prev = self.C.clone() if (self.cfg.spherical or self.cfg.empty_cluster == "reseed") \
+            else None
         k, d = self.k, self.d
         inertia = None
         if self._fresh or with_inertia or (self.n_iter % self.refresh == 0):
@@ -118,18 +119,26 @@ class BoundedLloydEngine(LloydEngine):
             self.gcounts.add_(self.counts)
         if self.shift is not None:
             self.shift.zero_()
-        lo.ops.finalize(self.gsums, self.gcounts, self.C, lo.policy, self.shift, lo.cm2,
-                        lo.cnorm)
-        if self.cfg.spherical:
-            self.C.div_(self.C.norm(dim=1, keepdim=True).clamp_min_(1e-30))
-            lo.prepare(self.C)
-        if self.cfg.empty_cluster == "reseed":
-            self._reseed()
-        # centroid drift in the kernels' own (bf16-rounded) centroid coordinates
-        dc = self.C.to(torch.bfloat16).float() - C_prev.to(torch.bfloat16).float()
-        torch.linalg.vector_norm(dc, dim=1, out=self.drift)
-        torch.nan_to_num_(self.drift, nan=float("inf"))
-        torch.amax(self.drift, dim=0, keepdim=True, out=self.maxdrift)
+        moved_after = self.cfg.spherical or self.cfg.empty_cluster == "reseed"
+        if not moved_after:
+            # the finalize kernel also emits each centroid's movement (bf16 coordinates,
+            # NaN stays NaN -> every row re-assigned) and its max
+            self.maxdrift.zero_()
+            lo.ops.finalize(self.gsums, self.gcounts, self.C, lo.policy, self.shift, lo.cm2,
+                            lo.cnorm, self.drift, self.maxdrift)
+        else:
+            lo.ops.finalize(self.gsums, self.gcounts, self.C, lo.policy, self.shift, lo.cm2,
+                            lo.cnorm)
+            if self.cfg.spherical:
+                self.C.div_(self.C.norm(dim=1, keepdim=True).clamp_min_(1e-30))
+                lo.prepare(self.C)
+            if self.cfg.empty_cluster == "reseed":
+                self._reseed()
+            # centroid drift in the kernels' own (bf16-rounded) centroid coordinates
+            dc = self.C.to(torch.bfloat16).float() - C_prev.to(torch.bfloat16).float()
+            torch.linalg.vector_norm(dc, dim=1, out=self.drift)
+            torch.nan_to_num_(self.drift, nan=float("inf"))
+            torch.amax(self.drift, dim=0, keepdim=True, out=self.maxdrift)
         # counts of the current assignment (ClusterResult.counts)
         self.counts.copy_(self.gcounts)
         self.n_iter += 1
