@@ -168,6 +168,10 @@ def build_parser():
     parser.add_argument("--algorithm", default="lloyd", choices=["lloyd", "bounded"],
                         help="bounded: exact Lloyd that re-assigns only the rows its Hamerly "
                              "bounds cannot settle (resident bf16 MFMA path)")
+    parser.add_argument("--num_batches", type=int, default=1,
+                        help="reference batch mode: cluster N array_split batches independently, "
+                             "sum the phase times and average the centers (default 1: one "
+                             "exact fit over all rows)")
     return parser
 
 
@@ -208,7 +212,12 @@ def run(args) -> int:
     result = None
     exc_name = None
     try:
-        x, n_global, row_off = load_shard(args.data_file, comm.rank, comm.world_size, "X")
+        if args.num_batches > 1:
+            from .data.npz import open_npz_member
+            x = open_npz_member(args.data_file, "X")  # batches are cut from the global rows
+            n_global, row_off = int(x.shape[0]), 0
+        else:
+            x, n_global, row_off = load_shard(args.data_file, comm.rank, comm.world_size, "X")
         d = x.shape[1]
         if (args.n_obs, args.n_dim) != (n_global, d) and comm.is_root:
             print(f"note: --n_obs/--n_dim are logged only; data file is {n_global}x{d}",
@@ -226,21 +235,30 @@ def run(args) -> int:
                             graph=args.graph, log_every=args.log_every,
                             spherical=args.spherical, algorithm=args.algorithm,
                             fp8_recheck=args.fp8_recheck)
-        xt = torch.from_numpy(np.asarray(x))
-        if args.method_name == "distributedKMeans":
-            model = KMeans(cfg, comm)
-        elif args.method_name == "distributedFuzzyCMeans":
-            model = FuzzyCMeans(cfg, comm)
-        else:
+
+        def make_model():
+            if args.method_name == "distributedKMeans":
+                return KMeans(cfg, comm)
+            if args.method_name == "distributedFuzzyCMeans":
+                return FuzzyCMeans(cfg, comm)
             from .models.minibatch import MiniBatchKMeans
-            model = MiniBatchKMeans(cfg, comm)
-        if args.torch_profile:
-            from .utils.timers import profiled
-            with profiled(args.torch_profile, comm.rank):
-                model.fit(xt, n_global=n_global, row_offset=row_off)
+            return MiniBatchKMeans(cfg, comm)
+
+        if args.num_batches > 1:
+            from .models.batched import fit_batches_averaged
+            result = fit_batches_averaged(make_model, x, n_global, args.num_batches,
+                                          comm.rank, comm.world_size)
+            x = np.asarray(x[:min(10000, n_global)])  # rows for --plot_out only
         else:
-            model.fit(xt, n_global=n_global, row_offset=row_off)
-        result = model.result_
+            model = make_model()
+            xt = torch.from_numpy(np.asarray(x))
+            if args.torch_profile:
+                from .utils.timers import profiled
+                with profiled(args.torch_profile, comm.rank):
+                    model.fit(xt, n_global=n_global, row_offset=row_off)
+            else:
+                model.fit(xt, n_global=n_global, row_offset=row_off)
+            result = model.result_
         if args.log_device_placement:
             name = (torch.cuda.get_device_name(comm.device) if comm.device.type == "cuda"
                     else "host")

@@ -97,3 +97,26 @@ def test_same_result_one_and_two_ranks(data, tmp_path):
         assert r.returncode == 0, r.stderr
         outs.append(np.loadtxt(cen, delimiter=","))
     np.testing.assert_allclose(outs[0], outs[1], rtol=1e-12)
+
+
+def test_num_batches_averages_independent_fits(data, tmp_path):
+    """--num_batches N: reference batch mode (`distribuitedClustering.py:296-318`): N
+    array_split batches clustered independently, centers averaged, times summed."""
+    from tensorflow_distributed_clustering_amd import ClusterConfig, KMeans
+    from tensorflow_distributed_clustering_amd.data.npz import open_npz_member
+    import torch
+    log = str(tmp_path / "log.csv")
+    cen = str(tmp_path / "c.csv")
+    r = run_cli(*base_args(data, log, gpus=2, extra=["--device", "cpu", "--num_batches", "3",
+                                                     "--dtype", "fp64", "--centroids_out", cen]))
+    assert r.returncode == 0, r.stderr
+    row = open(log).read().splitlines()[1].split(",")
+    assert row[2] == "2" and all(float(v) >= 0 for v in row[6:9])
+    got = np.loadtxt(cen, delimiter=",")
+    x = np.asarray(open_npz_member(data, "X"))
+    want = []
+    for part in np.array_split(x, 3):
+        km = KMeans(ClusterConfig(n_clusters=3, max_iter=20, dtype="fp64", seed=123128,
+                                  init="kmeans++")).fit(torch.from_numpy(part.copy()))
+        want.append(km.result_.centers)
+    np.testing.assert_allclose(got, np.mean(want, axis=0), rtol=1e-9, atol=1e-9)
