@@ -1,0 +1,18 @@
+# Per-step kernel summary from a rocprofv3 --kernel-trace SQLite database:
+#   python scripts/rocpd_step_summary.py run_results.db <kernel name marking one step> <steps>
+import sqlite3, sys, re, collections
+db, marker, nsteps = sys.argv[1], sys.argv[2], int(sys.argv[3])
+c = sqlite3.connect(db)
+rows = list(c.execute("select name, start, end from kernels order by start"))
+idx = [i for i, r in enumerate(rows) if marker in r[0]]
+first = idx[len(idx) - nsteps]
+sel = rows[first:]
+span = (sel[-1][2] - sel[0][1]) / 1e3 / nsteps
+agg = collections.defaultdict(lambda: [0, 0.0])
+for n, s, e in sel:
+    short = re.sub(r"\(.*", "", n)[:90]
+    agg[short][0] += 1; agg[short][1] += (e - s) / 1e3
+tot = sum(v[1] for v in agg.values()) / nsteps
+print(f"per step: wall span {span:.1f} us, kernel busy {tot:.1f} us, {len(sel)/nsteps:.1f} launches")
+for k, (n, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+    print(f"{t/nsteps:9.2f} us  {n/nsteps:5.2f}x  {k}")

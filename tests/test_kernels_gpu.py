@@ -411,14 +411,16 @@ def test_assign_bf16_top2(gpu, n, d, k):
     assert torch.equal(li, lab[idx.long()]) and torch.equal(e2, d2[idx.long()])
 
 
-def test_bounds_filter_and_scatter(gpu):
+@pytest.mark.parametrize("off", [0, 1])  # 1: unaligned views -> the scalar filter path
+def test_bounds_filter_and_scatter(gpu, off):
     from tensorflow_distributed_clustering_amd import _native
     ops = _native.require()
     n, k = 100_003, 50
     g = torch.Generator(device=gpu).manual_seed(0)
-    labels = torch.randint(k, (n,), generator=g, device=gpu, dtype=torch.int32)
-    ub = torch.rand(n, generator=g, device=gpu)
+    labels = torch.randint(k, (n + off,), generator=g, device=gpu, dtype=torch.int32)[off:]
+    ub = torch.rand(n + off, generator=g, device=gpu)[off:]
     lb = ub + torch.rand(n, generator=g, device=gpu) * 0.5
+    lb = torch.cat([lb[:off], lb])[off:] if off else lb
     drift = torch.rand(k, generator=g, device=gpu) * 0.1
     maxd = drift.max().reshape(1)
     ub2, lb2 = ub + drift[labels.long()], lb - maxd
