@@ -186,6 +186,29 @@ void fcm_small(const at::Tensor& X, const at::Tensor& C, double m, bool nan_to_z
         "fcm_small");
 }
 
+void fcm_rows(at::Tensor& G, const at::Tensor& xx, const std::optional<at::Tensor>& cc, double m,
+              bool nan_to_zero, at::Tensor& labels, const std::optional<at::Tensor>& colsum) {
+  check_cuda(G, "G");
+  TORCH_CHECK(G.scalar_type() == at::kFloat && G.dim() == 2 && G.is_contiguous(),
+              "tdc.fcm_rows: G fp32 contiguous [rows, K]");
+  const int64_t rows = G.size(0), K = G.size(1);
+  TORCH_CHECK(xx.scalar_type() == at::kFloat && xx.is_contiguous() && xx.numel() == rows,
+              "tdc.fcm_rows: xx fp32 [rows]");
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous() && labels.numel() == rows,
+              "tdc.fcm_rows: labels int32 [rows]");
+  for (const auto* t : {&cc, &colsum})
+    if (t->has_value() && (*t)->defined())
+      TORCH_CHECK((*t)->scalar_type() == at::kFloat && (*t)->is_contiguous() && (*t)->numel() == K,
+                  "tdc.fcm_rows: cc/colsum fp32 [K]");
+  TORCH_CHECK(m > 1.0, "tdc.fcm_rows: fuzzifier must be > 1");
+  const DevGuard guard(G.device());
+  check(tdc_fcm_rows(G.data_ptr<float>(), rows, (int)K, xx.data_ptr<float>(),
+                     static_cast<const float*>(opt_ptr(cc)), (float)m, nan_to_zero ? 1 : 0,
+                     labels.data_ptr<int32_t>(), static_cast<float*>(opt_ptr(colsum)),
+                     cur_stream()),
+        "fcm_rows");
+}
+
 void finalize(const std::optional<at::Tensor>& sums, const std::optional<at::Tensor>& counts,
               at::Tensor& C, int64_t policy, const std::optional<at::Tensor>& shift,
               const std::optional<at::Tensor>& Cm2, const std::optional<at::Tensor>& cnorm,
@@ -562,6 +585,7 @@ TORCH_LIBRARY(tdc, m) {
   m.def("update_sorted(Tensor X, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work) -> ()");
   m.def("fcm_small_supported(ScalarType dtype, int K, int D) -> bool", &fcm_small_supported);
   m.def("fcm_small(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) wx, Tensor(c!) ws) -> ()");
+  m.def("fcm_rows(Tensor(a!) G, Tensor xx, Tensor? cc, float m, bool nan_to_zero, Tensor(b!) labels, Tensor(c!)? colsum=None) -> ()");
   m.def("assign_bigd_supported(ScalarType dtype, int DP) -> bool", &assign_bigd_supported);
   m.def("assign_bigd(Tensor X, Tensor? Xs, Tensor xnorm, Tensor Cm2, Tensor? Cs, Tensor cnorm, int kg_tiles, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!)? keys, Tensor(d!)? labels2=None, Tensor(e!)? mind2=None) -> ()");
   m.def("recheck_top2(Tensor X, Tensor C, Tensor(a!) labels, Tensor labels2, Tensor d1, Tensor d2, float tau) -> int");
@@ -583,6 +607,7 @@ TORCH_LIBRARY_IMPL(tdc, CUDA, m) {
   m.impl("update", &update);
   m.impl("update_sorted", &update_sorted);
   m.impl("fcm_small", &fcm_small);
+  m.impl("fcm_rows", &fcm_rows);
   m.impl("finalize", &finalize);
   m.impl("assign_bigd", &assign_bigd);
   m.impl("recheck_top2", &recheck_top2);

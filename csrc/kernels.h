@@ -70,6 +70,11 @@ int tdc_fcm_small(int dtype, int acc_dtype, const void* X, int64_t N, int64_t ld
                   const void* C, int K, double m, int nan_to_zero, int32_t* labels, void* wx,
                   void* ws, hipStream_t stream);
 int tdc_fcm_small_supported(int dtype, int K, int D);
+// FCM memberships for large K*D, in place on G = -2 x.c (+ ||c||^2 if cc is null) (fp32
+// [rows, K]): G <- w = u^m, labels = argmax u, colsum (nullable, [K]) += sum_rows w.
+// xx = ||x||^2 [rows], cc = ||c||^2 [K] (nullable).
+int tdc_fcm_rows(float* G, int64_t rows, int K, const float* xx, const float* cc, float m,
+                 int nan_to_zero, int32_t* labels, float* colsum, hipStream_t stream);
 
 // N3  finalize: C = sums/counts (empty policy), max shift^2 -> shift (float, atomic max),
 // optional bf16 prep of the next assignment (Cm2 [Kp, DP] = -2*bf16(c), cnorm [Kp]).
