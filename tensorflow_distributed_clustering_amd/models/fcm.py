@@ -135,3 +135,29 @@ class FuzzyCMeans:
     @property
     def cluster_centers_(self):
         return self.result_.centers
+
+    def _centers_on(self, dev, dtype):
+        if self.result_ is None:
+            raise RuntimeError("fit() first")
+        return torch.as_tensor(self.result_.centers, device=dev).to(dtype)
+
+    def predict(self, x: torch.Tensor) -> torch.Tensor:
+        """Labels (argmax membership, `distribuitedClustering.py:141`) of new points against
+        the fitted centers, with the same local ops as the fit (no collectives)."""
+        x = torch.as_tensor(x)
+        d = int(x.shape[1])
+        ops = make_fcm_ops(x, self.cfg.n_clusters, self.cfg.dtype, self.fuzzifier(d),
+                           self.cfg.fcm_nan_to_zero, self.cfg.backend)
+        labels = torch.empty(int(x.shape[0]), dtype=torch.int32, device=x.device)
+        ops.assign(self._centers_on(x.device, ops.c_dtype), labels)
+        return labels
+
+    def memberships(self, x: torch.Tensor, chunk_rows: int = 1 << 16) -> torch.Tensor:
+        """Soft memberships u [n, K] of new points (fp64 oracle formula, chunked)."""
+        from ..ops import reference as ref
+        x = torch.as_tensor(x)
+        c = self._centers_on(x.device, torch.float64)
+        m = self.fuzzifier(int(x.shape[1]))
+        return torch.cat([ref.fcm_memberships(x[s:s + chunk_rows].double(), c, m,
+                                              self.cfg.fcm_nan_to_zero)
+                          for s in range(0, int(x.shape[0]), chunk_rows)])

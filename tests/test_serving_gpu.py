@@ -69,3 +69,18 @@ def test_predictor_reused_buffer_requantised(gpu, dtype, d):
     fresh = ClusterPredictor(c, dtype=dtype, device=gpu)
     assert torch.equal(lb, fresh.predict(b))
     assert torch.equal(la, fresh.predict(a))
+
+
+def test_fcm_predict_gemm_path(gpu):
+    """FuzzyCMeans.predict at D > 16 runs HipGemmFCM (hipBLASLt + fcm_rows) and reproduces
+    the fit's label pass."""
+    import tensorflow_distributed_clustering_amd as tdc
+    from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs
+    x = gaussian_blobs(50000, 64, 32, seed=4, dtype=torch.float32, device=gpu)
+    fcm = tdc.FuzzyCMeans(tdc.ClusterConfig(n_clusters=32, max_iter=3, dtype="fp32", seed=1,
+                                            fuzzifier=2.0)).fit(x)
+    assert fcm.result_.backend == "hip_fcm_gemm"
+    lab = fcm.predict(x)
+    assert (lab == fcm.result_.labels).float().mean().item() > 0.999
+    u = fcm.memberships(x[:1000])
+    assert (u.argmax(1).to(torch.int32) == lab[:1000]).float().mean().item() > 0.99
