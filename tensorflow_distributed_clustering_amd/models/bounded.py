@@ -57,8 +57,10 @@ class BoundedLloydEngine(LloydEngine):
         self.moved = torch.zeros(3, n, dtype=torch.int32, device=dev)  # idx | old | new
         self.cnt = torch.zeros(2, dtype=torch.int32, device=dev)       # active | moved
         self.minus = torch.zeros_like(self.buf)
-        self.gsums = torch.zeros(k, d, dtype=torch.float64, device=dev)
-        self.gcounts = torch.zeros(k, dtype=torch.float64, device=dev)
+        # fp64 running totals, laid out like buf[:k*d+k] so one kernel updates both
+        self.gbuf = torch.zeros(k * d + k, dtype=torch.float64, device=dev)
+        self.gsums = self.gbuf[: k * d].view(k, d)
+        self.gcounts = self.gbuf[k * d:]
         self.drift = torch.zeros(k, dtype=torch.float32, device=dev)
         self.maxdrift = torch.zeros(1, dtype=torch.float32, device=dev)
         self._fresh = True       # next step is a full assignment (first step / refresh)
@@ -87,17 +89,16 @@ class BoundedLloydEngine(LloydEngine):
             if with_inertia:
                 inertia = self.comm.sum_scalar(float(self.d1.double().sum()))
             self.comm.allreduce_bucketed_(self.buf, self.bucket_bytes)
-            self.gsums.copy_(self.sums)
-            self.gcounts.copy_(self.counts)
+            self.gbuf.copy_(self.buf[: self.gbuf.numel()])
             self.active_frac = 1.0
             self._fresh = False
         else:
             self.cnt.zero_()
             ops.bounds_filter(self.labels, self.ub, self.lb, self.drift, self.maxdrift,
                               self.slack, self.active, self.cnt[0:1])
-            m = int(self.cnt[0].item())
-            self.buf.zero_()
+            self.buf.zero_()  # queued ahead of the host read of the active count
             self.minus.zero_()
+            m = int(self.cnt[0].item())
             if m > 0:
                 act = self.active[:m]
                 ops.assign_bf16_top2(x, act, lo.cm2, lo.cnorm, self.blab[:m], self.d1[:m],
@@ -115,8 +116,7 @@ class BoundedLloydEngine(LloydEngine):
             self.active_frac = m / max(1, self.n_local)
             self.buf.sub_(self.minus)  # deltas: +x into new clusters, -x out of old ones
             self.comm.allreduce_bucketed_(self.buf, self.bucket_bytes)
-            self.gsums.add_(self.sums)
-            self.gcounts.add_(self.counts)
+            self.gbuf.add_(self.buf[: self.gbuf.numel()])
         if self.shift is not None:
             self.shift.zero_()
         moved_after = self.cfg.spherical or self.cfg.empty_cluster == "reseed"
