@@ -72,7 +72,11 @@ __global__ __launch_bounds__(256) void finalize_kernel(const ACC* __restrict__ s
           const float df = (float)nw - (float)old;
           sh += df * df;
           if (drift) {  // movement in the assignment kernels' own (bf16) coordinates
-            const float e = (float)(__bf16)(float)nw - (float)(__bf16)(float)old;
+            // a centroid that was already NaN can never win the argmin: leave it out
+            // (drift 0) instead of forcing every row to re-assign on every later step;
+            // one that comes back from NaN moved arbitrarily far (drift +inf)
+            const float nb = (float)(__bf16)(float)nw, ob = (float)(__bf16)(float)old;
+            const float e = isnan(ob) ? (isnan(nb) ? 0.f : INFINITY) : nb - ob;
             dsq = fmaf(e, e, dsq);
           }
         }

@@ -17,13 +17,40 @@ works on every batch as in the reference's in-graph replication.
 """
 from __future__ import annotations
 
+import dataclasses
+import os
 from typing import Callable, Optional
 
 import numpy as np
 import torch
 
-from ..parallel.dist import shard_bounds
+from ..parallel.dist import local_comm, shard_bounds
 from .kmeans import ClusterResult
+
+
+def batch_checkpoint_path(path: str, b: int) -> str:
+    """Checkpoint file of batch ``b`` (``run.npz`` -> ``run_b1.npz``): every batch resumes
+    from its own state; the base path receives the averaged centers at the end."""
+    if not path:
+        return path
+    root, ext = os.path.splitext(path)
+    return f"{root}_b{b}{ext}"
+
+
+def _shared_init(model, x_batch0: torch.Tensor, row_offset: int, n_batch0: int) -> np.ndarray:
+    """ONE set of initial centers for every batch, as the reference does: it builds
+    ``initial_centers = X[0:K]`` once (`distribuitedClustering.py:325`) and passes the same
+    array to each batch fit, which keeps cluster identities aligned before ``np.mean``.
+    Computed collectively with the model's configured init on batch 0's rows (``first_k``
+    gives exactly the reference's global ``X[0:K]``)."""
+    from .init import init_centers
+    cfg = model.cfg
+    comm = model.comm if model.comm is not None else local_comm(x_batch0.device)
+    dev = comm.device
+    method = cfg.init if cfg.init != "given" else "first_k"
+    c = init_centers(method, x_batch0.to(dev), row_offset, n_batch0, cfg.n_clusters, comm,
+                     cfg.seed)
+    return c.double().cpu().numpy()
 
 
 def batch_bounds(n_global: int, num_batches: int, b: int):
@@ -34,7 +61,8 @@ def batch_bounds(n_global: int, num_batches: int, b: int):
 def fit_batches_averaged(make_model: Callable[[], object], rows, n_global: int,
                          num_batches: int, rank: int, world: int,
                          init_centers_: Optional[np.ndarray] = None) -> ClusterResult:
-    """Fit ``num_batches`` independent models and average their centers.
+    """Fit ``num_batches`` independent models from one shared start and average their
+    centers.
 
     ``rows`` is indexable by global row (an ``np.memmap`` of the NPZ member or any
     array); this rank copies only its share of each batch.  ``make_model()`` returns a
@@ -47,19 +75,33 @@ def fit_batches_averaged(make_model: Callable[[], object], rows, n_global: int,
     if num_batches > n_global:
         raise ValueError(f"num_batches={num_batches} exceeds the {n_global} rows")
     centers, results = [], []
+    base_ckpt = ""
     for b in range(num_batches):
         bs, be = batch_bounds(n_global, num_batches, b)
         s, e = shard_bounds(be - bs, world, rank)
         x = torch.from_numpy(np.array(rows[bs + s: bs + e], copy=True))
         model = make_model()
+        base_ckpt = model.cfg.checkpoint_path
+        if base_ckpt:
+            model.cfg = dataclasses.replace(model.cfg,
+                                            checkpoint_path=batch_checkpoint_path(base_ckpt, b))
+        if init_centers_ is None:
+            init_centers_ = _shared_init(model, x, s, be - bs)
         model.fit(x, init_centers_=init_centers_, n_global=be - bs, row_offset=s)
         r = model.result_
         results.append(r)
         centers.append(np.asarray(r.centers, dtype=np.float64))
         del model, x
     first = results[0]
+    avg = np.mean(np.stack(centers), axis=0)
+    if base_ckpt and rank == 0:
+        from ..utils.checkpoint import Checkpoint, save
+        save(base_ckpt, Checkpoint("batched-average", max(r.n_iter for r in results), avg,
+                                   meta={"num_batches": num_batches,
+                                         "batch_checkpoints": [batch_checkpoint_path(base_ckpt, b)
+                                                               for b in range(num_batches)]}))
     return ClusterResult(
-        centers=np.mean(np.stack(centers), axis=0),
+        centers=avg,
         init_centers=first.init_centers,
         labels=None,  # per-batch labels refer to different center sets
         counts=None,

@@ -133,6 +133,9 @@ class BoundedLloydEngine(LloydEngine):
                 self.C.div_(self.C.norm(dim=1, keepdim=True).clamp_min_(1e-30))
                 lo.prepare(self.C)
             if self.cfg.empty_cluster == "reseed":
+                # _reseed() reads self.counts: give it the totals of the current
+                # assignment, not this step's all-reduced deltas
+                self.counts.copy_(self.gcounts)
                 self._reseed()
             # centroid drift in the kernels' own (bf16-rounded) centroid coordinates
             dc = self.C.to(torch.bfloat16).float() - C_prev.to(torch.bfloat16).float()

@@ -99,24 +99,34 @@ def test_same_result_one_and_two_ranks(data, tmp_path):
     np.testing.assert_allclose(outs[0], outs[1], rtol=1e-12)
 
 
-def test_num_batches_averages_independent_fits(data, tmp_path):
+def test_num_batches_averages_fits_from_shared_init(data, tmp_path):
     """--num_batches N: reference batch mode (`distribuitedClustering.py:296-318`): N
-    array_split batches clustered independently, centers averaged, times summed."""
+    array_split batches clustered independently from ONE shared initial center set (built
+    once, `:325`), centers averaged, times summed; each batch checkpoints to its own file."""
     from tensorflow_distributed_clustering_amd import ClusterConfig, KMeans
     from tensorflow_distributed_clustering_amd.data.npz import open_npz_member
+    from tensorflow_distributed_clustering_amd.utils import checkpoint as ck
     import torch
     log = str(tmp_path / "log.csv")
     cen = str(tmp_path / "c.csv")
+    path = str(tmp_path / "run.npz")
     r = run_cli(*base_args(data, log, gpus=2, extra=["--device", "cpu", "--num_batches", "3",
-                                                     "--dtype", "fp64", "--centroids_out", cen]))
+                                                     "--dtype", "fp64", "--centroids_out", cen,
+                                                     "--checkpoint", path]))
     assert r.returncode == 0, r.stderr
     row = open(log).read().splitlines()[1].split(",")
     assert row[2] == "2" and all(float(v) >= 0 for v in row[6:9])
     got = np.loadtxt(cen, delimiter=",")
     x = np.asarray(open_npz_member(data, "X"))
-    want = []
-    for part in np.array_split(x, 3):
-        km = KMeans(ClusterConfig(n_clusters=3, max_iter=20, dtype="fp64", seed=123128,
-                                  init="kmeans++")).fit(torch.from_numpy(part.copy()))
-        want.append(km.result_.centers)
+    parts = np.array_split(x, 3)
+    cfg = ClusterConfig(n_clusters=3, max_iter=20, dtype="fp64", seed=123128, init="kmeans++")
+    c0 = KMeans(cfg.replace(max_iter=0)).fit(torch.from_numpy(parts[0].copy())).result_.init_centers
+    want = [KMeans(cfg).fit(torch.from_numpy(p.copy()), init_centers_=c0).result_.centers
+            for p in parts]
     np.testing.assert_allclose(got, np.mean(want, axis=0), rtol=1e-9, atol=1e-9)
+    # per-batch checkpoints + the averaged result under the base path
+    for b in range(3):
+        assert ck.load(str(tmp_path / f"run_b{b}.npz")).n_iter >= 1
+    avg = ck.load(path)
+    assert avg.method == "batched-average" and avg.meta["num_batches"] == 3
+    np.testing.assert_allclose(avg.centers, got, rtol=1e-12)

@@ -145,13 +145,22 @@ def test_bounded_lloyd_matches_lloyd(gpu, d, k, policy):
 
 
 def test_bounded_lloyd_policies_and_spherical(gpu):
-    """bounded == Lloyd also with NaN-poisoned empty clusters (drift -> inf re-assigns
-    every row) and for spherical K-Means (centroids re-normalised after each update)."""
+    """bounded == Lloyd also with NaN-poisoned empty clusters (a centroid that turns NaN
+    re-assigns every row once, then drops out of the drift), with empty clusters re-seeded
+    (reseed must read the totals, not the step's deltas) and for spherical K-Means
+    (centroids re-normalised after each update)."""
     x = gaussian_blobs(200_000, 128, 300, seed=3, dtype=torch.bfloat16, device=gpu)
     base = tdc.ClusterConfig(n_clusters=512, max_iter=12, dtype="bf16", seed=2, init="random")
-    for cfg in (base.replace(empty_cluster="nan"), base.replace(spherical=True)):
+    for cfg in (base.replace(empty_cluster="nan"), base.replace(empty_cluster="reseed"),
+                base.replace(spherical=True)):
         a = tdc.KMeans(cfg, device=gpu).fit(x).result_
-        b = tdc.KMeans(cfg.replace(algorithm="bounded"), device=gpu).fit(x).result_
+        bm = tdc.KMeans(cfg.replace(algorithm="bounded"), device=gpu).fit(x)
+        b = bm.result_
         agree = (a.labels == b.labels).float().mean().item()
         assert agree > 0.999, (cfg.empty_cluster, cfg.spherical, agree)
         np.testing.assert_array_equal(np.isnan(a.centers).any(1), np.isnan(b.centers).any(1))
+        if cfg.empty_cluster == "nan":
+            assert np.isnan(b.centers).any()       # the case under test happened
+            assert bm.engine_.active_frac < 0.9    # NaN centroids no longer force full passes
+        if cfg.empty_cluster == "reseed":
+            np.testing.assert_allclose(a.centers, b.centers, rtol=0, atol=5e-2)
