@@ -145,8 +145,20 @@ void update(const at::Tensor& X, const at::Tensor& labels, at::Tensor& sums, at:
 
 int64_t update_sorted_workspace(int64_t N, int64_t K) { return tdc_update_sorted_workspace(N, (int)K); }
 
+// exact count split (kernels.h): both or neither, fp32 [>= K]
+void check_split(const std::optional<at::Tensor>& hi, const std::optional<at::Tensor>& lo,
+                 int64_t K, const char* op) {
+  const bool h = hi.has_value() && hi->defined(), l = lo.has_value() && lo->defined();
+  TORCH_CHECK(h == l, "tdc.", op, ": cnt_hi and cnt_lo go together");
+  if (!h) return;
+  for (const auto* t : {&hi, &lo})
+    TORCH_CHECK((*t)->scalar_type() == at::kFloat && (*t)->is_contiguous() && (*t)->numel() >= K,
+                "tdc.", op, ": cnt_hi/cnt_lo must be contiguous fp32 [K]");
+}
+
 void update_sorted(const at::Tensor& X, const at::Tensor& labels, at::Tensor& sums,
-                   at::Tensor& counts, at::Tensor& work) {
+                   at::Tensor& counts, at::Tensor& work, const std::optional<at::Tensor>& cnt_hi,
+                   const std::optional<at::Tensor>& cnt_lo) {
   check_cuda(X, "X");
   check_rows(X, "X");
   TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous() && labels.numel() >= X.size(0),
@@ -158,11 +170,14 @@ void update_sorted(const at::Tensor& X, const at::Tensor& labels, at::Tensor& su
   TORCH_CHECK(work.scalar_type() == at::kInt && work.is_contiguous() &&
                   work.numel() >= tdc_update_sorted_workspace(X.size(0), (int)sums.size(0)),
               "tdc.update_sorted: workspace too small");
+  check_split(cnt_hi, cnt_lo, sums.size(0), "update_sorted");
   const DevGuard guard(X.device());
   check(tdc_update_sorted(dcode(X.scalar_type()), dcode(sums.scalar_type()), X.data_ptr(),
                           X.size(0), X.stride(0), (int)sums.size(1), labels.data_ptr<int32_t>(),
                           (int)sums.size(0), sums.data_ptr(), counts.data_ptr(),
-                          work.data_ptr<int>(), num_cus(X.device().index()), cur_stream()),
+                          work.data_ptr<int>(), num_cus(X.device().index()), cur_stream(),
+                          nullptr, static_cast<float*>(opt_ptr(cnt_hi)),
+                          static_cast<float*>(opt_ptr(cnt_lo))),
         "update_sorted");
 }
 
@@ -299,7 +314,9 @@ void assign_bf16_indexed(const at::Tensor& X, const at::Tensor& rowidx, const at
 }
 
 void update_sorted_indexed(const at::Tensor& X, const at::Tensor& rowidx, const at::Tensor& labels,
-                           at::Tensor& sums, at::Tensor& counts, at::Tensor& work) {
+                           at::Tensor& sums, at::Tensor& counts, at::Tensor& work,
+                           const std::optional<at::Tensor>& cnt_hi,
+                           const std::optional<at::Tensor>& cnt_lo) {
   check_cuda(X, "X");
   check_rows(X, "X");
   const int64_t B = labels.numel();
@@ -314,12 +331,14 @@ void update_sorted_indexed(const at::Tensor& X, const at::Tensor& rowidx, const 
   TORCH_CHECK(work.scalar_type() == at::kInt && work.is_contiguous() &&
                   work.numel() >= tdc_update_sorted_workspace(B, (int)sums.size(0)),
               "tdc.update_sorted_indexed: workspace too small");
+  check_split(cnt_hi, cnt_lo, sums.size(0), "update_sorted_indexed");
   const DevGuard guard(X.device());
   check(tdc_update_sorted(dcode(X.scalar_type()), dcode(sums.scalar_type()), X.data_ptr(), B,
                           X.stride(0), (int)sums.size(1), labels.data_ptr<int32_t>(),
                           (int)sums.size(0), sums.data_ptr(), counts.data_ptr(),
                           work.data_ptr<int>(), num_cus(X.device().index()), cur_stream(),
-                          rowidx.data_ptr<int32_t>()),
+                          rowidx.data_ptr<int32_t>(), static_cast<float*>(opt_ptr(cnt_hi)),
+                          static_cast<float*>(opt_ptr(cnt_lo))),
         "update_sorted_indexed");
 }
 
@@ -582,7 +601,7 @@ TORCH_LIBRARY(tdc, m) {
   m.def("lloyd_small(Tensor X, Tensor C, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!) sums, Tensor(d!) counts) -> ()");
   m.def("update(Tensor X, Tensor labels, Tensor(a!) sums, Tensor(b!) counts) -> ()");
   m.def("update_sorted_workspace(int N, int K) -> int", &update_sorted_workspace);
-  m.def("update_sorted(Tensor X, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work) -> ()");
+  m.def("update_sorted(Tensor X, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work, Tensor(d!)? cnt_hi=None, Tensor(e!)? cnt_lo=None) -> ()");
   m.def("fcm_small_supported(ScalarType dtype, int K, int D) -> bool", &fcm_small_supported);
   m.def("fcm_small(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) wx, Tensor(c!) ws) -> ()");
   m.def("fcm_rows(Tensor(a!) G, Tensor xx, Tensor? cc, float m, bool nan_to_zero, Tensor(b!) labels, Tensor(c!)? colsum=None) -> ()");
@@ -593,7 +612,7 @@ TORCH_LIBRARY(tdc, m) {
   m.def("kpp_step(Tensor X, Tensor cand, Tensor(a!) closest, int mode, Tensor(b!) pots) -> ()");
   m.def("finalize(Tensor? sums, Tensor? counts, Tensor(a!) C, int policy, Tensor(b!)? shift, Tensor(c!)? Cm2, Tensor(d!)? cnorm, Tensor(e!)? drift=None, Tensor(f!)? maxdrift=None) -> ()");
   m.def("assign_bf16_indexed(Tensor X, Tensor rowidx, Tensor Cm2, Tensor cnorm, Tensor(a!) labels, Tensor(b!)? mind) -> ()");
-  m.def("update_sorted_indexed(Tensor X, Tensor rowidx, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work) -> ()");
+  m.def("update_sorted_indexed(Tensor X, Tensor rowidx, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work, Tensor(d!)? cnt_hi=None, Tensor(e!)? cnt_lo=None) -> ()");
   m.def("assign_bf16_top2(Tensor X, Tensor? rowidx, Tensor Cm2, Tensor cnorm, Tensor(a!) labels, Tensor(b!) mind, Tensor(c!) mind2) -> ()");
   m.def("bounds_filter(Tensor labels, Tensor(a!) ub, Tensor(b!) lb, Tensor drift, Tensor maxdrift, float slack, Tensor(c!) active, Tensor(d!) count) -> ()");
   m.def("bounds_scatter(Tensor active, Tensor count, Tensor blab, Tensor d1, Tensor d2, Tensor(a!) labels, Tensor(b!) ub, Tensor(c!) lb, Tensor(d!) moved_idx, Tensor(e!) moved_old, Tensor(f!) moved_new, Tensor(g!) mcount) -> ()");

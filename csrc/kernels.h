@@ -60,9 +60,13 @@ int tdc_update_lds(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t
 // workspace of tdc_update_sorted_workspace(N, K) elements.  sums/counts are accumulated
 // (caller zeroes them once per pass).
 // rowidx (nullable): labels[i] belongs to row rowidx[i] of X (N = number of labels).
+// cnt_hi / cnt_lo (nullable, fp32 [K]): the exact count split of an fp32 all-reduce
+// buffer, hi += c >> 12, lo += c & 4095 (each term stays an integer below 2^24, so the
+// fp32 all-reduce sums them exactly; count = 4096 hi + lo up to 2^36).
 int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
                       const int32_t* labels, int K, void* sums, void* counts, int* work,
-                      int num_cus, hipStream_t stream, const int32_t* rowidx = nullptr);
+                      int num_cus, hipStream_t stream, const int32_t* rowidx = nullptr,
+                      float* cnt_hi = nullptr, float* cnt_lo = nullptr);
 int64_t tdc_update_sorted_workspace(int64_t N, int K);
 
 // N4/N5  fused small-K Fuzzy C-Means tower: sum_i w_ki x_i, sum_i w_ki, argmax labels.

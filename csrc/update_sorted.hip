@@ -72,7 +72,9 @@ template <typename ACC>
 __global__ __launch_bounds__(1024) void scan_kernel(const int* __restrict__ cnt, int K,
                                                     int* __restrict__ offsets,
                                                     int* __restrict__ cursor,
-                                                    ACC* __restrict__ counts_acc) {
+                                                    ACC* __restrict__ counts_acc,
+                                                    float* __restrict__ cnt_hi,
+                                                    float* __restrict__ cnt_lo) {
   __shared__ int s_part[1024];
   const int tid = threadIdx.x;
   const int per = (K + 1023) / 1024;
@@ -94,6 +96,10 @@ __global__ __launch_bounds__(1024) void scan_kernel(const int* __restrict__ cnt,
     offsets[k] = run;
     cursor[k] = run;
     if (counts_acc) counts_acc[k] += (ACC)c;  // accumulate: streamed chunks add up
+    if (cnt_hi && c) {  // exact split for the fp32 all-reduce (kernels.h)
+      cnt_hi[k] += (float)(c >> 12);
+      cnt_lo[k] += (float)(c & 4095);
+    }
     run += c;
   }
   if (tid == 1023) offsets[K] = s_part[1023];
@@ -459,7 +465,8 @@ int dispatch_segsum(int x_dtype, const void* X, int64_t ldx, int D, const int32_
 
 int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
                       const int32_t* labels, int K, void* sums, void* counts, int* work,
-                      int num_cus, hipStream_t s, const int32_t* rowidx) {
+                      int num_cus, hipStream_t s, const int32_t* rowidx, float* cnt_hi,
+                      float* cnt_lo) {
   if (N <= 0) return 0;
   if (N >= (int64_t)1 << 31) return (int)hipErrorInvalidValue;
   // workspace layout (ints): cnt[K] | offsets[K+1] | cursor[K] | perm[N]
@@ -487,10 +494,10 @@ int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int6
   }
   if (acc_dtype == TDC_F64)
     hipLaunchKernelGGL(scan_kernel<double>, dim3(1), dim3(1024), 0, s, cnt, K, offsets, cursor,
-                       (double*)counts);
+                       (double*)counts, cnt_hi, cnt_lo);
   else
     hipLaunchKernelGGL(scan_kernel<float>, dim3(1), dim3(1024), 0, s, cnt, K, offsets, cursor,
-                       (float*)counts);
+                       (float*)counts, cnt_hi, cnt_lo);
   TDC_CHECK_LAUNCH();
   if (K <= LDS_HIST_MAX_K) {
     // one 1024-thread block per CU: 16 waves keep the LDS-rank -> store chains in flight

@@ -18,6 +18,7 @@ INITS = ("random", "first_k", "kmeans++", "kmeans||", "given")
 EMPTY_POLICIES = ("keep", "nan", "nan_any", "reseed", "zero")
 BACKENDS = ("auto", "hip", "torch")
 ALGORITHMS = ("lloyd", "bounded")
+COMM_MODES = ("auto", "allreduce", "rsag")
 
 
 @dataclass(frozen=True)
@@ -44,6 +45,11 @@ class ClusterConfig:
     checkpoint_*    periodic centroid checkpoints / resume (reference: none)
     algorithm       'lloyd' | 'bounded' (exact Lloyd that re-assigns only the rows its
                     Hamerly bounds cannot settle; resident bf16 MFMA path, else Lloyd)
+    comm_mode       partial-sum reduction: 'allreduce' (one packed all-reduce, every rank
+                    finalises all K), 'rsag' (reduce-scatter -> each rank finalises K/G
+                    centroids and preps their assign operands -> all-gather of the
+                    operands), 'auto' (rsag when the sums buffer >= 32 MiB and G > 1)
+    bucket_kb       split the all-reduce into calls of this many KiB (0: one call)
     """
 
     n_clusters: int
@@ -71,6 +77,8 @@ class ClusterConfig:
     spherical: bool = False     # cosine / spherical K-Means: unit rows, unit centroids
     algorithm: str = "lloyd"    # 'bounded': Lloyd with Hamerly bounds (models/bounded.py)
     fp8_recheck: float = 0.0    # fp8: exact re-check of near ties (relative margin; 0 = off)
+    comm_mode: str = "auto"     # 'allreduce' | 'rsag' | 'auto' (parallel/dist.py)
+    bucket_kb: int = 0          # all-reduce bucket size (0: one call per iteration)
 
     def __post_init__(self):
         if self.n_clusters <= 0:
@@ -87,6 +95,8 @@ class ClusterConfig:
             raise ValueError(f"backend must be one of {BACKENDS}")
         if self.algorithm not in ALGORITHMS:
             raise ValueError(f"algorithm must be one of {ALGORITHMS}")
+        if self.comm_mode not in COMM_MODES:
+            raise ValueError(f"comm_mode must be one of {COMM_MODES}")
 
     def replace(self, **kw) -> "ClusterConfig":
         return dataclasses.replace(self, **kw)

@@ -23,6 +23,7 @@ the *final* centroids (what the reference returns as ``cluster_idx``) runs untim
 """
 from __future__ import annotations
 
+import math
 import time
 from dataclasses import dataclass, field
 from typing import List, Optional
@@ -33,7 +34,7 @@ import torch
 from ..config import ClusterConfig
 from ..data.stream import HostSource, ResidentSource, plan_chunk_rows, plan_resident_rows
 from ..ops import acc_dtype_for, make_lloyd_ops, padded_dim
-from ..parallel.dist import Comm, local_comm
+from ..parallel.dist import Comm, join_counts, local_comm
 from ..utils import faults
 from ..utils.checkpoint import RunCheckpointer
 from ..utils.timers import DeviceTimer, sync
@@ -119,27 +120,89 @@ class LloydEngine:
         dev = self.device
         self._x0 = x0
         self._init_given = init_centers_
-        self.C = torch.zeros(k, self.d, dtype=self.local.c_dtype, device=dev)
         acc = acc_dtype_for(cfg.dtype, k, self.d)
+        # fp32 partial sums: the counts also travel as exact integer halves (hi, lo) in the
+        # same buffer (parallel/dist.split_counts); without the kernel support: fp64 buffer
+        self.count_split = (acc == torch.float32 and self.exact_counts_ok
+                            and self.local.supports_count_split())
+        if acc == torch.float32 and not self.count_split:
+            acc = torch.float64
+        self.rsag = self._use_rsag(comm, cfg, k * self.d * torch.tensor([], dtype=acc).element_size())
+        W = comm.world_size
+        if self.rsag:
+            align = math.lcm(max(1, self.local.row_align), W)
+            kpad = -(-k // align) * align
+            self.local.pad_rows(kpad)
+        else:
+            kpad = k
+        self.kpad = kpad
         # 'nan_any' (script compat): K extra "empty on this rank" flags ride in the same
         # all-reduce; a cluster empty on ANY rank becomes NaN everywhere, like the
         # reference's per-GPU reduce_mean of an empty gather (`distribuitedClustering.py:240,248`)
         self.nan_any = cfg.empty_cluster == "nan_any"
-        extra = k if self.nan_any else 0
-        self.buf = torch.zeros(k * self.d + k + extra, dtype=acc, device=dev)
-        self.sums = self.buf[: k * self.d].view(k, self.d)
-        self.counts = self.buf[k * self.d: k * self.d + k]
-        self.empty_flags = self.buf[k * self.d + k:] if self.nan_any else None
+        # buf = [sums kpad*D | counts kpad | (hi kpad | lo kpad) | (flags kpad)]: the sums
+        # block is what a reduce-scatter splits by rank; the small tail is all-reduced
+        nsmall = 1 + (2 if self.count_split else 0) + (1 if self.nan_any else 0)
+        self.buf = torch.zeros(kpad * self.d + nsmall * kpad, dtype=acc, device=dev)
+        self.sums_pad = self.buf[: kpad * self.d].view(kpad, self.d)
+        self.sums = self.sums_pad[:k]
+        self.small = self.buf[kpad * self.d:]
+        self.counts = self.small[:k]
+        row = 1
+        self.cnt_hi = self.cnt_lo = None
+        if self.count_split:
+            self.cnt_hi = self.small[kpad: kpad + k]
+            self.cnt_lo = self.small[2 * kpad: 2 * kpad + k]
+            self.local.set_count_split(self.cnt_hi, self.cnt_lo)
+            row = 3
+        self.empty_flags = self.small[row * kpad: row * kpad + k] if self.nan_any else None
+        self.C_pad = torch.zeros(kpad, self.d, dtype=self.local.c_dtype, device=dev)
+        self.C = self.C_pad[:k]
+        if self.rsag:
+            kr = kpad // W
+            self._kr = kr
+            self._r0 = comm.rank * kr
+            self._rs_out = torch.zeros(kr, self.d, dtype=acc, device=dev)
+            ops_ = self.local.gather_operands()
+            self._gathered = ops_ if ops_ is not None else [self.C_pad]
+            self._c_synced = True
         self.labels = torch.zeros(self.n_local, dtype=torch.int32, device=dev)
         mdt = torch.float64 if self.local.c_dtype == torch.float64 else torch.float32
         self.mind = torch.zeros(self.n_local, dtype=mdt, device=dev) if cfg.compute_inertia else None
         self.need_shift = cfg.tol > 0 or cfg.log_every > 0
         self.shift = torch.zeros(1, dtype=torch.float32, device=dev) if self.need_shift else None
-        self.bucket_bytes = 64 << 20
+        self.bucket_bytes = cfg.bucket_kb << 10
         self.n_iter = 0
         self.c0 = None
         if not defer_init:
             self.init_centroids()
+
+    # exact count halves in the buffer (subclasses with their own count bookkeeping: off)
+    exact_counts_ok = True
+    # reduce-scatter / all-gather mode allowed (subclasses that read the whole buf: off)
+    rsag_ok = True
+    RSAG_MIN_BYTES = 32 << 20
+
+    def _use_rsag(self, comm: Comm, cfg: ClusterConfig, sums_bytes: int) -> bool:
+        if comm.world_size <= 1 or not self.rsag_ok:
+            return False
+        if cfg.comm_mode == "rsag":
+            return True
+        return cfg.comm_mode == "auto" and sums_bytes >= self.RSAG_MIN_BYTES
+
+    def exact_counts(self) -> torch.Tensor:
+        """Global cluster sizes of the last update (fp64, exact past 2^24)."""
+        if self.count_split:
+            return join_counts(self.cnt_hi, self.cnt_lo)
+        return self.counts.double()
+
+    def centers(self) -> torch.Tensor:
+        """The full centroid table (rsag ranks only finalise their slice: gather the rest)."""
+        if self.rsag and not self._c_synced:
+            part = self.C_pad[self._r0: self._r0 + self._kr].contiguous()
+            self.comm.all_gather_(self.C_pad, part)
+            self._c_synced = True
+        return self.C
 
     def init_centroids(self):
         """Centroid init (collective: every rank calls it, in the same order).  Kept out
@@ -188,19 +251,46 @@ class LloydEngine:
         inertia = self.comm.sum_scalar(float(mind.double().sum())) if mind is not None else None
         if self.nan_any:
             self.empty_flags.copy_((self.counts == 0).to(self.buf.dtype))
-        self.comm.allreduce_bucketed_(self.buf, self.bucket_bytes)
-        if self.nan_any:
-            self.counts.masked_fill_(self.empty_flags > 0, 0)
-        if self.shift is not None:
-            self.shift.zero_()
-        self.local.finalize(self.sums, self.counts, self.C, self.shift)
+        if self.rsag:
+            self._reduce_scatter_finalize()
+        else:
+            self.comm.allreduce_bucketed_(self.buf, self.bucket_bytes)
+            if self.nan_any:
+                self.counts.masked_fill_(self.empty_flags > 0, 0)
+            if self.shift is not None:
+                self.shift.zero_()
+            self.local.finalize(self.sums, self.counts, self.C, self.shift)
         if self.cfg.spherical:  # project the means back to the sphere
+            self.centers()
             self.C.div_(self.C.norm(dim=1, keepdim=True).clamp_min_(1e-30))
             self.local.prepare(self.C)
         if self.cfg.empty_cluster == "reseed":
             self._reseed()
         self.n_iter += 1
         return inertia
+
+    def _reduce_scatter_finalize(self):
+        """rsag mode: reduce-scatter the sums (rank r gets centroid rows [r0, r0 + kr)),
+        all-reduce the small count tail, finalise + operand-prep the own slice, all-gather
+        the assign operands (bf16/fp8 tables: 2-4x fewer bytes than the fp32 centroids;
+        an all-reduce moves the fp32 sums twice)."""
+        comm, k, kr, r0 = self.comm, self.k, self._kr, self._r0
+        comm.reduce_scatter_(self._rs_out.view(-1), self.buf[: self.kpad * self.d])
+        comm.allreduce_(self.small)
+        if self.nan_any:
+            self.counts.masked_fill_(self.empty_flags > 0, 0)
+        if self.shift is not None:
+            self.shift.zero_()
+        r1 = min(k, r0 + kr)
+        nv = max(0, r1 - r0)
+        self.local.finalize_rows(self._rs_out[:nv], self.counts[r0:r0 + nv],
+                                 self.C_pad[r0:r0 + nv], self.shift, r0, kr)
+        for t in self._gathered:
+            part = t[r0:r0 + kr].contiguous()
+            comm.all_gather_(t, part)
+        self._c_synced = self._gathered[0] is self.C_pad
+        if self.shift is not None:
+            comm.allreduce_(self.shift, "max")
 
     # ------------------------------------------------------------ HIP graph replay
     def graphable(self) -> bool:
@@ -241,6 +331,7 @@ class LloydEngine:
         empty = torch.nonzero(self.counts == 0).flatten().cpu().tolist()
         if not empty:
             return
+        self.centers()
         idx = floyd_sample(self.n_global, len(empty), self.cfg.seed + 7919 * (self.n_iter + 1))
         rows = init_centers_from_source("rows", self.source, self.row_offset, self.n_global,
                                         len(empty), self.comm, 0, rows=idx, d=self.d)
@@ -401,7 +492,7 @@ class KMeans:
 
         # ------------------------------------------------------------ timed loop
         history = []
-        centers_host = lambda: eng.C.double().cpu().numpy()
+        centers_host = lambda: eng.centers().double().cpu().numpy()
         timer = DeviceTimer(dev)
         timer.start()
         for _ in range(max(0, cfg.max_iter - start_iter)):
@@ -427,11 +518,11 @@ class KMeans:
         # ------------------------------------------- final label pass (untimed)
         inertia = eng.label_pass() if cfg.label_pass else None
         n_iter = eng.n_iter
-        cnt = eng.counts.double().cpu().numpy() if n_iter > 0 else None
+        cnt = eng.exact_counts().cpu().numpy() if n_iter > 0 else None
         self.engine_ = eng
         self.local_ = eng.local
         self.result_ = ClusterResult(
-            centers=eng.C.double().cpu().numpy(), init_centers=eng.c0.cpu().numpy(),
+            centers=eng.centers().double().cpu().numpy(), init_centers=eng.c0.cpu().numpy(),
             labels=eng.labels, counts=cnt, n_iter=n_iter, inertia=inertia,
             setup_time=setup_time, initialization_time=initialization_time,
             computation_time=computation_time, backend=eng.local.name, history=history,

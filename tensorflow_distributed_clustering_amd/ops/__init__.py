@@ -27,6 +27,7 @@ from typing import Optional
 import torch
 
 from .. import _native
+from ..parallel.dist import split_counts
 from . import reference as ref
 
 POLICY_CODES = {"keep": 0, "reseed": 0, "nan": 1, "nan_any": 1, "zero": 2}
@@ -132,18 +133,24 @@ class NativeUpdate:
                                     device=device)
 
     deterministic = False
+    # (hi, lo) fp32 [K] views of the all-reduce buffer: exact count halves
+    # (parallel/dist.split_counts), accumulated by the scan kernel of the sorted update
+    count_split = None
 
     def __call__(self, x, labels, sums, counts):
-        if self.deterministic:
-            deterministic_update(x, labels, sums, counts)
+        if self.deterministic or self.kind == "lds":
+            if self.deterministic:
+                deterministic_update(x, labels, sums, counts)
+            else:
+                self.ops.update(x, labels, sums, counts)
+            if self.count_split is not None:
+                split_counts(torch.bincount(labels[: x.shape[0]].long(), minlength=sums.shape[0]),
+                             *self.count_split)
             return
-        if self.kind == "lds":
-            self.ops.update(x, labels, sums, counts)
-        else:
-            if self.work.numel() < int(self.ops.update_sorted_workspace(x.shape[0], sums.shape[0])):
-                self.work = torch.empty(int(self.ops.update_sorted_workspace(x.shape[0], sums.shape[0])),
-                                        dtype=torch.int32, device=x.device)
-            self.ops.update_sorted(x, labels, sums, counts, self.work)
+        if self.work.numel() < int(self.ops.update_sorted_workspace(x.shape[0], sums.shape[0])):
+            self.work = torch.empty(int(self.ops.update_sorted_workspace(x.shape[0], sums.shape[0])),
+                                    dtype=torch.int32, device=x.device)
+        self.ops.update_sorted(x, labels, sums, counts, self.work, *(self.count_split or (None, None)))
 
 
     def supports_indexed(self) -> bool:
@@ -154,7 +161,8 @@ class NativeUpdate:
         need = int(self.ops.update_sorted_workspace(rowidx.shape[0], sums.shape[0]))
         if self.work is None or self.work.numel() < need:
             self.work = torch.empty(need, dtype=torch.int32, device=x.device)
-        self.ops.update_sorted_indexed(x, rowidx, labels, sums, counts, self.work)
+        self.ops.update_sorted_indexed(x, rowidx, labels, sums, counts, self.work,
+                                       *(self.count_split or (None, None)))
 
 
 def deterministic_update(x, labels, sums, counts):
@@ -210,6 +218,38 @@ class _LocalOpsBase:
         C.copy_(ref_new)
         self.prepare(C)
 
+    # ------------------------------------------ reduce-scatter / all-gather (rsag) mode
+    # centroid-row multiple the assign operands need (MFMA tiles)
+    row_align = 1
+
+    def pad_rows(self, kpad: int):
+        """Give the assign operands ``kpad`` centroid rows (rsag: one equal slice per rank)."""
+
+    def gather_operands(self):
+        """Tensors (dim 0 = centroid rows, ``kpad`` of them) the assignment reads; the
+        rsag engine all-gathers these after each rank prepped its slice.  None: the
+        assignment reads the fp32/fp64 centroids themselves."""
+        return None
+
+    def finalize_rows(self, sums, counts, C, shift, r0: int, kr: int):
+        """Finalize the centroid rows ``C`` (= rows [r0, r0 + len(C)) of the full table) and
+        prep operand rows [r0, r0 + kr) (rows past K become padding).  ``shift`` (if given)
+        is raised to this slice's max shift^2."""
+        if C.shape[0] == 0:
+            return
+        new = ref.finalize(sums, counts, C, self.empty_cluster)
+        if shift is not None:
+            d = new.double() - C.double()
+            shift.fill_(max(float(shift.max()), float((d * d).sum(1).max())))
+        C.copy_(new)
+
+    # ------------------------------------------------------------- exact counts
+    def supports_count_split(self) -> bool:
+        return isinstance(getattr(self, "update", None), NativeUpdate)
+
+    def set_count_split(self, hi, lo):
+        self.update.count_split = (hi, lo)
+
 
 class TorchLloyd(_LocalOpsBase):
     name = "torch"
@@ -221,6 +261,14 @@ class TorchLloyd(_LocalOpsBase):
         self.c_dtype = tdt
         self.exact = (dtype == "fp64") if exact is None else exact
 
+    count_split = None
+
+    def supports_count_split(self) -> bool:
+        return True
+
+    def set_count_split(self, hi, lo):
+        self.count_split = (hi, lo)
+
     def step(self, C, labels, mind, sums, counts):
         lab, md = ref.assign(self.x, C.to(self.x.dtype), exact=self.exact)
         labels.copy_(lab)
@@ -229,6 +277,8 @@ class TorchLloyd(_LocalOpsBase):
         s, c = ref.cluster_sums(self.x, lab, self.k, acc_dtype=sums.dtype)
         sums.add_(s)
         counts.add_(c)
+        if self.count_split is not None:
+            split_counts(torch.bincount(lab.long(), minlength=self.k), *self.count_split)
 
     def assign(self, C, labels, mind):
         lab, md = ref.assign(self.x, C.to(self.x.dtype), exact=self.exact)
@@ -316,6 +366,21 @@ class HipBf16Lloyd(_LocalOpsBase):
         """Native mini-batch centre update + next-assignment operand prep (one launch)."""
         self.ops.sculley_update(sums, counts, C, v, shift, self.cm2, self.cnorm)
 
+    row_align = 64
+
+    def pad_rows(self, kpad):
+        if kpad != self.kp:
+            self.kp = kpad
+            self.cm2 = torch.zeros(kpad, self.dp, dtype=torch.bfloat16, device=self.device)
+            self.cnorm = torch.zeros(kpad, dtype=torch.float32, device=self.device)
+
+    def gather_operands(self):
+        return [self.cm2, self.cnorm]
+
+    def finalize_rows(self, sums, counts, C, shift, r0, kr):
+        self.ops.finalize(sums, counts, C, self.policy, shift, self.cm2[r0:r0 + kr],
+                          self.cnorm[r0:r0 + kr])
+
 
 class _GroupedAssign:
     """Shared state of the K-grouped wide-D kernels: point norms + merge keys."""
@@ -392,6 +457,22 @@ class HipWideBf16Lloyd(_GroupedAssign, _LocalOpsBase):
 
     def finalize(self, sums, counts, C, shift):
         self.ops.finalize(sums, counts, C, self.policy, shift, self.cm2, self.cnorm)
+
+    row_align = 32
+
+    def pad_rows(self, kpad):
+        if kpad != self.kp:
+            self.kp = kpad
+            self.cm2 = torch.zeros(kpad, self.dp, dtype=torch.bfloat16, device=self.device)
+            self.cnorm = torch.zeros(kpad, dtype=torch.float32, device=self.device)
+            self.kg = kgroup_tiles(self._row_bytes, self.kp)
+
+    def gather_operands(self):
+        return [self.cm2, self.cnorm]
+
+    def finalize_rows(self, sums, counts, C, shift, r0, kr):
+        self.ops.finalize(sums, counts, C, self.policy, shift, self.cm2[r0:r0 + kr],
+                          self.cnorm[r0:r0 + kr])
 
 
 class HipFp8Lloyd(_GroupedAssign, _LocalOpsBase):
@@ -496,6 +577,25 @@ class HipFp8Lloyd(_GroupedAssign, _LocalOpsBase):
         self.ops.finalize(sums, counts, C, self.policy, shift, None, None)
         self.prepare(C)
 
+    row_align = 32
+
+    def pad_rows(self, kpad):
+        if kpad != self.kp:
+            dev = self.device
+            self.kp = kpad
+            self.cm2 = torch.zeros(kpad, self.dp, dtype=torch.float8_e4m3fn, device=dev)
+            self.cs = torch.zeros(kpad, self.dp // 32, dtype=torch.uint8, device=dev)
+            self.cnorm = torch.zeros(kpad, dtype=torch.float32, device=dev)
+            self.kg = kgroup_tiles(self._row_bytes, self.kp)
+
+    def gather_operands(self):
+        return [self.cm2, self.cs, self.cnorm]
+
+    def finalize_rows(self, sums, counts, C, shift, r0, kr):
+        self.ops.finalize(sums, counts, C, self.policy, shift, None, None)
+        self.ops.quant_fp8(C, C.shape[0], 1, self.cm2[r0:r0 + kr], self.cs[r0:r0 + kr],
+                           self.cnorm[r0:r0 + kr])
+
 
 class _HipExactBase(_LocalOpsBase):
     def __init__(self, x, k, dtype, empty_cluster):
@@ -509,9 +609,16 @@ class _HipExactBase(_LocalOpsBase):
     def finalize(self, sums, counts, C, shift):
         self.ops.finalize(sums, counts, C, self.policy, shift, None, None)
 
+    def finalize_rows(self, sums, counts, C, shift, r0, kr):
+        if C.shape[0]:
+            self.ops.finalize(sums, counts, C, self.policy, shift, None, None)
+
 
 class HipSmallLloyd(_HipExactBase):
     name = "hip_small_fused"
+
+    def supports_count_split(self) -> bool:
+        return False  # the fused kernel accumulates counts itself (fp64 buffers only)
 
     def step(self, C, labels, mind, sums, counts):
         self.ops.lloyd_small(self.x, C, labels, mind, sums, counts)

@@ -31,6 +31,24 @@ def shard_bounds(n: int, world: int, rank: int) -> Tuple[int, int]:
     return start, start + base + (1 if rank < extra else 0)
 
 
+# exact cluster counts through an fp32 all-reduce: count = SPLIT * hi + lo with lo < SPLIT;
+# both halves are integers below 2^24 per rank, so the fp32 sum over up to 4096 ranks is
+# exact and counts stay exact up to 2^36 (ClusterConfig buffers with fp32 partial sums)
+COUNT_SPLIT = 4096
+
+
+def split_counts(c: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor):
+    """hi += c // SPLIT, lo += c % SPLIT for integer-valued counts ``c`` (any dtype)."""
+    ci = c.to(torch.int64)
+    hi.add_(torch.div(ci, COUNT_SPLIT, rounding_mode="floor").to(hi.dtype))
+    lo.add_(torch.remainder(ci, COUNT_SPLIT).to(lo.dtype))
+
+
+def join_counts(hi: torch.Tensor, lo: torch.Tensor) -> torch.Tensor:
+    """Exact fp64 counts from the all-reduced halves."""
+    return hi.double() * COUNT_SPLIT + lo.double()
+
+
 def shard_sizes(n: int, world: int) -> List[int]:
     return [shard_bounds(n, world, r)[1] - shard_bounds(n, world, r)[0] for r in range(world)]
 
@@ -68,13 +86,16 @@ class Comm:
         return t
 
     def allreduce_bucketed_(self, flat: torch.Tensor, bucket_bytes: int = 0) -> torch.Tensor:
-        """SUM all-reduce of a flat buffer, optionally split into buckets.
+        """SUM all-reduce of a flat buffer, in one call or in ``bucket_bytes`` pieces.
 
-        xGMI is point-to-point (7 links x ~153 GB/s per MI355X): one large
-        ring all-reduce is per-link bound, so very large buffers (K=65536 x
-        D=768 partial sums ~ 201 MB) are issued as several async buckets that
-        RCCL can run on separate channels; small buffers (K=1024: ~0.5 MB) are
-        latency bound and go as ONE call.
+        One call is the default and the fast path: RCCL already stripes a single
+        all-reduce over its channels (one ring per xGMI link pair), so one call
+        uses all 7 links of an MI355X; calls on one communicator run one after
+        another on its stream, so buckets add a latency per call and never run
+        "on separate links".  Buckets only bound the size of each call (e.g. to
+        keep RCCL's staging buffers small next to a 201 MB K=65536 x D=768
+        buffer); the large-K*D bandwidth win is :meth:`reduce_scatter_` +
+        :meth:`all_gather_` (``ClusterConfig.comm_mode='rsag'``).
         """
         if self.world_size <= 1:
             return flat
@@ -83,11 +104,27 @@ class Comm:
             dist.all_reduce(flat, group=self.group)
             return flat
         per = max(1, bucket_bytes // flat.element_size())
-        works = [dist.all_reduce(flat[s:s + per], group=self.group, async_op=True)
-                 for s in range(0, flat.numel(), per)]
-        for w in works:
-            w.wait()
+        for s in range(0, flat.numel(), per):
+            dist.all_reduce(flat[s:s + per], group=self.group)
         return flat
+
+    def reduce_scatter_(self, out: torch.Tensor, flat: torch.Tensor) -> torch.Tensor:
+        """SUM reduce-scatter: rank r receives block r of ``flat`` (``flat.numel() ==
+        world * out.numel()``), summed over ranks."""
+        if self.world_size <= 1:
+            out.copy_(flat.view_as(out))
+            return out
+        dist.reduce_scatter_tensor(out, flat, group=self.group)
+        return out
+
+    def all_gather_(self, out: torch.Tensor, part: torch.Tensor) -> torch.Tensor:
+        """``out`` = concatenation over ranks of ``part`` (``out.numel() == world *
+        part.numel()``; ``part`` must not alias ``out``)."""
+        if self.world_size <= 1:
+            out.copy_(part.view_as(out))
+            return out
+        dist.all_gather_into_tensor(out, part, group=self.group)
+        return out
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.world_size > 1:

@@ -28,13 +28,19 @@ def _worker(rank, world, port, method, init, q, n, d, k, iters, seed, extra):
     comm = D.init_comm("cpu")
     s, e = comm.shard(n)
     x = gaussian_blobs(e - s, d, k, seed=seed, row_offset=s, dtype=torch.float64)
-    cfg = tdc.ClusterConfig(n_clusters=k, max_iter=iters, dtype="fp64", init=init, seed=seed, **extra)
+    kw = dict(n_clusters=k, max_iter=iters, dtype="fp64", init=init, seed=seed)
+    kw.update(extra)
+    cfg = tdc.ClusterConfig(**kw)
     model = (tdc.KMeans if method == "kmeans" else tdc.FuzzyCMeans)(cfg, comm)
     model.fit(x, n_global=n, row_offset=s)
     r = model.result_
     labels = comm.gather_rows_to_root(r.labels)
+    info = {}
+    eng = getattr(model, "engine_", None)
+    if eng is not None and hasattr(eng, "rsag"):
+        info = dict(rsag=eng.rsag, split=eng.count_split, counts=r.counts)
     if rank == 0:
-        q.put((r.centers, labels.numpy(), r.inertia, r.n_iter, r.init_centers))
+        q.put((r.centers, labels.numpy(), r.inertia, r.n_iter, r.init_centers, info))
     D.destroy_comm()
 
 
@@ -57,8 +63,8 @@ def run_world(world, method="kmeans", init="random", n=6001, d=3, k=5, iters=6, 
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("init", ["random", "kmeans++"])
 def test_kmeans_dp_equals_single(world, init):
-    c1, l1, in1, it1, i1 = run_world(1, init=init)
-    cw, lw, inw, itw, iw = run_world(world, init=init)
+    c1, l1, in1, it1, i1, _ = run_world(1, init=init)
+    cw, lw, inw, itw, iw, _ = run_world(world, init=init)
     np.testing.assert_array_equal(i1, iw)  # init is world-size invariant
     np.testing.assert_allclose(cw, c1, rtol=1e-12, atol=1e-12)
     np.testing.assert_array_equal(lw, l1)
@@ -67,8 +73,8 @@ def test_kmeans_dp_equals_single(world, init):
 
 
 def test_kmeans_parallel_init_world_invariant():
-    c1, l1, in1, it1, i1 = run_world(1, init="kmeans||", k=8)
-    c2, l2, in2, it2, i2 = run_world(2, init="kmeans||", k=8)
+    c1, l1, in1, it1, i1, _ = run_world(1, init="kmeans||", k=8)
+    c2, l2, in2, it2, i2, _ = run_world(2, init="kmeans||", k=8)
     np.testing.assert_allclose(i2, i1, rtol=1e-12, atol=1e-12)
     np.testing.assert_allclose(c2, c1, rtol=1e-10, atol=1e-10)
 
@@ -81,10 +87,85 @@ def test_fcm_dp_equals_single():
 
 
 def test_dp_tolerance_stop_consistent():
-    c1, _, _, it1, _ = run_world(1, iters=200, extra={"tol": 1e-10})
-    c2, _, _, it2, _ = run_world(2, iters=200, extra={"tol": 1e-10})
+    c1, _, _, it1, _, _ = run_world(1, iters=200, extra={"tol": 1e-10})
+    c2, _, _, it2, _, _ = run_world(2, iters=200, extra={"tol": 1e-10})
     assert it1 == it2 and it1 < 200
     np.testing.assert_allclose(c2, c1, rtol=1e-12, atol=1e-12)
+
+
+# ---------------------------------------------------------------- collective layer
+# every reduction branch of LloydEngine (SURVEY §5.8 / scripts/distribuitedClustering.py:
+# 139-148,253-263, the reference's CPU add_n): one all-reduce, forced-small buckets,
+# reduce-scatter -> sliced finalize -> all-gather (K not a multiple of the world size),
+# and the exact fp32 count halves -- each equal to the single-rank fit
+@pytest.mark.parametrize("world,extra", [
+    (2, {"comm_mode": "allreduce"}),
+    (3, {"comm_mode": "allreduce", "bucket_kb": 1}),
+    (2, {"comm_mode": "rsag"}),
+    (3, {"comm_mode": "rsag", "empty_cluster": "nan_any"}),
+    (4, {"comm_mode": "rsag", "tol": 1e-12, "log_every": 2}),
+])
+def test_reduction_modes_equal_single(world, extra):
+    kw = dict(k=7, d=5, iters=5)
+    c1, l1, in1, it1, _, _ = run_world(1, extra=extra, **kw)
+    cw, lw, inw, itw, _, info = run_world(world, extra=extra, **kw)
+    assert info["rsag"] == (extra["comm_mode"] == "rsag")
+    np.testing.assert_allclose(cw, c1, rtol=1e-12, atol=1e-12)
+    np.testing.assert_array_equal(lw, l1)
+    assert itw == it1
+
+
+@pytest.mark.parametrize("world,mode", [(1, "allreduce"), (2, "allreduce"), (3, "rsag")])
+def test_fp32_buffer_exact_counts(world, mode):
+    # K*(D+1) > 65536: fp32 partial sums, counts ride as exact integer halves
+    kw = dict(k=520, d=127, n=4001, iters=2)
+    c, lab, _, _, _, info = run_world(world, extra={"dtype": "fp32", "comm_mode": mode}, **kw)
+    assert info["split"] and info["rsag"] == (mode == "rsag")
+    # counts of the last update = histogram of the labels it assigned (the final label
+    # pass reassigns against the updated centroids, so compare totals only)
+    assert info["counts"].sum() == kw["n"]
+    assert np.all(info["counts"] == np.round(info["counts"]))
+    c1, *_ = run_world(1, extra={"dtype": "fp32"}, **kw)
+    np.testing.assert_allclose(c, c1, rtol=2e-5, atol=2e-5)
+
+
+def _count_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    from tensorflow_distributed_clustering_amd.parallel import dist as D
+    D._COMM = None
+    comm = D.init_comm("cpu")
+    # synthetic per-rank cluster counts far above 2^24 (a 2^31-row shard's worth)
+    c = torch.tensor([3 * 2 ** 24 + 12345 * rank + 7, 2 ** 31 - 1 - rank, 0, 1 + rank,
+                      2 ** 24 + 1], dtype=torch.int64)
+    hi = torch.zeros(5, dtype=torch.float32)
+    lo = torch.zeros(5, dtype=torch.float32)
+    D.split_counts(c, hi, lo)
+    buf = torch.cat([hi, lo])
+    comm.allreduce_bucketed_(buf, 8)  # 2-element buckets: also the bucketed branch
+    naive = c.to(torch.float32)
+    comm.allreduce_(naive)
+    q.put((rank, D.join_counts(buf[:5], buf[5:]).numpy(), naive.double().numpy()))
+    D.destroy_comm()
+
+
+def test_counts_above_2p24_exact_through_fp32_allreduce():
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_count_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (a, b)) for r, a, b in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    exact = sum(np.array([3 * 2 ** 24 + 12345 * r + 7, 2 ** 31 - 1 - r, 0, 1 + r, 2 ** 24 + 1],
+                         dtype=np.int64) for r in range(world))
+    for r in range(world):
+        np.testing.assert_array_equal(res[r][0], exact.astype(np.float64))
+    assert not np.array_equal(res[0][1], exact.astype(np.float64))  # plain fp32 is not exact
 
 
 def _split_worker(rank, world, port, policy, q):

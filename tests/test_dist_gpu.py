@@ -21,7 +21,8 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q, dtype, n, d, k, iters, method, algorithm="lloyd"):
+def _worker(rank, world, port, q, dtype, n, d, k, iters, method, algorithm="lloyd",
+            comm_mode="auto"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
                       RANK=str(rank), LOCAL_RANK=str(rank), TDC_DIST_BACKEND="gloo")
     import tensorflow_distributed_clustering_amd as tdc
@@ -30,25 +31,31 @@ def _worker(rank, world, port, q, dtype, n, d, k, iters, method, algorithm="lloy
     D._COMM = None
     comm = D.init_comm("cuda")
     s, e = comm.shard(n)
-    tdt = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp64": torch.float64}[dtype]
+    tdt = {"bf16": torch.bfloat16, "fp8": torch.bfloat16, "fp32": torch.float32,
+           "fp64": torch.float64}[dtype]
     x = gaussian_blobs(e - s, d, k, seed=3, row_offset=s, dtype=tdt, device=comm.device)
     cfg = tdc.ClusterConfig(n_clusters=k, max_iter=iters, dtype=dtype, init="random", seed=3,
-                            algorithm=algorithm)
+                            algorithm=algorithm, comm_mode=comm_mode)
     model = (tdc.KMeans if method == "kmeans" else tdc.FuzzyCMeans)(cfg, comm)
     model.fit(x, n_global=n, row_offset=s)
     r = model.result_
     labels = comm.gather_rows_to_root(torch.as_tensor(r.labels, device=comm.device))
+    eng = model.engine_
+    info = dict(rsag=getattr(eng, "rsag", False), split=getattr(eng, "count_split", False),
+                counts=r.counts)
     if rank == 0:
-        q.put((np.asarray(r.centers), labels.cpu().numpy(), r.backend))
+        q.put((np.asarray(r.centers), labels.cpu().numpy(), r.backend, info))
     D.destroy_comm()
 
 
-def _run(world, dtype, n, d, k, iters=4, method="kmeans", algorithm="lloyd"):
+def _run(world, dtype, n, d, k, iters=4, method="kmeans", algorithm="lloyd", comm_mode="auto",
+         full=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker,
-                         args=(r, world, port, q, dtype, n, d, k, iters, method, algorithm))
+                         args=(r, world, port, q, dtype, n, d, k, iters, method, algorithm,
+                               comm_mode))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -56,7 +63,25 @@ def _run(world, dtype, n, d, k, iters=4, method="kmeans", algorithm="lloyd"):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    return out
+    return out if full else out[:3]
+
+
+@pytest.mark.parametrize("world,dtype,d,k", [(2, "bf16", 128, 1000), (3, "bf16", 128, 1000),
+                                             (2, "fp8", 256, 500), (2, "fp32", 96, 700)])
+def test_rsag_matches_one_rank(gpu, world, dtype, d, k):
+    """comm_mode='rsag': reduce-scatter of the fp32 sums, each rank finalises + preps the
+    operand rows of its K/G slice, all-gather of the bf16/fp8 operand tables (fp32 path:
+    the centroids); K is not a multiple of 64 x G, so the padded tail slice is covered.
+    The fp32 buffers also carry the exact count halves."""
+    n = 120_001
+    c1, l1, b1, i1 = _run(1, dtype, n, d, k, full=True)
+    c2, l2, b2, i2 = _run(world, dtype, n, d, k, comm_mode="rsag", full=True)
+    assert b1 == b2 and i2["rsag"] and not i1["rsag"]
+    assert i1["split"] and i2["split"]
+    assert i2["counts"].sum() == n and np.all(i2["counts"] == np.round(i2["counts"]))
+    tol = 1e-4 if dtype == "fp32" else 2e-3
+    np.testing.assert_allclose(c2, c1, rtol=tol, atol=tol)
+    assert (l1 == l2).mean() > 0.995
 
 
 def test_bf16_mfma_two_ranks_match_one(gpu):
