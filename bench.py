@@ -49,6 +49,10 @@ PRESETS = {
                        dtype="fp64", method="fcm"),
     "embed50m_fp8": dict(n_per_gpu=50_000_000, dim=768, k=65536, scaling="strong", mode="lloyd",
                          dtype="fp8"),
+    # FCM at the headline shape (fp32 memberships, m = 2; the reference's m = D = 128 would
+    # underflow every u^m)
+    "fcm10m": dict(n_per_gpu=10_000_000, dim=128, k=1024, scaling="weak", mode="lloyd",
+                   dtype="fp32", method="fcm", fuzzifier=2.0),
 }
 
 
@@ -71,6 +75,8 @@ def parse(argv=None):
     ap.add_argument("--batch-size", type=int, default=0, help="mini-batch rows per rank")
     ap.add_argument("--method", default="kmeans", choices=["kmeans", "fcm"],
                     help="fcm: distributed Fuzzy C-Means step (fuzzifier m = D, as the reference)")
+    ap.add_argument("--fuzzifier", type=float, default=None,
+                    help="FCM fuzzifier m (default: the reference's m = D)")
     ap.add_argument("--algorithm", default="lloyd", choices=["lloyd", "bounded"],
                     help="bounded: Lloyd with Hamerly bounds (not the headline metric's "
                          "algorithm; reported in config.algorithm)")
@@ -116,7 +122,8 @@ def main(argv=None):
           "fp64": torch.float64}[a.dtype]
     x = gaussian_blobs(e - s, a.dim, a.k, seed=a.seed, row_offset=s, dtype=dt, device=dev)
     cfg = tdc.ClusterConfig(n_clusters=a.k, max_iter=a.steps, dtype=a.dtype, init="random",
-                            seed=a.seed, compute_inertia=False, algorithm=a.algorithm)
+                            seed=a.seed, compute_inertia=False, algorithm=a.algorithm,
+                            fuzzifier=a.fuzzifier)
     if a.mode == "minibatch":
         from tensorflow_distributed_clustering_amd.models.minibatch import MiniBatchStepper
         eng = MiniBatchStepper(x, cfg.replace(batch_size=a.batch_size or (1 << 20)), comm,
@@ -183,6 +190,8 @@ def main(argv=None):
             out["phase_ms"] = breakdown
         if a.algorithm != "lloyd":
             out["config"]["algorithm"] = a.algorithm
+        if a.method == "fcm":
+            out["config"]["fuzzifier"] = a.fuzzifier if a.fuzzifier is not None else a.dim
             out["active_frac_last_step"] = getattr(eng, "active_frac", None)
         print(json.dumps(out), flush=True)
 

@@ -201,6 +201,139 @@ void fcm_small(const at::Tensor& X, const at::Tensor& C, double m, bool nan_to_z
         "fcm_small");
 }
 
+void fcm_tower_stats(const at::Tensor& X, const at::Tensor& C, double m, bool nan_to_zero,
+                     at::Tensor& labels, at::Tensor& rowinfo) {
+  check_cuda(X, "X");
+  check_rows(X, "X");
+  TORCH_CHECK(X.scalar_type() == at::kFloat || X.scalar_type() == at::kDouble,
+              "tdc.fcm_tower_stats: X fp32/fp64");
+  TORCH_CHECK(C.scalar_type() == X.scalar_type() && C.is_contiguous() && C.dim() == 2 &&
+                  C.size(1) == X.size(1), "tdc.fcm_tower_stats: C [K, D] in the X dtype");
+  TORCH_CHECK(X.size(1) >= 1 && X.size(1) <= 256, "tdc.fcm_tower_stats: D must be 1..256");
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous() && labels.numel() >= X.size(0),
+              "tdc.fcm_tower_stats: labels int32 [N]");
+  TORCH_CHECK(rowinfo.scalar_type() == X.scalar_type() && rowinfo.is_contiguous() &&
+                  rowinfo.numel() >= X.size(0), "tdc.fcm_tower_stats: rowinfo [N] in the X dtype");
+  TORCH_CHECK(m > 1.0, "tdc.fcm_tower_stats: fuzzifier must be > 1");
+  const DevGuard guard(X.device());
+  check(tdc_fcm_tower(0, dcode(X.scalar_type()), X.data_ptr(), X.size(0), X.stride(0),
+                      (int)X.size(1), C.data_ptr(), (int)C.size(0), m, nan_to_zero ? 1 : 0,
+                      labels.data_ptr<int32_t>(), rowinfo.data_ptr(), nullptr, nullptr,
+                      num_cus(X.device().index()), cur_stream()),
+        "fcm_tower_stats");
+}
+
+void fcm_tower_accum(const at::Tensor& X, const at::Tensor& C, double m, bool nan_to_zero,
+                     const at::Tensor& rowinfo, at::Tensor& wx, at::Tensor& ws) {
+  check_cuda(X, "X");
+  check_rows(X, "X");
+  TORCH_CHECK(X.scalar_type() == at::kFloat || X.scalar_type() == at::kDouble,
+              "tdc.fcm_tower_accum: X fp32/fp64");
+  TORCH_CHECK(C.scalar_type() == X.scalar_type() && C.is_contiguous() && C.dim() == 2 &&
+                  C.size(1) == X.size(1), "tdc.fcm_tower_accum: C [K, D] in the X dtype");
+  TORCH_CHECK(X.size(1) >= 1 && X.size(1) <= 256, "tdc.fcm_tower_accum: D must be 1..256");
+  TORCH_CHECK(rowinfo.scalar_type() == X.scalar_type() && rowinfo.is_contiguous() &&
+                  rowinfo.numel() >= X.size(0), "tdc.fcm_tower_accum: rowinfo [N]");
+  TORCH_CHECK(wx.scalar_type() == at::kDouble && ws.scalar_type() == at::kDouble &&
+                  wx.is_contiguous() && ws.is_contiguous() && wx.numel() == C.numel() &&
+                  ws.numel() == C.size(0), "tdc.fcm_tower_accum: wx [K, D] / ws [K] fp64");
+  TORCH_CHECK(m > 1.0, "tdc.fcm_tower_accum: fuzzifier must be > 1");
+  const DevGuard guard(X.device());
+  check(tdc_fcm_tower(1, dcode(X.scalar_type()), X.data_ptr(), X.size(0), X.stride(0),
+                      (int)X.size(1), C.data_ptr(), (int)C.size(0), m, nan_to_zero ? 1 : 0,
+                      nullptr, const_cast<void*>(rowinfo.data_ptr()), wx.data_ptr(), ws.data_ptr(),
+                      num_cus(X.device().index()), cur_stream()),
+        "fcm_tower_accum");
+}
+
+void fcm_split_rows(const at::Tensor& src, int64_t valid, int64_t neg2, at::Tensor& hi,
+                    at::Tensor& lo, const std::optional<at::Tensor>& norm) {
+  check_cuda(src, "src");
+  TORCH_CHECK(src.scalar_type() == at::kFloat && src.dim() == 2 && src.stride(1) == 1,
+              "tdc.fcm_split_rows: src fp32 rows");
+  TORCH_CHECK(hi.scalar_type() == at::kBFloat16 && lo.scalar_type() == at::kBFloat16 &&
+                  hi.is_contiguous() && lo.is_contiguous() && hi.dim() == 2 &&
+                  hi.sizes() == lo.sizes(), "tdc.fcm_split_rows: hi/lo bf16 [rows, DP]");
+  const int64_t rows = hi.size(0);
+  const int DP = (int)hi.size(1);
+  TORCH_CHECK(src.size(1) <= DP && valid <= rows && valid <= src.size(0),
+              "tdc.fcm_split_rows: shapes");
+  if (norm.has_value() && norm->defined())
+    TORCH_CHECK(norm->scalar_type() == at::kFloat && norm->is_contiguous() && norm->numel() >= rows,
+                "tdc.fcm_split_rows: norm fp32 [rows]");
+  const DevGuard guard(src.device());
+  check(tdc_fcm_split_rows(src.data_ptr<float>(), rows, valid, (int)src.size(1), src.stride(0), DP,
+                           (int)neg2, hi.data_ptr(), lo.data_ptr(),
+                           static_cast<float*>(opt_ptr(norm)), cur_stream()),
+        "fcm_split_rows");
+}
+
+void check_mfma_fcm(const at::Tensor& Xh, const at::Tensor& Xl, const at::Tensor& xx,
+                    const at::Tensor& Ch, const at::Tensor& Cl, const at::Tensor& cc, int64_t K,
+                    double m, const char* op) {
+  check_cuda(Xh, "Xh");
+  for (const at::Tensor* t : {&Xh, &Xl, &Ch, &Cl})
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->is_contiguous() && t->dim() == 2,
+                "tdc.", op, ": hi/lo operands must be contiguous bf16 [rows, DP]");
+  const int64_t DP = Xh.size(1);
+  TORCH_CHECK(DP == 32 || DP == 64 || DP == 128, "tdc.", op, ": DP must be 32/64/128");
+  TORCH_CHECK(Xl.sizes() == Xh.sizes() && Ch.size(1) == DP && Cl.sizes() == Ch.sizes(),
+              "tdc.", op, ": operand shapes");
+  TORCH_CHECK(Ch.size(0) % 128 == 0 && Ch.size(0) >= K && K > 0, "tdc.", op, ": Kp % 128, Kp >= K");
+  TORCH_CHECK(xx.scalar_type() == at::kFloat && xx.is_contiguous() && xx.numel() >= Xh.size(0),
+              "tdc.", op, ": xx fp32 [N]");
+  TORCH_CHECK(cc.scalar_type() == at::kFloat && cc.is_contiguous() && cc.numel() >= Ch.size(0),
+              "tdc.", op, ": cc fp32 [Kp]");
+  TORCH_CHECK(m > 1.0, "tdc.", op, ": fuzzifier must be > 1");
+}
+
+void fcm_mfma_stats(const at::Tensor& Xh, const at::Tensor& Xl, const at::Tensor& xx,
+                    const at::Tensor& Ch, const at::Tensor& Cl, const at::Tensor& cc, int64_t K,
+                    double m, bool nan_to_zero, at::Tensor& labels, at::Tensor& rowinfo) {
+  check_mfma_fcm(Xh, Xl, xx, Ch, Cl, cc, K, m, "fcm_mfma_stats");
+  const int64_t N = Xh.size(0);
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous() && labels.numel() >= N,
+              "tdc.fcm_mfma_stats: labels int32 [N]");
+  TORCH_CHECK(rowinfo.scalar_type() == at::kFloat && rowinfo.is_contiguous() && rowinfo.numel() >= N,
+              "tdc.fcm_mfma_stats: rowinfo fp32 [N]");
+  const DevGuard guard(Xh.device());
+  check(tdc_fcm_mfma(0, Xh.data_ptr(), Xl.data_ptr(), xx.data_ptr<float>(), N, (int)Xh.size(1), 0,
+                     Ch.data_ptr(), Cl.data_ptr(), cc.data_ptr<float>(), (int)K, (int)Ch.size(0),
+                     m, nan_to_zero ? 1 : 0, labels.data_ptr<int32_t>(), rowinfo.data_ptr<float>(),
+                     nullptr, nullptr, nullptr, num_cus(Xh.device().index()), cur_stream()),
+        "fcm_mfma_stats");
+}
+
+void fcm_mfma_accum(const at::Tensor& Xh, const at::Tensor& Xl, const at::Tensor& xx,
+                    const at::Tensor& rowinfo, const at::Tensor& Ch, const at::Tensor& Cl,
+                    const at::Tensor& cc, int64_t K, double m, bool nan_to_zero, at::Tensor& wx,
+                    at::Tensor& ws, at::Tensor& work) {
+  check_mfma_fcm(Xh, Xl, xx, Ch, Cl, cc, K, m, "fcm_mfma_accum");
+  const int nc = num_cus(Xh.device().index());
+  TORCH_CHECK(work.scalar_type() == at::kFloat && work.is_contiguous() &&
+                  work.numel() >= tdc_fcm_mfma_workspace(Xh.size(0), (int)K, (int)Ch.size(0),
+                                                         (int)Xh.size(1), nc),
+              "tdc.fcm_mfma_accum: work fp32 [fcm_mfma_workspace(...)]");
+  const int64_t N = Xh.size(0);
+  TORCH_CHECK(rowinfo.scalar_type() == at::kFloat && rowinfo.is_contiguous() && rowinfo.numel() >= N,
+              "tdc.fcm_mfma_accum: rowinfo fp32 [N]");
+  TORCH_CHECK(wx.scalar_type() == at::kDouble && ws.scalar_type() == at::kDouble &&
+                  wx.is_contiguous() && ws.is_contiguous() && wx.dim() == 2 && wx.size(0) == K &&
+                  wx.size(1) <= Xh.size(1) && ws.numel() == K,
+              "tdc.fcm_mfma_accum: wx [K, D] / ws [K] fp64");
+  const DevGuard guard(Xh.device());
+  check(tdc_fcm_mfma(1, Xh.data_ptr(), Xl.data_ptr(), xx.data_ptr<float>(), N, (int)Xh.size(1),
+                     (int)wx.size(1), Ch.data_ptr(), Cl.data_ptr(), cc.data_ptr<float>(), (int)K,
+                     (int)Ch.size(0), m, nan_to_zero ? 1 : 0, nullptr,
+                     const_cast<float*>(rowinfo.data_ptr<float>()), wx.data_ptr<double>(),
+                     ws.data_ptr<double>(), work.data_ptr<float>(), nc, cur_stream()),
+        "fcm_mfma_accum");
+}
+
+int64_t fcm_mfma_workspace(const at::Tensor& like, int64_t N, int64_t K, int64_t Kp, int64_t DP) {
+  return tdc_fcm_mfma_workspace(N, (int)K, (int)Kp, (int)DP, num_cus(like.device().index()));
+}
+
 void fcm_rows(at::Tensor& G, const at::Tensor& xx, const std::optional<at::Tensor>& cc, double m,
               bool nan_to_zero, at::Tensor& labels, const std::optional<at::Tensor>& colsum) {
   check_cuda(G, "G");
@@ -604,6 +737,12 @@ TORCH_LIBRARY(tdc, m) {
   m.def("update_sorted(Tensor X, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work, Tensor(d!)? cnt_hi=None, Tensor(e!)? cnt_lo=None) -> ()");
   m.def("fcm_small_supported(ScalarType dtype, int K, int D) -> bool", &fcm_small_supported);
   m.def("fcm_small(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) wx, Tensor(c!) ws) -> ()");
+  m.def("fcm_tower_stats(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) rowinfo) -> ()");
+  m.def("fcm_tower_accum(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor rowinfo, Tensor(a!) wx, Tensor(b!) ws) -> ()");
+  m.def("fcm_split_rows(Tensor src, int valid, int neg2, Tensor(a!) hi, Tensor(b!) lo, Tensor(c!)? norm) -> ()");
+  m.def("fcm_mfma_stats(Tensor Xh, Tensor Xl, Tensor xx, Tensor Ch, Tensor Cl, Tensor cc, int K, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) rowinfo) -> ()");
+  m.def("fcm_mfma_accum(Tensor Xh, Tensor Xl, Tensor xx, Tensor rowinfo, Tensor Ch, Tensor Cl, Tensor cc, int K, float m, bool nan_to_zero, Tensor(a!) wx, Tensor(b!) ws, Tensor(c!) work) -> ()");
+  m.def("fcm_mfma_workspace(Tensor like, int N, int K, int Kp, int DP) -> int");
   m.def("fcm_rows(Tensor(a!) G, Tensor xx, Tensor? cc, float m, bool nan_to_zero, Tensor(b!) labels, Tensor(c!)? colsum=None) -> ()");
   m.def("assign_bigd_supported(ScalarType dtype, int DP) -> bool", &assign_bigd_supported);
   m.def("assign_bigd(Tensor X, Tensor? Xs, Tensor xnorm, Tensor Cm2, Tensor? Cs, Tensor cnorm, int kg_tiles, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!)? keys, Tensor(d!)? labels2=None, Tensor(e!)? mind2=None) -> ()");
@@ -627,6 +766,12 @@ TORCH_LIBRARY_IMPL(tdc, CUDA, m) {
   m.impl("update_sorted", &update_sorted);
   m.impl("fcm_small", &fcm_small);
   m.impl("fcm_rows", &fcm_rows);
+  m.impl("fcm_tower_stats", &fcm_tower_stats);
+  m.impl("fcm_split_rows", &fcm_split_rows);
+  m.impl("fcm_mfma_stats", &fcm_mfma_stats);
+  m.impl("fcm_mfma_accum", &fcm_mfma_accum);
+  m.impl("fcm_mfma_workspace", &fcm_mfma_workspace);
+  m.impl("fcm_tower_accum", &fcm_tower_accum);
   m.impl("finalize", &finalize);
   m.impl("assign_bigd", &assign_bigd);
   m.impl("recheck_top2", &recheck_top2);

@@ -16,41 +16,9 @@
 // membership everywhere, :125-126); 0 gives the correct one-hot membership.
 #include "tdc_common.h"
 #include "kernels.h"
+#include "fcm_math.h"
 
 namespace tdc {
-
-__device__ __forceinline__ float tdc_exp2(float v) { return exp2f(v); }
-__device__ __forceinline__ double tdc_exp2(double v) { return exp2(v); }
-__device__ __forceinline__ float tdc_log2(float v) { return log2f(v); }
-__device__ __forceinline__ double tdc_log2(double v) { return log2(v); }
-
-// t = (d^2)^expo, expo = -1/(m-1).  pmode picks a transcendental-free form for the common
-// fuzzifiers: 1: m=2 (1/d2), 2: m=3 (1/sqrt d2), 3: m=5 (the reference's m = D = 5:
-// 1/sqrt(sqrt d2)); 0: exp2(expo * log2 d2).
-template <typename T>
-__device__ __forceinline__ T fcm_t(T dd, T expo, int pmode) {
-  switch (pmode) {
-    case 1: return (T)1 / dd;
-    case 2: return rsqrt(dd);          // one rsqrt instead of sqrt + divide
-    case 3: return rsqrt(sqrt(dd));
-    default: return tdc_exp2(tdc_log2(dd) * expo);
-  }
-}
-// w = u^m: binary powering for integer m in [1, 16] (mint), else exp2(m log2 u)
-template <typename T>
-__device__ __forceinline__ T fcm_w(T u, T m, int mint) {
-  if (mint > 0) {
-    T r = (mint & 1) ? u : (T)1;
-    T b = u;
-#pragma unroll
-    for (int e = mint >> 1; e > 0; e >>= 1) {
-      b = b * b;
-      if (e & 1) r = r * b;
-    }
-    return r;
-  }
-  return u > (T)0 ? tdc_exp2(m * tdc_log2(u)) : (T)0;
-}
 
 template <typename T, typename ACC, int KMAX, int DMAX>
 __global__ __launch_bounds__(256) void fcm_small_kernel(

@@ -1,0 +1,603 @@
+// N4/N5 on MFMA: the Fuzzy C-Means tower for large K x D in fp32, on bf16 matrix cores.
+//
+// Reference per GPU per iteration (scripts/distribuitedClustering.py:108-137): [N,K,D]
+// difference tiles -> d -> t = d^(-2/(m-1)) -> u = t / sum_k t -> NaN -> 0 -> W = u^m ->
+// MatMul(W, X) (cuBLAS DGEMM) and Sum(W).  Both matrix products run here on
+// v_mfma_f32_32x32x16_bf16 with fp32-grade operands from a hi/lo bf16 split
+// (x = xh + xl, -2c = ch + cl, each lo = bf16(v - hi)):
+//   x.(-2c) ~= xh.ch + xh.cl + xl.ch      (three MFMAs; the dropped xl.cl is 2^-16 relative)
+//   sum_i w_ik x_i = W^T Xh + W^T Xl      (W = u^m rounded to bf16; sum_i w_ik from the same
+//                                          rounded w, so each centroid is an exact convex
+//                                          combination of its weights)
+// Two kernels, like fcm_tower.hip:
+//   fcm_mfma_stats: 4 waves x 2 tiles of 32 points; the hi/lo point fragments stay in VGPRs,
+//     64-centroid hi/lo stages stream through LDS; per point sum_k t, the zero-distance
+//     count and argmin d2 -> rowinfo (see fcm_tower.hip) and the label.
+//   fcm_mfma_accum: block = 128 centroids (32 per wave, hi/lo fragments in VGPRs) x a row
+//     range.  64-point hi/lo X tiles are staged in LDS once and read twice: by rows (the
+//     distance A operand) and transposed with ds_read_b64_tr_b16 (the W^T X B operand).
+//     The distance accumulator (rows = points, lane = centroid) becomes the A operand of
+//     W^T X without leaving registers (cdna_hip_programming.md "An accumulator tile as
+//     the next MFMA's operand").  The [32 x D] W^T X tile of each wave lives in fp32
+//     accumulators for the whole row range and is flushed once (fp64 atomics).
+//     Blocks are mapped so that the K tiles of one row range run on the same XCD and
+//     share its L2 copy of the X tile.
+// Distances within 2^-14 (||x||^2 + ||c||^2) of zero count as zero (the bf16x3 noise
+// floor): a point on a centroid keeps the reference's NaN -> 0 semantics.
+#include "tdc_common.h"
+#include "kernels.h"
+#include "fcm_math.h"
+
+namespace tdc {
+namespace {
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr float ZERO_FLOOR = 6.103515625e-05f;  // 2^-14
+
+struct MParam {
+  float expo, m;
+  int pmode, mint, nz;
+};
+
+// 16-byte chunk c of row r of a [rows][DP] bf16 LDS image, XOR-swizzled so that both the
+// row reads (lane = row) and the transposed reads spread over the banks (guide T10 (b)).
+template <int DP>
+__device__ __forceinline__ int xoff(int r, int c) {
+  constexpr int CPR = DP / 8;
+  const int sw = (((r & 3) << 2) | ((r >> 2) & 3)) & (CPR - 1);
+  return r * DP * 2 + 16 * (c ^ sw);
+}
+
+// centroid stage image: same swizzle as the Lloyd kernels (rows of DP bf16)
+template <int DP>
+__device__ __forceinline__ int coff(int r, int c) {
+  constexpr int CPR = DP / 8;
+  constexpr int G = CPR < 16 ? CPR : 16;
+  constexpr int RPB = 16 / G;
+  return r * DP * 2 + 16 * (c ^ ((r / RPB) & (G - 1)));
+}
+
+__device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) {
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// Membership arithmetic specialised at compile time (a runtime fuzzifier switch inside the
+// unrolled epilogues quadrupled the code and thrashed the instruction cache):
+//   MODE 2: m = 2  -> t = 1/d2 (v_rcp_f32), w = u*u
+//   MODE 0: any m  -> t = 2^(expo log2 d2), w = 2^(m log2 u)
+template <int MODE>
+__device__ __forceinline__ float mt(float d2, float expo) {
+  if constexpr (MODE == 2) return __builtin_amdgcn_rcpf(d2);  // rcp(0) = +inf
+  else return __builtin_amdgcn_exp2f(expo * __builtin_amdgcn_logf(d2));  // log2(0) = -inf
+}
+template <int MODE>
+__device__ __forceinline__ float mw(float u, float m) {
+  if constexpr (MODE == 2) return u * u;
+  else return u > 0.f ? __builtin_amdgcn_exp2f(m * __builtin_amdgcn_logf(u)) : 0.f;
+}
+
+#define TDC_GLOAD16(dst, src) \
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst) : "v"(src) : "memory")
+
+// ---------------------------------------------------------------------------------------
+// pass 1: per-row statistics
+// ---------------------------------------------------------------------------------------
+template <int DP, int MODE>
+__global__ __launch_bounds__(256, 1) void fcm_mfma_stats_kernel(
+    const __bf16* __restrict__ Xh, const __bf16* __restrict__ Xl, const float* __restrict__ xx,
+    int64_t N, const __bf16* __restrict__ Ch, const __bf16* __restrict__ Cl,
+    const float* __restrict__ cc, int K, int nstages, MParam prm, int32_t* __restrict__ labels,
+    float* __restrict__ rowinfo) {
+  constexpr int P = 2;
+  constexpr int BN = 64;
+  constexpr int CPR = DP / 8;
+  constexpr int KS = DP / 16;
+  constexpr int HALF = DP / 2;
+  constexpr int IMGB = BN * DP * 2;           // bytes of one (hi or lo) stage image
+  constexpr int CHUNKS = 2 * BN * CPR;        // 16-byte chunks per stage
+  constexpr int CPT = CHUNKS / 256;
+  static_assert(CHUNKS % 256 == 0, "stage chunks must split over 256 threads");
+  __shared__ __attribute__((aligned(16))) char s_c[2][2 * IMGB];
+  __shared__ __attribute__((aligned(16))) float s_n[2][BN];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t pbase = (int64_t)blockIdx.x * (4 * P * 32) + (int64_t)w * (P * 32);
+
+  bf16x8 bh[P][KS], bl[P][KS];
+  float xn[P], zf[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    int64_t row = pbase + p * 32 + r;
+    if (row >= N) row = N - 1;
+    const bf16x8* sh = reinterpret_cast<const bf16x8*>(Xh + row * DP + h * HALF);
+    const bf16x8* sl = reinterpret_cast<const bf16x8*>(Xl + row * DP + h * HALF);
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      bh[p][kk] = sh[kk];
+      bl[p][kk] = sl[kk];
+    }
+    xn[p] = xx[row];
+    zf[p] = ZERO_FLOOR * xn[p];
+  }
+
+  // stage t: chunk q of the thread -> (hi/lo, row, chunk) -> swizzled LDS slot
+  uint4 pre[CPT];
+  float npre = 0.f;
+#define TDC_STAGE_LOAD(T_)                                                                \
+  {                                                                                       \
+    _Pragma("unroll") for (int i = 0; i < CPT; ++i) {                                     \
+      const int q = tid + i * 256;                                                        \
+      const int hl = q / (BN * CPR), rem = q % (BN * CPR);                                \
+      const __bf16* src = (hl ? Cl : Ch) + ((int64_t)(T_) * BN + rem / CPR) * DP + (rem % CPR) * 8; \
+      TDC_GLOAD16(pre[i], src);                                                           \
+    }                                                                                     \
+    if (tid < BN) npre = cc[(T_) * BN + tid];                                             \
+  }
+#define TDC_STAGE_STORE(B_)                                                               \
+  {                                                                                       \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                      \
+    _Pragma("unroll") for (int i = 0; i < CPT; ++i) {                                     \
+      const int q = tid + i * 256;                                                        \
+      const int hl = q / (BN * CPR), rem = q % (BN * CPR);                                \
+      *reinterpret_cast<uint4*>(&s_c[B_][hl * IMGB + coff<DP>(rem / CPR, rem % CPR)]) = pre[i]; \
+    }                                                                                     \
+    if (tid < BN) s_n[B_][tid] = npre;                                                    \
+  }
+  TDC_STAGE_LOAD(0)
+  TDC_STAGE_STORE(0)
+  __syncthreads();
+
+  float S[P], best[P];
+  int bt[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    S[p] = 0.f;
+    best[p] = INFINITY;
+    bt[p] = 0;
+  }
+
+  for (int t = 0; t < nstages; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nstages) TDC_STAGE_LOAD(t + 1)
+    const char* cb = s_c[buf];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int row = q * 32 + r;
+      f32x16 acc[P];
+      f32x16 init;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const f32x4 n4 = *reinterpret_cast<const f32x4*>(&s_n[buf][q * 32 + 8 * g4 + 4 * h]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) init[4 * g4 + e] = n4[e];
+      }
+      bf16x8 ah = as_bf16x8(*reinterpret_cast<const uint4*>(cb + coff<DP>(row, h * (CPR / 2))));
+      bf16x8 al = as_bf16x8(*reinterpret_cast<const uint4*>(cb + IMGB + coff<DP>(row, h * (CPR / 2))));
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        const int kn = kk + 1 < KS ? kk + 1 : kk;
+        const bf16x8 ahn = as_bf16x8(*reinterpret_cast<const uint4*>(cb + coff<DP>(row, h * (CPR / 2) + kn)));
+        const bf16x8 aln = as_bf16x8(*reinterpret_cast<const uint4*>(cb + IMGB + coff<DP>(row, h * (CPR / 2) + kn)));
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+          acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[p][kk], kk == 0 ? init : acc[p], 0, 0, 0);
+          acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[p][kk], acc[p], 0, 0, 0);
+          acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[p][kk], acc[p], 0, 0, 0);
+        }
+        ah = ahn;
+        al = aln;
+      }
+      // epilogue: register i = centroid (i&3)+8(i>>2)+4h of this 32-tile (ascending in i).
+      // d2 is clamped at the zero floor zf (t stays finite; a row whose min d2 <= zf is
+      // "on a centroid", decided at the end); pad centroids (last stage only) are masked.
+      const int kvalid = K - (t * BN + q * 32 + 4 * h);
+      if (kvalid >= 28) {  // every centroid of this lane's 16 rows exists
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+          float mpk = INFINITY, sp = 0.f;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float d2 = fmaxf(acc[p][i] + xn[p], zf[p]);
+            sp += mt<MODE>(d2, prm.expo);
+            mpk = __builtin_fminf(mpk, __uint_as_float((__float_as_uint(d2) & ~15u) | (unsigned)i));
+          }
+          S[p] += sp;
+          const bool up = mpk < best[p];
+          best[p] = up ? mpk : best[p];
+          bt[p] = up ? (2 * t + q) : bt[p];
+        }
+      } else {
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+          float mpk = INFINITY, sp = 0.f;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const bool v = (i & 3) + 8 * (i >> 2) < kvalid;
+            const float d2 = fmaxf(acc[p][i] + xn[p], zf[p]);
+            sp += v ? mt<MODE>(d2, prm.expo) : 0.f;
+            const float pk = __uint_as_float((__float_as_uint(d2) & ~15u) | (unsigned)i);
+            mpk = v ? __builtin_fminf(mpk, pk) : mpk;
+          }
+          S[p] += sp;
+          const bool up = mpk < best[p];
+          best[p] = up ? mpk : best[p];
+          bt[p] = up ? (2 * t + q) : bt[p];
+        }
+      }
+    }
+    if (t + 1 < nstages) TDC_STAGE_STORE(buf ^ 1)
+    __syncthreads();
+  }
+#undef TDC_STAGE_LOAD
+#undef TDC_STAGE_STORE
+
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    S[p] += __shfl_xor(S[p], 32, 64);
+    const unsigned e0 = __float_as_uint(best[p]) & 15u;
+    const int l0 = bt[p] * 32 + (int)(e0 & 3) + 8 * (int)(e0 >> 2) + 4 * h;
+    const float v0 = __uint_as_float(__float_as_uint(best[p]) & ~15u);
+    const float v1 = __shfl_xor(v0, 32, 64);
+    const int l1 = __shfl_xor(l0, 32, 64);
+    const bool other = (v1 < v0) || (v1 == v0 && l1 < l0);
+    const int64_t row = pbase + p * 32 + r;
+    if (h == 0 && row < N) {
+      // on a centroid: the nearest distance is at the floor (one zero-distance centroid
+      // is assumed for the one-hot case; the exact tower counts duplicates)
+      const bool on = (other ? v1 : v0) <= __uint_as_float(__float_as_uint(zf[p]) & ~15u);
+      labels[row] = (on && prm.nz) ? 0 : (other ? l1 : l0);
+      rowinfo[row] = on ? (prm.nz ? 0.f : -1.f) : __builtin_amdgcn_rcpf(S[p]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// pass 2: W^T X and the column sums of a 128-centroid tile over a row range; the block's
+// [128 x D] fp32 partial goes to its own slab (no atomics), reduced by fcm_reduce_kernel
+// ---------------------------------------------------------------------------------------
+template <int DP, int MODE, bool NZ>
+__global__ __launch_bounds__(256, 1) void fcm_mfma_accum_kernel(
+    const __bf16* __restrict__ Xh, const __bf16* __restrict__ Xl, const float* __restrict__ xx,
+    const float* __restrict__ rowinfo, int64_t N, const __bf16* __restrict__ Ch,
+    const __bf16* __restrict__ Cl, const float* __restrict__ cc, int K, int nkt,
+    int64_t rows_per_split, int xcd_map, MParam prm, float* __restrict__ part,
+    float* __restrict__ part_ws, int KP) {
+  constexpr int TP = 64;                  // points per LDS tile (two 32-point sub-tiles)
+  constexpr int CPR = DP / 8;
+  constexpr int KS = DP / 16;
+  constexpr int HALF = DP / 2;
+  constexpr int NDT = DP / 32;            // 32-feature output tiles
+  constexpr int IMG = TP * DP * 2;        // bytes of one hi (or lo) image
+  constexpr int CHUNKS = 2 * TP * CPR;
+  constexpr int CPT = CHUNKS / 256;
+  static_assert(CHUNKS % 256 == 0, "tile chunks must split over 256 threads");
+  __shared__ __attribute__((aligned(16))) char s_x[2][2 * IMG];
+  __shared__ __attribute__((aligned(16))) float s_xx[2][TP];
+  __shared__ __attribute__((aligned(16))) float s_in[2][TP];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  // XCD-aware order: the K tiles of one row range are consecutive on one XCD
+  int64_t L = blockIdx.x;
+  if (xcd_map) {
+    const int64_t per = (int64_t)gridDim.x / 8;
+    L = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+  }
+  const int kt = (int)(L % nkt);
+  const int64_t split = L / nkt;
+  const int64_t a = split * rows_per_split;
+  const int64_t b = min(N, a + rows_per_split);
+  const int kw = kt * 128 + w * 32;       // this wave's 32 centroids
+  const int kc = kw + r;                  // this lane's centroid (column of the distances)
+
+  bf16x8 ch[KS], cl[KS];
+  float ccl;
+  {
+    const bf16x8* sh = reinterpret_cast<const bf16x8*>(Ch + (int64_t)kc * DP + h * HALF);
+    const bf16x8* sl = reinterpret_cast<const bf16x8*>(Cl + (int64_t)kc * DP + h * HALF);
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      ch[kk] = sh[kk];
+      cl[kk] = sl[kk];
+    }
+    ccl = cc[kc];
+  }
+
+  f32x16 out[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) out[dt][i] = 0.f;
+  float wsum = 0.f;
+
+  uint4 pre[CPT];
+  float pv = 0.f;
+#define TDC_TILE_LOAD(R0_)                                                                \
+  {                                                                                       \
+    _Pragma("unroll") for (int i = 0; i < CPT; ++i) {                                     \
+      const int q = tid + i * 256;                                                        \
+      const int hl = q / (TP * CPR), rem = q % (TP * CPR);                                \
+      int64_t gr = (R0_) + rem / CPR;                                                     \
+      gr = gr < b ? gr : b - 1;                                                           \
+      const __bf16* src = (hl ? Xl : Xh) + gr * DP + (rem % CPR) * 8;                     \
+      TDC_GLOAD16(pre[i], src);                                                           \
+    }                                                                                     \
+    if (tid < 2 * TP) {                                                                   \
+      const int64_t gr = (R0_) + (tid & (TP - 1));                                        \
+      pv = gr < b ? (tid < TP ? xx[gr] : rowinfo[gr]) : 0.f;                              \
+    }                                                                                     \
+  }
+#define TDC_TILE_STORE(B_)                                                                \
+  {                                                                                       \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                      \
+    _Pragma("unroll") for (int i = 0; i < CPT; ++i) {                                     \
+      const int q = tid + i * 256;                                                        \
+      const int hl = q / (TP * CPR), rem = q % (TP * CPR);                                \
+      *reinterpret_cast<uint4*>(&s_x[B_][hl * IMG + xoff<DP>(rem / CPR, rem % CPR)]) = pre[i]; \
+    }                                                                                     \
+    if (tid < TP) s_xx[B_][tid] = pv;                                                     \
+    else if (tid < 2 * TP) s_in[B_][tid - TP] = pv;                                       \
+  }
+  if (a < b) {
+    TDC_TILE_LOAD(a)
+    TDC_TILE_STORE(0)
+  }
+  __syncthreads();
+
+  // transposed-read lane geometry (T10): group g, row q4, column quad p4
+  const int g = lane >> 4, gi = lane & 15, q4 = gi >> 2, p4 = gi & 3;
+  int buf = 0;
+  for (int64_t r0 = a; r0 < b; r0 += TP) {
+    const bool more = r0 + TP < b;
+    if (more) TDC_TILE_LOAD(r0 + TP)
+    const char* xh = s_x[buf];
+    const char* xl = s_x[buf] + IMG;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      // ---- distances: rows (registers) = points, lane column = centroid ----
+      f32x16 acc;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = ccl;
+      const int prow = sub * 32 + r;
+      bf16x8 ah = as_bf16x8(*reinterpret_cast<const uint4*>(xh + xoff<DP>(prow, h * (CPR / 2))));
+      bf16x8 al = as_bf16x8(*reinterpret_cast<const uint4*>(xl + xoff<DP>(prow, h * (CPR / 2))));
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        const int kn = kk + 1 < KS ? kk + 1 : kk;
+        const bf16x8 ahn = as_bf16x8(*reinterpret_cast<const uint4*>(xh + xoff<DP>(prow, h * (CPR / 2) + kn)));
+        const bf16x8 aln = as_bf16x8(*reinterpret_cast<const uint4*>(xl + xoff<DP>(prow, h * (CPR / 2) + kn)));
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, ch[kk], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, cl[kk], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, ch[kk], acc, 0, 0, 0);
+        ah = ahn;
+        al = aln;
+      }
+      // ---- memberships -> w = wh + wl (bf16 pair); register i = point (i&3)+8(i>>2)+4h ----
+      // padded rows carry info 0 (w = 0); pad centroids give finite w whose slab rows the
+      // reduction never reads
+      bf16x8 wh[2], wl[2];
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int pt = sub * 32 + 8 * g4 + 4 * h;
+        const f32x4 xq = *reinterpret_cast<const f32x4*>(&s_xx[buf][pt]);
+        const f32x4 iq = *reinterpret_cast<const f32x4*>(&s_in[buf][pt]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * g4 + e;
+          const float zf = ZERO_FLOOR * xq[e];
+          const float d2 = fmaxf(acc[i] + xq[e], zf);
+          float u = mt<MODE>(d2, prm.expo) * iq[e];
+          if constexpr (!NZ) u = iq[e] < 0.f ? (d2 <= zf ? 1.f : 0.f) : u;
+          const float wv = mw<MODE>(u, prm.m);
+          wsum += wv;
+          const __bf16 bhv = (__bf16)wv;
+          wh[i >> 3][i & 7] = bhv;
+          wl[i >> 3][i & 7] = (__bf16)(wv - (float)bhv);
+        }
+      }
+      // ---- W^T X: A = W (row = centroid, k = points), B = X^T via transposed reads ----
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          const int c0 = (dt * 32 + 16 * (g & 1)) >> 3;  // first 8-feature chunk of the block
+          const int rA = sub * 32 + 16 * s + 4 * (g >> 1) + q4;
+          const int oA = xoff<DP>(rA, c0 + (p4 >> 1)) + 8 * (p4 & 1);
+          const int oB = xoff<DP>(rA + 8, c0 + (p4 >> 1)) + 8 * (p4 & 1);
+          const s16x4 h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xh + oA));
+          const s16x4 h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xh + oB));
+          const s16x4 l0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xl + oA));
+          const s16x4 l1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xl + oB));
+          const bf16x8 xbh = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7));
+          const bf16x8 xbl = __builtin_bit_cast(bf16x8, __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7));
+          out[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[s], xbh, out[dt], 0, 0, 0);
+          out[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[s], xbl, out[dt], 0, 0, 0);
+          out[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl[s], xbh, out[dt], 0, 0, 0);
+        }
+      }
+    }
+    if (more) TDC_TILE_STORE(buf ^ 1)
+    __syncthreads();
+    buf ^= 1;
+  }
+#undef TDC_TILE_LOAD
+#undef TDC_TILE_STORE
+
+  // ---- slab: out rows (registers) = centroids kw + (i&3)+8(i>>2)+4h, lane = feature ----
+  float* slab = part + split * (int64_t)KP * DP;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int k = kw + (i & 3) + 8 * (i >> 2) + 4 * h;
+      slab[(int64_t)k * DP + dt * 32 + r] = out[dt][i];
+    }
+  }
+  wsum += __shfl_xor(wsum, 32, 64);
+  if (h == 0) part_ws[split * (int64_t)KP + kc] = wsum;
+}
+
+// wx[k, d] += sum_s part[s, k, d] (fp64), ws[k] += sum_s part_ws[s, k]
+__global__ __launch_bounds__(256) void fcm_reduce_kernel(const float* __restrict__ part,
+                                                         const float* __restrict__ part_ws,
+                                                         int64_t splits, int K, int KP, int DP,
+                                                         int D, double* __restrict__ wx,
+                                                         double* __restrict__ ws) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t tot = (int64_t)K * DP;
+  if (e < tot) {
+    const int k = (int)(e / DP), d = (int)(e % DP);
+    if (d < D) {
+      double s = 0.0;
+      for (int64_t sp = 0; sp < splits; ++sp) s += (double)part[(sp * KP + k) * (int64_t)DP + d];
+      wx[(int64_t)k * D + d] += s;
+    }
+  } else if (e < tot + K) {
+    const int k = (int)(e - tot);
+    double s = 0.0;
+    for (int64_t sp = 0; sp < splits; ++sp) s += (double)part_ws[sp * KP + k];
+    ws[k] += s;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// operand prep: rows of fp32 [rows, ld] (d valid columns) -> hi/lo bf16 [rows, DP] (+ norm)
+// neg2: centroids (hi/lo of -2c, norm of c); pad rows (>= valid) are zero, norm 0
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict__ src, int64_t rows,
+                                                         int64_t valid, int d, int64_t ld, int DP,
+                                                         int neg2, __bf16* __restrict__ hi,
+                                                         __bf16* __restrict__ lo,
+                                                         float* __restrict__ norm) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows;
+       row += (int64_t)gridDim.x * 4) {
+    float s = 0.f;
+    for (int c = lane; c < DP; c += 64) {
+      const float v = (row < valid && c < d) ? src[row * ld + c] : 0.f;
+      s = fmaf(v, v, s);
+      const float t = neg2 ? -2.f * v : v;
+      const __bf16 vh = (__bf16)t;
+      hi[row * DP + c] = vh;
+      lo[row * DP + c] = (__bf16)(t - (float)vh);
+    }
+    s = wave_sum(s);
+    // centroid pad rows: a huge norm keeps their distances (and memberships) negligible
+    if (lane == 0 && norm) norm[row] = (neg2 && row >= valid) ? 1.0e30f : s;
+  }
+}
+
+MParam make_mparam(double m, int nz) {
+  MParam p;
+  p.expo = (float)(-1.0 / (m - 1.0));
+  p.m = (float)m;
+  p.pmode = fcm_pmode(m);
+  p.mint = fcm_mint(m);
+  p.nz = nz;
+  return p;
+}
+
+template <int DP>
+int launch_mstats(const void* Xh, const void* Xl, const float* xx, int64_t N, const void* Ch,
+                  const void* Cl, const float* cc, int K, int Kp, double m, int nz,
+                  int32_t* labels, float* rowinfo, hipStream_t s) {
+  const int64_t blocks = (N + 255) / 256;
+  const MParam p = make_mparam(m, nz);
+#define TDC_LS(MODE)                                                                          \
+  hipLaunchKernelGGL((fcm_mfma_stats_kernel<DP, MODE>), dim3((unsigned)blocks), dim3(256), 0, s, \
+                     (const __bf16*)Xh, (const __bf16*)Xl, xx, N, (const __bf16*)Ch,          \
+                     (const __bf16*)Cl, cc, K, Kp / 64, p, labels, rowinfo)
+  if (m == 2.0) TDC_LS(2); else TDC_LS(0);
+#undef TDC_LS
+  TDC_CHECK_LAUNCH();
+  return 0;
+}
+
+// row ranges of the accumulate pass: ~2 blocks per CU in total, whole 64-point tiles
+inline void accum_geometry(int64_t N, int K, int num_cus, int* nkt, int64_t* splits, int64_t* rps) {
+  *nkt = (K + 127) / 128;
+  const int64_t tiles = (N + 63) / 64;
+  int64_t sp = ((int64_t)num_cus * 2 + *nkt - 1) / *nkt;
+  if (sp > tiles) sp = tiles;
+  if (sp < 1) sp = 1;
+  *rps = ((tiles + sp - 1) / sp) * 64;
+  *splits = (N + *rps - 1) / *rps;
+}
+
+template <int DP>
+int launch_maccum(const void* Xh, const void* Xl, const float* xx, const float* rowinfo,
+                  int64_t N, const void* Ch, const void* Cl, const float* cc, int K, int Kp,
+                  int D, double m, int nz, float* part, double* wx, double* ws, int num_cus,
+                  hipStream_t s) {
+  int nkt;
+  int64_t splits, rps;
+  accum_geometry(N, K, num_cus, &nkt, &splits, &rps);
+  const int64_t nb = splits * nkt;
+  const int xcd = (nb % 8 == 0) ? 1 : 0;
+  float* part_ws = part + splits * (int64_t)Kp * DP;
+  const MParam p = make_mparam(m, nz);
+#define TDC_LA(MODE, NZV)                                                                     \
+  hipLaunchKernelGGL((fcm_mfma_accum_kernel<DP, MODE, NZV>), dim3((unsigned)nb), dim3(256), 0, s, \
+                     (const __bf16*)Xh, (const __bf16*)Xl, xx, rowinfo, N, (const __bf16*)Ch, \
+                     (const __bf16*)Cl, cc, K, nkt, rps, xcd, p, part, part_ws, Kp)
+  if (m == 2.0) {
+    if (nz) TDC_LA(2, true); else TDC_LA(2, false);
+  } else {
+    if (nz) TDC_LA(0, true); else TDC_LA(0, false);
+  }
+#undef TDC_LA
+  TDC_CHECK_LAUNCH();
+  const int64_t tot = (int64_t)K * DP + K;
+  hipLaunchKernelGGL(fcm_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, part,
+                     part_ws, splits, K, Kp, DP, D, wx, ws);
+  TDC_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace
+}  // namespace tdc
+
+using namespace tdc;
+
+int tdc_fcm_split_rows(const float* src, int64_t rows, int64_t valid, int d, int64_t ld, int DP,
+                       int neg2, void* hi, void* lo, float* norm, hipStream_t s) {
+  if (rows <= 0) return 0;
+  int64_t blocks = (rows + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(split_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, rows, valid,
+                     d, ld, DP, neg2, (__bf16*)hi, (__bf16*)lo, norm);
+  TDC_CHECK_LAUNCH();
+  return 0;
+}
+
+int64_t tdc_fcm_mfma_workspace(int64_t N, int K, int Kp, int DP, int num_cus) {
+  int nkt;
+  int64_t splits, rps;
+  accum_geometry(N, K, num_cus, &nkt, &splits, &rps);
+  return splits * (int64_t)Kp * (DP + 1);
+}
+
+int tdc_fcm_mfma(int pass, const void* Xh, const void* Xl, const float* xx, int64_t N, int DP,
+                 int D, const void* Ch, const void* Cl, const float* cc, int K, int Kp, double m,
+                 int nan_to_zero, int32_t* labels, float* rowinfo, double* wx, double* ws,
+                 float* work, int num_cus, hipStream_t s) {
+  if (N <= 0 || K <= 0) return 0;
+  if (Kp % 128 != 0 || Kp < K) return (int)hipErrorInvalidValue;
+#define TDC_FM(DPV)                                                                           \
+  if (DP == DPV) {                                                                            \
+    if (pass == 0)                                                                            \
+      return launch_mstats<DPV>(Xh, Xl, xx, N, Ch, Cl, cc, K, Kp, m, nan_to_zero, labels,     \
+                                rowinfo, s);                                                  \
+    return launch_maccum<DPV>(Xh, Xl, xx, rowinfo, N, Ch, Cl, cc, K, Kp, D, m, nan_to_zero,   \
+                              work, wx, ws, num_cus, s);                                      \
+  }
+  TDC_FM(32)
+  TDC_FM(64)
+  TDC_FM(128)
+#undef TDC_FM
+  return (int)hipErrorInvalidValue;
+}

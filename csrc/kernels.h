@@ -80,6 +80,28 @@ int tdc_fcm_small_supported(int dtype, int K, int D);
 int tdc_fcm_rows(float* G, int64_t rows, int K, const float* xx, const float* cc, float m,
                  int nan_to_zero, int32_t* labels, float* colsum, hipStream_t stream);
 
+// N4/N5 for any K and D <= 256 (fp32 / fp64, exact difference-form distances), two passes:
+// pass 0 (stats): labels = argmax_k u, rowinfo [N] (X dtype) = 1/sum_k t (> 0), 0 (all
+// memberships 0: nan_to_zero on a centroid) or -nzero (one-hot over the zero distances);
+// pass 1 (accum): wx [K, D] += sum_i w_ik x_i, ws [K] += sum_i w_ik (fp64, accumulated).
+int tdc_fcm_tower(int pass, int dtype, const void* X, int64_t N, int64_t ldx, int D, const void* C,
+                  int K, double m, int nan_to_zero, int32_t* labels, void* rowinfo, void* wx,
+                  void* ws, int num_cus, hipStream_t stream);
+
+// N4/N5 on MFMA (fp32 FCM, large K x D): hi/lo bf16 operands.  split_rows: fp32 rows
+// [rows, ld] (d valid columns, rows >= valid are zero padding) -> hi/lo bf16 [rows, DP]
+// (of -2v when neg2) + norm [rows] = ||v||^2 (nullable).  fcm_mfma pass 0: labels +
+// rowinfo (fp32, as tdc_fcm_tower); pass 1: wx [K, D] / ws [K] (fp64) += W^T X / sum W.
+// DP in {32, 64, 128}; Ch/Cl/cc have Kp rows (Kp % 128 == 0).
+int tdc_fcm_split_rows(const float* src, int64_t rows, int64_t valid, int d, int64_t ld, int DP,
+                       int neg2, void* hi, void* lo, float* norm, hipStream_t stream);
+// work: fp32 [tdc_fcm_mfma_workspace(...)] per-block partial slabs of pass 1.
+int tdc_fcm_mfma(int pass, const void* Xh, const void* Xl, const float* xx, int64_t N, int DP,
+                 int D, const void* Ch, const void* Cl, const float* cc, int K, int Kp, double m,
+                 int nan_to_zero, int32_t* labels, float* rowinfo, double* wx, double* ws,
+                 float* work, int num_cus, hipStream_t stream);
+int64_t tdc_fcm_mfma_workspace(int64_t N, int K, int Kp, int DP, int num_cus);
+
 // N3  finalize: C = sums/counts (empty policy), max shift^2 -> shift (float, atomic max),
 // optional bf16 prep of the next assignment (Cm2 [Kp, DP] = -2*bf16(c), cnorm [Kp]).
 // sums == nullptr: prep only (C unchanged).

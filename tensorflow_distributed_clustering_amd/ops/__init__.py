@@ -738,6 +738,134 @@ class HipSmallFCM(_LocalOpsBase):
         self.ops.finalize(sums, counts, C, 0, shift, None, None)
 
 
+class HipTowerFCM(_LocalOpsBase):
+    """FCM for any K and D <= 256 in fp32 / fp64 (csrc/fcm_tower.hip): a stats pass (row
+    normaliser + argmax label per row, exact difference-form distances) and an accumulate
+    pass (centroid tile x row range: the tile's sum_i w x_i and sum_i w in registers).
+    No host syncs; ``rowinfo`` [N] is the only intermediate."""
+    name = "hip_fcm_tower"
+
+    def __init__(self, x, k, dtype="fp64", m=2.0, nan_to_zero=True):
+        super().__init__(x, k, "keep")
+        self.ops = _native.require()
+        tdt = torch.float64 if dtype == "fp64" else torch.float32
+        self.x = x.to(tdt).contiguous()
+        self.c_dtype = tdt
+        self.m = float(m)
+        self.nan_to_zero = bool(nan_to_zero)
+        self.rowinfo = torch.empty(self.n, dtype=tdt, device=self.device)
+        self._wx = self._ws = None
+
+    def bind(self, x):
+        super().bind(x)
+        if self.rowinfo.numel() < self.n:
+            self.rowinfo = torch.empty(self.n, dtype=self.c_dtype, device=self.device)
+        return self
+
+    def step(self, C, labels, wx, ws):
+        C = C.to(self.c_dtype).contiguous()
+        ri = self.rowinfo[: self.n]
+        self.ops.fcm_tower_stats(self.x, C, self.m, self.nan_to_zero, labels, ri)
+        self.ops.fcm_tower_accum(self.x, C, self.m, self.nan_to_zero, ri, wx, ws)
+
+    def assign(self, C, labels):
+        self.ops.fcm_tower_stats(self.x, C.to(self.c_dtype).contiguous(), self.m,
+                                 self.nan_to_zero, labels, self.rowinfo[: self.n])
+
+    def finalize(self, sums, counts, C, shift):
+        self.ops.finalize(sums, counts, C, 0, shift, None, None)
+
+
+FCM_MFMA_DIMS = (32, 64, 128)
+FCM_MFMA_MIN_K = 32  # below: the SIMT tower (a 128-centroid MFMA tile would be mostly padding)
+
+
+def fcm_mfma_dim(d: int) -> Optional[int]:
+    for p in FCM_MFMA_DIMS:
+        if d <= p:
+            return p
+    return None
+
+
+class HipMfmaFCM(_LocalOpsBase):
+    """fp32 FCM on bf16 matrix cores (csrc/fcm_mfma.hip): the shard is split once into
+    hi/lo bf16 rows (+ fp32 norms), the centroids every iteration; a stats pass (row
+    normaliser + label) and an accumulate pass (distances -> w -> W^T X, all on MFMA)."""
+    name = "hip_fcm_mfma"
+
+    def __init__(self, x, k, m=2.0, nan_to_zero=True):
+        super().__init__(x, k, "keep")
+        self.ops = _native.require()
+        self.dp = fcm_mfma_dim(self.d)
+        if self.dp is None:
+            raise ValueError(f"MFMA FCM supports D <= {FCM_MFMA_DIMS[-1]}, got {self.d}")
+        self.c_dtype = torch.float32
+        self.m = float(m)
+        self.nan_to_zero = bool(nan_to_zero)
+        self.kp = -(-k // 128) * 128
+        dev = self.device
+        self.ch = torch.zeros(self.kp, self.dp, dtype=torch.bfloat16, device=dev)
+        self.cl = torch.zeros_like(self.ch)
+        self.cc = torch.zeros(self.kp, dtype=torch.float32, device=dev)
+        self.xh = self.xl = self.xx = self.rowinfo = None
+        self.work = None
+        self._set_x(x)
+
+    @property
+    def layout(self):
+        return (torch.float32, self.d)
+
+    def _work(self):
+        need = int(self.ops.fcm_mfma_workspace(self.cc, self.n, self.k, self.kp, self.dp))
+        if self.work is None or self.work.numel() < need:
+            self.work = torch.empty(need, dtype=torch.float32, device=self.device)
+        return self.work
+
+    def _set_x(self, x):
+        n = int(x.shape[0])
+        if self.xh is None or self.xh.shape[0] < n:
+            dev = self.device
+            self.xh = torch.empty(n, self.dp, dtype=torch.bfloat16, device=dev)
+            self.xl = torch.empty_like(self.xh)
+            self.xx = torch.empty(n, dtype=torch.float32, device=dev)
+            self.rowinfo = torch.empty(n, dtype=torch.float32, device=dev)
+        xf = x if (x.dtype == torch.float32 and x.stride(1) == 1) else x.float().contiguous()
+        self.n = n
+        self.ops.fcm_split_rows(xf[:, : self.d], n, 0, self.xh[:n], self.xl[:n], self.xx[:n])
+        self.x = None  # the hi/lo rows are the shard from here on
+
+    def bind(self, x):
+        if x.shape[1] != self.d:
+            raise ValueError(f"chunk width {x.shape[1]} != {self.d}")
+        self._set_x(x)
+        return self
+
+    def prepare(self, C):
+        self.ops.fcm_split_rows(C.float().contiguous(), self.k, 1, self.ch, self.cl, self.cc)
+
+    def _ops_args(self):
+        n = self.n
+        return self.xh[:n], self.xl[:n], self.xx[:n]
+
+    def step(self, C, labels, wx, ws):
+        self.prepare(C)
+        xh, xl, xx = self._ops_args()
+        ri = self.rowinfo[: self.n]
+        self.ops.fcm_mfma_stats(xh, xl, xx, self.ch, self.cl, self.cc, self.k, self.m,
+                                self.nan_to_zero, labels, ri)
+        self.ops.fcm_mfma_accum(xh, xl, xx, ri, self.ch, self.cl, self.cc, self.k, self.m,
+                                self.nan_to_zero, wx, ws, self._work())
+
+    def assign(self, C, labels):
+        self.prepare(C)
+        xh, xl, xx = self._ops_args()
+        self.ops.fcm_mfma_stats(xh, xl, xx, self.ch, self.cl, self.cc, self.k, self.m,
+                                self.nan_to_zero, labels, self.rowinfo[: self.n])
+
+    def finalize(self, sums, counts, C, shift):
+        self.ops.finalize(sums, counts, C, 0, shift, None, None)
+
+
 class HipGemmFCM(_LocalOpsBase):
     """FCM for large K*D: fp32 library GEMMs (hipBLASLt) for ``-2 X C^T`` and ``W^T X``
     around the fused ``fcm_rows`` HIP kernel (distances -> memberships -> u^m -> labels in
@@ -818,6 +946,10 @@ def make_fcm_ops(x: torch.Tensor, k: int, dtype: str = "fp64", m: float = 2.0,
     tdt = torch.float64 if dtype == "fp64" else torch.float32
     if _native.require().fcm_small_supported(tdt, k, d):
         return HipSmallFCM(x, k, dtype, m, nan_to_zero)
-    if dtype == "fp32" and d > 16:
+    if dtype == "fp32" and d > 16 and k >= FCM_MFMA_MIN_K and fcm_mfma_dim(d) is not None:
+        return HipMfmaFCM(x, k, m, nan_to_zero)
+    if d <= 256:
+        return HipTowerFCM(x, k, dtype, m, nan_to_zero)
+    if dtype == "fp32":
         return HipGemmFCM(x, k, m, nan_to_zero)
     return TorchFCM(x, k, dtype, m, nan_to_zero)

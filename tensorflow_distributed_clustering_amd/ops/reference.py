@@ -118,16 +118,19 @@ def fcm_memberships(x: torch.Tensor, c: torch.Tensor, m: float,
 
 def fcm_partial(x: torch.Tensor, c: torch.Tensor, m: float, nan_to_zero: bool = True,
                 acc_dtype: torch.dtype = torch.float64,
-                chunk_elems: int = _DEF_CHUNK_ELEMS) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-    """FCM tower: (sum_i w_ki x_i [K, D], sum_i w_ki [K], labels argmax_k u [n])."""
+                chunk_elems: int = _DEF_CHUNK_ELEMS,
+                exact: Optional[bool] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """FCM tower: (sum_i w_ki x_i [K, D], sum_i w_ki [K], labels argmax_k u [n]).
+    ``exact``: difference-form distances (default: for D <= 16, as fcm_memberships)."""
     n, k = x.shape[0], c.shape[0]
     wx = torch.zeros(k, x.shape[1], dtype=acc_dtype, device=x.device)
     ws = torch.zeros(k, dtype=acc_dtype, device=x.device)
     labels = torch.empty(n, dtype=torch.int32, device=x.device)
-    step = _chunk_rows(n, k, max(1, chunk_elems // max(1, x.shape[1] if x.shape[1] <= 16 else 4)))
+    ex = exact if exact is not None else x.shape[1] <= 16
+    step = _chunk_rows(n, k, max(1, chunk_elems // max(1, x.shape[1] if ex else 4)))
     for s in range(0, n, step):
         xs = x[s:s + step]
-        u = fcm_memberships(xs, c, m, nan_to_zero)
+        u = fcm_memberships(xs, c, m, nan_to_zero, exact=ex)
         w = u.pow(m)
         wx += (w.t().to(acc_dtype) @ xs.to(acc_dtype))
         ws += w.sum(0).to(acc_dtype)

@@ -123,6 +123,9 @@ class Comm:
         if self.world_size <= 1:
             out.copy_(part.view_as(out))
             return out
+        if out.dtype in (torch.float8_e4m3fn, torch.float8_e5m2):
+            # a gather moves bytes: fp8 operand tables travel as uint8 (gloo has no fp8)
+            out, part = out.view(torch.uint8), part.view(torch.uint8)
         dist.all_gather_into_tensor(out, part, group=self.group)
         return out
 

@@ -1,0 +1,102 @@
+"""Native FCM towers against the fp64 PyTorch oracle (``ops/reference.fcm_partial``, the
+reference's op chain `scripts/distribuitedClustering.py:108-137`).
+
+* ``fcm_tower_*`` (csrc/fcm_tower.hip): fp32/fp64, any K, D <= 256, exact difference-form
+  distances -- the path of every shape fcm_small does not cover;
+* ``fcm_mfma_*`` (csrc/fcm_mfma.hip): fp32 on bf16 matrix cores with hi/lo split operands.
+
+Each case includes a point exactly on a centroid (the NaN -> 0 guard, or the one-hot limit
+with ``nan_to_zero=False``) and a ragged N.
+"""
+import pytest
+import torch
+
+from tensorflow_distributed_clustering_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(n, k, d, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, d, generator=g, dtype=torch.float64)
+    c = x[torch.randperm(n, generator=g)[:k]] + 0.05 * torch.randn(k, d, generator=g,
+                                                                   dtype=torch.float64)
+    x[7] = c[min(3, k - 1)]  # a point exactly on a centroid
+    return x, c
+
+
+def _check(wx, ws, lab, x, c, m, nz, rtol, agree):
+    # exact difference form: a point ON a centroid is at distance exactly 0
+    a, b, lr = ref.fcm_partial(x.double(), c.double(), m, nz, exact=True)
+    cen = wx / ws.clamp_min(1e-300)[:, None]
+    cen_ref = a / b.clamp_min(1e-300)[:, None]
+    ok = b > 1e-12 * b.max()
+    torch.testing.assert_close(ws[ok], b[ok], rtol=rtol, atol=rtol * float(b.max()) * 1e-3)
+    torch.testing.assert_close(cen[ok], cen_ref[ok], rtol=rtol, atol=rtol)
+    assert (lab.long().cpu() == lr.long().cpu()).double().mean().item() >= agree
+
+
+@pytest.mark.parametrize("dt", [torch.float64, torch.float32])
+@pytest.mark.parametrize("k,d", [(32, 5), (20, 9), (100, 3), (64, 40), (300, 17), (129, 128),
+                                 (50, 256), (1000, 12)])
+@pytest.mark.parametrize("m", [2.0, 2.5])
+@pytest.mark.parametrize("nz", [True, False])
+def test_fcm_tower_matches_oracle(gpu, dt, k, d, m, nz):
+    from tensorflow_distributed_clustering_amd import _native
+    ops = _native.require()
+    n = 6001 if k * d > 20000 else 20011
+    x, c = _data(n, k, d, k * 7 + d)
+    xg, cg = x.to(dt).to(gpu), c.to(dt).to(gpu)
+    lab = torch.empty(n, dtype=torch.int32, device=gpu)
+    ri = torch.empty(n, dtype=dt, device=gpu)
+    wx = torch.zeros(k, d, dtype=torch.float64, device=gpu)
+    ws = torch.zeros(k, dtype=torch.float64, device=gpu)
+    ops.fcm_tower_stats(xg, cg, m, nz, lab, ri)
+    ops.fcm_tower_accum(xg, cg, m, nz, ri, wx, ws)
+    rtol = 1e-9 if dt == torch.float64 else 2e-4 * m
+    _check(wx.cpu(), ws.cpu(), lab, xg.cpu(), cg.cpu(), m, nz, rtol,
+           0.99999 if dt == torch.float64 else 0.999)
+
+
+@pytest.mark.parametrize("k,d", [(32, 17), (100, 64), (257, 128), (1024, 128), (130, 33),
+                                 (64, 128)])
+@pytest.mark.parametrize("m", [2.0, 3.0, 1.5])
+@pytest.mark.parametrize("nz", [True, False])
+def test_fcm_mfma_matches_oracle(gpu, k, d, m, nz):
+    from tensorflow_distributed_clustering_amd.ops import HipMfmaFCM
+    n = 20001
+    x, c = _data(n, k, d, k + d)
+    xg, cg = x.float().to(gpu), c.float().to(gpu)
+    ops = HipMfmaFCM(xg, k, m, nz)
+    lab = torch.empty(n, dtype=torch.int32, device=gpu)
+    wx = torch.zeros(k, d, dtype=torch.float64, device=gpu)
+    ws = torch.zeros(k, dtype=torch.float64, device=gpu)
+    ops.step(cg, lab, wx, ws)
+    # bf16x3 distances: |d2 error| ~ 2^-17 (|x|^2 + |c|^2), relative to the small d2 of a
+    # point next to its centroid (|x|^2 / d2 ~ 400 here) -> ~0.1 % per (m - 1) in t
+    _check(wx.cpu(), ws.cpu(), lab, xg.cpu(), cg.cpu(), m, nz, 2e-3 * m, 0.998)
+    lab2 = torch.empty_like(lab)
+    ops.assign(cg, lab2)
+    assert torch.equal(lab, lab2)
+
+
+@pytest.mark.parametrize("dtype,d,k,backend", [("fp64", 5, 32, "hip_fcm_tower"),
+                                               ("fp64", 64, 100, "hip_fcm_tower"),
+                                               ("fp32", 12, 64, "hip_fcm_tower"),
+                                               ("fp32", 128, 256, "hip_fcm_mfma")])
+def test_fcm_fit_native_backends(gpu, dtype, d, k, backend):
+    """Every FCM shape class runs a native backend and follows the fp64 torch fit."""
+    import tensorflow_distributed_clustering_amd as tdc
+    from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs
+    x = gaussian_blobs(30000, d, k, seed=2, dtype=torch.float64, device=gpu)
+    # start next to (not on) data rows: a row exactly on a centroid is the reference's
+    # discontinuous NaN -> 0 case, where exact and GEMM-form oracles legitimately differ
+    c0 = (x[:k].cpu() + 0.01).numpy()
+    cfg = tdc.ClusterConfig(n_clusters=k, max_iter=4, dtype=dtype, init="given", fuzzifier=2.0)
+    r = tdc.FuzzyCMeans(cfg).fit(x, init_centers_=c0).result_
+    assert r.backend == backend
+    o = tdc.FuzzyCMeans(cfg.replace(dtype="fp64", backend="torch"),
+                        device="cpu").fit(x.cpu(), init_centers_=c0).result_
+    tol = 1e-8 if dtype == "fp64" else 3e-3
+    torch.testing.assert_close(torch.as_tensor(r.centers), torch.as_tensor(o.centers),
+                               rtol=tol, atol=tol)

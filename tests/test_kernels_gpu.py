@@ -497,14 +497,13 @@ def test_fcm_rows_kernel(gpu, m, nan_to_zero, k):
 
 @pytest.mark.parametrize("m", [2.0, 32.0])
 def test_hip_gemm_fcm_step_matches_reference(gpu, m):
-    from tensorflow_distributed_clustering_amd.ops import HipGemmFCM, make_fcm_ops
+    from tensorflow_distributed_clustering_amd.ops import HipGemmFCM
     g = torch.Generator().manual_seed(5)
     n, d, k = 30000, 32, 300
     x = torch.randn(n, d, generator=g, dtype=torch.float64)
     c = x[torch.randperm(n, generator=g)[:k]] + 0.01
     x32, c32 = x.float().to(gpu), c.float().to(gpu)
-    ops = make_fcm_ops(x32, k, "fp32", m)
-    assert isinstance(ops, HipGemmFCM)
+    ops = HipGemmFCM(x32, k, m)  # the library-GEMM FCM (selected for D > 128 fp32 only)
     ops.rows = 17001  # several chunks incl. a ragged tail
     assert ops.splits > 1  # batched W^T X with a remainder (17001 = 16 * 1062 + 9)
     ops.splits, ops.part = 16, ops.part[:16]

@@ -72,14 +72,14 @@ def test_predictor_reused_buffer_requantised(gpu, dtype, d):
 
 
 def test_fcm_predict_gemm_path(gpu):
-    """FuzzyCMeans.predict at D > 16 runs HipGemmFCM (hipBLASLt + fcm_rows) and reproduces
-    the fit's label pass."""
+    """FuzzyCMeans.predict at D > 16 runs the MFMA FCM tower and reproduces the fit's label
+    pass."""
     import tensorflow_distributed_clustering_amd as tdc
     from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs
     x = gaussian_blobs(50000, 64, 32, seed=4, dtype=torch.float32, device=gpu)
     fcm = tdc.FuzzyCMeans(tdc.ClusterConfig(n_clusters=32, max_iter=3, dtype="fp32", seed=1,
                                             fuzzifier=2.0)).fit(x)
-    assert fcm.result_.backend == "hip_fcm_gemm"
+    assert fcm.result_.backend == "hip_fcm_mfma"
     lab = fcm.predict(x)
     assert (lab == fcm.result_.labels).float().mean().item() > 0.999
     u = fcm.memberships(x[:1000])
