@@ -247,7 +247,8 @@ void fcm_tower_accum(const at::Tensor& X, const at::Tensor& C, double m, bool na
 }
 
 void fcm_split_rows(const at::Tensor& src, int64_t valid, int64_t neg2, at::Tensor& hi,
-                    at::Tensor& lo, const std::optional<at::Tensor>& norm) {
+                    at::Tensor& lo, const std::optional<at::Tensor>& norm,
+                    const std::optional<at::Tensor>& shift) {
   check_cuda(src, "src");
   TORCH_CHECK(src.scalar_type() == at::kFloat && src.dim() == 2 && src.stride(1) == 1,
               "tdc.fcm_split_rows: src fp32 rows");
@@ -261,9 +262,13 @@ void fcm_split_rows(const at::Tensor& src, int64_t valid, int64_t neg2, at::Tens
   if (norm.has_value() && norm->defined())
     TORCH_CHECK(norm->scalar_type() == at::kFloat && norm->is_contiguous() && norm->numel() >= rows,
                 "tdc.fcm_split_rows: norm fp32 [rows]");
+  if (shift.has_value() && shift->defined())
+    TORCH_CHECK(shift->scalar_type() == at::kFloat && shift->is_contiguous() &&
+                    shift->numel() >= src.size(1), "tdc.fcm_split_rows: shift fp32 [d]");
   const DevGuard guard(src.device());
   check(tdc_fcm_split_rows(src.data_ptr<float>(), rows, valid, (int)src.size(1), src.stride(0), DP,
-                           (int)neg2, hi.data_ptr(), lo.data_ptr(),
+                           (int)neg2, static_cast<const float*>(opt_ptr(shift)), hi.data_ptr(),
+                           lo.data_ptr(),
                            static_cast<float*>(opt_ptr(norm)), cur_stream()),
         "fcm_split_rows");
 }
@@ -739,7 +744,7 @@ TORCH_LIBRARY(tdc, m) {
   m.def("fcm_small(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) wx, Tensor(c!) ws) -> ()");
   m.def("fcm_tower_stats(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) rowinfo) -> ()");
   m.def("fcm_tower_accum(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor rowinfo, Tensor(a!) wx, Tensor(b!) ws) -> ()");
-  m.def("fcm_split_rows(Tensor src, int valid, int neg2, Tensor(a!) hi, Tensor(b!) lo, Tensor(c!)? norm) -> ()");
+  m.def("fcm_split_rows(Tensor src, int valid, int neg2, Tensor(a!) hi, Tensor(b!) lo, Tensor(c!)? norm, Tensor? shift=None) -> ()");
   m.def("fcm_mfma_stats(Tensor Xh, Tensor Xl, Tensor xx, Tensor Ch, Tensor Cl, Tensor cc, int K, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) rowinfo) -> ()");
   m.def("fcm_mfma_accum(Tensor Xh, Tensor Xl, Tensor xx, Tensor rowinfo, Tensor Ch, Tensor Cl, Tensor cc, int K, float m, bool nan_to_zero, Tensor(a!) wx, Tensor(b!) ws, Tensor(c!) work) -> ()");
   m.def("fcm_mfma_workspace(Tensor like, int N, int K, int Kp, int DP) -> int");

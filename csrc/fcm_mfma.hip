@@ -22,8 +22,10 @@
 //     accumulators for the whole row range and is flushed once (fp64 atomics).
 //     Blocks are mapped so that the K tiles of one row range run on the same XCD and
 //     share its L2 copy of the X tile.
-// Distances within 2^-14 (||x||^2 + ||c||^2) of zero count as zero (the bf16x3 noise
-// floor): a point on a centroid keeps the reference's NaN -> 0 semantics.
+// Distances within 2^-16 ||x||^2 of zero count as zero (an exact hit computes 2 xl^2 ~
+// 2^-17 ||x||^2): a point on a centroid keeps the reference's NaN -> 0 semantics.  Rows
+// and centroids are shifted by a fixed vector (the shard mean) before the split, so the
+// expansion's cancellation is relative to the data spread, not to its offset.
 #include "tdc_common.h"
 #include "kernels.h"
 #include "fcm_math.h"
@@ -35,7 +37,7 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-constexpr float ZERO_FLOOR = 6.103515625e-05f;  // 2^-14
+constexpr float ZERO_FLOOR = 1.52587890625e-05f;  // 2^-16 (an exact hit computes ~2^-17 |x|^2)
 
 struct MParam {
   float expo, m;
@@ -85,52 +87,52 @@ __device__ __forceinline__ float mw(float u, float m) {
 // ---------------------------------------------------------------------------------------
 // pass 1: per-row statistics
 // ---------------------------------------------------------------------------------------
-template <int DP, int MODE>
-__global__ __launch_bounds__(256, 1) void fcm_mfma_stats_kernel(
+// WAVES waves x one 32-point tile each share every centroid stage (8 waves: 2 per SIMD, so
+// one wave's epilogue VALU runs beside the other's MFMAs); within a wave the epilogue of
+// half q-1 is issued after the MFMAs of half q (software pipeline, as the Lloyd kernels).
+template <int DP, int MODE, int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats_kernel(
     const __bf16* __restrict__ Xh, const __bf16* __restrict__ Xl, const float* __restrict__ xx,
     int64_t N, const __bf16* __restrict__ Ch, const __bf16* __restrict__ Cl,
     const float* __restrict__ cc, int K, int nstages, MParam prm, int32_t* __restrict__ labels,
     float* __restrict__ rowinfo) {
-  constexpr int P = 2;
+  constexpr int NT = WAVES * 64;
   constexpr int BN = 64;
   constexpr int CPR = DP / 8;
   constexpr int KS = DP / 16;
   constexpr int HALF = DP / 2;
   constexpr int IMGB = BN * DP * 2;           // bytes of one (hi or lo) stage image
   constexpr int CHUNKS = 2 * BN * CPR;        // 16-byte chunks per stage
-  constexpr int CPT = CHUNKS / 256;
-  static_assert(CHUNKS % 256 == 0, "stage chunks must split over 256 threads");
+  constexpr int CPT = CHUNKS / NT;
+  static_assert(CHUNKS % NT == 0, "stage chunks must split over the block");
   __shared__ __attribute__((aligned(16))) char s_c[2][2 * IMGB];
   __shared__ __attribute__((aligned(16))) float s_n[2][BN];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int64_t pbase = (int64_t)blockIdx.x * (4 * P * 32) + (int64_t)w * (P * 32);
+  const int64_t row0 = (int64_t)blockIdx.x * (WAVES * 32) + (int64_t)w * 32 + r;
 
-  bf16x8 bh[P][KS], bl[P][KS];
-  float xn[P], zf[P];
-#pragma unroll
-  for (int p = 0; p < P; ++p) {
-    int64_t row = pbase + p * 32 + r;
-    if (row >= N) row = N - 1;
+  bf16x8 bh[KS], bl[KS];
+  float xn, zf;
+  {
+    const int64_t row = row0 < N ? row0 : N - 1;
     const bf16x8* sh = reinterpret_cast<const bf16x8*>(Xh + row * DP + h * HALF);
     const bf16x8* sl = reinterpret_cast<const bf16x8*>(Xl + row * DP + h * HALF);
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) {
-      bh[p][kk] = sh[kk];
-      bl[p][kk] = sl[kk];
+      bh[kk] = sh[kk];
+      bl[kk] = sl[kk];
     }
-    xn[p] = xx[row];
-    zf[p] = ZERO_FLOOR * xn[p];
+    xn = xx[row];
+    zf = ZERO_FLOOR * xn;
   }
 
-  // stage t: chunk q of the thread -> (hi/lo, row, chunk) -> swizzled LDS slot
   uint4 pre[CPT];
   float npre = 0.f;
 #define TDC_STAGE_LOAD(T_)                                                                \
   {                                                                                       \
     _Pragma("unroll") for (int i = 0; i < CPT; ++i) {                                     \
-      const int q = tid + i * 256;                                                        \
+      const int q = tid + i * NT;                                                         \
       const int hl = q / (BN * CPR), rem = q % (BN * CPR);                                \
       const __bf16* src = (hl ? Cl : Ch) + ((int64_t)(T_) * BN + rem / CPR) * DP + (rem % CPR) * 8; \
       TDC_GLOAD16(pre[i], src);                                                           \
@@ -141,7 +143,7 @@ __global__ __launch_bounds__(256, 1) void fcm_mfma_stats_kernel(
   {                                                                                       \
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                      \
     _Pragma("unroll") for (int i = 0; i < CPT; ++i) {                                     \
-      const int q = tid + i * 256;                                                        \
+      const int q = tid + i * NT;                                                         \
       const int hl = q / (BN * CPR), rem = q % (BN * CPR);                                \
       *reinterpret_cast<uint4*>(&s_c[B_][hl * IMGB + coff<DP>(rem / CPR, rem % CPR)]) = pre[i]; \
     }                                                                                     \
@@ -151,107 +153,91 @@ __global__ __launch_bounds__(256, 1) void fcm_mfma_stats_kernel(
   TDC_STAGE_STORE(0)
   __syncthreads();
 
-  float S[P], best[P];
-  int bt[P];
-#pragma unroll
-  for (int p = 0; p < P; ++p) {
-    S[p] = 0.f;
-    best[p] = INFINITY;
-    bt[p] = 0;
+  float S = 0.f, best = INFINITY;
+  int bt = 0;
+
+  // MFMAs of half Q of the stage in buffer cb/ns into ACC (init = ||c||^2 rows)
+#define TDC_PHASE(ACC, Q)                                                                 \
+  {                                                                                       \
+    const int crow = (Q) * 32 + r;                                                        \
+    f32x16 init;                                                                          \
+    _Pragma("unroll") for (int g4 = 0; g4 < 4; ++g4) {                                    \
+      const f32x4 n4 = *reinterpret_cast<const f32x4*>(&ns[(Q) * 32 + 8 * g4 + 4 * h]);   \
+      _Pragma("unroll") for (int e = 0; e < 4; ++e) init[4 * g4 + e] = n4[e];             \
+    }                                                                                     \
+    bf16x8 ah = as_bf16x8(*reinterpret_cast<const uint4*>(cb + coff<DP>(crow, h * (CPR / 2)))); \
+    bf16x8 al = as_bf16x8(*reinterpret_cast<const uint4*>(cb + IMGB + coff<DP>(crow, h * (CPR / 2)))); \
+    _Pragma("unroll") for (int kk = 0; kk < KS; ++kk) {                                   \
+      const int kn = kk + 1 < KS ? kk + 1 : kk;                                           \
+      const bf16x8 ahn = as_bf16x8(*reinterpret_cast<const uint4*>(cb + coff<DP>(crow, h * (CPR / 2) + kn))); \
+      const bf16x8 aln = as_bf16x8(*reinterpret_cast<const uint4*>(cb + IMGB + coff<DP>(crow, h * (CPR / 2) + kn))); \
+      ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[kk], kk == 0 ? init : ACC, 0, 0, 0); \
+      ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[kk], ACC, 0, 0, 0);           \
+      ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[kk], ACC, 0, 0, 0);           \
+      ah = ahn;                                                                           \
+      al = aln;                                                                           \
+    }                                                                                     \
+  }
+  // epilogue of half Q of stage T_: register i = centroid (i&3)+8(i>>2)+4h (ascending);
+  // d2 clamped at the zero floor (a row whose min d2 is at the floor is "on a centroid");
+  // pad centroids (last stage only) masked
+#define TDC_EPI(ACC, Q, T_)                                                               \
+  {                                                                                       \
+    const int kvalid = K - ((T_) * BN + (Q) * 32 + 4 * h);                                \
+    float mpk = INFINITY, sp = 0.f;                                                       \
+    if (kvalid >= 28) {                                                                   \
+      _Pragma("unroll") for (int i = 0; i < 16; ++i) {                                    \
+        const float d2 = fmaxf(ACC[i] + xn, zf);                                          \
+        sp += mt<MODE>(d2, prm.expo);                                                     \
+        mpk = __builtin_fminf(mpk, __uint_as_float((__float_as_uint(d2) & ~15u) | (unsigned)i)); \
+      }                                                                                   \
+    } else {                                                                              \
+      _Pragma("unroll") for (int i = 0; i < 16; ++i) {                                    \
+        const bool v = (i & 3) + 8 * (i >> 2) < kvalid;                                   \
+        const float d2 = fmaxf(ACC[i] + xn, zf);                                          \
+        sp += v ? mt<MODE>(d2, prm.expo) : 0.f;                                           \
+        const float pk = __uint_as_float((__float_as_uint(d2) & ~15u) | (unsigned)i);     \
+        mpk = v ? __builtin_fminf(mpk, pk) : mpk;                                         \
+      }                                                                                   \
+    }                                                                                     \
+    S += sp;                                                                              \
+    const bool up = mpk < best;                                                           \
+    best = up ? mpk : best;                                                               \
+    bt = up ? (2 * (T_) + (Q)) : bt;                                                      \
   }
 
+  f32x16 acc0, acc1;
   for (int t = 0; t < nstages; ++t) {
     const int buf = t & 1;
     if (t + 1 < nstages) TDC_STAGE_LOAD(t + 1)
     const char* cb = s_c[buf];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int row = q * 32 + r;
-      f32x16 acc[P];
-      f32x16 init;
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const f32x4 n4 = *reinterpret_cast<const f32x4*>(&s_n[buf][q * 32 + 8 * g4 + 4 * h]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) init[4 * g4 + e] = n4[e];
-      }
-      bf16x8 ah = as_bf16x8(*reinterpret_cast<const uint4*>(cb + coff<DP>(row, h * (CPR / 2))));
-      bf16x8 al = as_bf16x8(*reinterpret_cast<const uint4*>(cb + IMGB + coff<DP>(row, h * (CPR / 2))));
-#pragma unroll
-      for (int kk = 0; kk < KS; ++kk) {
-        const int kn = kk + 1 < KS ? kk + 1 : kk;
-        const bf16x8 ahn = as_bf16x8(*reinterpret_cast<const uint4*>(cb + coff<DP>(row, h * (CPR / 2) + kn)));
-        const bf16x8 aln = as_bf16x8(*reinterpret_cast<const uint4*>(cb + IMGB + coff<DP>(row, h * (CPR / 2) + kn)));
-#pragma unroll
-        for (int p = 0; p < P; ++p) {
-          acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[p][kk], kk == 0 ? init : acc[p], 0, 0, 0);
-          acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[p][kk], acc[p], 0, 0, 0);
-          acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[p][kk], acc[p], 0, 0, 0);
-        }
-        ah = ahn;
-        al = aln;
-      }
-      // epilogue: register i = centroid (i&3)+8(i>>2)+4h of this 32-tile (ascending in i).
-      // d2 is clamped at the zero floor zf (t stays finite; a row whose min d2 <= zf is
-      // "on a centroid", decided at the end); pad centroids (last stage only) are masked.
-      const int kvalid = K - (t * BN + q * 32 + 4 * h);
-      if (kvalid >= 28) {  // every centroid of this lane's 16 rows exists
-#pragma unroll
-        for (int p = 0; p < P; ++p) {
-          float mpk = INFINITY, sp = 0.f;
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const float d2 = fmaxf(acc[p][i] + xn[p], zf[p]);
-            sp += mt<MODE>(d2, prm.expo);
-            mpk = __builtin_fminf(mpk, __uint_as_float((__float_as_uint(d2) & ~15u) | (unsigned)i));
-          }
-          S[p] += sp;
-          const bool up = mpk < best[p];
-          best[p] = up ? mpk : best[p];
-          bt[p] = up ? (2 * t + q) : bt[p];
-        }
-      } else {
-#pragma unroll
-        for (int p = 0; p < P; ++p) {
-          float mpk = INFINITY, sp = 0.f;
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const bool v = (i & 3) + 8 * (i >> 2) < kvalid;
-            const float d2 = fmaxf(acc[p][i] + xn[p], zf[p]);
-            sp += v ? mt<MODE>(d2, prm.expo) : 0.f;
-            const float pk = __uint_as_float((__float_as_uint(d2) & ~15u) | (unsigned)i);
-            mpk = v ? __builtin_fminf(mpk, pk) : mpk;
-          }
-          S[p] += sp;
-          const bool up = mpk < best[p];
-          best[p] = up ? mpk : best[p];
-          bt[p] = up ? (2 * t + q) : bt[p];
-        }
-      }
-    }
+    const float* ns = s_n[buf];
+    TDC_PHASE(acc0, 0)
+    if (t > 0) TDC_EPI(acc1, 1, t - 1)
+    TDC_PHASE(acc1, 1)
+    TDC_EPI(acc0, 0, t)
     if (t + 1 < nstages) TDC_STAGE_STORE(buf ^ 1)
     __syncthreads();
   }
+  TDC_EPI(acc1, 1, nstages - 1)
+#undef TDC_PHASE
+#undef TDC_EPI
 #undef TDC_STAGE_LOAD
 #undef TDC_STAGE_STORE
 
-#pragma unroll
-  for (int p = 0; p < P; ++p) {
-    S[p] += __shfl_xor(S[p], 32, 64);
-    const unsigned e0 = __float_as_uint(best[p]) & 15u;
-    const int l0 = bt[p] * 32 + (int)(e0 & 3) + 8 * (int)(e0 >> 2) + 4 * h;
-    const float v0 = __uint_as_float(__float_as_uint(best[p]) & ~15u);
-    const float v1 = __shfl_xor(v0, 32, 64);
-    const int l1 = __shfl_xor(l0, 32, 64);
-    const bool other = (v1 < v0) || (v1 == v0 && l1 < l0);
-    const int64_t row = pbase + p * 32 + r;
-    if (h == 0 && row < N) {
-      // on a centroid: the nearest distance is at the floor (one zero-distance centroid
-      // is assumed for the one-hot case; the exact tower counts duplicates)
-      const bool on = (other ? v1 : v0) <= __uint_as_float(__float_as_uint(zf[p]) & ~15u);
-      labels[row] = (on && prm.nz) ? 0 : (other ? l1 : l0);
-      rowinfo[row] = on ? (prm.nz ? 0.f : -1.f) : __builtin_amdgcn_rcpf(S[p]);
-    }
+  S += __shfl_xor(S, 32, 64);
+  const unsigned e0 = __float_as_uint(best) & 15u;
+  const int l0 = bt * 32 + (int)(e0 & 3) + 8 * (int)(e0 >> 2) + 4 * h;
+  const float v0 = __uint_as_float(__float_as_uint(best) & ~15u);
+  const float v1 = __shfl_xor(v0, 32, 64);
+  const int l1 = __shfl_xor(l0, 32, 64);
+  const bool other = (v1 < v0) || (v1 == v0 && l1 < l0);
+  if (h == 0 && row0 < N) {
+    // on a centroid: the nearest distance is at the floor (one zero-distance centroid is
+    // assumed for the one-hot case; the exact tower counts duplicates)
+    const bool on = (other ? v1 : v0) <= __uint_as_float(__float_as_uint(zf) & ~15u);
+    labels[row0] = (on && prm.nz) ? 0 : (other ? l1 : l0);
+    rowinfo[row0] = on ? (prm.nz ? 0.f : -1.f) : __builtin_amdgcn_rcpf(S);
   }
 }
 
@@ -356,12 +342,14 @@ __global__ __launch_bounds__(256, 1) void fcm_mfma_accum_kernel(
     if (more) TDC_TILE_LOAD(r0 + TP)
     const char* xh = s_x[buf];
     const char* xl = s_x[buf] + IMG;
+    // distances of both 32-point halves first, so the membership VALU of half 0 can issue
+    // beside the MFMAs of half 1 and of the W^T X products
+    f32x16 acc[2];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       // ---- distances: rows (registers) = points, lane column = centroid ----
-      f32x16 acc;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[i] = ccl;
+      for (int i = 0; i < 16; ++i) acc[sub][i] = ccl;
       const int prow = sub * 32 + r;
       bf16x8 ah = as_bf16x8(*reinterpret_cast<const uint4*>(xh + xoff<DP>(prow, h * (CPR / 2))));
       bf16x8 al = as_bf16x8(*reinterpret_cast<const uint4*>(xl + xoff<DP>(prow, h * (CPR / 2))));
@@ -370,12 +358,15 @@ __global__ __launch_bounds__(256, 1) void fcm_mfma_accum_kernel(
         const int kn = kk + 1 < KS ? kk + 1 : kk;
         const bf16x8 ahn = as_bf16x8(*reinterpret_cast<const uint4*>(xh + xoff<DP>(prow, h * (CPR / 2) + kn)));
         const bf16x8 aln = as_bf16x8(*reinterpret_cast<const uint4*>(xl + xoff<DP>(prow, h * (CPR / 2) + kn)));
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, ch[kk], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, cl[kk], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, ch[kk], acc, 0, 0, 0);
+        acc[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, ch[kk], acc[sub], 0, 0, 0);
+        acc[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, cl[kk], acc[sub], 0, 0, 0);
+        acc[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, ch[kk], acc[sub], 0, 0, 0);
         ah = ahn;
         al = aln;
       }
+    }
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
       // ---- memberships -> w = wh + wl (bf16 pair); register i = point (i&3)+8(i>>2)+4h ----
       // padded rows carry info 0 (w = 0); pad centroids give finite w whose slab rows the
       // reduction never reads
@@ -389,7 +380,7 @@ __global__ __launch_bounds__(256, 1) void fcm_mfma_accum_kernel(
         for (int e = 0; e < 4; ++e) {
           const int i = 4 * g4 + e;
           const float zf = ZERO_FLOOR * xq[e];
-          const float d2 = fmaxf(acc[i] + xq[e], zf);
+          const float d2 = fmaxf(acc[sub][i] + xq[e], zf);
           float u = mt<MODE>(d2, prm.expo) * iq[e];
           if constexpr (!NZ) u = iq[e] < 0.f ? (d2 <= zf ? 1.f : 0.f) : u;
           const float wv = mw<MODE>(u, prm.m);
@@ -470,7 +461,8 @@ __global__ __launch_bounds__(256) void fcm_reduce_kernel(const float* __restrict
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict__ src, int64_t rows,
                                                          int64_t valid, int d, int64_t ld, int DP,
-                                                         int neg2, __bf16* __restrict__ hi,
+                                                         int neg2, const float* __restrict__ shift,
+                                                         __bf16* __restrict__ hi,
                                                          __bf16* __restrict__ lo,
                                                          float* __restrict__ norm) {
   const int lane = threadIdx.x & 63;
@@ -478,7 +470,7 @@ __global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict
        row += (int64_t)gridDim.x * 4) {
     float s = 0.f;
     for (int c = lane; c < DP; c += 64) {
-      const float v = (row < valid && c < d) ? src[row * ld + c] : 0.f;
+      const float v = (row < valid && c < d) ? src[row * ld + c] - (shift ? shift[c] : 0.f) : 0.f;
       s = fmaf(v, v, s);
       const float t = neg2 ? -2.f * v : v;
       const __bf16 vh = (__bf16)t;
@@ -505,10 +497,11 @@ template <int DP>
 int launch_mstats(const void* Xh, const void* Xl, const float* xx, int64_t N, const void* Ch,
                   const void* Cl, const float* cc, int K, int Kp, double m, int nz,
                   int32_t* labels, float* rowinfo, hipStream_t s) {
-  const int64_t blocks = (N + 255) / 256;
+  constexpr int WAVES = 8;
+  const int64_t blocks = (N + WAVES * 32 - 1) / (WAVES * 32);
   const MParam p = make_mparam(m, nz);
 #define TDC_LS(MODE)                                                                          \
-  hipLaunchKernelGGL((fcm_mfma_stats_kernel<DP, MODE>), dim3((unsigned)blocks), dim3(256), 0, s, \
+  hipLaunchKernelGGL((fcm_mfma_stats_kernel<DP, MODE, WAVES>), dim3((unsigned)blocks), dim3(WAVES * 64), 0, s, \
                      (const __bf16*)Xh, (const __bf16*)Xl, xx, N, (const __bf16*)Ch,          \
                      (const __bf16*)Cl, cc, K, Kp / 64, p, labels, rowinfo)
   if (m == 2.0) TDC_LS(2); else TDC_LS(0);
@@ -564,12 +557,13 @@ int launch_maccum(const void* Xh, const void* Xl, const float* xx, const float* 
 using namespace tdc;
 
 int tdc_fcm_split_rows(const float* src, int64_t rows, int64_t valid, int d, int64_t ld, int DP,
-                       int neg2, void* hi, void* lo, float* norm, hipStream_t s) {
+                       int neg2, const float* shift, void* hi, void* lo, float* norm,
+                       hipStream_t s) {
   if (rows <= 0) return 0;
   int64_t blocks = (rows + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(split_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, rows, valid,
-                     d, ld, DP, neg2, (__bf16*)hi, (__bf16*)lo, norm);
+                     d, ld, DP, neg2, shift, (__bf16*)hi, (__bf16*)lo, norm);
   TDC_CHECK_LAUNCH();
   return 0;
 }

@@ -93,8 +93,10 @@ int tdc_fcm_tower(int pass, int dtype, const void* X, int64_t N, int64_t ldx, in
 // (of -2v when neg2) + norm [rows] = ||v||^2 (nullable).  fcm_mfma pass 0: labels +
 // rowinfo (fp32, as tdc_fcm_tower); pass 1: wx [K, D] / ws [K] (fp64) += W^T X / sum W.
 // DP in {32, 64, 128}; Ch/Cl/cc have Kp rows (Kp % 128 == 0).
+// shift (nullable, fp32 [d]) is subtracted from every row first.
 int tdc_fcm_split_rows(const float* src, int64_t rows, int64_t valid, int d, int64_t ld, int DP,
-                       int neg2, void* hi, void* lo, float* norm, hipStream_t stream);
+                       int neg2, const float* shift, void* hi, void* lo, float* norm,
+                       hipStream_t stream);
 // work: fp32 [tdc_fcm_mfma_workspace(...)] per-block partial slabs of pass 1.
 int tdc_fcm_mfma(int pass, const void* Xh, const void* Xl, const float* xx, int64_t N, int DP,
                  int D, const void* Ch, const void* Cl, const float* cc, int K, int Kp, double m,

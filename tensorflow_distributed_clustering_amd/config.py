@@ -79,6 +79,7 @@ class ClusterConfig:
     fp8_recheck: float = 0.0    # fp8: exact re-check of near ties (relative margin; 0 = off)
     comm_mode: str = "auto"     # 'allreduce' | 'rsag' | 'auto' (parallel/dist.py)
     bucket_kb: int = 0          # all-reduce bucket size (0: one call per iteration)
+    oom_recovery: bool = True   # mid-run OOM on any rank -> roll back one step, go streamed
 
     def __post_init__(self):
         if self.n_clusters <= 0:

@@ -173,6 +173,31 @@ class HostSource:
         torch.cuda.current_stream(self.device).synchronize()
 
 
+class PlainHostSource:
+    """Host-resident shard streamed as plain row slices (any dtype, e.g. fp64 FCM, which
+    the bf16/fp32 RowStreamer does not produce): pinned staging + one H2D per chunk."""
+
+    def __init__(self, x_host: np.ndarray, layout: Layout, device, row_offset: int = 0):
+        self.x = x_host
+        self.n_rows, self.d = x_host.shape
+        self.layout = layout
+        self.device = torch.device(device)
+        self.row_offset = row_offset
+
+    def chunks(self, chunk_rows: int) -> Iterator[Tuple[int, torch.Tensor]]:
+        chunk_rows = min(chunk_rows or self.n_rows, self.n_rows)
+        dt, width = self.layout
+        for s in range(0, self.n_rows, chunk_rows):
+            part = torch.from_numpy(np.ascontiguousarray(self.x[s:s + chunk_rows])).to(dt)
+            if self.device.type == "cuda":
+                part = part.pin_memory().to(self.device, non_blocking=True)
+            yield self.row_offset + s, to_layout(part, (dt, width))
+
+    def rows(self, idx: torch.Tensor) -> torch.Tensor:
+        sel = torch.from_numpy(np.ascontiguousarray(self.x[idx.cpu().numpy()]))
+        return sel.to(self.layout[0]).to(self.device)
+
+
 def plan_chunk_rows(n_rows: int, row_bytes: int, k: int, d: int, device,
                     budget_gb: float = 0.0, reserve_frac: float = 0.15,
                     per_row_extra: int = 16) -> int:

@@ -6,61 +6,160 @@ W X (cuBLAS DGEMM) and sum(W); CPU AddN + Div + Assign (`:139-148`).  The fuzzif
 is the data dimension (``m := M``, `:97,121,129`) -- reproduced when
 ``cfg.fuzzifier is None`` -- and the label pass is ``argmax_k u`` (`:141`).
 
-Here: one fused HIP kernel per rank (N4/N5) for small K x D, one packed all-reduce of
-[sum W X | sum W], and the N3 divide.
+Here: the native FCM tower per rank (``ops.make_fcm_ops``: fused small-K*D kernel, exact
+SIMT tower, or the bf16x3 MFMA tower), one packed all-reduce of [sum W X | sum W], the N3
+divide.  Like K-Means, the shard may stay on the host and stream through HBM in chunks
+(the partials of all chunks add up before the single all-reduce, so a streamed pass is the
+exact FCM step), and an out-of-memory error -- while building the engine or inside any
+iteration, on any rank -- makes every rank continue streamed with smaller chunks (the
+reference doubled its batch count and restarted on ResourceExhaustedError, `:331-360`).
 """
 from __future__ import annotations
 
 import time
 from typing import Optional
 
+import numpy as np
 import torch
 
 from ..config import ClusterConfig
+from ..data.stream import (HostSource, PlainHostSource, ResidentSource, plan_chunk_rows,
+                           plan_resident_rows)
 from ..ops import make_fcm_ops
 from ..parallel.dist import Comm, local_comm
 from ..utils import faults
 from ..utils.checkpoint import RunCheckpointer
 from ..utils.timers import DeviceTimer, sync
-from .init import init_centers
+from .init import init_centers, init_centers_from_source
 from .kmeans import ClusterResult, _shard_geometry
 
 
-class FcmEngine:
-    """Resident state of one distributed FCM run; ``step()`` = one iteration (fused tower
-    kernel, one packed all-reduce of [sum W X | sum W], the N3 divide).  Timed by bench.py."""
+def fcm_dtype(cfg: ClusterConfig) -> torch.dtype:
+    """Memberships need exact-difference-grade distances: bf16/fp8 configs run fp32."""
+    return torch.float64 if cfg.dtype == "fp64" else torch.float32
 
-    def __init__(self, x_local, cfg: ClusterConfig, comm: Comm, n_global: int, row_offset: int,
-                 init_centers_=None, m: Optional[float] = None):
+
+class FcmEngine:
+    """Resident or streamed state of one distributed FCM run; ``step()`` = one iteration
+    (native tower over the shard or its chunks, one packed all-reduce of
+    [sum W X | sum W | oom flag], the N3 divide).  Timed by bench.py."""
+
+    def __init__(self, source, cfg: ClusterConfig, comm: Comm, n_global: int, row_offset: int,
+                 init_centers_=None, m: Optional[float] = None, chunk_rows: int = 0,
+                 defer_init: bool = False):
         self.cfg, self.comm = cfg, comm
-        k, d = cfg.n_clusters, int(x_local.shape[1])
-        self.k, self.d = k, d
+        self.n_global, self.row_offset = n_global, row_offset
+        k = cfg.n_clusters
+        tdt = fcm_dtype(cfg)
+        dt_name = "fp64" if tdt == torch.float64 else "fp32"
+        if isinstance(source, torch.Tensor):
+            d = int(source.shape[1])
+            dev = source.device
+            self._x0 = source
+            self.n_local = int(source.shape[0])
+        else:
+            d = int(source.d)
+            dev = torch.device(getattr(source, "device", comm.device))
+            self._x0 = None
+            self.n_local = int(source.n_rows)
+        self.k, self.d, self.device = k, d, dev
         self.m = float(m) if m is not None else (float(cfg.fuzzifier) if cfg.fuzzifier is not None
                                                  else float(d))
-        dev = x_local.device
-        self.device = dev
-        self.local = make_fcm_ops(x_local, k, cfg.dtype, self.m, cfg.fcm_nan_to_zero, cfg.backend)
-        self.c0 = init_centers(cfg.init, x_local, row_offset, n_global, k, comm, cfg.seed,
-                               given=init_centers_)
-        self.C = self.c0.to(self.local.c_dtype).clone().contiguous()
-        self.buf = torch.zeros(k * d + k, dtype=torch.float64, device=dev)
+        if isinstance(source, torch.Tensor) and not chunk_rows:
+            self.local = make_fcm_ops(source, k, dt_name, self.m, cfg.fcm_nan_to_zero, cfg.backend)
+            self.source = None
+        else:
+            if isinstance(source, torch.Tensor):  # device-resident shard, walked in chunks
+                source = ResidentSource(source.to(tdt), (tdt, d), row_offset)
+            probe = torch.zeros(1, d, dtype=tdt, device=dev)
+            self.local = make_fcm_ops(probe, k, dt_name, self.m, cfg.fcm_nan_to_zero, cfg.backend)
+            self.source = source
+        self.chunk_rows = chunk_rows
+        self.streamed = self.source is not None
+        self._init_given = init_centers_
+        # [sum W X | sum W | oom flag] (fp64)
+        self.oom_guard = bool(cfg.oom_recovery)
+        self.buf = torch.zeros(k * d + k + (1 if self.oom_guard else 0), dtype=torch.float64,
+                               device=dev)
         self.wx = self.buf[: k * d].view(k, d)
-        self.ws = self.buf[k * d:]
-        self.labels = torch.zeros(self.local.n, dtype=torch.int32, device=dev)
+        self.ws = self.buf[k * d: k * d + k]
+        self.oom_flag = self.buf[-1:] if self.oom_guard else None
+        self.C = torch.zeros(k, d, dtype=self.local.c_dtype, device=dev)
+        self.labels = torch.zeros(self.n_local, dtype=torch.int32, device=dev)
         self.shift = torch.zeros(1, dtype=torch.float32, device=dev) if cfg.tol > 0 else None
         self.n_iter = 0
+        self.c0 = None
+        if not defer_init:
+            self.init_centroids()
+
+    def init_centroids(self):
+        cfg = self.cfg
+        if self._x0 is not None:
+            c0 = init_centers(cfg.init, self._x0, self.row_offset, self.n_global, self.k,
+                              self.comm, cfg.seed, given=self._init_given)
+        else:
+            c0 = init_centers_from_source(cfg.init, self.source, self.row_offset, self.n_global,
+                                          self.k, self.comm, cfg.seed, given=self._init_given,
+                                          d=self.d)
+        self.c0 = c0
+        self.C.copy_(c0.to(self.local.c_dtype))
+        self._x0 = None
+        return self
+
+    def _chunks(self):
+        return self.source.chunks(self.chunk_rows)
+
+    def _local_step(self):
+        if not self.streamed:
+            self.local.step(self.C, self.labels, self.wx, self.ws)
+            return
+        for start, chunk in self._chunks():
+            s = start - self.row_offset
+            self.local.bind(chunk).step(self.C, self.labels[s:s + chunk.shape[0]], self.wx,
+                                        self.ws)
 
     def step(self):
         self.buf.zero_()
-        self.local.step(self.C, self.labels, self.wx, self.ws)
+        try:
+            if self.oom_guard:
+                faults.maybe_fail(str(self.n_iter + 1), self.comm.rank, kinds=("oom",))
+            self._local_step()
+        except Exception as e:  # noqa: BLE001 - filtered right below
+            if self.oom_flag is None or not faults.is_oom(e):
+                raise
+            self.buf.zero_()
+            self.oom_flag.fill_(1.0)  # every rank still joins the all-reduce and sees it
         self.comm.allreduce_(self.buf)
         if self.shift is not None:
             self.shift.zero_()
         self.local.finalize(self.wx, self.ws, self.C, self.shift)
         self.n_iter += 1
 
+    # mid-run OOM recovery (same protocol as LloydEngine)
+    def oom_pending(self) -> bool:
+        return self.oom_flag is not None and float(self.oom_flag.item()) > 0
+
+    def save_state(self):
+        if getattr(self, "_c_prev", None) is None:
+            self._c_prev = torch.empty_like(self.C)
+        self._c_prev.copy_(self.C)
+        self._n_prev = self.n_iter
+
+    def rollback(self) -> np.ndarray:
+        self.C.copy_(self._c_prev)
+        self.n_iter = self._n_prev
+        return self.C.double().cpu().numpy()
+
+    def centers(self) -> torch.Tensor:
+        return self.C
+
     def label_pass(self):
-        self.local.assign(self.C, self.labels)
+        if not self.streamed:
+            self.local.assign(self.C, self.labels)
+            return
+        for start, chunk in self._chunks():
+            s = start - self.row_offset
+            self.local.bind(chunk).assign(self.C, self.labels[s:s + chunk.shape[0]])
 
 
 class FuzzyCMeans:
@@ -73,42 +172,137 @@ class FuzzyCMeans:
     def fuzzifier(self, d: int) -> float:
         return float(self.cfg.fuzzifier) if self.cfg.fuzzifier is not None else float(d)
 
+    def _target_device(self, x):
+        if self.device is not None:
+            return torch.device(self.device)
+        if self.comm is not None:
+            return self.comm.device
+        if isinstance(x, torch.Tensor):
+            return x.device
+        return torch.device(getattr(x, "device", "cpu"))
+
+    def _make_source(self, x_local, dev, row_offset, chunk_override: int = 0):
+        """(source, chunk_rows): the resident shard, or a host source streamed in chunks
+        when it does not fit the HBM budget (or cfg.chunk_rows / an OOM retry asks)."""
+        cfg = self.cfg
+        want = chunk_override or cfg.chunk_rows
+        if hasattr(x_local, "chunks"):
+            return x_local, want or (1 << 22)
+        tdt = fcm_dtype(cfg)
+        if isinstance(x_local, torch.Tensor) and x_local.device.type != "cpu":
+            return x_local.to(dev), want
+        xn = x_local.numpy() if isinstance(x_local, torch.Tensor) else np.asarray(x_local)
+        n, d = xn.shape
+        if dev.type == "cuda":
+            es = 8 if tdt == torch.float64 else 4
+            # MFMA tower keeps hi/lo bf16 rows + norms + row info next to the chunk
+            row_bytes = d * es + 4 * d + 16
+            chunk = want or plan_chunk_rows(n, row_bytes, cfg.n_clusters, d, dev,
+                                            cfg.hbm_budget_gb)
+            if chunk:
+                layout = (tdt, d)
+                if tdt == torch.float32:
+                    resident = 0 if want else plan_resident_rows(n, d * es, chunk, cfg.n_clusters,
+                                                                 d, dev, cfg.hbm_budget_gb)
+                    return HostSource(xn, layout, dev, row_offset, resident_rows=resident), chunk
+                return PlainHostSource(xn, layout, dev, row_offset), chunk
+        elif want:
+            return PlainHostSource(xn, (tdt, d), dev, row_offset), want
+        return torch.as_tensor(xn).to(dev), want
+
+    def _build_engine(self, first, x_local, dev, comm, n_global, row_offset, n_local, init_c,
+                      start_iter, m):
+        """FcmEngine with the collective setup-OOM agreement (see KMeans._build_engine);
+        ``first`` is a one-element list that is emptied here."""
+        cfg = self.cfg
+        chunk = 0
+        err = None
+        for attempt in range(cfg.max_oom_retries + 1):
+            err = None
+            eng = source = None
+            try:
+                if first:
+                    source, chunk_rows = first.pop()
+                else:
+                    source, chunk_rows = self._make_source(x_local, dev, row_offset, chunk)
+                chunk = chunk_rows or chunk
+                faults.maybe_fail("setup", comm.rank)
+                eng = FcmEngine(source, cfg, comm, n_global, row_offset, init_c, m, chunk_rows,
+                                defer_init=True)
+            except Exception as e:  # noqa: BLE001 - filtered right below
+                if not faults.is_oom(e):
+                    raise
+                err = e
+            if comm.max_scalar(1.0 if err is not None else 0.0) == 0.0:
+                eng.init_centroids()
+                eng.n_iter = start_iter
+                return eng
+            del eng, source
+            if dev.type == "cuda":
+                torch.cuda.empty_cache()
+            chunk = max(1024, (chunk or n_local) // 2)
+            if comm.is_root:
+                print(f"[fcm] out of memory while building the engine "
+                      f"({type(err).__name__ if err else 'peer rank'}); retrying streamed with "
+                      f"chunk_rows={chunk}", flush=True)
+        raise err if err is not None else faults.oom_error("out of memory on a peer rank")
+
     def fit(self, x_local, init_centers_=None, n_global=None, row_offset=None) -> "FuzzyCMeans":
         cfg = self.cfg
         if cfg.spherical:
             raise ValueError("spherical=True is implemented for KMeans (Lloyd) only")
         t0 = time.perf_counter()
-        x_local = torch.as_tensor(x_local)
-        dev = torch.device(self.device) if self.device is not None else (
-            self.comm.device if self.comm is not None else x_local.device)
-        if x_local.device != dev:
-            x_local = x_local.to(dev)
+        if not hasattr(x_local, "chunks") and not isinstance(x_local, (torch.Tensor, np.ndarray)):
+            x_local = np.asarray(x_local)
+        dev = self._target_device(x_local)
         if self.comm is None:
             self.comm = local_comm(dev)
         comm = self.comm
+        n_local = int(x_local.n_rows if hasattr(x_local, "n_rows") else x_local.shape[0])
+        d = int(x_local.d if hasattr(x_local, "d") else x_local.shape[1])
         if n_global is None or row_offset is None:
-            n_global, row_offset = _shard_geometry(int(x_local.shape[0]), comm)
-        k, d = cfg.n_clusters, int(x_local.shape[1])
+            n_global, row_offset = _shard_geometry(n_local, comm)
+        first = [self._make_source(x_local, dev, row_offset)]
         sync(dev)
         initialization_time = time.perf_counter() - t0
 
         t1 = time.perf_counter()
         ckpt = RunCheckpointer(cfg, comm, "distributedFuzzyCMeans")
-        resumed = ckpt.load_for_resume(k, d)
+        resumed = ckpt.load_for_resume(cfg.n_clusters, d)
         start_iter = 0
         if resumed is not None:
             init_centers_, start_iter = resumed.centers, resumed.n_iter
-        eng = FcmEngine(x_local, cfg, comm, n_global, row_offset, init_centers_, self.fuzzifier(d))
-        eng.n_iter = start_iter
+        m = self.fuzzifier(d)
+        eng = self._build_engine(first, x_local, dev, comm, n_global, row_offset, n_local,
+                                 init_centers_, start_iter, m)
+        self.engine_ = eng
         sync(dev)
         setup_time = time.perf_counter() - t1
 
         timer = DeviceTimer(dev)
         timer.start()
         history = []
-        centers_host = lambda: eng.C.double().cpu().numpy()
-        for _ in range(start_iter, cfg.max_iter):
+        centers_host = lambda: self.engine_.C.double().cpu().numpy()
+        while eng.n_iter < cfg.max_iter:
+            if eng.oom_guard:
+                eng.save_state()
             eng.step()
+            if eng.oom_guard and eng.oom_pending():
+                c_host, n_back, c0 = eng.rollback(), eng._n_prev, eng.c0
+                chunk = max(1024, (eng.chunk_rows or n_local) // 2)
+                del eng
+                self.engine_ = None
+                if dev.type == "cuda":
+                    torch.cuda.empty_cache()
+                if comm.is_root:
+                    print(f"[fcm] out of memory in iteration {n_back + 1}; continuing streamed "
+                          f"with chunk_rows={chunk}", flush=True)
+                eng = self._build_engine([self._make_source(x_local, dev, row_offset, chunk)],
+                                         x_local, dev, comm, n_global, row_offset, n_local,
+                                         c_host, n_back, m)
+                eng.c0 = c0
+                self.engine_ = eng
+                continue
             n_iter = eng.n_iter
             if eng.shift is not None:
                 sv = float(eng.shift.item())
@@ -116,7 +310,7 @@ class FuzzyCMeans:
                 if sv <= cfg.tol:
                     break
             ckpt.maybe_save(n_iter, centers_host)
-            faults.maybe_fail(str(n_iter), comm.rank)
+            faults.maybe_fail(str(n_iter), comm.rank, kinds=("crash",))
         computation_time = timer.stop()
         n_iter = eng.n_iter
         ckpt.maybe_save(n_iter, centers_host, final=True)
@@ -129,7 +323,7 @@ class FuzzyCMeans:
             labels=eng.labels, counts=eng.ws.double().cpu().numpy(), n_iter=n_iter, inertia=None,
             setup_time=setup_time, initialization_time=initialization_time,
             computation_time=computation_time, backend=eng.local.name, history=history,
-            n_global=n_global)
+            n_global=n_global, streamed=eng.streamed)
         return self
 
     @property

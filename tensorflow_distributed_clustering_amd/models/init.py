@@ -300,12 +300,12 @@ def init_centers(method: str, x_local: torch.Tensor, row_offset: int, n_global: 
 # ------------------------------------------------------------------ chunk sources
 def _source_rows(source, local_idx, d: int) -> torch.Tensor:
     """float64 rows (local indices) of a chunk source, on the source's device."""
-    from ..data.stream import HostSource, ResidentSource, SyntheticSource
+    from ..data.stream import HostSource, PlainHostSource, ResidentSource, SyntheticSource
     from ..data.synth import gaussian_blob_rows
     if isinstance(source, ResidentSource):
         idx = torch.as_tensor(local_idx, dtype=torch.int64, device=source.x.device)
         return source.x.index_select(0, idx)[:, :d].double()
-    if isinstance(source, HostSource):
+    if isinstance(source, (HostSource, PlainHostSource)):
         rows = np.asarray(source.x[np.asarray(local_idx, dtype=np.int64)], dtype=np.float64)
         return torch.from_numpy(rows).to(source.device)
     if isinstance(source, SyntheticSource):

@@ -143,7 +143,10 @@ class LloydEngine:
         # buf = [sums kpad*D | counts kpad | (hi kpad | lo kpad) | (flags kpad)]: the sums
         # block is what a reduce-scatter splits by rank; the small tail is all-reduced
         nsmall = 1 + (2 if self.count_split else 0) + (1 if self.nan_any else 0)
-        self.buf = torch.zeros(kpad * self.d + nsmall * kpad, dtype=acc, device=dev)
+        # + 1 slot: "a rank ran out of memory in this step's local work" (oom_pending)
+        self.oom_guard = bool(cfg.oom_recovery) and self.oom_guard_ok
+        self.buf = torch.zeros(kpad * self.d + nsmall * kpad + (1 if self.oom_guard else 0),
+                               dtype=acc, device=dev)
         self.sums_pad = self.buf[: kpad * self.d].view(kpad, self.d)
         self.sums = self.sums_pad[:k]
         self.small = self.buf[kpad * self.d:]
@@ -156,6 +159,7 @@ class LloydEngine:
             self.local.set_count_split(self.cnt_hi, self.cnt_lo)
             row = 3
         self.empty_flags = self.small[row * kpad: row * kpad + k] if self.nan_any else None
+        self.oom_flag = self.buf[-1:] if self.oom_guard else None
         self.C_pad = torch.zeros(kpad, self.d, dtype=self.local.c_dtype, device=dev)
         self.C = self.C_pad[:k]
         if self.rsag:
@@ -179,6 +183,8 @@ class LloydEngine:
 
     # exact count halves in the buffer (subclasses with their own count bookkeeping: off)
     exact_counts_ok = True
+    # mid-run OOM flag in the buffer (subclasses with their own step: off)
+    oom_guard_ok = True
     # reduce-scatter / all-gather mode allowed (subclasses that read the whole buf: off)
     rsag_ok = True
     RSAG_MIN_BYTES = 32 << 20
@@ -239,15 +245,18 @@ class LloydEngine:
     def _eager_step(self, with_inertia: bool = False) -> Optional[float]:
         self.buf.zero_()
         mind = self.mind if (with_inertia and self.mind is not None) else None
-        if not self.streamed:
-            self.local.step(self.C, self.labels, mind, self.sums, self.counts)
-        else:
-            for start, chunk in self._chunks():
-                s = start - self.source.row_offset  # chunk starts are source-global
-                e = s + chunk.shape[0]
-                self.local.bind(chunk).step(self.C, self.labels[s:e],
-                                            None if mind is None else mind[s:e],
-                                            self.sums, self.counts)
+        try:
+            if self.oom_guard:
+                faults.maybe_fail(str(self.n_iter + 1), self.comm.rank, kinds=("oom",))
+            self._local_step(mind)
+        except Exception as e:  # noqa: BLE001 - filtered right below
+            if self.oom_flag is None or not faults.is_oom(e):
+                raise
+            # every rank still joins this step's collectives; the flag makes them all see it
+            self.buf.zero_()
+            self.oom_flag.fill_(1.0)
+            if mind is not None:
+                mind.zero_()
         inertia = self.comm.sum_scalar(float(mind.double().sum())) if mind is not None else None
         if self.nan_any:
             self.empty_flags.copy_((self.counts == 0).to(self.buf.dtype))
@@ -268,6 +277,43 @@ class LloydEngine:
             self._reseed()
         self.n_iter += 1
         return inertia
+
+    def _local_step(self, mind):
+        if not self.streamed:
+            self.local.step(self.C, self.labels, mind, self.sums, self.counts)
+        else:
+            for start, chunk in self._chunks():
+                s = start - self.source.row_offset  # chunk starts are source-global
+                e = s + chunk.shape[0]
+                self.local.bind(chunk).step(self.C, self.labels[s:e],
+                                            None if mind is None else mind[s:e],
+                                            self.sums, self.counts)
+
+    # ----------------------------------------------------------- mid-run OOM recovery
+    def oom_pending(self) -> bool:
+        """Did any rank run out of memory in the last step (host sync; fit() checks it)?"""
+        return self.oom_flag is not None and float(self.oom_flag.item()) > 0
+
+    def save_state(self):
+        """Keep the pre-step centroids (this rank's slice under rsag) for a rollback."""
+        if self.rsag:
+            src = self.C_pad[self._r0: self._r0 + self._kr]
+        else:
+            src = self.C
+        if getattr(self, "_c_prev", None) is None or self._c_prev.shape != src.shape:
+            self._c_prev = torch.empty_like(src)
+        self._c_prev.copy_(src)
+        self._n_prev = self.n_iter
+
+    def rollback(self) -> np.ndarray:
+        """Centroids before the failed step (replicated, host fp64); resets n_iter."""
+        if self.rsag:
+            self.C_pad[self._r0: self._r0 + self._kr].copy_(self._c_prev)
+            self._c_synced = False
+        else:
+            self.C.copy_(self._c_prev)
+        self.n_iter = self._n_prev
+        return self.centers().double().cpu().numpy()
 
     def _reduce_scatter_finalize(self):
         """rsag mode: reduce-scatter the sums (rank r gets centroid rows [r0, r0 + kr)),
@@ -418,6 +464,8 @@ class KMeans:
 
     def _build_engine(self, first, x_local, dev, comm, n_global, row_offset, n_local,
                       init_centers_, start_iter):
+        """``first``: a one-element list holding the first (source, chunk_rows); it is
+        emptied here, so a retry after an OOM does not keep the failed device copy alive."""
         """LloydEngine with collective OOM handling: if any rank runs out of memory while
         building the engine, every rank halves the streamed chunk and retries (the
         reference doubled its batch count on ResourceExhaustedError,
@@ -428,11 +476,10 @@ class KMeans:
             err = None
             eng = source = None
             try:
-                if attempt == 0:
-                    source, chunk_rows = first
+                if first:
+                    source, chunk_rows = first.pop()
                 else:
                     source, chunk_rows = self._make_source(x_local, dev, row_offset, chunk)
-                first = None
                 faults.maybe_fail("setup", comm.rank)
                 cls = LloydEngine
                 if cfg.algorithm == "bounded":
@@ -456,6 +503,28 @@ class KMeans:
                       f"({type(err).__name__ if err else 'peer rank'}); retrying streamed with "
                       f"chunk_rows={chunk}", flush=True)
         raise err if err is not None else faults.oom_error("out of memory on a peer rank")
+
+    def _recover_oom(self, eng, x_local, dev, comm, n_global, row_offset, n_local):
+        """A rank ran out of memory inside the last step (flag in the all-reduce buffer):
+        every rank rolls back to the pre-step centroids and continues from the same
+        iteration on a streamed engine with half the chunk (the reference restarted the
+        whole run with twice the batches, `scripts/distribuitedClustering.py:357-360`)."""
+        c_host = eng.rollback()
+        n_back = eng.n_iter
+        chunk = max(1024, (eng.chunk_rows or n_local) // 2)
+        c0 = eng.c0
+        del eng
+        self.engine_ = None
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
+        if comm.is_root:
+            print(f"[kmeans] out of memory in iteration {n_back + 1}; continuing streamed with "
+                  f"chunk_rows={chunk}", flush=True)
+        eng = self._build_engine([self._make_source(x_local, dev, row_offset, chunk)], x_local,
+                                 dev, comm, n_global, row_offset, n_local, c_host, n_back)
+        eng.c0 = c0
+        self.engine_ = eng
+        return eng
 
     def fit(self, x_local, init_centers_: Optional[np.ndarray] = None,
             n_global: Optional[int] = None, row_offset: Optional[int] = None) -> "KMeans":
@@ -482,9 +551,9 @@ class KMeans:
             if comm.is_root:
                 print(f"[kmeans] resuming from {cfg.checkpoint_path} at iteration {start_iter}",
                       flush=True)
+        first = [first]  # handed over: _build_engine drops it before any retry
         eng = self._build_engine(first, x_local, dev, comm, n_global, row_offset, n_local,
                                  init_centers_, start_iter)
-        del first
         if cfg.graph and eng.graphable() and comm.world_size == 1:
             eng.capture()
         sync(dev)
@@ -492,12 +561,18 @@ class KMeans:
 
         # ------------------------------------------------------------ timed loop
         history = []
-        centers_host = lambda: eng.centers().double().cpu().numpy()
+        centers_host = lambda: self.engine_.centers().double().cpu().numpy()
+        self.engine_ = eng
         timer = DeviceTimer(dev)
         timer.start()
-        for _ in range(max(0, cfg.max_iter - start_iter)):
+        while eng.n_iter < cfg.max_iter:
             log_pt = cfg.log_every > 0 and (eng.n_iter + 1) % cfg.log_every == 0
+            if eng.oom_guard:
+                eng.save_state()
             inertia_it = eng.step(with_inertia=log_pt and cfg.compute_inertia)
+            if eng.oom_guard and eng.oom_pending():
+                eng = self._recover_oom(eng, x_local, dev, comm, n_global, row_offset, n_local)
+                continue
             n = eng.n_iter
             if eng.need_shift and (cfg.tol > 0 or log_pt):
                 sv = float(eng.shift.item())
@@ -511,7 +586,7 @@ class KMeans:
                 if cfg.tol > 0 and sv <= cfg.tol:
                     break
             ckpt.maybe_save(n, centers_host)
-            faults.maybe_fail(str(n), comm.rank)
+            faults.maybe_fail(str(n), comm.rank, kinds=("crash",))
         computation_time = timer.stop()
         ckpt.maybe_save(eng.n_iter, centers_host, final=True)
 

@@ -808,7 +808,7 @@ class HipMfmaFCM(_LocalOpsBase):
         self.cl = torch.zeros_like(self.ch)
         self.cc = torch.zeros(self.kp, dtype=torch.float32, device=dev)
         self.xh = self.xl = self.xx = self.rowinfo = None
-        self.work = None
+        self.work = self.mu = None
         self._set_x(x)
 
     @property
@@ -831,7 +831,12 @@ class HipMfmaFCM(_LocalOpsBase):
             self.rowinfo = torch.empty(n, dtype=torch.float32, device=dev)
         xf = x if (x.dtype == torch.float32 and x.stride(1) == 1) else x.float().contiguous()
         self.n = n
-        self.ops.fcm_split_rows(xf[:, : self.d], n, 0, self.xh[:n], self.xl[:n], self.xx[:n])
+        if self.mu is None and n >= 64:  # (not from a 1-row probe of a streamed engine)
+            # fixed shift (first shard / chunk mean): distances are shift-invariant, and the
+            # expansion's cancellation error scales with |x - mu|^2 instead of |x|^2
+            self.mu = xf[:, : self.d].double().mean(0).float()
+        self.ops.fcm_split_rows(xf[:, : self.d], n, 0, self.xh[:n], self.xl[:n], self.xx[:n],
+                                self.mu)
         self.x = None  # the hi/lo rows are the shard from here on
 
     def bind(self, x):
@@ -841,7 +846,8 @@ class HipMfmaFCM(_LocalOpsBase):
         return self
 
     def prepare(self, C):
-        self.ops.fcm_split_rows(C.float().contiguous(), self.k, 1, self.ch, self.cl, self.cc)
+        self.ops.fcm_split_rows(C.float().contiguous(), self.k, 1, self.ch, self.cl, self.cc,
+                                self.mu)
 
     def _ops_args(self):
         n = self.n

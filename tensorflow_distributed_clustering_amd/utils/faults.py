@@ -4,7 +4,9 @@
 
 * ``crash@N``      raise :class:`InjectedFault` after iteration N completes
 * ``oom@setup``    raise an out-of-memory error while the engine is being built
-* ``oom@N``        raise an out-of-memory error after iteration N
+* ``oom@N``        raise an out-of-memory error inside iteration N's local step (the
+                   engines flag it in the all-reduce buffer, every rank rolls back to the
+                   centroids before the step and continues streamed)
 
 ``:rank`` restricts the fault to one rank (default: every rank).  Each entry fires at
 most once per process, so a retry after an injected setup OOM goes through.
@@ -37,9 +39,9 @@ def oom_error(msg: str):
     return cls(msg)
 
 
-def maybe_fail(when: str, rank: int = 0) -> None:
+def maybe_fail(when: str, rank: int = 0, kinds=("crash", "oom")) -> None:
     for e, kind, w, r in _entries():
-        if w != str(when) or (r is not None and r != rank) or e in _FIRED:
+        if w != str(when) or (r is not None and r != rank) or e in _FIRED or kind not in kinds:
             continue
         _FIRED.add(e)
         if kind == "crash":

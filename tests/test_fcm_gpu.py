@@ -91,7 +91,7 @@ def test_fcm_fit_native_backends(gpu, dtype, d, k, backend):
     x = gaussian_blobs(30000, d, k, seed=2, dtype=torch.float64, device=gpu)
     # start next to (not on) data rows: a row exactly on a centroid is the reference's
     # discontinuous NaN -> 0 case, where exact and GEMM-form oracles legitimately differ
-    c0 = (x[:k].cpu() + 0.01).numpy()
+    c0 = (x[:k].cpu() + 0.3).numpy()
     cfg = tdc.ClusterConfig(n_clusters=k, max_iter=4, dtype=dtype, init="given", fuzzifier=2.0)
     r = tdc.FuzzyCMeans(cfg).fit(x, init_centers_=c0).result_
     assert r.backend == backend

@@ -176,6 +176,72 @@ def test_oom_on_one_rank_retries_on_all_ranks():
     np.testing.assert_allclose(centers, single.result_.centers, rtol=1e-10, atol=1e-10)
 
 
+def _midrun_worker(rank, world, port, method, fault, q):
+    env = dict(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+               RANK=str(rank), LOCAL_RANK=str(rank))
+    if fault:
+        env["TDC_FAULT"] = fault
+    os.environ.update(env)
+    torch.set_num_threads(1)
+    import tensorflow_distributed_clustering_amd as tdc
+    from tensorflow_distributed_clustering_amd.parallel import dist as D
+    D._COMM = None
+    comm = D.init_comm("cpu")
+    s, e = comm.shard(4001)
+    x = gaussian_blobs(e - s, 3, 5, seed=2, row_offset=s, dtype=torch.float64)
+    cfg = tdc.ClusterConfig(n_clusters=5, max_iter=6, dtype="fp64", seed=1, init="first_k",
+                            fuzzifier=2.0)
+    model = (tdc.KMeans if method == "kmeans" else tdc.FuzzyCMeans)(cfg, comm)
+    r = model.fit(x, n_global=4001, row_offset=s).result_
+    if rank == 0:
+        q.put((r.centers, r.streamed, r.n_iter))
+    D.destroy_comm()
+
+
+def _run_midrun(method, fault):
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_midrun_worker, args=(r, 2, port, method, fault, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return out
+
+
+@pytest.mark.parametrize("method", ["kmeans", "fcm"])
+def test_mid_run_oom_on_one_rank_continues_streamed(method):
+    """TDC_FAULT=oom@3:1: rank 1 runs out of memory inside iteration 3.  The flag rides in
+    the packed all-reduce, both ranks roll back to the centroids before iteration 3 and
+    finish on a streamed engine with the same result as an undisturbed run (the reference
+    restarted the whole run with doubled batches, scripts/distribuitedClustering.py:357-360)."""
+    c_ref, streamed_ref, it_ref = _run_midrun(method, "")
+    c, streamed, it = _run_midrun(method, "oom@3:1")
+    assert not streamed_ref and streamed and it == it_ref == 6
+    np.testing.assert_allclose(c, c_ref, rtol=1e-10, atol=1e-10)
+
+
+def test_fcm_setup_oom_retries_streamed(monkeypatch, capsys):
+    monkeypatch.setenv("TDC_FAULT", "oom@setup")
+    from tensorflow_distributed_clustering_amd.utils import faults
+    faults._FIRED.clear()
+    x = gaussian_blobs(3000, 3, 4, seed=5, dtype=torch.float64)
+    cfg = tdc.ClusterConfig(n_clusters=4, max_iter=5, dtype="fp64", init="first_k", fuzzifier=2.0)
+    r = tdc.FuzzyCMeans(cfg).fit(x.numpy()).result_
+    assert r.streamed and "retrying streamed" in capsys.readouterr().out
+    monkeypatch.delenv("TDC_FAULT")
+    ref = tdc.FuzzyCMeans(cfg).fit(x.numpy()).result_
+    np.testing.assert_allclose(r.centers, ref.centers, rtol=1e-10, atol=1e-10)
+
+
 def test_cli_log_every_profile_and_timeout_flags(tmp_path):
     data = tmp_path / "d.npz"
     X = gaussian_blobs(3000, 3, 4, seed=9, dtype=torch.float64).numpy()

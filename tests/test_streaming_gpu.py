@@ -164,3 +164,23 @@ def test_bounded_lloyd_policies_and_spherical(gpu):
             assert bm.engine_.active_frac < 0.9    # NaN centroids no longer force full passes
         if cfg.empty_cluster == "reseed":
             np.testing.assert_allclose(a.centers, b.centers, rtol=0, atol=5e-2)
+
+
+@pytest.mark.parametrize("dtype,backend", [("fp32", "hip_fcm_mfma"), ("fp64", "hip_fcm_tower")])
+def test_fcm_hbm_budget_streams_and_matches_resident(gpu, dtype, backend):
+    """FCM with --hbm_budget_gb below the shard: host-resident rows stream through HBM in
+    chunks (fp32: native RowStreamer + hybrid residency; fp64: plain pinned slices) and
+    the result equals the resident fit (same partials, summed over chunks)."""
+    import numpy as np
+    import tensorflow_distributed_clustering_amd as tdc
+    from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs
+    n, d, k = 400_000, 64, 64
+    x = gaussian_blobs(n, d, k, seed=6, dtype=torch.float64).numpy()
+    c0 = x[:k] + 0.3
+    cfg = tdc.ClusterConfig(n_clusters=k, max_iter=4, dtype=dtype, init="given", fuzzifier=2.0)
+    res = tdc.FuzzyCMeans(cfg, device=gpu).fit(x, init_centers_=c0).result_
+    st = tdc.FuzzyCMeans(cfg.replace(hbm_budget_gb=0.05), device=gpu).fit(x, init_centers_=c0).result_
+    assert not res.streamed and st.streamed and res.backend == st.backend == backend
+    tol = 1e-9 if dtype == "fp64" else 2e-4
+    np.testing.assert_allclose(st.centers, res.centers, rtol=tol, atol=tol)
+    assert (st.labels == res.labels).float().mean().item() > 0.999
