@@ -42,26 +42,35 @@ __global__ __launch_bounds__(256) void lloyd_small_kernel(
     for (int d = 0; d < DMAX; ++d) acc[k][d] = 0;
   }
 
-  // KMAX >= 16 (K up to 16, e.g. the reference's K=15): the register tiles leave ~2 waves
-  // per SIMD, too few to cover the 8-B row loads, so contiguous 256-row tiles are staged
-  // through LDS with 16-B loads (K=15 D=5 fp64: 26.3 -> 32.5 G points/s; slower at
-  // small KMAX, where occupancy already hides the loads: docs/PERF_NOTES.md)
+  // Rows are staged per WAVE: the wave's 64 contiguous rows (64 x D x 8 B = 2.5 KiB at
+  // D=5 fp64) arrive as fully coalesced 16-B loads into a wave-private LDS slice and
+  // every lane then reads its own row -- no block barrier, so the waves of a CU keep
+  // their loads in flight independently (the 8-B strided row loads touched each cache
+  // line D times; the earlier block-wide 256-row staging needed two barriers per tile).
+  const int lane_ = tid & 63, wv_ = tid >> 6;
+  __shared__ __attribute__((aligned(16))) T s_xw[4][KMAX >= 16 ? 64 * DMAX : 1];
+  T* s_x = s_xw[wv_];
+  // measured (ref25m presets, D=5 fp64): K=15 0.77 -> 0.75 ms/iter staged; at K=3 the
+  // high-occupancy strided loads win (0.25 vs 0.30 ms), so small register tiles skip it
   constexpr bool STAGE = KMAX >= 16;
-  __shared__ __attribute__((aligned(16))) T s_x[STAGE ? 256 * DMAX : 1];
   const bool tiled = STAGE && ldx == D && ((uintptr_t)X % 16) == 0;
-  const int64_t ntile = (N + 255) / 256;
-  for (int64_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
-    const int64_t i = tile * 256 + tid;
-    if (tiled) {
-      __syncthreads();  // previous tile consumed
-      stage_rows_lds(X, N, D, tile * 256, s_x);
-      __syncthreads();
+  const int64_t ntile = (N + 63) / 64;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wv_; tile < ntile; tile += (int64_t)gridDim.x * 4) {
+    const int64_t i = tile * 64 + lane_;
+    const bool full = tiled && tile * 64 + 64 <= N;  // wave-uniform
+    if (full) {
+      const uint4* src = reinterpret_cast<const uint4*>(X + tile * 64 * D);
+      const int nch = 4 * D * (int)sizeof(T);  // 16-B chunks of 64 rows
+      for (int c = lane_; c < nch; c += 64) reinterpret_cast<uint4*>(s_x)[c] = src[c];
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
     if (i >= N) continue;
     T x[DMAX];
 #pragma unroll
     for (int d = 0; d < DMAX; ++d)
-      x[d] = (d < D) ? (tiled ? s_x[tid * D + d] : X[i * ldx + d]) : (T)0;
+      x[d] = (d < D) ? (full ? s_x[lane_ * D + d] : X[i * ldx + d]) : (T)0;
+    if (full) __builtin_amdgcn_wave_barrier();  // every lane read its row before the refill
     T bd = (T)INFINITY;  // NaN distances (poisoned centroid, empty_cluster='nan') never win
     int best = 0;
 #pragma unroll

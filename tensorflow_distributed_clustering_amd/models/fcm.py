@@ -31,7 +31,7 @@ from ..utils import faults
 from ..utils.checkpoint import RunCheckpointer
 from ..utils.timers import DeviceTimer, sync
 from .init import init_centers, init_centers_from_source
-from .kmeans import ClusterResult, _shard_geometry
+from .kmeans import ClusterResult, OomGuard, _shard_geometry
 
 
 def fcm_dtype(cfg: ClusterConfig) -> torch.dtype:
@@ -39,7 +39,7 @@ def fcm_dtype(cfg: ClusterConfig) -> torch.dtype:
     return torch.float64 if cfg.dtype == "fp64" else torch.float32
 
 
-class FcmEngine:
+class FcmEngine(OomGuard):
     """Resident or streamed state of one distributed FCM run; ``step()`` = one iteration
     (native tower over the shard or its chunks, one packed all-reduce of
     [sum W X | sum W | oom flag], the N3 divide).  Timed by bench.py."""
@@ -135,20 +135,7 @@ class FcmEngine:
         self.local.finalize(self.wx, self.ws, self.C, self.shift)
         self.n_iter += 1
 
-    # mid-run OOM recovery (same protocol as LloydEngine)
-    def oom_pending(self) -> bool:
-        return self.oom_flag is not None and float(self.oom_flag.item()) > 0
-
-    def save_state(self):
-        if getattr(self, "_c_prev", None) is None:
-            self._c_prev = torch.empty_like(self.C)
-        self._c_prev.copy_(self.C)
-        self._n_prev = self.n_iter
-
-    def rollback(self) -> np.ndarray:
-        self.C.copy_(self._c_prev)
-        self.n_iter = self._n_prev
-        return self.C.double().cpu().numpy()
+    rsag = False  # (OomGuard) the FCM partials always go through one all-reduce
 
     def centers(self) -> torch.Tensor:
         return self.C
@@ -283,33 +270,48 @@ class FuzzyCMeans:
         timer.start()
         history = []
         centers_host = lambda: self.engine_.C.double().cpu().numpy()
-        while eng.n_iter < cfg.max_iter:
+        while True:
+            if eng.oom_guard:
+                bad = eng.failed_step(lag=0 if eng.n_iter >= cfg.max_iter else 1)
+                if bad is not None:
+                    c_host, c0 = eng.rollback(bad), eng.c0
+                    n_back = eng.n_iter
+                    chunk = max(1024, (eng.chunk_rows or n_local) // 2)
+                    del eng
+                    self.engine_ = None
+                    if dev.type == "cuda":
+                        torch.cuda.empty_cache()
+                    if comm.is_root:
+                        print(f"[fcm] out of memory in iteration {n_back + 1}; continuing "
+                              f"streamed with chunk_rows={chunk}", flush=True)
+                    eng = self._build_engine([self._make_source(x_local, dev, row_offset, chunk)],
+                                             x_local, dev, comm, n_global, row_offset, n_local,
+                                             c_host, n_back, m)
+                    eng.c0 = c0
+                    self.engine_ = eng
+                    continue
+            if eng.n_iter >= cfg.max_iter:
+                break
             if eng.oom_guard:
                 eng.save_state()
             eng.step()
-            if eng.oom_guard and eng.oom_pending():
-                c_host, n_back, c0 = eng.rollback(), eng._n_prev, eng.c0
-                chunk = max(1024, (eng.chunk_rows or n_local) // 2)
-                del eng
-                self.engine_ = None
-                if dev.type == "cuda":
-                    torch.cuda.empty_cache()
-                if comm.is_root:
-                    print(f"[fcm] out of memory in iteration {n_back + 1}; continuing streamed "
-                          f"with chunk_rows={chunk}", flush=True)
-                eng = self._build_engine([self._make_source(x_local, dev, row_offset, chunk)],
-                                         x_local, dev, comm, n_global, row_offset, n_local,
-                                         c_host, n_back, m)
-                eng.c0 = c0
-                self.engine_ = eng
-                continue
+            if eng.oom_guard:
+                eng.post_flag()
             n_iter = eng.n_iter
             if eng.shift is not None:
+                if eng.oom_guard and eng.failed_step(lag=0) is not None:
+                    continue
                 sv = float(eng.shift.item())
                 history.append({"iter": n_iter, "shift": sv})
                 if sv <= cfg.tol:
+                    if eng.oom_guard and eng.failed_step(lag=1) is not None:
+                        continue
                     break
-            ckpt.maybe_save(n_iter, centers_host)
+            if ckpt.due(n_iter):
+                if eng.oom_guard and (eng.failed_step(lag=0) is not None
+                                      or eng.failed_step(lag=1) is not None):
+                    continue
+                ckpt.maybe_save(n_iter, centers_host)
             faults.maybe_fail(str(n_iter), comm.rank, kinds=("crash",))
         computation_time = timer.stop()
         n_iter = eng.n_iter

@@ -71,7 +71,66 @@ def _shard_geometry(n_local: int, comm: Comm):
     return int(sum(sizes)), int(sum(sizes[: comm.rank]))
 
 
-class LloydEngine:
+class OomGuard:
+    """Mid-run OOM rollback state shared by the Lloyd and FCM engines.
+
+    A rank that runs out of memory in its local step sets the flag slot of the packed
+    all-reduce buffer, so every rank learns it from the same collective.  The flag of step
+    n is copied to pinned host memory asynchronously and read while step n+1 runs (the
+    host stays <= 2 steps ahead, no per-step sync); the centroids of the last two step
+    starts are kept, so a flag seen one step late still rolls back to the state before the
+    failed step.  Engines provide ``rsag``, ``C`` (+ ``C_pad``/``_r0``/``_kr`` under rsag),
+    ``buf``, ``oom_flag``, ``device``, ``n_iter`` and ``centers()``."""
+
+    def save_state(self):
+        """Keep the pre-step centroids (this rank's slice under rsag) for a rollback."""
+        src = self.C_pad[self._r0: self._r0 + self._kr] if self.rsag else self.C
+        ring = getattr(self, "_ring", None)
+        if ring is None or ring[0].shape != src.shape:
+            ring = self._ring = [torch.empty_like(src), torch.empty_like(src)]
+            self._ring_iter = [-1, -1]
+            self._flag_host = torch.zeros(2, dtype=self.buf.dtype,
+                                          pin_memory=self.device.type == "cuda")
+            self._flag_ev = [None, None]
+        slot = self.n_iter & 1
+        ring[slot].copy_(src)
+        self._ring_iter[slot] = self.n_iter
+
+    def post_flag(self):
+        """After step(): queue the copy of this step's OOM flag (no host sync)."""
+        slot = (self.n_iter - 1) & 1
+        if self.device.type == "cuda":
+            self._flag_host[slot:slot + 1].copy_(self.oom_flag, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._flag_ev[slot] = ev
+        else:
+            self._flag_host[slot:slot + 1].copy_(self.oom_flag)
+
+    def failed_step(self, lag: int = 1) -> Optional[int]:
+        """Index (0-based) of a step whose flag is set, checking the step ``lag`` steps
+        back (lag 0: the last one, a host sync)."""
+        n = self.n_iter - 1 - lag
+        if n < 0 or getattr(self, "_ring", None) is None or self._ring_iter[n & 1] != n:
+            return None
+        ev = self._flag_ev[n & 1]
+        if ev is not None:
+            ev.synchronize()
+        return n if float(self._flag_host[n & 1]) > 0 else None
+
+    def rollback(self, step: int) -> np.ndarray:
+        """Centroids at the start of ``step`` (replicated, host fp64); resets n_iter."""
+        prev = self._ring[step & 1]
+        if self.rsag:
+            self.C_pad[self._r0: self._r0 + self._kr].copy_(prev)
+            self._c_synced = False
+        else:
+            self.C.copy_(prev)
+        self.n_iter = step
+        return self.centers().double().cpu().numpy()
+
+
+class LloydEngine(OomGuard):
     """Resident state of one distributed Lloyd run: operands, centroids, buffers.
 
     ``source`` is a device tensor (the resident shard) or a chunk source from
@@ -289,32 +348,6 @@ class LloydEngine:
                                             None if mind is None else mind[s:e],
                                             self.sums, self.counts)
 
-    # ----------------------------------------------------------- mid-run OOM recovery
-    def oom_pending(self) -> bool:
-        """Did any rank run out of memory in the last step (host sync; fit() checks it)?"""
-        return self.oom_flag is not None and float(self.oom_flag.item()) > 0
-
-    def save_state(self):
-        """Keep the pre-step centroids (this rank's slice under rsag) for a rollback."""
-        if self.rsag:
-            src = self.C_pad[self._r0: self._r0 + self._kr]
-        else:
-            src = self.C
-        if getattr(self, "_c_prev", None) is None or self._c_prev.shape != src.shape:
-            self._c_prev = torch.empty_like(src)
-        self._c_prev.copy_(src)
-        self._n_prev = self.n_iter
-
-    def rollback(self) -> np.ndarray:
-        """Centroids before the failed step (replicated, host fp64); resets n_iter."""
-        if self.rsag:
-            self.C_pad[self._r0: self._r0 + self._kr].copy_(self._c_prev)
-            self._c_synced = False
-        else:
-            self.C.copy_(self._c_prev)
-        self.n_iter = self._n_prev
-        return self.centers().double().cpu().numpy()
-
     def _reduce_scatter_finalize(self):
         """rsag mode: reduce-scatter the sums (rank r gets centroid rows [r0, r0 + kr)),
         all-reduce the small count tail, finalise + operand-prep the own slice, all-gather
@@ -504,12 +537,12 @@ class KMeans:
                       f"chunk_rows={chunk}", flush=True)
         raise err if err is not None else faults.oom_error("out of memory on a peer rank")
 
-    def _recover_oom(self, eng, x_local, dev, comm, n_global, row_offset, n_local):
+    def _recover_oom(self, eng, step, x_local, dev, comm, n_global, row_offset, n_local):
         """A rank ran out of memory inside the last step (flag in the all-reduce buffer):
         every rank rolls back to the pre-step centroids and continues from the same
         iteration on a streamed engine with half the chunk (the reference restarted the
         whole run with twice the batches, `scripts/distribuitedClustering.py:357-360`)."""
-        c_host = eng.rollback()
+        c_host = eng.rollback(step)
         n_back = eng.n_iter
         chunk = max(1024, (eng.chunk_rows or n_local) // 2)
         c0 = eng.c0
@@ -565,16 +598,25 @@ class KMeans:
         self.engine_ = eng
         timer = DeviceTimer(dev)
         timer.start()
-        while eng.n_iter < cfg.max_iter:
+        while True:
+            if eng.oom_guard:
+                bad = eng.failed_step(lag=0 if eng.n_iter >= cfg.max_iter else 1)
+                if bad is not None:
+                    eng = self._recover_oom(eng, bad, x_local, dev, comm, n_global, row_offset,
+                                            n_local)
+                    continue
+            if eng.n_iter >= cfg.max_iter:
+                break
             log_pt = cfg.log_every > 0 and (eng.n_iter + 1) % cfg.log_every == 0
             if eng.oom_guard:
                 eng.save_state()
             inertia_it = eng.step(with_inertia=log_pt and cfg.compute_inertia)
-            if eng.oom_guard and eng.oom_pending():
-                eng = self._recover_oom(eng, x_local, dev, comm, n_global, row_offset, n_local)
-                continue
+            if eng.oom_guard:
+                eng.post_flag()
             n = eng.n_iter
             if eng.need_shift and (cfg.tol > 0 or log_pt):
+                if eng.oom_guard and eng.failed_step(lag=0) is not None:
+                    continue  # this step failed: recovered at the top of the loop
                 sv = float(eng.shift.item())
                 rec = {"iter": n, "shift": sv}
                 if inertia_it is not None:
@@ -584,8 +626,14 @@ class KMeans:
                     extra = f" inertia {inertia_it:.6e}" if inertia_it is not None else ""
                     print(f"[kmeans] iter {n} max centroid shift^2 {sv:.3e}{extra}", flush=True)
                 if cfg.tol > 0 and sv <= cfg.tol:
+                    if eng.oom_guard and eng.failed_step(lag=1) is not None:
+                        continue
                     break
-            ckpt.maybe_save(n, centers_host)
+            if ckpt.due(n):
+                if eng.oom_guard and (eng.failed_step(lag=0) is not None
+                                      or eng.failed_step(lag=1) is not None):
+                    continue  # never checkpoint centroids of a failed step
+                ckpt.maybe_save(n, centers_host)
             faults.maybe_fail(str(n), comm.rank, kinds=("crash",))
         computation_time = timer.stop()
         ckpt.maybe_save(eng.n_iter, centers_host, final=True)

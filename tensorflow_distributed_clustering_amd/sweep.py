@@ -69,7 +69,9 @@ def command(run: Run, args) -> List[str]:
         out = os.path.join(args.log_dir, run.name)
         # the program itself follows "--" (no shell/env hop: the profiler's preload must
         # see the python process directly)
-        return ["rocprofv3", "--kernel-trace", "--stats", "-d", out, "-o", "run", "--"] + cli
+        # csv output: *_kernel_stats.csv per run (compileResults.py input), not a rocpd db
+        return ["rocprofv3", "--kernel-trace", "--stats", "-f", "csv", "-d", out, "-o", "run",
+                "--"] + cli
     return cli
 
 

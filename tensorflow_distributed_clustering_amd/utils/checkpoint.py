@@ -78,6 +78,10 @@ class RunCheckpointer:
                              f"not {self.method} ({k}, {d})")
         return ck
 
+    def due(self, n_iter: int) -> bool:
+        """Would maybe_save(n_iter) write a periodic checkpoint?"""
+        return bool(self.path) and self.every > 0 and n_iter % self.every == 0
+
     def maybe_save(self, n_iter: int, centers_fn, arrays_fn=None, final: bool = False) -> bool:
         if not self.path:
             return False

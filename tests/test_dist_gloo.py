@@ -37,8 +37,9 @@ def _worker(rank, world, port, method, init, q, n, d, k, iters, seed, extra):
     labels = comm.gather_rows_to_root(r.labels)
     info = {}
     eng = getattr(model, "engine_", None)
-    if eng is not None and hasattr(eng, "rsag"):
-        info = dict(rsag=eng.rsag, split=eng.count_split, counts=r.counts)
+    if eng is not None:
+        info = dict(rsag=getattr(eng, "rsag", False), split=getattr(eng, "count_split", False),
+                    counts=r.counts)
     if rank == 0:
         q.put((r.centers, labels.numpy(), r.inertia, r.n_iter, r.init_centers, info))
     D.destroy_comm()
