@@ -75,6 +75,9 @@ def parse(argv=None):
     ap.add_argument("--batch-size", type=int, default=0, help="mini-batch rows per rank")
     ap.add_argument("--method", default="kmeans", choices=["kmeans", "fcm"],
                     help="fcm: distributed Fuzzy C-Means step (fuzzifier m = D, as the reference)")
+    ap.add_argument("--init", default="random", choices=["random", "kmeans++", "kmeans||", "first_k"],
+                    help="centroid init (timed separately as init_s; the north star's random "
+                         "rows by default; kmeans++ switches to sampled k-means|| above K=2048)")
     ap.add_argument("--fuzzifier", type=float, default=None,
                     help="FCM fuzzifier m (default: the reference's m = D)")
     ap.add_argument("--algorithm", default="lloyd", choices=["lloyd", "bounded"],
@@ -121,7 +124,7 @@ def main(argv=None):
     dt = {"fp8": torch.bfloat16, "bf16": torch.bfloat16, "fp32": torch.float32,
           "fp64": torch.float64}[a.dtype]
     x = gaussian_blobs(e - s, a.dim, a.k, seed=a.seed, row_offset=s, dtype=dt, device=dev)
-    cfg = tdc.ClusterConfig(n_clusters=a.k, max_iter=a.steps, dtype=a.dtype, init="random",
+    cfg = tdc.ClusterConfig(n_clusters=a.k, max_iter=a.steps, dtype=a.dtype, init=a.init,
                             seed=a.seed, compute_inertia=False, algorithm=a.algorithm,
                             fuzzifier=a.fuzzifier)
     if a.mode == "minibatch":
@@ -131,17 +134,28 @@ def main(argv=None):
         points_per_step = eng.batch_rows * world
     elif a.method == "fcm":
         from tensorflow_distributed_clustering_amd.models.fcm import FcmEngine
-        eng = FcmEngine(x, cfg, comm, n_global, s)
+        eng = FcmEngine(x, cfg, comm, n_global, s, defer_init=True)
         points_per_step = n_global
     elif a.algorithm == "bounded":
         from tensorflow_distributed_clustering_amd.models.bounded import BoundedLloydEngine
-        eng = BoundedLloydEngine(x, cfg, comm, n_global, s)
+        eng = BoundedLloydEngine(x, cfg, comm, n_global, s, defer_init=True)
         points_per_step = n_global
     else:
-        eng = LloydEngine(x, cfg, comm, n_global, s)
+        eng = LloydEngine(x, cfg, comm, n_global, s, defer_init=True)
         points_per_step = n_global
-        if a.graph and dev.type == "cuda":
-            eng.capture(include_collectives=world > 1)
+    init_s = None
+    if hasattr(eng, "init_centroids") and getattr(eng, "c0", None) is None:
+        # the centroid init, timed on its own (never inside the timed steps)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        t_i = time.perf_counter()
+        eng.init_centroids()
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        init_s = comm.max_scalar(time.perf_counter() - t_i)
+    if a.mode == "lloyd" and a.method == "kmeans" and a.algorithm == "lloyd" and a.graph \
+            and dev.type == "cuda":
+        eng.capture(include_collectives=world > 1)
 
     for _ in range(a.warmup):
         eng.step()
@@ -178,6 +192,7 @@ def main(argv=None):
             "dtype": a.dtype,
             "data": "synthetic gaussian blobs (on-device, counter-based), random-row init",
             "preset": a.preset,
+            "init": {"method": a.init, "seconds": init_s},
             "iters_per_sec": 1e3 / ms,
             "backend": eng.local.name,
             "config": {"model": ("kmeans-minibatch" if a.mode == "minibatch" else

@@ -305,14 +305,14 @@ void fcm_mfma_stats(const at::Tensor& Xh, const at::Tensor& Xl, const at::Tensor
   check(tdc_fcm_mfma(0, Xh.data_ptr(), Xl.data_ptr(), xx.data_ptr<float>(), N, (int)Xh.size(1), 0,
                      Ch.data_ptr(), Cl.data_ptr(), cc.data_ptr<float>(), (int)K, (int)Ch.size(0),
                      m, nan_to_zero ? 1 : 0, labels.data_ptr<int32_t>(), rowinfo.data_ptr<float>(),
-                     nullptr, nullptr, nullptr, num_cus(Xh.device().index()), cur_stream()),
+                     nullptr, nullptr, nullptr, nullptr, num_cus(Xh.device().index()), cur_stream()),
         "fcm_mfma_stats");
 }
 
 void fcm_mfma_accum(const at::Tensor& Xh, const at::Tensor& Xl, const at::Tensor& xx,
                     const at::Tensor& rowinfo, const at::Tensor& Ch, const at::Tensor& Cl,
                     const at::Tensor& cc, int64_t K, double m, bool nan_to_zero, at::Tensor& wx,
-                    at::Tensor& ws, at::Tensor& work) {
+                    at::Tensor& ws, at::Tensor& work, const std::optional<at::Tensor>& shift) {
   check_mfma_fcm(Xh, Xl, xx, Ch, Cl, cc, K, m, "fcm_mfma_accum");
   const int nc = num_cus(Xh.device().index());
   TORCH_CHECK(work.scalar_type() == at::kFloat && work.is_contiguous() &&
@@ -331,7 +331,8 @@ void fcm_mfma_accum(const at::Tensor& Xh, const at::Tensor& Xl, const at::Tensor
                      (int)wx.size(1), Ch.data_ptr(), Cl.data_ptr(), cc.data_ptr<float>(), (int)K,
                      (int)Ch.size(0), m, nan_to_zero ? 1 : 0, nullptr,
                      const_cast<float*>(rowinfo.data_ptr<float>()), wx.data_ptr<double>(),
-                     ws.data_ptr<double>(), work.data_ptr<float>(), nc, cur_stream()),
+                     ws.data_ptr<double>(), work.data_ptr<float>(),
+                     static_cast<const float*>(opt_ptr(shift)), nc, cur_stream()),
         "fcm_mfma_accum");
 }
 
@@ -746,7 +747,7 @@ TORCH_LIBRARY(tdc, m) {
   m.def("fcm_tower_accum(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor rowinfo, Tensor(a!) wx, Tensor(b!) ws) -> ()");
   m.def("fcm_split_rows(Tensor src, int valid, int neg2, Tensor(a!) hi, Tensor(b!) lo, Tensor(c!)? norm, Tensor? shift=None) -> ()");
   m.def("fcm_mfma_stats(Tensor Xh, Tensor Xl, Tensor xx, Tensor Ch, Tensor Cl, Tensor cc, int K, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) rowinfo) -> ()");
-  m.def("fcm_mfma_accum(Tensor Xh, Tensor Xl, Tensor xx, Tensor rowinfo, Tensor Ch, Tensor Cl, Tensor cc, int K, float m, bool nan_to_zero, Tensor(a!) wx, Tensor(b!) ws, Tensor(c!) work) -> ()");
+  m.def("fcm_mfma_accum(Tensor Xh, Tensor Xl, Tensor xx, Tensor rowinfo, Tensor Ch, Tensor Cl, Tensor cc, int K, float m, bool nan_to_zero, Tensor(a!) wx, Tensor(b!) ws, Tensor(c!) work, Tensor? shift=None) -> ()");
   m.def("fcm_mfma_workspace(Tensor like, int N, int K, int Kp, int DP) -> int");
   m.def("fcm_rows(Tensor(a!) G, Tensor xx, Tensor? cc, float m, bool nan_to_zero, Tensor(b!) labels, Tensor(c!)? colsum=None) -> ()");
   m.def("assign_bigd_supported(ScalarType dtype, int DP) -> bool", &assign_bigd_supported);

@@ -314,7 +314,8 @@ __global__ __launch_bounds__(256, 1) void fcm_mfma_accum_kernel(
     }                                                                                     \
     if (tid < 2 * TP) {                                                                   \
       const int64_t gr = (R0_) + (tid & (TP - 1));                                        \
-      pv = gr < b ? (tid < TP ? xx[gr] : rowinfo[gr]) : 0.f;                              \
+      /* padded rows: a huge norm keeps t finite (rcp(0) * info 0 would be NaN) */       \
+      pv = gr < b ? (tid < TP ? xx[gr] : rowinfo[gr]) : (tid < TP ? 1.0e30f : 0.f);       \
     }                                                                                     \
   }
 #define TDC_TILE_STORE(B_)                                                                \
@@ -368,8 +369,8 @@ __global__ __launch_bounds__(256, 1) void fcm_mfma_accum_kernel(
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       // ---- memberships -> w = wh + wl (bf16 pair); register i = point (i&3)+8(i>>2)+4h ----
-      // padded rows carry info 0 (w = 0); pad centroids give finite w whose slab rows the
-      // reduction never reads
+      // padded rows carry info 0 and a huge norm (w = 0); pad centroids give finite w whose
+      // slab rows the reduction never reads
       bf16x8 wh[2], wl[2];
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
@@ -432,20 +433,25 @@ __global__ __launch_bounds__(256, 1) void fcm_mfma_accum_kernel(
   if (h == 0) part_ws[split * (int64_t)KP + kc] = wsum;
 }
 
-// wx[k, d] += sum_s part[s, k, d] (fp64), ws[k] += sum_s part_ws[s, k]
+// wx[k, d] += sum_s part[s, k, d] + mu[d] sum_s part_ws[s, k] (fp64: the slabs hold
+// sum w (x - mu) of the shifted rows), ws[k] += sum_s part_ws[s, k]
 __global__ __launch_bounds__(256) void fcm_reduce_kernel(const float* __restrict__ part,
                                                          const float* __restrict__ part_ws,
                                                          int64_t splits, int K, int KP, int DP,
-                                                         int D, double* __restrict__ wx,
+                                                         int D, const float* __restrict__ mu,
+                                                         double* __restrict__ wx,
                                                          double* __restrict__ ws) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t tot = (int64_t)K * DP;
   if (e < tot) {
     const int k = (int)(e / DP), d = (int)(e % DP);
     if (d < D) {
-      double s = 0.0;
-      for (int64_t sp = 0; sp < splits; ++sp) s += (double)part[(sp * KP + k) * (int64_t)DP + d];
-      wx[(int64_t)k * D + d] += s;
+      double s = 0.0, w = 0.0;
+      for (int64_t sp = 0; sp < splits; ++sp) {
+        s += (double)part[(sp * KP + k) * (int64_t)DP + d];
+        w += (double)part_ws[sp * KP + k];
+      }
+      wx[(int64_t)k * D + d] += s + (mu ? (double)mu[d] * w : 0.0);
     }
   } else if (e < tot + K) {
     const int k = (int)(e - tot);
@@ -524,8 +530,8 @@ inline void accum_geometry(int64_t N, int K, int num_cus, int* nkt, int64_t* spl
 template <int DP>
 int launch_maccum(const void* Xh, const void* Xl, const float* xx, const float* rowinfo,
                   int64_t N, const void* Ch, const void* Cl, const float* cc, int K, int Kp,
-                  int D, double m, int nz, float* part, double* wx, double* ws, int num_cus,
-                  hipStream_t s) {
+                  int D, double m, int nz, float* part, const float* mu, double* wx, double* ws,
+                  int num_cus, hipStream_t s) {
   int nkt;
   int64_t splits, rps;
   accum_geometry(N, K, num_cus, &nkt, &splits, &rps);
@@ -546,7 +552,7 @@ int launch_maccum(const void* Xh, const void* Xl, const float* xx, const float* 
   TDC_CHECK_LAUNCH();
   const int64_t tot = (int64_t)K * DP + K;
   hipLaunchKernelGGL(fcm_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, part,
-                     part_ws, splits, K, Kp, DP, D, wx, ws);
+                     part_ws, splits, K, Kp, DP, D, mu, wx, ws);
   TDC_CHECK_LAUNCH();
   return 0;
 }
@@ -578,7 +584,7 @@ int64_t tdc_fcm_mfma_workspace(int64_t N, int K, int Kp, int DP, int num_cus) {
 int tdc_fcm_mfma(int pass, const void* Xh, const void* Xl, const float* xx, int64_t N, int DP,
                  int D, const void* Ch, const void* Cl, const float* cc, int K, int Kp, double m,
                  int nan_to_zero, int32_t* labels, float* rowinfo, double* wx, double* ws,
-                 float* work, int num_cus, hipStream_t s) {
+                 float* work, const float* shift, int num_cus, hipStream_t s) {
   if (N <= 0 || K <= 0) return 0;
   if (Kp % 128 != 0 || Kp < K) return (int)hipErrorInvalidValue;
 #define TDC_FM(DPV)                                                                           \
@@ -587,7 +593,7 @@ int tdc_fcm_mfma(int pass, const void* Xh, const void* Xl, const float* xx, int6
       return launch_mstats<DPV>(Xh, Xl, xx, N, Ch, Cl, cc, K, Kp, m, nan_to_zero, labels,     \
                                 rowinfo, s);                                                  \
     return launch_maccum<DPV>(Xh, Xl, xx, rowinfo, N, Ch, Cl, cc, K, Kp, D, m, nan_to_zero,   \
-                              work, wx, ws, num_cus, s);                                      \
+                              work, shift, wx, ws, num_cus, s);                               \
   }
   TDC_FM(32)
   TDC_FM(64)

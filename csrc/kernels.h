@@ -97,11 +97,13 @@ int tdc_fcm_tower(int pass, int dtype, const void* X, int64_t N, int64_t ldx, in
 int tdc_fcm_split_rows(const float* src, int64_t rows, int64_t valid, int d, int64_t ld, int DP,
                        int neg2, const float* shift, void* hi, void* lo, float* norm,
                        hipStream_t stream);
-// work: fp32 [tdc_fcm_mfma_workspace(...)] per-block partial slabs of pass 1.
+// work: fp32 [tdc_fcm_mfma_workspace(...)] per-block partial slabs of pass 1; shift
+// (nullable, fp32 [D]): the vector subtracted from rows and centroids at the split, added
+// back as shift * sum w in the reduction.
 int tdc_fcm_mfma(int pass, const void* Xh, const void* Xl, const float* xx, int64_t N, int DP,
                  int D, const void* Ch, const void* Cl, const float* cc, int K, int Kp, double m,
                  int nan_to_zero, int32_t* labels, float* rowinfo, double* wx, double* ws,
-                 float* work, int num_cus, hipStream_t stream);
+                 float* work, const float* shift, int num_cus, hipStream_t stream);
 int64_t tdc_fcm_mfma_workspace(int64_t N, int K, int Kp, int DP, int num_cus);
 
 // N3  finalize: C = sums/counts (empty policy), max shift^2 -> shift (float, atomic max),

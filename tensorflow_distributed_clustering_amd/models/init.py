@@ -240,12 +240,36 @@ def weighted_kmeanspp(c: torch.Tensor, w: torch.Tensor, k: int, seed: int,
     return centers
 
 
+# Greedy k-means++ is K dependent sweeps over the shard (~3 kernels + 4 small collectives
+# per centre); above this K, init='kmeans++' runs the sampled k-means|| below instead
+# (override: TDC_KPP_MAX_K).  K = 65536 greedy would be ~131K full sweeps -- hours.
+KPP_MAX_K = int(__import__("os").environ.get("TDC_KPP_MAX_K", 2048))
+# k-means|| on a uniform sample of this many rows per centre (sampled mode)
+KPAR_SAMPLE_PER_K = 8
+# weighted k-means++ recluster up to this many centres; above it the K centres are drawn
+# from the candidates by weight without replacement (Python-level greedy is O(K) steps)
+RECLUSTER_MAX_K = 2048
+
+
 def init_kmeans_parallel(x_local, row_offset, n_global, k, comm: Comm, seed,
-                         rounds: int = 5, oversample: float = 2.0):
+                         rounds: int = 5, oversample: float = 2.0, sample: int = 0):
     """Scalable k-means++ ("k-means||"): ``rounds`` passes that each keep every point
     with probability min(1, l d^2 / phi) (l = oversample*K), then weighted k-means++ on
     the ~l*rounds candidates.  O(rounds) sweeps over the data instead of K, and each pass
-    is one chunked GEMM + one all-reduce -- the seeding that scales to K=65536."""
+    is one chunked GEMM + one all-reduce.
+
+    ``sample`` > 0 (large K): the rounds run on a uniform world-invariant sample of that
+    many rows, replicated on every rank (one gather), with 2 rounds at l = K, and the K
+    centres are drawn from the candidates by cluster mass (RECLUSTER_MAX_K) -- the whole
+    seeding of K = 65536 is a few GEMM passes over a 0.5M-row sample."""
+    if sample and sample < n_global:
+        idx = floyd_sample(n_global, sample, seed + 31)
+        xs = gather_global_rows(x_local, row_offset, idx, comm,
+                                dtype=torch.float32 if x_local.device.type == "cuda"
+                                else torch.float64)
+        from ..parallel.dist import local_comm
+        return init_kmeans_parallel(xs, 0, sample, k, local_comm(xs.device), seed,
+                                    rounds=min(rounds, 2), oversample=min(oversample, 1.0))
     dev = x_local.device
     n_local = x_local.shape[0]
     rows = torch.arange(row_offset, row_offset + n_local, dtype=torch.int64, device=dev)
@@ -271,6 +295,13 @@ def init_kmeans_parallel(x_local, row_offset, n_global, k, comm: Comm, seed,
     _, lab = _min_sqdist(x_local, C)
     w = torch.bincount(lab, minlength=C.shape[0]).double()
     comm.allreduce_(w)
+    if k > RECLUSTER_MAX_K:
+        # K centres from the candidates by cluster mass, without replacement (seeded,
+        # on the host so every rank draws the same set)
+        g = torch.Generator().manual_seed(int(seed) + 101)
+        wp = w.cpu() + 1e-12
+        pick = torch.multinomial(wp, k, replacement=False, generator=g)
+        return C[pick.to(C.device)].double()
     return weighted_kmeanspp(C, w, k, seed)
 
 
@@ -290,10 +321,12 @@ def init_centers(method: str, x_local: torch.Tensor, row_offset: int, n_global: 
         return init_random(x_local, row_offset, n_global, k, comm, seed)
     if method == "first_k":
         return init_first_k(x_local, row_offset, n_global, k, comm, seed)
-    if method == "kmeans++":
+    if method == "kmeans++" and k <= KPP_MAX_K:
         return init_kmeanspp(x_local, row_offset, n_global, k, comm, seed)
-    if method == "kmeans||":
-        return init_kmeans_parallel(x_local, row_offset, n_global, k, comm, seed)
+    if method in ("kmeans++", "kmeans||"):
+        sample = KPAR_SAMPLE_PER_K * k if k > KPP_MAX_K else 0
+        return init_kmeans_parallel(x_local, row_offset, n_global, k, comm, seed,
+                                    sample=min(sample, n_global) if sample else 0)
     raise ValueError(f"unknown init {method!r}")
 
 
@@ -358,6 +391,5 @@ def init_centers_from_source(method: str, source, row_offset: int, n_global: int
         sample = gather_rows_from_source(source, row_offset, floyd_sample(n_global, m, seed + 1),
                                          comm, d)
         from ..parallel.dist import local_comm
-        fn = init_kmeanspp if method == "kmeans++" else init_kmeans_parallel
-        return fn(sample, 0, m, k, local_comm(sample.device), seed)
+        return init_centers(method, sample, 0, m, k, local_comm(sample.device), seed)
     raise ValueError(f"unknown init {method!r}")

@@ -860,7 +860,7 @@ class HipMfmaFCM(_LocalOpsBase):
         self.ops.fcm_mfma_stats(xh, xl, xx, self.ch, self.cl, self.cc, self.k, self.m,
                                 self.nan_to_zero, labels, ri)
         self.ops.fcm_mfma_accum(xh, xl, xx, ri, self.ch, self.cl, self.cc, self.k, self.m,
-                                self.nan_to_zero, wx, ws, self._work())
+                                self.nan_to_zero, wx, ws, self._work(), self.mu)
 
     def assign(self, C, labels):
         self.prepare(C)

@@ -242,3 +242,13 @@ def test_dist_debug_detects_collective_mismatch():
         p.join(timeout=60)
     assert all(res[r] for r in (0, 1)), res
     assert any("shape" in res[r].lower() or "mismatch" in res[r].lower() for r in (0, 1)), res
+
+
+def test_large_k_kmeanspp_is_sampled_kmeans_parallel_world_invariant(monkeypatch):
+    """Above KPP_MAX_K, init='kmeans++' seeds with k-means|| on a world-invariant uniform
+    sample (greedy k-means++ would be K dependent sweeps): same centres at world 1 and 2."""
+    monkeypatch.setenv("TDC_KPP_MAX_K", "8")
+    _, _, _, _, i1, _ = run_world(1, init="kmeans++", k=24, iters=1)
+    _, _, _, _, i2, _ = run_world(2, init="kmeans++", k=24, iters=1)
+    np.testing.assert_allclose(i2, i1, rtol=1e-12, atol=1e-12)
+    assert len(np.unique(i1, axis=0)) == 24

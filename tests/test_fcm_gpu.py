@@ -87,11 +87,12 @@ def test_fcm_mfma_matches_oracle(gpu, k, d, m, nz):
 def test_fcm_fit_native_backends(gpu, dtype, d, k, backend):
     """Every FCM shape class runs a native backend and follows the fp64 torch fit."""
     import tensorflow_distributed_clustering_amd as tdc
-    from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs
+    from tensorflow_distributed_clustering_amd.data.synth import blob_centers, gaussian_blobs
     x = gaussian_blobs(30000, d, k, seed=2, dtype=torch.float64, device=gpu)
-    # start next to (not on) data rows: a row exactly on a centroid is the reference's
-    # discontinuous NaN -> 0 case, where exact and GEMM-form oracles legitimately differ
-    c0 = (x[:k].cpu() + 0.3).numpy()
+    # one start per blob, off its centre: two centroids sharing a blob split along a
+    # direction any rounding difference decides (a symmetric saddle), and a start ON a
+    # data row is the reference's discontinuous NaN -> 0 case
+    c0 = blob_centers(k, d, 2) + 0.3
     cfg = tdc.ClusterConfig(n_clusters=k, max_iter=4, dtype=dtype, init="given", fuzzifier=2.0)
     r = tdc.FuzzyCMeans(cfg).fit(x, init_centers_=c0).result_
     assert r.backend == backend
