@@ -106,6 +106,26 @@ void assign_simt(const at::Tensor& X, const at::Tensor& C, at::Tensor& labels,
         "assign_simt");
 }
 
+void assign_exact(const at::Tensor& X, const at::Tensor& C, at::Tensor& labels,
+                  const std::optional<at::Tensor>& mind) {
+  check_cuda(X, "X");
+  check_rows(X, "X");
+  TORCH_CHECK(X.scalar_type() == at::kFloat || X.scalar_type() == at::kDouble,
+              "tdc.assign_exact: X fp32/fp64");
+  TORCH_CHECK(C.scalar_type() == X.scalar_type() && C.is_contiguous() && C.dim() == 2 &&
+                  C.size(1) == X.size(1), "tdc.assign_exact: C [K, D] in the X dtype");
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous() && labels.numel() >= X.size(0),
+              "tdc.assign_exact: labels int32 [N]");
+  if (mind.has_value() && mind->defined())
+    TORCH_CHECK(mind->scalar_type() == X.scalar_type() && mind->is_contiguous() &&
+                    mind->numel() >= X.size(0), "tdc.assign_exact: mind [N] in the X dtype");
+  const DevGuard guard(X.device());
+  check(tdc_assign_exact(dcode(X.scalar_type()), X.data_ptr(), X.size(0), X.stride(0),
+                         (int)X.size(1), C.data_ptr(), (int)C.size(0), labels.data_ptr<int32_t>(),
+                         opt_ptr(mind), num_cus(X.device().index()), cur_stream()),
+        "assign_exact");
+}
+
 bool lloyd_small_supported(at::ScalarType dtype, int64_t K, int64_t D) {
   if (dtype != at::kFloat && dtype != at::kDouble) return false;
   return tdc_lloyd_small_supported(dcode(dtype), (int)K, (int)D) != 0;
@@ -736,6 +756,7 @@ void kpp_step(const at::Tensor& X, const at::Tensor& cand, at::Tensor& closest, 
 TORCH_LIBRARY(tdc, m) {
   m.def("assign_bf16(Tensor X, Tensor Cm2, Tensor cnorm, Tensor(a!) labels, Tensor(b!)? mind) -> ()");
   m.def("assign_simt(Tensor X, Tensor C, Tensor(a!) labels, Tensor(b!)? mind) -> ()");
+  m.def("assign_exact(Tensor X, Tensor C, Tensor(a!) labels, Tensor(b!)? mind) -> ()");
   m.def("lloyd_small_supported(ScalarType dtype, int K, int D) -> bool", &lloyd_small_supported);
   m.def("lloyd_small(Tensor X, Tensor C, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!) sums, Tensor(d!) counts) -> ()");
   m.def("update(Tensor X, Tensor labels, Tensor(a!) sums, Tensor(b!) counts) -> ()");
@@ -767,6 +788,7 @@ TORCH_LIBRARY(tdc, m) {
 TORCH_LIBRARY_IMPL(tdc, CUDA, m) {
   m.impl("assign_bf16", &assign_bf16);
   m.impl("assign_simt", &assign_simt);
+  m.impl("assign_exact", &assign_exact);
   m.impl("lloyd_small", &lloyd_small);
   m.impl("update", &update);
   m.impl("update_sorted", &update_sorted);

@@ -43,6 +43,10 @@ int tdc_bounds_scatter(const int32_t* active, const int* count, int64_t cap,
 int tdc_assign_simt(int dtype, const void* X, int64_t N, int64_t ldx, int D, const void* C,
                     int K, int32_t* labels, void* mind, hipStream_t stream);
 
+// N1 (exact, any D)  difference-form tiled assignment (fp32 / fp64), LDS use independent of D.
+int tdc_assign_exact(int dtype, const void* X, int64_t N, int64_t ldx, int D, const void* C, int K,
+                     int32_t* labels, void* mind, int num_cus, hipStream_t stream);
+
 // Fused small-K Lloyd step (assign + per-cluster sums/counts in registers), fp32/fp64.
 // Returns hipErrorInvalidValue if (K, D) exceeds the compiled register tiles.
 int tdc_lloyd_small(int dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,

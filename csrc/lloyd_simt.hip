@@ -339,6 +339,112 @@ int tdc_lloyd_small(int dtype, int acc_dtype, const void* X, int64_t N, int64_t 
   return (int)hipErrorInvalidValue;
 }
 
+// ------------------------------------------------------------------------------------
+// exact assignment for ANY D (fp32 / fp64, difference form like the reference's
+// Sub/Square/Sum, `scripts/distribuitedClustering.py:228-230`): 64-row x 64-centroid block
+// tiles, 16 x 16 threads with a 4 x 4 register micro-tile, rows and centroids staged
+// through LDS in 16-feature chunks (LDS use independent of D), argmin kept per row and
+// merged over the 16 centroid lanes at the end.  Replaces the library-GEMM fallback for
+// fp32 D > 64 / fp64 D > 32 (the GEMM expansion loses the exact-difference precision).
+// ------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void assign_exact_kernel(const T* __restrict__ X, int64_t N,
+                                                           int64_t ldx, int D,
+                                                           const T* __restrict__ C, int K,
+                                                           int32_t* __restrict__ labels,
+                                                           T* __restrict__ mind) {
+  constexpr int R = 64, KT = 64, DC = 16;
+  __shared__ T s_x[R][DC + 1];
+  __shared__ T s_c[KT][DC + 1];
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  for (int64_t r0 = (int64_t)blockIdx.x * R; r0 < N; r0 += (int64_t)gridDim.x * R) {
+    T best[4];
+    int bk[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      best[i] = (T)INFINITY;
+      bk[i] = 0;
+    }
+    for (int k0 = 0; k0 < K; k0 += KT) {
+      T acc[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = (T)0;
+      for (int dc = 0; dc < D; dc += DC) {
+        __syncthreads();
+        for (int e = tid; e < R * DC; e += 256) {
+          const int r = e / DC, d = e % DC;
+          s_x[r][d] = (r0 + r < N && dc + d < D) ? X[(r0 + r) * ldx + dc + d] : (T)0;
+          s_c[r][d] = (k0 + r < K && dc + d < D) ? C[(int64_t)(k0 + r) * D + dc + d] : (T)0;
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int d = 0; d < DC; ++d) {
+          T xv[4], cv[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) xv[i] = s_x[ty + 16 * i][d];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) cv[j] = s_c[tx + 16 * j][d];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const T df = xv[i] - cv[j];
+              acc[i][j] = fma(df, df, acc[i][j]);
+            }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = k0 + tx + 16 * j;  // ascending per thread: strict < keeps the first
+        if (k < K) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (acc[i][j] < best[i]) {
+              best[i] = acc[i][j];
+              bk[i] = k;
+            }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        const T ob = __shfl_xor(best[i], o, 64);
+        const int ok = __shfl_xor(bk[i], o, 64);
+        if (ob < best[i] || (ob == best[i] && ok < bk[i])) {
+          best[i] = ob;
+          bk[i] = ok;
+        }
+      }
+      const int64_t row = r0 + ty + 16 * i;
+      if (tx == 0 && row < N) {
+        labels[row] = bk[i];
+        if (mind) mind[row] = best[i];
+      }
+    }
+  }
+}
+
+int tdc_assign_exact(int dtype, const void* X, int64_t N, int64_t ldx, int D, const void* C, int K,
+                     int32_t* labels, void* mind, int num_cus, hipStream_t s) {
+  if (N <= 0) return 0;
+  int64_t blocks = (N + 63) / 64;
+  if (blocks > (int64_t)num_cus * 8) blocks = (int64_t)num_cus * 8;
+  if (dtype == TDC_F32)
+    hipLaunchKernelGGL(assign_exact_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s,
+                       (const float*)X, N, ldx, D, (const float*)C, K, labels, (float*)mind);
+  else if (dtype == TDC_F64)
+    hipLaunchKernelGGL(assign_exact_kernel<double>, dim3((unsigned)blocks), dim3(256), 0, s,
+                       (const double*)X, N, ldx, D, (const double*)C, K, labels, (double*)mind);
+  else
+    return (int)hipErrorInvalidValue;
+  TDC_CHECK_LAUNCH();
+  return 0;
+}
+
 int tdc_assign_simt(int dtype, const void* X, int64_t N, int64_t ldx, int D, const void* C,
                     int K, int32_t* labels, void* mind, hipStream_t s) {
   if (N <= 0) return 0;

@@ -16,7 +16,8 @@ Variants (picked by :func:`make_lloyd_ops`):
                           update from the full-precision shard
 ``HipSmallLloyd``         fused fp32/fp64 assign+accumulate (reference configs)
 ``HipSimtLloyd``          fp32/fp64 exact SIMT assign + LDS update
-``HipGemmLloyd``          fp32/fp64 large-D: library GEMM assign + LDS update
+``HipExactLloyd``         fp32/fp64 large-D (and bf16 D > 512): tiled exact assign
+``HipGemmLloyd``          fp32/fp64 large-D via library GEMM (comparisons only)
 ``TorchLloyd``            plain PyTorch (CPU ranks, oracle)
 ========================  =====================================================
 """
@@ -638,8 +639,23 @@ class HipSimtLloyd(_HipExactBase):
         self.ops.assign_simt(self.x, C, labels, mind)
 
 
+class HipExactLloyd(_HipExactBase):
+    """Large-D fp32/fp64: native tiled difference-form assignment (csrc/lloyd_simt.hip
+    assign_exact, any D) + native update."""
+    name = "hip_exact_tiled"
+
+    def step(self, C, labels, mind, sums, counts):
+        self.assign(C, labels, mind)
+        self.update(self.x, labels, sums, counts)
+
+    def assign(self, C, labels, mind):
+        self.ops.assign_exact(self.x, C, labels, mind)
+
+
 class HipGemmLloyd(_HipExactBase):
-    """Large-D fp32/fp64: distance via the vendor GEMM (plain library GEMM), native update."""
+    """Large-D fp32/fp64 via the vendor GEMM expansion (library GEMM), native update:
+    faster than the exact kernel at very large K*D but not difference-form exact
+    (``backend`` never selects it automatically; kept for comparisons)."""
     name = "hip_gemm"
 
     def step(self, C, labels, mind, sums, counts):
@@ -675,14 +691,14 @@ def _make_lloyd_ops(x, k, dtype, backend, empty_cluster, deterministic):
             return HipBf16Lloyd(x, k, empty_cluster)
         if wide_bf16_dim(d) is not None:
             return HipWideBf16Lloyd(x, k, empty_cluster)
-        return HipGemmLloyd(x, k, "fp32", empty_cluster)
+        return HipExactLloyd(x, k, "fp32", empty_cluster)  # bf16 D > 512: exact fp32 tiles
     tdt = TORCH_DTYPES[dtype]
     ops = _native.require()
     if ops.lloyd_small_supported(tdt, k, d) and not deterministic:
         return HipSmallLloyd(x, k, dtype, empty_cluster)
     if d <= (64 if dtype == "fp32" else 32):
         return HipSimtLloyd(x, k, dtype, empty_cluster)
-    return HipGemmLloyd(x, k, dtype, empty_cluster)
+    return HipExactLloyd(x, k, dtype, empty_cluster)
 
 
 # ----------------------------------------------------------------------------- FCM

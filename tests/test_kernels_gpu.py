@@ -515,3 +515,37 @@ def test_hip_gemm_fcm_step_matches_reference(gpu, m):
     torch.testing.assert_close(ws, b, rtol=5e-4 * m, atol=1e-6 * n)
     torch.testing.assert_close(wx, a, rtol=5e-4 * m, atol=1e-5 * n)
     assert (labels == lr).double().mean().item() > 0.999
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64])
+@pytest.mark.parametrize("n,d,k", [(5000, 96, 100), (4001, 128, 1000), (3000, 256, 130),
+                                   (2000, 768, 257), (1500, 33, 65)])
+def test_assign_exact_wide_d(gpu, dt, n, d, k):
+    """Exact tiled assignment for wide D (replaces the library GEMM): difference-form
+    distances, labels at the exact minimum, min distances to rounding."""
+    from tensorflow_distributed_clustering_amd import _native
+    ops = _native.require()
+    x64, c64 = _bf16_case(n, d, k, "cpu", seed=n + d)
+    x64, c64 = x64.double(), c64.double()
+    x, c = x64.to(dt).to(gpu), c64.to(dt).to(gpu)
+    labels = torch.full((n,), -1, dtype=torch.int32, device=gpu)
+    mind = torch.zeros(n, dtype=dt, device=gpu)
+    ops.assign_exact(x, c, labels, mind)
+    rel = 1e-13 if dt == torch.float64 else 2e-6
+    best = _check_labels(x.double().cpu(), c.double().cpu(), labels.cpu(), rel=rel)
+    torch.testing.assert_close(mind.double().cpu(), best, rtol=1e-12 if dt == torch.float64 else 1e-5,
+                               atol=1e-9)
+
+
+@pytest.mark.parametrize("dtype,d", [("fp64", 48), ("fp32", 96), ("bf16", 768)])
+def test_wide_d_lloyd_is_native(gpu, dtype, d):
+    """fp64 D > 32, fp32 D > 64 and bf16 D > 512 run the native exact kernels (no GEMM)."""
+    import tensorflow_distributed_clustering_amd as tdc
+    from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs
+    x = gaussian_blobs(20000, d, 20, seed=3, dtype=torch.float64, device=gpu)
+    r = tdc.KMeans(tdc.ClusterConfig(n_clusters=20, max_iter=3, dtype=dtype, seed=2)).fit(x).result_
+    assert r.backend == "hip_exact_tiled"
+    o = tdc.KMeans(tdc.ClusterConfig(n_clusters=20, max_iter=3, dtype="fp64", seed=2,
+                                     backend="torch"), device="cpu").fit(x.cpu()).result_
+    torch.testing.assert_close(torch.as_tensor(r.centers), torch.as_tensor(o.centers),
+                               rtol=1e-4, atol=1e-4)
