@@ -838,22 +838,26 @@ class HipMfmaFCM(_LocalOpsBase):
         return self.work
 
     def _set_x(self, x):
-        n = int(x.shape[0])
+        """Hold the rows; they are split into hi/lo at the next step, once the shift (the
+        mean of the first centroids -- replicated, so resident, streamed and every world
+        size use the same one) is known."""
+        self._xsrc = x if (x.dtype == torch.float32 and x.stride(1) == 1) else x.float().contiguous()
+        self.n = int(x.shape[0])
+        self._dirty = True
+        self.x = None
+
+    def _split_x(self):
+        n = self.n
         if self.xh is None or self.xh.shape[0] < n:
             dev = self.device
             self.xh = torch.empty(n, self.dp, dtype=torch.bfloat16, device=dev)
             self.xl = torch.empty_like(self.xh)
             self.xx = torch.empty(n, dtype=torch.float32, device=dev)
             self.rowinfo = torch.empty(n, dtype=torch.float32, device=dev)
-        xf = x if (x.dtype == torch.float32 and x.stride(1) == 1) else x.float().contiguous()
-        self.n = n
-        if self.mu is None and n >= 64:  # (not from a 1-row probe of a streamed engine)
-            # fixed shift (first shard / chunk mean): distances are shift-invariant, and the
-            # expansion's cancellation error scales with |x - mu|^2 instead of |x|^2
-            self.mu = xf[:, : self.d].double().mean(0).float()
-        self.ops.fcm_split_rows(xf[:, : self.d], n, 0, self.xh[:n], self.xl[:n], self.xx[:n],
-                                self.mu)
-        self.x = None  # the hi/lo rows are the shard from here on
+        self.ops.fcm_split_rows(self._xsrc[:, : self.d], n, 0, self.xh[:n], self.xl[:n],
+                                self.xx[:n], self.mu)
+        self._xsrc = None  # the hi/lo rows are the shard from here on
+        self._dirty = False
 
     def bind(self, x):
         if x.shape[1] != self.d:
@@ -862,8 +866,14 @@ class HipMfmaFCM(_LocalOpsBase):
         return self
 
     def prepare(self, C):
-        self.ops.fcm_split_rows(C.float().contiguous(), self.k, 1, self.ch, self.cl, self.cc,
-                                self.mu)
+        Cf = C.float().contiguous()
+        if self.mu is None:
+            # fixed shift: distances are shift-invariant and the expansion's cancellation
+            # error scales with |x - mu|^2 instead of |x|^2
+            self.mu = Cf.double().mean(0).float()
+        self.ops.fcm_split_rows(Cf, self.k, 1, self.ch, self.cl, self.cc, self.mu)
+        if self._dirty:
+            self._split_x()
 
     def _ops_args(self):
         n = self.n
