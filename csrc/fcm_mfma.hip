@@ -37,6 +37,10 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
+#ifndef TDC_FCM_SCHED
+#define TDC_FCM_SCHED 0
+#endif
+
 constexpr float ZERO_FLOOR = 1.52587890625e-05f;  // 2^-16 (an exact hit computes ~2^-17 |x|^2)
 
 struct MParam {
@@ -343,75 +347,112 @@ __global__ __launch_bounds__(256, 1) void fcm_mfma_accum_kernel(
     if (more) TDC_TILE_LOAD(r0 + TP)
     const char* xh = s_x[buf];
     const char* xl = s_x[buf] + IMG;
-    // distances of both 32-point halves first, so the membership VALU of half 0 can issue
-    // beside the MFMAs of half 1 and of the W^T X products
-    f32x16 acc[2];
+    // Software pipeline over the two 32-point halves, written out explicitly so that the
+    // membership VALU of one half issues between the MFMAs of the other (one wave per
+    // SIMD: nothing else hides it):
+    //   dist(0) | dist(1) + memberships(0) | W^T X(0) + memberships(1) | W^T X(1)
+    constexpr int EPK = 16 / KS;          // membership elements per distance k-step
+    constexpr int EPW = 16 / (2 * NDT);   // membership elements per W^T X (s, dt) step
+    f32x16 acc0, acc1;
+    bf16x8 wh0[2], wl0[2], wh1[2], wl1[2];
+    f32x4 xq[4], iq[4];
+#define TDC_DIST(ACC, SUB, INTERLEAVE)                                                    \
+  {                                                                                       \
+    _Pragma("unroll") for (int i = 0; i < 16; ++i) ACC[i] = ccl;                         \
+    const int prow = (SUB) * 32 + r;                                                      \
+    bf16x8 ah = as_bf16x8(*reinterpret_cast<const uint4*>(xh + xoff<DP>(prow, h * (CPR / 2)))); \
+    bf16x8 al = as_bf16x8(*reinterpret_cast<const uint4*>(xl + xoff<DP>(prow, h * (CPR / 2)))); \
+    _Pragma("unroll") for (int kk = 0; kk < KS; ++kk) {                                   \
+      const int kn = kk + 1 < KS ? kk + 1 : kk;                                           \
+      const bf16x8 ahn = as_bf16x8(*reinterpret_cast<const uint4*>(xh + xoff<DP>(prow, h * (CPR / 2) + kn))); \
+      const bf16x8 aln = as_bf16x8(*reinterpret_cast<const uint4*>(xl + xoff<DP>(prow, h * (CPR / 2) + kn))); \
+      ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, ch[kk], ACC, 0, 0, 0);            \
+      ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, cl[kk], ACC, 0, 0, 0);            \
+      ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, ch[kk], ACC, 0, 0, 0);            \
+      INTERLEAVE(kk * EPK, EPK)                                                           \
+      ah = ahn;                                                                           \
+      al = aln;                                                                           \
+    }                                                                                     \
+  }
+  // memberships of elements [I0, I0 + CNT) of half SUB (distances in ACC) -> WH/WL
+#define TDC_MEMB(ACC, WH, WL, I0, CNT)                                                    \
+  _Pragma("unroll") for (int q = 0; q < (CNT); ++q) {                                     \
+    const int i = (I0) + q, g4 = i >> 2, e = i & 3;                                       \
+    const float zf = ZERO_FLOOR * xq[g4][e];                                              \
+    const float d2 = fmaxf(ACC[i] + xq[g4][e], zf);                                       \
+    float u = mt<MODE>(d2, prm.expo) * iq[g4][e];                                         \
+    if constexpr (!NZ) u = iq[g4][e] < 0.f ? (d2 <= zf ? 1.f : 0.f) : u;                  \
+    const float wv = mw<MODE>(u, prm.m);                                                  \
+    wsum += wv;                                                                           \
+    const __bf16 bhv = (__bf16)wv;                                                        \
+    WH[i >> 3][i & 7] = bhv;                                                              \
+    WL[i >> 3][i & 7] = (__bf16)(wv - (float)bhv);                                        \
+  }
+#define TDC_LOADQ(SUB)                                                                    \
+  _Pragma("unroll") for (int g4 = 0; g4 < 4; ++g4) {                                      \
+    const int pt = (SUB) * 32 + 8 * g4 + 4 * h;                                           \
+    xq[g4] = *reinterpret_cast<const f32x4*>(&s_xx[buf][pt]);                             \
+    iq[g4] = *reinterpret_cast<const f32x4*>(&s_in[buf][pt]);                             \
+  }
+  // W^T X of half SUB (weights WH/WL): A = W (row = centroid, k = points), B = X^T via
+  // transposed reads (T10); INTERLEAVE runs between the (s, dt) steps
+#define TDC_TRLD(SUB, T_, H0, H1, L0, L1)                                                \
+  {                                                                                       \
+    const int s_ = (T_) / NDT, dt_ = (T_) % NDT;                                          \
+    const int c0 = (dt_ * 32 + 16 * (g & 1)) >> 3;                                        \
+    const int rA = (SUB) * 32 + 16 * s_ + 4 * (g >> 1) + q4;                              \
+    const int oA = xoff<DP>(rA, c0 + (p4 >> 1)) + 8 * (p4 & 1);                           \
+    const int oB = xoff<DP>(rA + 8, c0 + (p4 >> 1)) + 8 * (p4 & 1);                       \
+    H0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xh + oA));                  \
+    H1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xh + oB));                  \
+    L0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xl + oA));                  \
+    L1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xl + oB));                  \
+  }
+  // W^T X of half SUB (weights WH/WL): A = W (row = centroid, k = points), B = X^T via
+  // transposed reads (T10), prefetched one (s, dt) step ahead; INTERLEAVE runs between
+#define TDC_WTX(SUB, WH, WL, INTERLEAVE)                                                  \
+  {                                                                                       \
+    s16x4 h0, h1, l0, l1;                                                                 \
+    TDC_TRLD(SUB, 0, h0, h1, l0, l1)                                                      \
+    _Pragma("unroll") for (int t = 0; t < 2 * NDT; ++t) {                                 \
+      s16x4 nh0, nh1, nl0, nl1;                                                           \
+      TDC_TRLD(SUB, (t + 1 < 2 * NDT ? t + 1 : t), nh0, nh1, nl0, nl1)                    \
+      const int s = t / NDT, dt = t % NDT;                                                \
+      const bf16x8 xbh = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7)); \
+      const bf16x8 xbl = __builtin_bit_cast(bf16x8, __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7)); \
+      out[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(WH[s], xbh, out[dt], 0, 0, 0);    \
+      out[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(WH[s], xbl, out[dt], 0, 0, 0);    \
+      out[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(WL[s], xbh, out[dt], 0, 0, 0);    \
+      INTERLEAVE(t * EPW, EPW)                                                            \
+      h0 = nh0; h1 = nh1; l0 = nl0; l1 = nl1;                                             \
+    }                                                                                     \
+  }
+#define TDC_NONE(I0, CNT)
+#define TDC_MEMB0(I0, CNT) TDC_MEMB(acc0, wh0, wl0, I0, CNT)
+#define TDC_MEMB1(I0, CNT) TDC_MEMB(acc1, wh1, wl1, I0, CNT)
+    TDC_DIST(acc0, 0, TDC_NONE)
+    TDC_LOADQ(0)
+    TDC_DIST(acc1, 1, TDC_MEMB0)
+    TDC_LOADQ(1)
+    TDC_WTX(0, wh0, wl0, TDC_MEMB1)
+    TDC_WTX(1, wh1, wl1, TDC_NONE)
+#undef TDC_NONE
+#undef TDC_MEMB0
+#undef TDC_MEMB1
+#undef TDC_DIST
+#undef TDC_MEMB
+#undef TDC_LOADQ
+#undef TDC_WTX
+#undef TDC_TRLD
+#if TDC_FCM_SCHED
+    // interleave: one MFMA, then ~5 VALU and a DS read (the membership arithmetic of one
+    // half beside the MFMAs of the other; one wave per SIMD cannot hide it otherwise)
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      // ---- distances: rows (registers) = points, lane column = centroid ----
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[sub][i] = ccl;
-      const int prow = sub * 32 + r;
-      bf16x8 ah = as_bf16x8(*reinterpret_cast<const uint4*>(xh + xoff<DP>(prow, h * (CPR / 2))));
-      bf16x8 al = as_bf16x8(*reinterpret_cast<const uint4*>(xl + xoff<DP>(prow, h * (CPR / 2))));
-#pragma unroll
-      for (int kk = 0; kk < KS; ++kk) {
-        const int kn = kk + 1 < KS ? kk + 1 : kk;
-        const bf16x8 ahn = as_bf16x8(*reinterpret_cast<const uint4*>(xh + xoff<DP>(prow, h * (CPR / 2) + kn)));
-        const bf16x8 aln = as_bf16x8(*reinterpret_cast<const uint4*>(xl + xoff<DP>(prow, h * (CPR / 2) + kn)));
-        acc[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, ch[kk], acc[sub], 0, 0, 0);
-        acc[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, cl[kk], acc[sub], 0, 0, 0);
-        acc[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, ch[kk], acc[sub], 0, 0, 0);
-        ah = ahn;
-        al = aln;
-      }
+    for (int i = 0; i < 96; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
     }
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      // ---- memberships -> w = wh + wl (bf16 pair); register i = point (i&3)+8(i>>2)+4h ----
-      // padded rows carry info 0 and a huge norm (w = 0); pad centroids give finite w whose
-      // slab rows the reduction never reads
-      bf16x8 wh[2], wl[2];
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int pt = sub * 32 + 8 * g4 + 4 * h;
-        const f32x4 xq = *reinterpret_cast<const f32x4*>(&s_xx[buf][pt]);
-        const f32x4 iq = *reinterpret_cast<const f32x4*>(&s_in[buf][pt]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 4 * g4 + e;
-          const float zf = ZERO_FLOOR * xq[e];
-          const float d2 = fmaxf(acc[sub][i] + xq[e], zf);
-          float u = mt<MODE>(d2, prm.expo) * iq[e];
-          if constexpr (!NZ) u = iq[e] < 0.f ? (d2 <= zf ? 1.f : 0.f) : u;
-          const float wv = mw<MODE>(u, prm.m);
-          wsum += wv;
-          const __bf16 bhv = (__bf16)wv;
-          wh[i >> 3][i & 7] = bhv;
-          wl[i >> 3][i & 7] = (__bf16)(wv - (float)bhv);
-        }
-      }
-      // ---- W^T X: A = W (row = centroid, k = points), B = X^T via transposed reads ----
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) {
-          const int c0 = (dt * 32 + 16 * (g & 1)) >> 3;  // first 8-feature chunk of the block
-          const int rA = sub * 32 + 16 * s + 4 * (g >> 1) + q4;
-          const int oA = xoff<DP>(rA, c0 + (p4 >> 1)) + 8 * (p4 & 1);
-          const int oB = xoff<DP>(rA + 8, c0 + (p4 >> 1)) + 8 * (p4 & 1);
-          const s16x4 h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xh + oA));
-          const s16x4 h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xh + oB));
-          const s16x4 l0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xl + oA));
-          const s16x4 l1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xl + oB));
-          const bf16x8 xbh = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7));
-          const bf16x8 xbl = __builtin_bit_cast(bf16x8, __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7));
-          out[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[s], xbh, out[dt], 0, 0, 0);
-          out[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[s], xbl, out[dt], 0, 0, 0);
-          out[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl[s], xbh, out[dt], 0, 0, 0);
-        }
-      }
-    }
+#endif
     if (more) TDC_TILE_STORE(buf ^ 1)
     __syncthreads();
     buf ^= 1;
