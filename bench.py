@@ -83,6 +83,12 @@ def parse(argv=None):
     ap.add_argument("--algorithm", default="lloyd", choices=["lloyd", "bounded"],
                     help="bounded: Lloyd with Hamerly bounds (not the headline metric's "
                          "algorithm; reported in config.algorithm)")
+    ap.add_argument("--source", default="device", choices=["device", "host"],
+                    help="host: the shard lives in host memory (fp32) and streams through "
+                         "HBM via the native RowStreamer (pinned ring + copy stream), with "
+                         "the hybrid-residency planner under --hbm-budget-gb")
+    ap.add_argument("--hbm-budget-gb", type=float, default=0.0,
+                    help="per-GPU HBM budget of the stream planner (--source host)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step from a captured HIP graph (1 GPU; RCCL capture for N>1)")
     ap.add_argument("--profile-steps", action="store_true",
@@ -123,7 +129,11 @@ def main(argv=None):
     s, e = shard_bounds(n_global, world, rank)
     dt = {"fp8": torch.bfloat16, "bf16": torch.bfloat16, "fp32": torch.float32,
           "fp64": torch.float64}[a.dtype]
-    x = gaussian_blobs(e - s, a.dim, a.k, seed=a.seed, row_offset=s, dtype=dt, device=dev)
+    src_info = None
+    if a.source == "host":
+        x, src_info = host_shard(a, e - s, s, dev, torch)
+    else:
+        x = gaussian_blobs(e - s, a.dim, a.k, seed=a.seed, row_offset=s, dtype=dt, device=dev)
     cfg = tdc.ClusterConfig(n_clusters=a.k, max_iter=a.steps, dtype=a.dtype, init=a.init,
                             seed=a.seed, compute_inertia=False, algorithm=a.algorithm,
                             fuzzifier=a.fuzzifier)
@@ -141,7 +151,11 @@ def main(argv=None):
         eng = BoundedLloydEngine(x, cfg, comm, n_global, s, defer_init=True)
         points_per_step = n_global
     else:
-        eng = LloydEngine(x, cfg, comm, n_global, s, defer_init=True)
+        if src_info is not None:
+            eng = LloydEngine(x, cfg, comm, n_global, s, chunk_rows=src_info["chunk_rows"],
+                              defer_init=True)
+        else:
+            eng = LloydEngine(x, cfg, comm, n_global, s, defer_init=True)
         points_per_step = n_global
     init_s = None
     if hasattr(eng, "init_centroids") and getattr(eng, "c0", None) is None:
@@ -162,6 +176,7 @@ def main(argv=None):
     comm.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
+    h2d0 = getattr(x, "bytes_h2d", 0) if src_info is not None else 0
     t0 = time.perf_counter()
     for _ in range(a.steps):
         eng.step()
@@ -169,6 +184,8 @@ def main(argv=None):
         torch.cuda.synchronize(dev)
     comm.barrier()
     elapsed = comm.max_scalar(time.perf_counter() - t0)
+    if src_info is not None:
+        src_info["h2d_GBps"] = (x.bytes_h2d - h2d0) / elapsed / 1e9
 
     ms = elapsed / max(1, a.steps) * 1e3
     pps = points_per_step * a.steps / elapsed
@@ -203,12 +220,46 @@ def main(argv=None):
         }
         if breakdown:
             out["phase_ms"] = breakdown
+        if src_info is not None:
+            out["data"] = "synthetic gaussian blobs in HOST memory (fp32), streamed via RowStreamer"
+            out["source"] = src_info
         if a.algorithm != "lloyd":
             out["config"]["algorithm"] = a.algorithm
         if a.method == "fcm":
             out["config"]["fuzzifier"] = a.fuzzifier if a.fuzzifier is not None else a.dim
             out["active_frac_last_step"] = getattr(eng, "active_frac", None)
         print(json.dumps(out), flush=True)
+
+
+def host_shard(a, n_rows, row_offset, dev, torch):
+    """The rank's shard generated in host memory (fp32) and wrapped in a HostSource with the
+    hybrid-residency planner: the first rows that fit the budget stay in HBM, the rest
+    streams every pass (RowStreamer threads convert to the kernel layout into a pinned
+    ring; H2D on a copy stream)."""
+    import numpy as np
+    from tensorflow_distributed_clustering_amd.data.stream import (HostSource, plan_chunk_rows,
+                                                                   plan_resident_rows)
+    from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs
+    from tensorflow_distributed_clustering_amd.ops import padded_dim
+    xh = np.empty((n_rows, a.dim), dtype=np.float32)
+    step = 1 << 24
+    t0 = time.perf_counter()
+    for r0 in range(0, n_rows, step):
+        r1 = min(n_rows, r0 + step)
+        xh[r0:r1] = gaussian_blobs(r1 - r0, a.dim, a.k, seed=a.seed, row_offset=row_offset + r0,
+                                   dtype=torch.float32, device=dev).cpu().numpy()
+        if (r0 // step) % 8 == 0:
+            print(f"[bench] host shard {r1}/{n_rows} rows ({time.perf_counter() - t0:.0f} s)",
+                  file=sys.stderr, flush=True)
+    width = padded_dim(a.dim) if a.dtype == "bf16" else a.dim
+    es = 2 if a.dtype == "bf16" else 4
+    layout = (torch.bfloat16 if a.dtype == "bf16" else torch.float32, width)
+    chunk = a.batch_size if a.mode == "minibatch" and a.batch_size else \
+        (plan_chunk_rows(n_rows, width * es, a.k, a.dim, dev, a.hbm_budget_gb) or (1 << 22))
+    resident = plan_resident_rows(n_rows, width * es, chunk, a.k, a.dim, dev, a.hbm_budget_gb)
+    src = HostSource(xh, layout, dev, row_offset, resident_rows=resident, n_threads=16)
+    return src, {"rows": n_rows, "resident_rows": resident, "chunk_rows": chunk,
+                 "hbm_budget_gb": a.hbm_budget_gb}
 
 
 def vs_baseline(a, world, pps):

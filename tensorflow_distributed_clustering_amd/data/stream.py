@@ -108,6 +108,7 @@ class HostSource:
         # only the remainder streams every pass (data 1.5x HBM -> 1/3 of it crosses PCIe)
         self.resident_rows = int(min(max(0, resident_rows), self.n_rows)) if self.device.type == "cuda" else 0
         self._resident = None
+        self.bytes_h2d = 0  # streamed (non-resident) bytes handed to the device so far
 
     def chunks(self, chunk_rows: int) -> Iterator[Tuple[int, torch.Tensor]]:
         chunk_rows = min(chunk_rows or self.n_rows, self.n_rows)
@@ -164,6 +165,7 @@ class HostSource:
                 ev.record(copy_stream)
             h2d_done[j] = ev
             compute.wait_event(ev)
+            self.bytes_h2d += rows * width * devbuf[b].element_size()
             yield self.row_offset + s, devbuf[b][:rows]
             done = torch.cuda.Event()
             done.record(compute)

@@ -89,6 +89,8 @@ class FcmEngine(OomGuard):
         self.shift = torch.zeros(1, dtype=torch.float32, device=dev) if cfg.tol > 0 else None
         self.n_iter = 0
         self.c0 = None
+        if self.oom_guard:
+            self._oom_alloc()
         if not defer_init:
             self.init_centroids()
 

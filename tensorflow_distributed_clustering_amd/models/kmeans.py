@@ -82,18 +82,25 @@ class OomGuard:
     failed step.  Engines provide ``rsag``, ``C`` (+ ``C_pad``/``_r0``/``_kr`` under rsag),
     ``buf``, ``oom_flag``, ``device``, ``n_iter`` and ``centers()``."""
 
+    def _oom_alloc(self):
+        """Ring of pre-step centroids, pinned flag slots and events (allocated at setup,
+        never inside the timed loop: a pinned allocation costs ~1 ms)."""
+        src = self.C_pad[self._r0: self._r0 + self._kr] if self.rsag else self.C
+        self._ring = [torch.empty_like(src), torch.empty_like(src)]
+        self._ring_iter = [-1, -1]
+        self._flag_host = torch.zeros(2, dtype=self.buf.dtype,
+                                      pin_memory=self.device.type == "cuda")
+        self._flag_ev = ([torch.cuda.Event(), torch.cuda.Event()]
+                         if self.device.type == "cuda" else [None, None])
+        self._flag_set = [False, False]
+
     def save_state(self):
         """Keep the pre-step centroids (this rank's slice under rsag) for a rollback."""
+        if getattr(self, "_ring", None) is None:
+            self._oom_alloc()
         src = self.C_pad[self._r0: self._r0 + self._kr] if self.rsag else self.C
-        ring = getattr(self, "_ring", None)
-        if ring is None or ring[0].shape != src.shape:
-            ring = self._ring = [torch.empty_like(src), torch.empty_like(src)]
-            self._ring_iter = [-1, -1]
-            self._flag_host = torch.zeros(2, dtype=self.buf.dtype,
-                                          pin_memory=self.device.type == "cuda")
-            self._flag_ev = [None, None]
         slot = self.n_iter & 1
-        ring[slot].copy_(src)
+        self._ring[slot].copy_(src)
         self._ring_iter[slot] = self.n_iter
 
     def post_flag(self):
@@ -101,17 +108,18 @@ class OomGuard:
         slot = (self.n_iter - 1) & 1
         if self.device.type == "cuda":
             self._flag_host[slot:slot + 1].copy_(self.oom_flag, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-            self._flag_ev[slot] = ev
+            self._flag_ev[slot].record()
         else:
             self._flag_host[slot:slot + 1].copy_(self.oom_flag)
+        self._flag_set[slot] = True
 
     def failed_step(self, lag: int = 1) -> Optional[int]:
         """Index (0-based) of a step whose flag is set, checking the step ``lag`` steps
         back (lag 0: the last one, a host sync)."""
         n = self.n_iter - 1 - lag
         if n < 0 or getattr(self, "_ring", None) is None or self._ring_iter[n & 1] != n:
+            return None
+        if not self._flag_set[n & 1]:
             return None
         ev = self._flag_ev[n & 1]
         if ev is not None:
@@ -237,6 +245,8 @@ class LloydEngine(OomGuard):
         self.bucket_bytes = cfg.bucket_kb << 10
         self.n_iter = 0
         self.c0 = None
+        if self.oom_guard:
+            self._oom_alloc()
         if not defer_init:
             self.init_centroids()
 
