@@ -131,18 +131,24 @@ bool lloyd_small_supported(at::ScalarType dtype, int64_t K, int64_t D) {
   return tdc_lloyd_small_supported(dcode(dtype), (int)K, (int)D) != 0;
 }
 
-void lloyd_small(const at::Tensor& X, const at::Tensor& C, at::Tensor& labels,
+void lloyd_small(const at::Tensor& X, const at::Tensor& C, const std::optional<at::Tensor>& labels,
                  const std::optional<at::Tensor>& mind, at::Tensor& sums, at::Tensor& counts) {
   check_cuda(X, "X");
   check_rows(X, "X");
-  TORCH_CHECK(C.scalar_type() == X.scalar_type() && C.is_contiguous(), "tdc.lloyd_small: C");
+  TORCH_CHECK(C.scalar_type() == X.scalar_type() && C.is_contiguous() && X.size(1) == C.size(1),
+              "tdc.lloyd_small: C");
   TORCH_CHECK(sums.scalar_type() == counts.scalar_type(), "tdc.lloyd_small: sums/counts dtype");
   TORCH_CHECK(sums.is_contiguous() && counts.is_contiguous(), "tdc.lloyd_small: contiguity");
+  TORCH_CHECK(sums.numel() == C.numel() && counts.numel() == C.size(0),
+              "tdc.lloyd_small: sums [K, D] / counts [K]");
+  const int64_t n = X.size(0);
+  if (labels) TORCH_CHECK(labels->numel() >= n && labels->is_contiguous(), "tdc.lloyd_small: labels");
+  if (mind) TORCH_CHECK(mind->numel() >= n && mind->is_contiguous(), "tdc.lloyd_small: mind");
   const DevGuard guard(X.device());
-  check(tdc_lloyd_small(dcode(X.scalar_type()), dcode(sums.scalar_type()), X.data_ptr(),
-                        X.size(0), X.stride(0), (int)C.size(1), C.data_ptr(), (int)C.size(0),
-                        labels.data_ptr<int32_t>(), opt_ptr(mind), sums.data_ptr(),
-                        counts.data_ptr(), cur_stream()),
+  check(tdc_lloyd_small(dcode(X.scalar_type()), dcode(sums.scalar_type()), X.data_ptr(), n,
+                        X.stride(0), (int)C.size(1), C.data_ptr(), (int)C.size(0),
+                        labels ? labels->data_ptr<int32_t>() : nullptr, opt_ptr(mind),
+                        sums.data_ptr(), counts.data_ptr(), cur_stream()),
         "lloyd_small");
 }
 
@@ -207,17 +213,21 @@ bool fcm_small_supported(at::ScalarType dtype, int64_t K, int64_t D) {
 }
 
 void fcm_small(const at::Tensor& X, const at::Tensor& C, double m, bool nan_to_zero,
-               at::Tensor& labels, at::Tensor& wx, at::Tensor& ws) {
+               const std::optional<at::Tensor>& labels, at::Tensor& wx, at::Tensor& ws) {
   check_cuda(X, "X");
   check_rows(X, "X");
-  TORCH_CHECK(C.scalar_type() == X.scalar_type() && C.is_contiguous(), "tdc.fcm_small: C");
+  TORCH_CHECK(C.scalar_type() == X.scalar_type() && C.is_contiguous() && X.size(1) == C.size(1),
+              "tdc.fcm_small: C");
   TORCH_CHECK(wx.scalar_type() == ws.scalar_type() && wx.is_contiguous() && ws.is_contiguous(),
               "tdc.fcm_small: wx/ws");
+  TORCH_CHECK(wx.numel() == C.numel() && ws.numel() == C.size(0), "tdc.fcm_small: wx [K, D] / ws [K]");
+  const int64_t n = X.size(0);
+  if (labels) TORCH_CHECK(labels->numel() >= n && labels->is_contiguous(), "tdc.fcm_small: labels");
   const DevGuard guard(X.device());
-  check(tdc_fcm_small(dcode(X.scalar_type()), dcode(wx.scalar_type()), X.data_ptr(), X.size(0),
+  check(tdc_fcm_small(dcode(X.scalar_type()), dcode(wx.scalar_type()), X.data_ptr(), n,
                       X.stride(0), (int)C.size(1), C.data_ptr(), (int)C.size(0), m,
-                      nan_to_zero ? 1 : 0, labels.data_ptr<int32_t>(), wx.data_ptr(),
-                      ws.data_ptr(), cur_stream()),
+                      nan_to_zero ? 1 : 0, labels ? labels->data_ptr<int32_t>() : nullptr,
+                      wx.data_ptr(), ws.data_ptr(), cur_stream()),
         "fcm_small");
 }
 
@@ -758,12 +768,12 @@ TORCH_LIBRARY(tdc, m) {
   m.def("assign_simt(Tensor X, Tensor C, Tensor(a!) labels, Tensor(b!)? mind) -> ()");
   m.def("assign_exact(Tensor X, Tensor C, Tensor(a!) labels, Tensor(b!)? mind) -> ()");
   m.def("lloyd_small_supported(ScalarType dtype, int K, int D) -> bool", &lloyd_small_supported);
-  m.def("lloyd_small(Tensor X, Tensor C, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!) sums, Tensor(d!) counts) -> ()");
+  m.def("lloyd_small(Tensor X, Tensor C, Tensor(a!)? labels, Tensor(b!)? mind, Tensor(c!) sums, Tensor(d!) counts) -> ()");
   m.def("update(Tensor X, Tensor labels, Tensor(a!) sums, Tensor(b!) counts) -> ()");
   m.def("update_sorted_workspace(int N, int K) -> int", &update_sorted_workspace);
   m.def("update_sorted(Tensor X, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work, Tensor(d!)? cnt_hi=None, Tensor(e!)? cnt_lo=None) -> ()");
   m.def("fcm_small_supported(ScalarType dtype, int K, int D) -> bool", &fcm_small_supported);
-  m.def("fcm_small(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) wx, Tensor(c!) ws) -> ()");
+  m.def("fcm_small(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!)? labels, Tensor(b!) wx, Tensor(c!) ws) -> ()");
   m.def("fcm_tower_stats(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) rowinfo) -> ()");
   m.def("fcm_tower_accum(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor rowinfo, Tensor(a!) wx, Tensor(b!) ws) -> ()");
   m.def("fcm_split_rows(Tensor src, int valid, int neg2, Tensor(a!) hi, Tensor(b!) lo, Tensor(c!)? norm, Tensor? shift=None) -> ()");

@@ -20,6 +20,7 @@
 
 namespace tdc {
 
+// labels may be null (the fit's final label pass writes them).
 template <typename T, typename ACC, int KMAX, int DMAX>
 __global__ __launch_bounds__(256) void fcm_small_kernel(
     const T* __restrict__ X, int64_t N, int64_t ldx, int D, const T* __restrict__ C, int K,
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(256) void fcm_small_kernel(
       }
       t[k] = (u > (T)0) ? fcm_w(u, m, mint) : (T)0;
     }
-    labels[i] = best;
+    if (labels) labels[i] = best;
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
       wsum[k] += t[k];
@@ -117,9 +118,11 @@ __global__ __launch_bounds__(256) void fcm_small_kernel(
 template <typename T, typename ACC, int KMAX, int DMAX>
 int launch_fcm(const void* X, int64_t N, int64_t ldx, int D, const void* C, int K, double m,
                int nan_to_zero, int32_t* labels, void* wx, void* ws, hipStream_t s) {
-  int64_t g = (N + 256 * 8 - 1) / (256 * 8);
+  // exactly the blocks the GPU holds at once (see launch_small, csrc/lloyd_simt.hip)
+  static const int resident = resident_blocks(fcm_small_kernel<T, ACC, KMAX, DMAX>, 256);
+  int64_t g = (N + 255) / 256;
   if (g < 1) g = 1;
-  if (g > 2048) g = 2048;
+  if (g > resident) g = resident;
   const T expo = (T)(-1.0 / (m - 1.0));
   const int pmode = m == 2.0 ? 1 : (m == 3.0 ? 2 : (m == 5.0 ? 3 : 0));
   const int mint = (m == (double)(int)m && m >= 1.0 && m <= 16.0) ? (int)m : 0;
@@ -133,9 +136,11 @@ int launch_fcm(const void* X, int64_t N, int64_t ldx, int D, const void* C, int 
 template <typename T, typename ACC>
 int dispatch_fcm(const void* X, int64_t N, int64_t ldx, int D, const void* C, int K, double m,
                  int nz, int32_t* labels, void* wx, void* ws, hipStream_t s) {
-#define TDC_FCM(KM, DM) \
-  if (K <= KM && D <= DM) return launch_fcm<T, ACC, KM, DM>(X, N, ldx, D, C, K, m, nz, labels, wx, ws, s);
+#define TDC_FCM(KM, DM)                                                                    \
+  if (K <= KM && D <= DM)                                                                  \
+    return launch_fcm<T, ACC, KM, DM>(X, N, ldx, D, C, K, m, nz, labels, wx, ws, s);
   TDC_FCM(4, 4)
+  TDC_FCM(4, 6)  // the reference's own configs: D = 5, K <= 4
   TDC_FCM(4, 8)
   TDC_FCM(8, 4)
   TDC_FCM(8, 8)
@@ -292,14 +297,17 @@ __global__ __launch_bounds__(256) void fcm_rows_kernel(float* __restrict__ G, in
 int tdc_fcm_rows(float* G, int64_t rows, int K, const float* xx, const float* cc, float m,
                  int nan_to_zero, int32_t* labels, float* colsum, hipStream_t s) {
   if (rows <= 0) return 0;
-  // persistent waves: each visits ~64 rows, so the column-sum flush is 1 atomic per column
-  // per 64 rows (2048 blocks keep 32 waves per CU in flight)
-  int64_t blocks = (rows + 3) / 4;
-  if (blocks > 2048) blocks = 2048;
-  const dim3 grid((unsigned)blocks);
+  // persistent waves, exactly the blocks resident at once (every block the same row
+  // count, so a larger grid would leave a partial second round); the column-sum flush is
+  // one atomic per column per block
+  const int64_t want = (rows + 3) / 4;
 #define TDC_FR(NVV)                                                                           \
-  hipLaunchKernelGGL(tdc::fcm_rows_kernel<NVV>, grid, dim3(256), 0, s, G, rows, K, xx, cc, m, \
-                     nan_to_zero, labels, colsum)
+  do {                                                                                        \
+    static const int res = resident_blocks(tdc::fcm_rows_kernel<NVV>, 256);                   \
+    const dim3 grid((unsigned)(want < res ? want : res));                                     \
+    hipLaunchKernelGGL(tdc::fcm_rows_kernel<NVV>, grid, dim3(256), 0, s, G, rows, K, xx, cc,  \
+                       m, nan_to_zero, labels, colsum);                                       \
+  } while (0)
   if (K <= 256) TDC_FR(4);
   else if (K <= 1024) TDC_FR(16);
   else if (K <= 2048) TDC_FR(32);

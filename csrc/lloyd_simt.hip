@@ -19,6 +19,7 @@ namespace tdc {
 // ------------------------------------------------------------------------------------
 // fused small-K Lloyd step
 // ------------------------------------------------------------------------------------
+// labels may be null: the fit's final label pass writes them, the steps need only the sums.
 template <typename T, typename ACC, int KMAX, int DMAX>
 __global__ __launch_bounds__(256) void lloyd_small_kernel(
     const T* __restrict__ X, int64_t N, int64_t ldx, int D, const T* __restrict__ C, int K,
@@ -88,7 +89,7 @@ __global__ __launch_bounds__(256) void lloyd_small_kernel(
         }
       }
     }
-    labels[i] = best;
+    if (labels) labels[i] = best;
     if (mind) mind[i] = bd;
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
@@ -283,7 +284,10 @@ int grid_for(int64_t N, int per_block, int cap) {
 template <typename T, typename ACC, int KMAX, int DMAX>
 int launch_small(const void* X, int64_t N, int64_t ldx, int D, const void* C, int K,
                  int32_t* labels, void* mind, void* sums, void* counts, hipStream_t s) {
-  const int g = grid_for(N, 256 * 8, 2048);
+  // grid-stride over the rows with exactly the blocks the GPU holds at once: a larger grid
+  // leaves a second, partial round of blocks running at a fraction of the occupancy
+  static const int resident = resident_blocks(lloyd_small_kernel<T, ACC, KMAX, DMAX>, 256);
+  const int g = grid_for(N, 256, resident);
   hipLaunchKernelGGL((lloyd_small_kernel<T, ACC, KMAX, DMAX>), dim3(g), dim3(256), 0, s,
                      (const T*)X, N, ldx, D, (const T*)C, K, labels, (T*)mind, (ACC*)sums,
                      (ACC*)counts);
@@ -295,10 +299,11 @@ int launch_small(const void* X, int64_t N, int64_t ldx, int D, const void* C, in
 template <typename T, typename ACC>
 int dispatch_small(const void* X, int64_t N, int64_t ldx, int D, const void* C, int K,
                    int32_t* labels, void* mind, void* sums, void* counts, hipStream_t s) {
-#define TDC_SMALL(KM, DM)                                                          \
-  if (K <= KM && D <= DM)                                                          \
+#define TDC_SMALL(KM, DM)                                                                 \
+  if (K <= KM && D <= DM)                                                                 \
     return launch_small<T, ACC, KM, DM>(X, N, ldx, D, C, K, labels, mind, sums, counts, s);
   TDC_SMALL(4, 4)
+  TDC_SMALL(4, 6)  // the reference's own configs: D = 5, K <= 4
   TDC_SMALL(4, 8)
   TDC_SMALL(8, 4)
   TDC_SMALL(8, 8)
@@ -431,8 +436,13 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(const T* __restrict__
 int tdc_assign_exact(int dtype, const void* X, int64_t N, int64_t ldx, int D, const void* C, int K,
                      int32_t* labels, void* mind, int num_cus, hipStream_t s) {
   if (N <= 0) return 0;
+  (void)num_cus;
   int64_t blocks = (N + 63) / 64;
-  if (blocks > (int64_t)num_cus * 8) blocks = (int64_t)num_cus * 8;
+  // grid-stride over 64-row tiles with the blocks resident at once (no partial 2nd round)
+  static const int res32 = resident_blocks(assign_exact_kernel<float>, 256);
+  static const int res64 = resident_blocks(assign_exact_kernel<double>, 256);
+  const int64_t resident = dtype == TDC_F64 ? res64 : res32;
+  if (blocks > resident) blocks = resident;
   if (dtype == TDC_F32)
     hipLaunchKernelGGL(assign_exact_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s,
                        (const float*)X, N, ldx, D, (const float*)C, K, labels, (float*)mind);

@@ -63,4 +63,18 @@ __device__ __forceinline__ int stage_rows_lds(const T* __restrict__ X, int64_t N
   return rows;
 }
 
+// Blocks of `kernel` (block threads, static LDS only) the whole GPU holds at once: the
+// grid of a grid-stride kernel.  A larger grid leaves a second, partial round of blocks
+// that runs at a fraction of the occupancy (every block has the same row count).
+template <typename F>
+inline int resident_blocks(F kernel, int block) {
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, 0) != hipSuccess)
+    per = 1;
+  return (per > 0 ? per : 1) * (cus > 0 ? cus : 1);
+}
+
 }  // namespace tdc

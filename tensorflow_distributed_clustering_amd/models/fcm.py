@@ -86,6 +86,8 @@ class FcmEngine(OomGuard):
         self.oom_flag = self.buf[-1:] if self.oom_guard else None
         self.C = torch.zeros(k, d, dtype=self.local.c_dtype, device=dev)
         self.labels = torch.zeros(self.n_local, dtype=torch.int32, device=dev)
+        if hasattr(self.local, "skip_step_labels"):
+            self.local.skip_step_labels = bool(cfg.label_pass)  # the final pass writes them
         self.shift = torch.zeros(1, dtype=torch.float32, device=dev) if cfg.tol > 0 else None
         self.n_iter = 0
         self.c0 = None

@@ -238,6 +238,9 @@ class LloydEngine(OomGuard):
             self._gathered = ops_ if ops_ is not None else [self.C_pad]
             self._c_synced = True
         self.labels = torch.zeros(self.n_local, dtype=torch.int32, device=dev)
+        if hasattr(self.local, "skip_step_labels"):
+            # the fit's final label pass writes the labels: the steps need only the sums
+            self.local.skip_step_labels = bool(cfg.label_pass)
         mdt = torch.float64 if self.local.c_dtype == torch.float64 else torch.float32
         self.mind = torch.zeros(self.n_local, dtype=mdt, device=dev) if cfg.compute_inertia else None
         self.need_shift = cfg.tol > 0 or cfg.log_every > 0

@@ -23,6 +23,7 @@ Variants (picked by :func:`make_lloyd_ops`):
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -618,11 +619,16 @@ class _HipExactBase(_LocalOpsBase):
 class HipSmallLloyd(_HipExactBase):
     name = "hip_small_fused"
 
+    def __init__(self, x, k, dtype, empty_cluster):
+        super().__init__(x, k, dtype, empty_cluster)
+        self.skip_step_labels = False  # set by the engine when a final label pass follows
+
     def supports_count_split(self) -> bool:
         return False  # the fused kernel accumulates counts itself (fp64 buffers only)
 
     def step(self, C, labels, mind, sums, counts):
-        self.ops.lloyd_small(self.x, C, labels, mind, sums, counts)
+        self.ops.lloyd_small(self.x, C, None if self.skip_step_labels else labels, mind, sums,
+                             counts)
 
     def assign(self, C, labels, mind):
         self.ops.assign_simt(self.x, C, labels, mind)
@@ -740,9 +746,11 @@ class HipSmallFCM(_LocalOpsBase):
         self.m = float(m)
         self.nan_to_zero = nan_to_zero
         self._wx = None
+        self.skip_step_labels = False  # set by the engine when a final label pass follows
 
     def step(self, C, labels, wx, ws):
-        self.ops.fcm_small(self.x, C, self.m, self.nan_to_zero, labels, wx, ws)
+        self.ops.fcm_small(self.x, C, self.m, self.nan_to_zero,
+                           None if self.skip_step_labels else labels, wx, ws)
 
     def assign(self, C, labels):
         if self._wx is None:

@@ -171,3 +171,4 @@ def test_fcm_predict_and_memberships_match_fit():
     assert u.shape == (4000, 3)
     torch.testing.assert_close(u.sum(1), torch.ones(4000, dtype=torch.float64))
     assert torch.equal(u.argmax(1).to(torch.int32), lab)
+

@@ -101,3 +101,26 @@ def test_fcm_fit_native_backends(gpu, dtype, d, k, backend):
     tol = 1e-8 if dtype == "fp64" else 3e-3
     torch.testing.assert_close(torch.as_tensor(r.centers), torch.as_tensor(o.centers),
                                rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64])
+@pytest.mark.parametrize("k,d,n", [(3, 5, 50001), (4, 6, 127), (8, 8, 9000)])
+def test_fcm_small_no_labels(gpu, dt, k, d, n):
+    """The fit's step form (labels = None) == with labels; labels == argmax membership."""
+    from tensorflow_distributed_clustering_amd import _native
+    ops = _native.require()
+    g = torch.Generator().manual_seed(k * 11 + n)
+    x = torch.randn(n, d, generator=g, dtype=torch.float64).to(dt).to(gpu)
+    c = torch.randn(k, d, generator=g, dtype=torch.float64).to(dt).to(gpu)
+    out = []
+    for lab in (torch.full((n,), -1, dtype=torch.int32, device=gpu), None):
+        wx = torch.zeros(k, d, dtype=torch.float64, device=gpu)
+        ws = torch.zeros(k, dtype=torch.float64, device=gpu)
+        ops.fcm_small(x, c, 5.0, True, lab, wx, ws)
+        out.append((wx, ws, lab))
+    u = ref.fcm_memberships(x.double(), c.double(), 5.0, True)
+    agree = (u.argmax(1).to(torch.int32) == out[0][2]).float().mean().item()
+    assert agree > 0.999, agree
+    tol = 1e-10 if dt == torch.float64 else 1e-5
+    torch.testing.assert_close(out[1][0], out[0][0], rtol=tol, atol=tol)
+    torch.testing.assert_close(out[1][1], out[0][1], rtol=tol, atol=tol)

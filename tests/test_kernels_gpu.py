@@ -148,6 +148,28 @@ def test_lloyd_small_fused(gpu, dt, k, d):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.float64])
+@pytest.mark.parametrize("k,d,n", [(3, 5, 50001), (4, 6, 127), (8, 8, 9000)])
+def test_lloyd_small_no_labels(gpu, dt, k, d, n):
+    """The fit's step form (labels = None, the final label pass writes them) == with labels."""
+    from tensorflow_distributed_clustering_amd import _native
+    ops = _native.require()
+    g = torch.Generator().manual_seed(k * 7 + n)
+    x = torch.randn(n, d, generator=g, dtype=torch.float64).to(dt).to(gpu)
+    c = torch.randn(k, d, generator=g, dtype=torch.float64).to(dt).to(gpu)
+    out = []
+    for lab in (torch.full((n,), -1, dtype=torch.int32, device=gpu), None):
+        sums = torch.zeros(k, d, dtype=torch.float64, device=gpu)
+        counts = torch.zeros(k, dtype=torch.float64, device=gpu)
+        ops.lloyd_small(x, c, lab, None, sums, counts)
+        out.append((sums, counts, lab))
+    assert int(out[0][2].min()) >= 0
+    s_ref, c_ref = ref.cluster_sums(x.double(), out[0][2], k)
+    assert torch.equal(out[0][1], c_ref) and torch.equal(out[1][1], c_ref)
+    tol = 1e-10 if dt == torch.float64 else 2e-4
+    torch.testing.assert_close(out[1][0], s_ref, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64])
 @pytest.mark.parametrize("k,d", [(300, 5), (1000, 17), (64, 32)])
 def test_assign_simt(gpu, dt, k, d):
     from tensorflow_distributed_clustering_amd import _native
