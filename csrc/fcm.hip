@@ -20,12 +20,18 @@
 
 namespace tdc {
 
-// labels may be null (the fit's final label pass writes them).
-template <typename T, typename ACC, int KMAX, int DMAX>
+// labels may be null (the fit's final label pass writes them).  FM: compile-time fuzzifier
+// form (fcm_math.h fm_t / fm_w: m = 2, m = 5, any m) -- a runtime switch per centroid
+// inlined K copies of every form and their divergent branches into the row loop.
+// LPR lanes share a row, lane part p owning clusters p*KL .. p*KL+KL-1 (see
+// lloyd_small_kernel): the row normaliser, the on-centroid count and the argmax meet by
+// lane swaps.
+template <typename T, typename ACC, int KL, int DMAX, int FM, int LPR>
 __global__ __launch_bounds__(256) void fcm_small_kernel(
     const T* __restrict__ X, int64_t N, int64_t ldx, int D, const T* __restrict__ C, int K,
-    T expo, T m, int pmode, int mint, int nan_to_zero, int32_t* __restrict__ labels,
-    ACC* __restrict__ wx, ACC* __restrict__ ws) {
+    T expo, T m, int nan_to_zero, int32_t* __restrict__ labels, ACC* __restrict__ wx,
+    ACC* __restrict__ ws) {
+  constexpr int KMAX = KL * LPR;
   __shared__ T s_c[KMAX * DMAX];
   __shared__ T s_red[4][KMAX * (DMAX + 1)];
   const int tid = threadIdx.x;
@@ -34,74 +40,113 @@ __global__ __launch_bounds__(256) void fcm_small_kernel(
     s_c[i] = (k < K && d < D) ? C[k * D + d] : (T)0;
   }
   __syncthreads();
+  const int part = LPR == 1 ? 0 : (tid % LPR);
+  const T* sc = s_c + part * KL * DMAX;
 
-  T acc[KMAX][DMAX];
-  T wsum[KMAX];
+  T acc[KL][DMAX];
+  T wsum[KL];
 #pragma unroll
-  for (int k = 0; k < KMAX; ++k) {
+  for (int k = 0; k < KL; ++k) {
     wsum[k] = 0;
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) acc[k][d] = 0;
   }
   const T inf = (T)INFINITY;
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + tid; i < N; i += stride) {
-    T x[DMAX];
-#pragma unroll
-    for (int d = 0; d < DMAX; ++d) x[d] = (d < D) ? X[i * ldx + d] : (T)0;
-    T t[KMAX];
+  // grid-stride, ping-pong prefetch of the row's next row (see lloyd_small_kernel)
+  auto row = [&](T (&x)[DMAX], int64_t r) {
+    row_mask(D, x);
+    // larger / split tiles: centroids re-read from LDS every row (see lloyd_small_kernel)
+    if constexpr (KL >= 8 || LPR > 1) asm volatile("" ::: "memory");
+    T t[KL];
     T tsum = 0;
     int nzero = 0;
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      T dd = 0;
+    for (int j = 0; j < KL; ++j) {
+      const int k = part * KL + j;
+      t[j] = (T)0;
+      if (LPR > 1 || k < K) {  // LPR == 1: wave-uniform skip
+        T dd = 0;
 #pragma unroll
-      for (int d = 0; d < DMAX; ++d) {
-        const T df = x[d] - s_c[k * DMAX + d];
-        dd = fma(df, df, dd);
+        for (int d = 0; d < DMAX; ++d) {
+          const T df = x[d] - sc[j * DMAX + d];
+          dd = fma(df, df, dd);
+        }
+        const T tk = fm_t<FM>(dd, expo);
+        const bool on = k < K;
+        t[j] = !on ? (T)0 : (dd == (T)0 ? inf : tk);
+        nzero += (on && dd == (T)0);
+        tsum += t[j];
       }
-      const bool on = (k < K);
-      t[k] = !on ? (T)0 : (dd == (T)0 ? inf : fcm_t(dd, expo, pmode));
-      nzero += (on && dd == (T)0);
-      tsum += t[k];
     }
-    // memberships u_k, argmax label, weights w_k = u_k^m (all in t[])
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1) {
+      tsum += __shfl_xor(tsum, o, 64);
+      nzero += __shfl_xor(nzero, o, 64);
+    }
+    // memberships u_k, argmax label, weights w_k = u_k^m (all in t[]); a row past N
+    // (the prefetch's clamped duplicate) gets zero weight
+    const bool valid = r < N;
     int best = 0;
     T bu = (T)-1;
-    const T inv = (T)1 / tsum;
+    const T inv = valid ? (T)1 / tsum : (T)0;
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      T u;
-      if (nzero == 0) {
-        u = t[k] * inv;
-      } else if (nan_to_zero) {
-        u = (T)0;  // inf/inf = NaN -> 0 and finite/inf = 0  (reference guard)
-      } else {
-        u = (t[k] == inf) ? (T)1 / (T)nzero : (T)0;
+    for (int j = 0; j < KL; ++j) {
+      const int k = part * KL + j;
+      if (LPR > 1 || k < K) {
+        T u;
+        if (nzero == 0) {
+          u = t[j] * inv;
+        } else if (nan_to_zero || !valid) {
+          u = (T)0;  // inf/inf = NaN -> 0 and finite/inf = 0  (reference guard)
+        } else {
+          u = (t[j] == inf) ? (T)1 / (T)nzero : (T)0;
+        }
+        if (k < K && u > bu) {
+          bu = u;
+          best = k;
+        }
+        t[j] = (u > (T)0) ? fm_w<FM>(u, m) : (T)0;
       }
-      if (k < K && u > bu) {
-        bu = u;
-        best = k;
+    }
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1) {  // argmax over the row's lanes, first index on ties
+      const T ou = __shfl_xor(bu, o, 64);
+      const int ob = __shfl_xor(best, o, 64);
+      if (ou > bu || (ou == bu && ob < best)) {
+        bu = ou;
+        best = ob;
       }
-      t[k] = (u > (T)0) ? fcm_w(u, m, mint) : (T)0;
     }
-    if (labels) labels[i] = best;
+    if (labels && valid && part == 0) labels[r] = best;
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      wsum[k] += t[k];
+    for (int j = 0; j < KL; ++j) {
+      if (LPR > 1 || part * KL + j < K) {
+        wsum[j] += t[j];
 #pragma unroll
-      for (int d = 0; d < DMAX; ++d) acc[k][d] = fma(t[k], x[d], acc[k][d]);
+        for (int d = 0; d < DMAX; ++d) acc[j][d] = fma(t[j], x[d], acc[j][d]);
+      }
     }
+  };
+  const int64_t stride = (int64_t)gridDim.x * (256 / LPR);
+  int64_t r = ((int64_t)blockIdx.x * 256 + tid) / LPR;
+  T xa[DMAX], xb[DMAX];
+  if (r < N) row_load(X, r, N, ldx, D, xa);
+  for (; r < N; r += 2 * stride) {
+    row_load(X, r + stride, N, ldx, D, xb);
+    row(xa, r);
+    row_load(X, r + 2 * stride, N, ldx, D, xa);
+    row(xb, r + stride);
   }
 
   const int lane = tid & 63, w = tid >> 6;
 #pragma unroll
-  for (int k = 0; k < KMAX; ++k) {
+  for (int j = 0; j < KL; ++j) {
 #pragma unroll
     for (int d = 0; d <= DMAX; ++d) {
-      T v = (d < DMAX) ? acc[k][d] : wsum[k];
-      v = wave_sum(v);
-      if (lane == 0) s_red[w][k * (DMAX + 1) + d] = v;
+      T v = (d < DMAX) ? acc[j][d] : wsum[j];
+#pragma unroll
+      for (int o = 32; o >= LPR; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane < LPR) s_red[w][(lane * KL + j) * (DMAX + 1) + d] = v;
     }
   }
   __syncthreads();
@@ -115,41 +160,58 @@ __global__ __launch_bounds__(256) void fcm_small_kernel(
   }
 }
 
-template <typename T, typename ACC, int KMAX, int DMAX>
-int launch_fcm(const void* X, int64_t N, int64_t ldx, int D, const void* C, int K, double m,
-               int nan_to_zero, int32_t* labels, void* wx, void* ws, hipStream_t s) {
+template <typename T, typename ACC, int KL, int DMAX, int FM, int LPR>
+int launch_fcm_fm(const void* X, int64_t N, int64_t ldx, int D, const void* C, int K, double m,
+                  int nan_to_zero, int32_t* labels, void* wx, void* ws, hipStream_t s) {
   // exactly the blocks the GPU holds at once (see launch_small, csrc/lloyd_simt.hip)
-  static const int resident = resident_blocks(fcm_small_kernel<T, ACC, KMAX, DMAX>, 256);
-  int64_t g = (N + 255) / 256;
+  static const int resident =
+      resident_blocks(fcm_small_kernel<T, ACC, KL, DMAX, FM, LPR>, 256);
+  int64_t g = (N * LPR + 255) / 256;
   if (g < 1) g = 1;
   if (g > resident) g = resident;
-  const T expo = (T)(-1.0 / (m - 1.0));
-  const int pmode = m == 2.0 ? 1 : (m == 3.0 ? 2 : (m == 5.0 ? 3 : 0));
-  const int mint = (m == (double)(int)m && m >= 1.0 && m <= 16.0) ? (int)m : 0;
-  hipLaunchKernelGGL((fcm_small_kernel<T, ACC, KMAX, DMAX>), dim3((unsigned)g), dim3(256), 0, s,
-                     (const T*)X, N, ldx, D, (const T*)C, K, expo, (T)m, pmode, mint, nan_to_zero,
-                     labels, (ACC*)wx, (ACC*)ws);
+  hipLaunchKernelGGL((fcm_small_kernel<T, ACC, KL, DMAX, FM, LPR>), dim3((unsigned)g),
+                     dim3(256), 0, s, (const T*)X, N, ldx, D, (const T*)C, K,
+                     (T)(-1.0 / (m - 1.0)), (T)m, nan_to_zero, labels, (ACC*)wx, (ACC*)ws);
   TDC_CHECK_LAUNCH();
   return 0;
+}
+
+template <typename T, typename ACC, int KL, int DMAX, int LPR>
+int launch_fcm(const void* X, int64_t N, int64_t ldx, int D, const void* C, int K, double m,
+               int nan_to_zero, int32_t* labels, void* wx, void* ws, hipStream_t s) {
+  switch (fcm_fm(m)) {
+    case 2:
+      return launch_fcm_fm<T, ACC, KL, DMAX, 2, LPR>(X, N, ldx, D, C, K, m, nan_to_zero, labels,
+                                                     wx, ws, s);
+    case 5:
+      return launch_fcm_fm<T, ACC, KL, DMAX, 5, LPR>(X, N, ldx, D, C, K, m, nan_to_zero, labels,
+                                                     wx, ws, s);
+    default:
+      return launch_fcm_fm<T, ACC, KL, DMAX, 0, LPR>(X, N, ldx, D, C, K, m, nan_to_zero, labels,
+                                                     wx, ws, s);
+  }
 }
 
 template <typename T, typename ACC>
 int dispatch_fcm(const void* X, int64_t N, int64_t ldx, int D, const void* C, int K, double m,
                  int nz, int32_t* labels, void* wx, void* ws, hipStream_t s) {
-#define TDC_FCM(KM, DM)                                                                    \
-  if (K <= KM && D <= DM)                                                                  \
-    return launch_fcm<T, ACC, KM, DM>(X, N, ldx, D, C, K, m, nz, labels, wx, ws, s);
-  TDC_FCM(4, 4)
-  TDC_FCM(4, 6)  // the reference's own configs: D = 5, K <= 4
-  TDC_FCM(4, 8)
-  TDC_FCM(8, 4)
-  TDC_FCM(8, 8)
-  TDC_FCM(16, 4)
+#define TDC_FCM(KL, DM, LPR)                                                                 \
+  if (K <= (KL) * (LPR) && D <= DM)                                                          \
+    return launch_fcm<T, ACC, KL, DM, LPR>(X, N, ldx, D, C, K, m, nz, labels, wx, ws, s);
+  TDC_FCM(4, 4, 1)
+  if (D == 5) {  // the reference's own configs (D = 5, K in {3, 6, 9, 12, 15}): exact tiles
+    TDC_FCM(4, 5, 1)
+    TDC_FCM(4, 5, 2)
+    TDC_FCM(6, 5, 2)
+    TDC_FCM(8, 5, 2)
+  }
+  TDC_FCM(4, 8, 1)
+  TDC_FCM(8, 4, 1)
+  TDC_FCM(8, 8, 1)
+  TDC_FCM(16, 4, 1)
   if constexpr (sizeof(T) == 4) {
-    TDC_FCM(16, 8)
-    TDC_FCM(32, 4)
-  } else {
-    TDC_FCM(16, 5)
+    TDC_FCM(16, 8, 1)
+    TDC_FCM(32, 4, 1)
   }
 #undef TDC_FCM
   return (int)hipErrorInvalidValue;

@@ -27,6 +27,64 @@ __device__ __forceinline__ T fcm_t(T dd, T expo, int pmode) {
     default: return tdc_exp2(tdc_log2(dd) * expo);
   }
 }
+
+// dd^(-1/P) for finite dd > 0, P in {1, 2, 4}, fp64 to a few ulp: the exponent is split
+// off (dd = r 2^(P q), r in [0.5, 2^P)), r^(-1/P) is seeded in fp32 (~1e-7) and refined by
+// two Newton steps on y^-P = r, y <- y ((P+1) - r y^P) / P.  ~16 fp64 operations and no
+// branches, against ~40 for the correctly rounded divide / sqrt / rsqrt sequences.
+// dd = 0 gives NaN: callers select +inf for on-centroid rows before using it.
+template <int P>
+__device__ __forceinline__ double root_rcp(double dd) {
+  static_assert(P == 1 || P == 2 || P == 4, "root_rcp: P in {1, 2, 4}");
+  const int e = __builtin_amdgcn_frexp_exp(dd);
+  const int q = P == 1 ? e : (P == 2 ? (e >> 1) : (e >> 2));  // floor(e / P)
+  const double r = __builtin_amdgcn_ldexp(dd, -P * q);
+  const float rf = (float)r;
+  double y;
+  if constexpr (P == 1) y = (double)__builtin_amdgcn_rcpf(rf);
+  else if constexpr (P == 2) y = (double)__builtin_amdgcn_rsqf(rf);
+  else y = (double)__builtin_amdgcn_rsqf(__builtin_amdgcn_sqrtf(rf));  // raw v_sqrt_f32: a seed
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    if constexpr (P == 1) {
+      y = y * fma(-r, y, 2.0);
+    } else if constexpr (P == 2) {
+      y = y * fma(-r, y * y, 3.0) * 0.5;
+    } else {
+      const double y2 = y * y;
+      y = y * fma(-r, y2 * y2, 5.0) * 0.25;
+    }
+  }
+  return __builtin_amdgcn_ldexp(y, -q);
+}
+
+// Compile-time fuzzifier forms (the fused small-K kernel): FM = 2 (m = 2), 5 (m = 5, the
+// reference's m = D = 5 configs) or 0 (any m: exp2 / log2).  t = (d^2)^(-1/(m-1)), w = u^m.
+template <int FM>
+__device__ __forceinline__ float fm_t(float dd, float expo) {
+  if constexpr (FM == 2) return __builtin_amdgcn_rcpf(dd);
+  else if constexpr (FM == 5) return __builtin_amdgcn_rsqf(__builtin_sqrtf(dd));
+  else return exp2f(log2f(dd) * expo);
+}
+template <int FM>
+__device__ __forceinline__ double fm_t(double dd, double expo) {
+  if constexpr (FM == 2) return root_rcp<1>(dd);
+  else if constexpr (FM == 5) return root_rcp<4>(dd);
+  else return exp2(log2(dd) * expo);
+}
+template <int FM, typename T>
+__device__ __forceinline__ T fm_w(T u, T m) {
+  if constexpr (FM == 2) {
+    return u * u;
+  } else if constexpr (FM == 5) {
+    const T u2 = u * u;
+    return u2 * u2 * u;
+  } else {
+    return u > (T)0 ? tdc_exp2(m * tdc_log2(u)) : (T)0;
+  }
+}
+inline int fcm_fm(double m) { return m == 2.0 ? 2 : (m == 5.0 ? 5 : 0); }
+
 // w = u^m: binary powering for integer m in [1, 16] (mint), else exp2(m log2 u)
 template <typename T>
 __device__ __forceinline__ T fcm_w(T u, T m, int mint) {

@@ -20,11 +20,15 @@ namespace tdc {
 // fused small-K Lloyd step
 // ------------------------------------------------------------------------------------
 // labels may be null: the fit's final label pass writes them, the steps need only the sums.
-template <typename T, typename ACC, int KMAX, int DMAX>
+// LPR lanes share a row: lane part p = lane % LPR owns clusters p*KL .. p*KL+KL-1, so the
+// K x D fp64 accumulators per lane shrink LPR-fold (K = 15, D = 5: 245 VGPRs / 2 waves per
+// SIMD at LPR = 1, ~140 / 3 waves at LPR = 2); the partial argmins meet by lane swaps.
+template <typename T, typename ACC, int KL, int DMAX, int LPR>
 __global__ __launch_bounds__(256) void lloyd_small_kernel(
     const T* __restrict__ X, int64_t N, int64_t ldx, int D, const T* __restrict__ C, int K,
     int32_t* __restrict__ labels, T* __restrict__ mind, ACC* __restrict__ sums,
     ACC* __restrict__ counts) {
+  constexpr int KMAX = KL * LPR;
   __shared__ T s_c[KMAX * DMAX];
   __shared__ T s_red[4][KMAX * (DMAX + 1)];
   const int tid = threadIdx.x;
@@ -33,82 +37,95 @@ __global__ __launch_bounds__(256) void lloyd_small_kernel(
     s_c[i] = (k < K && d < D) ? C[k * D + d] : (T)0;
   }
   __syncthreads();
+  const int part = LPR == 1 ? 0 : (tid % LPR);
+  const T* sc = s_c + part * KL * DMAX;
 
-  T acc[KMAX][DMAX];
-  int cnt[KMAX];
+  T acc[KL][DMAX];
+  int cnt[KL];
 #pragma unroll
-  for (int k = 0; k < KMAX; ++k) {
+  for (int k = 0; k < KL; ++k) {
     cnt[k] = 0;
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) acc[k][d] = 0;
   }
 
-  // Rows are staged per WAVE: the wave's 64 contiguous rows (64 x D x 8 B = 2.5 KiB at
-  // D=5 fp64) arrive as fully coalesced 16-B loads into a wave-private LDS slice and
-  // every lane then reads its own row -- no block barrier, so the waves of a CU keep
-  // their loads in flight independently (the 8-B strided row loads touched each cache
-  // line D times; the earlier block-wide 256-row staging needed two barriers per tile).
-  const int lane_ = tid & 63, wv_ = tid >> 6;
-  __shared__ __attribute__((aligned(16))) T s_xw[4][KMAX >= 16 ? 64 * DMAX : 1];
-  T* s_x = s_xw[wv_];
-  // measured (ref25m presets, D=5 fp64): K=15 0.77 -> 0.75 ms/iter staged; at K=3 the
-  // high-occupancy strided loads win (0.25 vs 0.30 ms), so small register tiles skip it
-  constexpr bool STAGE = KMAX >= 16;
-  const bool tiled = STAGE && ldx == D && ((uintptr_t)X % 16) == 0;
-  const int64_t ntile = (N + 63) / 64;
-  for (int64_t tile = (int64_t)blockIdx.x * 4 + wv_; tile < ntile; tile += (int64_t)gridDim.x * 4) {
-    const int64_t i = tile * 64 + lane_;
-    const bool full = tiled && tile * 64 + 64 <= N;  // wave-uniform
-    if (full) {
-      const uint4* src = reinterpret_cast<const uint4*>(X + tile * 64 * D);
-      const int nch = 4 * D * (int)sizeof(T);  // 16-B chunks of 64 rows
-      for (int c = lane_; c < nch; c += 64) reinterpret_cast<uint4*>(s_x)[c] = src[c];
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    }
-    if (i >= N) continue;
-    T x[DMAX];
-#pragma unroll
-    for (int d = 0; d < DMAX; ++d)
-      x[d] = (d < D) ? (full ? s_x[lane_ * D + d] : X[i * ldx + d]) : (T)0;
-    if (full) __builtin_amdgcn_wave_barrier();  // every lane read its row before the refill
+  // One row per LPR lanes, grid-stride, ping-pong prefetch: the loads of the next row are
+  // issued before the current row's distances and one-hot accumulation, into the other
+  // register set (no copy, so the compiler's vmcnt waits stay partial); with two waves per
+  // SIMD and no prefetch the HBM latency was exposed.  (Wave-private LDS staging of 64-row
+  // tiles with 16-B loads measured no better than these 8-B row loads:
+  // docs/PERF_NOTES.md "Reference configs".)
+  auto row = [&](T (&x)[DMAX], int64_t r) {
+    row_mask(D, x);
+    // larger tiles: re-read the centroids from LDS (broadcast) every row instead of
+    // letting the compiler hoist K x D of them into VGPRs next to the K x D accumulators
+    if constexpr (KL >= 8 || LPR > 1) asm volatile("" ::: "memory");
+    const bool valid = r < N;
     T bd = (T)INFINITY;  // NaN distances (poisoned centroid, empty_cluster='nan') never win
     int best = 0;
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      if (k < K) {
+    for (int j = 0; j < KL; ++j) {
+      const int k = part * KL + j;
+      if (LPR > 1 || k < K) {  // LPR == 1: wave-uniform skip
         T dd = 0;
 #pragma unroll
         for (int d = 0; d < DMAX; ++d) {
-          const T df = x[d] - s_c[k * DMAX + d];
+          const T df = x[d] - sc[j * DMAX + d];
           dd = fma(df, df, dd);
         }
-        if (dd < bd) {  // strict: first minimum wins (TF ArgMin)
+        if (k < K && dd < bd) {  // strict: first minimum wins (TF ArgMin)
           bd = dd;
           best = k;
         }
       }
     }
-    if (labels) labels[i] = best;
-    if (mind) mind[i] = bd;
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k) {
-      const T sel = (k == best) ? (T)1 : (T)0;
-      cnt[k] += (k == best);
-#pragma unroll
-      for (int d = 0; d < DMAX; ++d) acc[k][d] = fma(sel, x[d], acc[k][d]);
+    for (int o = 1; o < LPR; o <<= 1) {  // partial argmins of the row's lanes
+      const T od = __shfl_xor(bd, o, 64);
+      const int ob = __shfl_xor(best, o, 64);
+      if (od < bd || (od == bd && ob < best)) {
+        bd = od;
+        best = ob;
+      }
     }
+    if (valid && part == 0) {
+      if (labels) labels[r] = best;
+      if (mind) mind[r] = bd;
+    }
+    if (!valid) best = -1;
+#pragma unroll
+    for (int j = 0; j < KL; ++j) {
+      const int k = part * KL + j;
+      if (LPR > 1 || k < K) {
+        const T sel = (k == best) ? (T)1 : (T)0;
+        cnt[j] += (k == best);
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d) acc[j][d] = fma(sel, x[d], acc[j][d]);
+      }
+    }
+  };
+  const int64_t stride = (int64_t)gridDim.x * (256 / LPR);
+  int64_t r = ((int64_t)blockIdx.x * 256 + tid) / LPR;
+  T xa[DMAX], xb[DMAX];
+  if (r < N) row_load(X, r, N, ldx, D, xa);
+  for (; r < N; r += 2 * stride) {
+    row_load(X, r + stride, N, ldx, D, xb);
+    row(xa, r);
+    row_load(X, r + 2 * stride, N, ldx, D, xa);
+    row(xb, r + stride);
   }
 
-  // wave reduce -> LDS -> block total -> one global atomic per (k, d)
+  // wave reduce over the lanes of one part -> LDS -> block total -> one global atomic
+  // per (k, d)
   const int lane = tid & 63, w = tid >> 6;
 #pragma unroll
-  for (int k = 0; k < KMAX; ++k) {
+  for (int j = 0; j < KL; ++j) {
 #pragma unroll
     for (int d = 0; d <= DMAX; ++d) {
-      T v = (d < DMAX) ? acc[k][d] : (T)cnt[k];
-      v = wave_sum(v);
-      if (lane == 0) s_red[w][k * (DMAX + 1) + d] = v;
+      T v = (d < DMAX) ? acc[j][d] : (T)cnt[j];
+#pragma unroll
+      for (int o = 32; o >= LPR; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane < LPR) s_red[w][(lane * KL + j) * (DMAX + 1) + d] = v;
     }
   }
   __syncthreads();
@@ -281,42 +298,47 @@ int grid_for(int64_t N, int per_block, int cap) {
   return (int)g;
 }
 
-template <typename T, typename ACC, int KMAX, int DMAX>
+template <typename T, typename ACC, int KL, int DMAX, int LPR>
 int launch_small(const void* X, int64_t N, int64_t ldx, int D, const void* C, int K,
                  int32_t* labels, void* mind, void* sums, void* counts, hipStream_t s) {
   // grid-stride over the rows with exactly the blocks the GPU holds at once: a larger grid
   // leaves a second, partial round of blocks running at a fraction of the occupancy
-  static const int resident = resident_blocks(lloyd_small_kernel<T, ACC, KMAX, DMAX>, 256);
-  const int g = grid_for(N, 256, resident);
-  hipLaunchKernelGGL((lloyd_small_kernel<T, ACC, KMAX, DMAX>), dim3(g), dim3(256), 0, s,
+  static const int resident = resident_blocks(lloyd_small_kernel<T, ACC, KL, DMAX, LPR>, 256);
+  const int g = grid_for(N * LPR, 256, resident);
+  hipLaunchKernelGGL((lloyd_small_kernel<T, ACC, KL, DMAX, LPR>), dim3(g), dim3(256), 0, s,
                      (const T*)X, N, ldx, D, (const T*)C, K, labels, (T*)mind, (ACC*)sums,
                      (ACC*)counts);
   TDC_CHECK_LAUNCH();
   return 0;
 }
 
-// (KMAX, DMAX) register tiles compiled for the fused kernel
+// (clusters per lane, DMAX, lanes per row) register tiles compiled for the fused kernel
 template <typename T, typename ACC>
 int dispatch_small(const void* X, int64_t N, int64_t ldx, int D, const void* C, int K,
                    int32_t* labels, void* mind, void* sums, void* counts, hipStream_t s) {
-#define TDC_SMALL(KM, DM)                                                                 \
-  if (K <= KM && D <= DM)                                                                 \
-    return launch_small<T, ACC, KM, DM>(X, N, ldx, D, C, K, labels, mind, sums, counts, s);
-  TDC_SMALL(4, 4)
-  TDC_SMALL(4, 6)  // the reference's own configs: D = 5, K <= 4
-  TDC_SMALL(4, 8)
-  TDC_SMALL(8, 4)
-  TDC_SMALL(8, 8)
-  TDC_SMALL(16, 4)
-  if constexpr (sizeof(T) == 4) {
-    TDC_SMALL(16, 8)
-    TDC_SMALL(8, 16)
+#define TDC_SMALL(KL, DM, LPR)                                                            \
+  if (K <= (KL) * (LPR) && D <= DM)                                                       \
+    return launch_small<T, ACC, KL, DM, LPR>(X, N, ldx, D, C, K, labels, mind, sums, counts, s);
+  TDC_SMALL(4, 4, 1)
+  if (D == 5) {  // the reference's own configs (D = 5, K in {3, 6, 9, 12, 15}): exact tiles
+    TDC_SMALL(4, 5, 1)
+    TDC_SMALL(4, 5, 2)
+    TDC_SMALL(6, 5, 2)
+    TDC_SMALL(8, 5, 2)
   }
-  TDC_SMALL(4, 16)
+  TDC_SMALL(4, 8, 1)
+  TDC_SMALL(8, 4, 1)
+  TDC_SMALL(8, 8, 1)
+  TDC_SMALL(16, 4, 1)
   if constexpr (sizeof(T) == 4) {
-    TDC_SMALL(32, 4)
+    TDC_SMALL(16, 8, 1)
+    TDC_SMALL(8, 16, 1)
+  }
+  TDC_SMALL(4, 16, 1)
+  if constexpr (sizeof(T) == 4) {
+    TDC_SMALL(32, 4, 1)
   } else {
-    TDC_SMALL(16, 6)
+    TDC_SMALL(16, 6, 1)
   }
 #undef TDC_SMALL
   return (int)hipErrorInvalidValue;

@@ -63,6 +63,23 @@ __device__ __forceinline__ int stage_rows_lds(const T* __restrict__ X, int64_t N
   return rows;
 }
 
+// Row `row` of a row-major X into registers, branch-free: the row is clamped to N - 1 and
+// features d >= D re-read feature D - 1 (always in bounds), so the loads need no exec-mask
+// branches and the compiler's vmcnt tracking stays exact across a ping-pong prefetch loop.
+// row_mask zeroes the d >= D copies once the data is used.
+template <typename T, int DMAX>
+__device__ __forceinline__ void row_load(const T* __restrict__ X, int64_t row, int64_t N,
+                                         int64_t ldx, int D, T (&v)[DMAX]) {
+  const T* p = X + (row < N ? row : N - 1) * ldx;
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) v[d] = p[d < D ? d : D - 1];
+}
+template <typename T, int DMAX>
+__device__ __forceinline__ void row_mask(int D, T (&v)[DMAX]) {
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) v[d] = d < D ? v[d] : (T)0;
+}
+
 // Blocks of `kernel` (block threads, static LDS only) the whole GPU holds at once: the
 // grid of a grid-stride kernel.  A larger grid leaves a second, partial round of blocks
 // that runs at a fraction of the occupancy (every block has the same row count).

@@ -119,7 +119,8 @@ def test_update_sorted(gpu, xdt, n, d, k):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.float64])
-@pytest.mark.parametrize("k,d", [(3, 5), (15, 5), (8, 2), (16, 8), (4, 16), (32, 3)])
+@pytest.mark.parametrize("k,d", [(3, 5), (6, 5), (9, 5), (12, 5), (15, 5), (16, 5), (8, 2),
+                                 (16, 8), (4, 16), (32, 3)])
 def test_lloyd_small_fused(gpu, dt, k, d):
     from tensorflow_distributed_clustering_amd import _native
     ops = _native.require()
@@ -190,8 +191,9 @@ def test_assign_simt(gpu, dt, k, d):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.float64])
-@pytest.mark.parametrize("k,d,m", [(3, 5, 5.0), (15, 5, 5.0), (3, 3, 2.0), (8, 2, 2.0), (6, 4, 1.7),
-                                   (5, 3, 3.0), (4, 4, 4.0), (7, 2, 2.5)])
+@pytest.mark.parametrize("k,d,m", [(3, 5, 5.0), (6, 5, 5.0), (9, 5, 5.0), (12, 5, 2.0),
+                                   (15, 5, 5.0), (16, 5, 1.5), (3, 3, 2.0), (8, 2, 2.0),
+                                   (6, 4, 1.7), (5, 3, 3.0), (4, 4, 4.0), (7, 2, 2.5)])
 @pytest.mark.parametrize("nan_to_zero", [True, False])
 def test_fcm_small(gpu, dt, k, d, m, nan_to_zero):
     from tensorflow_distributed_clustering_amd import _native
