@@ -276,7 +276,7 @@ class FuzzyCMeans:
         centers_host = lambda: self.engine_.C.double().cpu().numpy()
         while True:
             if eng.oom_guard:
-                bad = eng.failed_step(lag=0 if eng.n_iter >= cfg.max_iter else 1)
+                bad = eng.failed_step(final=eng.n_iter >= cfg.max_iter)
                 if bad is not None:
                     c_host, c0 = eng.rollback(bad), eng.c0
                     n_back = eng.n_iter
@@ -303,17 +303,14 @@ class FuzzyCMeans:
                 eng.post_flag()
             n_iter = eng.n_iter
             if eng.shift is not None:
-                if eng.oom_guard and eng.failed_step(lag=0) is not None:
+                if eng.oom_guard and eng.failed_step(final=True) is not None:
                     continue
                 sv = float(eng.shift.item())
                 history.append({"iter": n_iter, "shift": sv})
                 if sv <= cfg.tol:
-                    if eng.oom_guard and eng.failed_step(lag=1) is not None:
-                        continue
                     break
             if ckpt.due(n_iter):
-                if eng.oom_guard and (eng.failed_step(lag=0) is not None
-                                      or eng.failed_step(lag=1) is not None):
+                if eng.oom_guard and eng.failed_step(final=True) is not None:
                     continue
                 ckpt.maybe_save(n_iter, centers_host)
             faults.maybe_fail(str(n_iter), comm.rank, kinds=("crash",))

@@ -75,66 +75,83 @@ class OomGuard:
     """Mid-run OOM rollback state shared by the Lloyd and FCM engines.
 
     A rank that runs out of memory in its local step sets the flag slot of the packed
-    all-reduce buffer, so every rank learns it from the same collective.  The flag of step
-    n is copied to pinned host memory asynchronously and read while step n+1 runs (the
-    host stays <= 2 steps ahead, no per-step sync); the centroids of the last two step
-    starts are kept, so a flag seen one step late still rolls back to the state before the
-    failed step.  Engines provide ``rsag``, ``C`` (+ ``C_pad``/``_r0``/``_kr`` under rsag),
-    ``buf``, ``oom_flag``, ``device``, ``n_iter`` and ``centers()``."""
+    all-reduce buffer, so every rank learns it from the same collective.  The flag of each
+    step is copied to pinned host memory asynchronously; :meth:`failed_step` reads the flags
+    in order, at most ``OOM_LAG`` steps behind the host (the host never waits for the step
+    it just queued, so launches stay ahead of the GPU), or all of them with ``final``.  The
+    pre-step centroids of the last ``OOM_LAG + 2`` steps are kept, so a flag seen late
+    still rolls back to the state before the failed step.  Engines provide ``rsag``, ``C``
+    (+ ``C_pad``/``_r0``/``_kr`` under rsag), ``buf``, ``oom_flag``, ``device``, ``n_iter``
+    and ``centers()``."""
+
+    OOM_LAG = 3
 
     def _oom_alloc(self):
         """Ring of pre-step centroids, pinned flag slots and events (allocated at setup,
         never inside the timed loop: a pinned allocation costs ~1 ms)."""
         src = self.C_pad[self._r0: self._r0 + self._kr] if self.rsag else self.C
-        self._ring = [torch.empty_like(src), torch.empty_like(src)]
-        self._ring_iter = [-1, -1]
-        self._flag_host = torch.zeros(2, dtype=self.buf.dtype,
+        R = self.OOM_LAG + 2
+        self._ring = [torch.empty_like(src) for _ in range(R)]
+        self._ring_iter = [-1] * R
+        self._flag_host = torch.zeros(R, dtype=self.buf.dtype,
                                       pin_memory=self.device.type == "cuda")
-        self._flag_ev = ([torch.cuda.Event(), torch.cuda.Event()]
-                         if self.device.type == "cuda" else [None, None])
-        self._flag_set = [False, False]
+        self._flag_ev = ([torch.cuda.Event() for _ in range(R)]
+                         if self.device.type == "cuda" else [None] * R)
+        self._flag_step = [-1] * R
+        self._checked = -1  # every step <= this one is known to have completed cleanly
 
     def save_state(self):
         """Keep the pre-step centroids (this rank's slice under rsag) for a rollback."""
         if getattr(self, "_ring", None) is None:
             self._oom_alloc()
         src = self.C_pad[self._r0: self._r0 + self._kr] if self.rsag else self.C
-        slot = self.n_iter & 1
+        slot = self.n_iter % len(self._ring)
         self._ring[slot].copy_(src)
         self._ring_iter[slot] = self.n_iter
 
     def post_flag(self):
         """After step(): queue the copy of this step's OOM flag (no host sync)."""
-        slot = (self.n_iter - 1) & 1
+        step = self.n_iter - 1
+        slot = step % len(self._ring)
         if self.device.type == "cuda":
             self._flag_host[slot:slot + 1].copy_(self.oom_flag, non_blocking=True)
             self._flag_ev[slot].record()
         else:
             self._flag_host[slot:slot + 1].copy_(self.oom_flag)
-        self._flag_set[slot] = True
+        self._flag_step[slot] = step
 
-    def failed_step(self, lag: int = 1) -> Optional[int]:
-        """Index (0-based) of a step whose flag is set, checking the step ``lag`` steps
-        back (lag 0: the last one, a host sync)."""
-        n = self.n_iter - 1 - lag
-        if n < 0 or getattr(self, "_ring", None) is None or self._ring_iter[n & 1] != n:
+    def failed_step(self, final: bool = False) -> Optional[int]:
+        """Index (0-based) of the first step whose flag is set, among the steps not yet
+        checked that are ``OOM_LAG`` or more steps old (``final``: all of them -- a host
+        sync on the last step)."""
+        if getattr(self, "_ring", None) is None:
             return None
-        if not self._flag_set[n & 1]:
-            return None
-        ev = self._flag_ev[n & 1]
-        if ev is not None:
-            ev.synchronize()
-        return n if float(self._flag_host[n & 1]) > 0 else None
+        R = len(self._ring)
+        upto = self.n_iter - 1 if final else self.n_iter - 1 - self.OOM_LAG
+        while self._checked < upto:
+            n = self._checked + 1
+            slot = n % R
+            if self._flag_step[slot] == n:
+                ev = self._flag_ev[slot]
+                if ev is not None:
+                    ev.synchronize()
+                if float(self._flag_host[slot]) > 0:
+                    return n
+            self._checked = n
+        return None
 
     def rollback(self, step: int) -> np.ndarray:
         """Centroids at the start of ``step`` (replicated, host fp64); resets n_iter."""
-        prev = self._ring[step & 1]
+        slot = step % len(self._ring)
+        assert self._ring_iter[slot] == step, "rollback state of the failed step is gone"
+        prev = self._ring[slot]
         if self.rsag:
             self.C_pad[self._r0: self._r0 + self._kr].copy_(prev)
             self._c_synced = False
         else:
             self.C.copy_(prev)
         self.n_iter = step
+        self._checked = step - 1
         return self.centers().double().cpu().numpy()
 
 
@@ -613,7 +630,7 @@ class KMeans:
         timer.start()
         while True:
             if eng.oom_guard:
-                bad = eng.failed_step(lag=0 if eng.n_iter >= cfg.max_iter else 1)
+                bad = eng.failed_step(final=eng.n_iter >= cfg.max_iter)
                 if bad is not None:
                     eng = self._recover_oom(eng, bad, x_local, dev, comm, n_global, row_offset,
                                             n_local)
@@ -628,8 +645,8 @@ class KMeans:
                 eng.post_flag()
             n = eng.n_iter
             if eng.need_shift and (cfg.tol > 0 or log_pt):
-                if eng.oom_guard and eng.failed_step(lag=0) is not None:
-                    continue  # this step failed: recovered at the top of the loop
+                if eng.oom_guard and eng.failed_step(final=True) is not None:
+                    continue  # a step failed: recovered at the top of the loop
                 sv = float(eng.shift.item())
                 rec = {"iter": n, "shift": sv}
                 if inertia_it is not None:
@@ -639,12 +656,9 @@ class KMeans:
                     extra = f" inertia {inertia_it:.6e}" if inertia_it is not None else ""
                     print(f"[kmeans] iter {n} max centroid shift^2 {sv:.3e}{extra}", flush=True)
                 if cfg.tol > 0 and sv <= cfg.tol:
-                    if eng.oom_guard and eng.failed_step(lag=1) is not None:
-                        continue
                     break
             if ckpt.due(n):
-                if eng.oom_guard and (eng.failed_step(lag=0) is not None
-                                      or eng.failed_step(lag=1) is not None):
+                if eng.oom_guard and eng.failed_step(final=True) is not None:
                     continue  # never checkpoint centroids of a failed step
                 ckpt.maybe_save(n, centers_host)
             faults.maybe_fail(str(n), comm.rank, kinds=("crash",))
