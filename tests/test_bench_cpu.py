@@ -39,3 +39,16 @@ def test_bench_fcm_and_minibatch_presets():
     d = _run(["--preset", "minibatch1b", "--n-per-gpu", "50000", "--k", "32", "--batch-size", "4096",
               "--steps", "2", "--warmup", "1", "--dtype", "fp32"])
     assert d["config"]["model"] == "kmeans-minibatch" and d["config"]["global_batch"] == 4096
+
+
+def test_bench_host_source():
+    """--source host: the shard lives in host memory and goes through HostSource (streamed
+    Lloyd with chunk_rows, and mini-batch chunks); the JSON says so and carries the
+    stream geometry (on a GPU box it also reports the achieved H2D GB/s)."""
+    d = _run(["--n-per-gpu", "30000", "--k", "16", "--dim", "8", "--dtype", "fp32", "--steps", "2",
+              "--warmup", "1", "--source", "host"])
+    assert "HOST memory" in d["data"] and d["source"]["rows"] == 30000
+    assert d["config"]["model"] == "kmeans-lloyd" and d["source"]["chunk_rows"] > 0
+    d = _run(["--preset", "minibatch1b", "--n-per-gpu", "30000", "--k", "16", "--batch-size", "4096",
+              "--steps", "3", "--warmup", "1", "--dtype", "fp32", "--source", "host"])
+    assert d["config"]["model"] == "kmeans-minibatch" and d["source"]["chunk_rows"] == 4096
