@@ -249,8 +249,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats_kernel(
 // pass 2: W^T X and the column sums of a 128-centroid tile over a row range; the block's
 // [128 x D] fp32 partial goes to its own slab (no atomics), reduced by fcm_reduce_kernel
 // ---------------------------------------------------------------------------------------
-template <int DP, int MODE, bool NZ>
-__global__ __launch_bounds__(256, 1) void fcm_mfma_accum_kernel(
+// WAVES = 4: one wave per SIMD, each wave owns 32 centroids over both 32-point halves of a
+// tile, memberships of one half software-pipelined between the MFMAs of the other.
+// WAVES = 8: two waves per SIMD, wave w owns centroid group w & 3 and point half w >> 2
+// (no intra-wave pipeline: the other wave on the SIMD issues its MFMAs under this wave's
+// membership VALU); the two halves' W^T X partials meet in LDS at the end.
+template <int DP, int MODE, bool NZ, int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     const __bf16* __restrict__ Xh, const __bf16* __restrict__ Xl, const float* __restrict__ xx,
     const float* __restrict__ rowinfo, int64_t N, const __bf16* __restrict__ Ch,
     const __bf16* __restrict__ Cl, const float* __restrict__ cc, int K, int nkt,
@@ -262,9 +267,11 @@ __global__ __launch_bounds__(256, 1) void fcm_mfma_accum_kernel(
   constexpr int HALF = DP / 2;
   constexpr int NDT = DP / 32;            // 32-feature output tiles
   constexpr int IMG = TP * DP * 2;        // bytes of one hi (or lo) image
+  constexpr int NT = WAVES * 64;
   constexpr int CHUNKS = 2 * TP * CPR;
-  constexpr int CPT = CHUNKS / 256;
-  static_assert(CHUNKS % 256 == 0, "tile chunks must split over 256 threads");
+  constexpr int CPT = CHUNKS / NT;
+  static_assert(CHUNKS % NT == 0, "tile chunks must split over the block's threads");
+  static_assert(WAVES == 4 || WAVES == 8, "4 or 8 waves");
   __shared__ __attribute__((aligned(16))) char s_x[2][2 * IMG];
   __shared__ __attribute__((aligned(16))) float s_xx[2][TP];
   __shared__ __attribute__((aligned(16))) float s_in[2][TP];
@@ -281,7 +288,8 @@ __global__ __launch_bounds__(256, 1) void fcm_mfma_accum_kernel(
   const int64_t split = L / nkt;
   const int64_t a = split * rows_per_split;
   const int64_t b = min(N, a + rows_per_split);
-  const int kw = kt * 128 + w * 32;       // this wave's 32 centroids
+  const int cg = w & 3;                   // centroid group
+  const int kw = kt * 128 + cg * 32;      // this wave's 32 centroids
   const int kc = kw + r;                  // this lane's centroid (column of the distances)
 
   bf16x8 ch[KS], cl[KS];
@@ -309,7 +317,7 @@ __global__ __launch_bounds__(256, 1) void fcm_mfma_accum_kernel(
 #define TDC_TILE_LOAD(R0_)                                                                \
   {                                                                                       \
     _Pragma("unroll") for (int i = 0; i < CPT; ++i) {                                     \
-      const int q = tid + i * 256;                                                        \
+      const int q = tid + i * NT;                                                         \
       const int hl = q / (TP * CPR), rem = q % (TP * CPR);                                \
       int64_t gr = (R0_) + rem / CPR;                                                     \
       gr = gr < b ? gr : b - 1;                                                           \
@@ -326,7 +334,7 @@ __global__ __launch_bounds__(256, 1) void fcm_mfma_accum_kernel(
   {                                                                                       \
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                      \
     _Pragma("unroll") for (int i = 0; i < CPT; ++i) {                                     \
-      const int q = tid + i * 256;                                                        \
+      const int q = tid + i * NT;                                                         \
       const int hl = q / (TP * CPR), rem = q % (TP * CPR);                                \
       *reinterpret_cast<uint4*>(&s_x[B_][hl * IMG + xoff<DP>(rem / CPR, rem % CPR)]) = pre[i]; \
     }                                                                                     \
@@ -430,12 +438,39 @@ __global__ __launch_bounds__(256, 1) void fcm_mfma_accum_kernel(
 #define TDC_NONE(I0, CNT)
 #define TDC_MEMB0(I0, CNT) TDC_MEMB(acc0, wh0, wl0, I0, CNT)
 #define TDC_MEMB1(I0, CNT) TDC_MEMB(acc1, wh1, wl1, I0, CNT)
-    TDC_DIST(acc0, 0, TDC_NONE)
-    TDC_LOADQ(0)
-    TDC_DIST(acc1, 1, TDC_MEMB0)
-    TDC_LOADQ(1)
-    TDC_WTX(0, wh0, wl0, TDC_MEMB1)
-    TDC_WTX(1, wh1, wl1, TDC_NONE)
+    if constexpr (WAVES == 4) {
+      TDC_DIST(acc0, 0, TDC_NONE)
+      TDC_LOADQ(0)
+      TDC_DIST(acc1, 1, TDC_MEMB0)
+      TDC_LOADQ(1)
+      TDC_WTX(0, wh0, wl0, TDC_MEMB1)
+      TDC_WTX(1, wh1, wl1, TDC_NONE)
+    } else {
+      // 8 waves: row statistics read from LDS per group of 4 elements (no xq/iq arrays
+      // live across the distance MFMAs: the 2-wave register budget is 256)
+      const int sub = w >> 2;
+      TDC_DIST(acc0, sub, TDC_NONE)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int pt = sub * 32 + 8 * g4 + 4 * h;
+        xq[0] = *reinterpret_cast<const f32x4*>(&s_xx[buf][pt]);
+        iq[0] = *reinterpret_cast<const f32x4*>(&s_in[buf][pt]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * g4 + e;
+          const float zf = ZERO_FLOOR * xq[0][e];
+          const float d2 = fmaxf(acc0[i] + xq[0][e], zf);
+          float u = mt<MODE>(d2, prm.expo) * iq[0][e];
+          if constexpr (!NZ) u = iq[0][e] < 0.f ? (d2 <= zf ? 1.f : 0.f) : u;
+          const float wv = mw<MODE>(u, prm.m);
+          wsum += wv;
+          const __bf16 bhv = (__bf16)wv;
+          wh0[i >> 3][i & 7] = bhv;
+          wl0[i >> 3][i & 7] = (__bf16)(wv - (float)bhv);
+        }
+      }
+      TDC_WTX(sub, wh0, wl0, TDC_NONE)
+    }
 #undef TDC_NONE
 #undef TDC_MEMB0
 #undef TDC_MEMB1
@@ -460,6 +495,29 @@ __global__ __launch_bounds__(256, 1) void fcm_mfma_accum_kernel(
 #undef TDC_TILE_LOAD
 #undef TDC_TILE_STORE
 
+  if constexpr (WAVES == 8) {
+    // the point-half-1 waves hand their W^T X partials (and column sums) to the half-0
+    // waves of the same centroid group through the (now idle) tile buffers
+    static_assert(4 * 32 * DP * 4 <= (int)sizeof(s_x), "exchange fits the tile buffers");
+    float* xo = reinterpret_cast<float*>(&s_x[0][0]) + cg * 32 * DP;
+    float* xw = &s_xx[0][0] + cg * 32;
+    __syncthreads();
+    const float wpair = wsum + __shfl_xor(wsum, 32, 64);  // all lanes take part in the swap
+    if (w >= 4) {
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) xo[(i * NDT + dt) * 64 + lane] = out[dt][i];
+      if (h == 0) xw[r] = wpair;
+    }
+    __syncthreads();
+    if (w >= 4) return;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) out[dt][i] += xo[(i * NDT + dt) * 64 + lane];
+    wsum += (h == 0) ? xw[r] : 0.f;
+  }
   // ---- slab: out rows (registers) = centroids kw + (i&3)+8(i>>2)+4h, lane = feature ----
   float* slab = part + split * (int64_t)KP * DP;
 #pragma unroll
@@ -580,10 +638,18 @@ int launch_maccum(const void* Xh, const void* Xl, const float* xx, const float* 
   const int xcd = (nb % 8 == 0) ? 1 : 0;
   float* part_ws = part + splits * (int64_t)Kp * DP;
   const MParam p = make_mparam(m, nz);
+  static const int waves = getenv("TDC_FCM_WAVES") ? atoi(getenv("TDC_FCM_WAVES")) : 8;
 #define TDC_LA(MODE, NZV)                                                                     \
-  hipLaunchKernelGGL((fcm_mfma_accum_kernel<DP, MODE, NZV>), dim3((unsigned)nb), dim3(256), 0, s, \
-                     (const __bf16*)Xh, (const __bf16*)Xl, xx, rowinfo, N, (const __bf16*)Ch, \
-                     (const __bf16*)Cl, cc, K, nkt, rps, xcd, p, part, part_ws, Kp)
+  if (waves == 4)                                                                             \
+    hipLaunchKernelGGL((fcm_mfma_accum_kernel<DP, MODE, NZV, 4>), dim3((unsigned)nb), dim3(256), \
+                       0, s, (const __bf16*)Xh, (const __bf16*)Xl, xx, rowinfo, N,             \
+                       (const __bf16*)Ch, (const __bf16*)Cl, cc, K, nkt, rps, xcd, p, part,    \
+                       part_ws, Kp);                                                          \
+  else                                                                                        \
+    hipLaunchKernelGGL((fcm_mfma_accum_kernel<DP, MODE, NZV, 8>), dim3((unsigned)nb), dim3(512), \
+                       0, s, (const __bf16*)Xh, (const __bf16*)Xl, xx, rowinfo, N,             \
+                       (const __bf16*)Ch, (const __bf16*)Cl, cc, K, nkt, rps, xcd, p, part,    \
+                       part_ws, Kp)
   if (m == 2.0) {
     if (nz) TDC_LA(2, true); else TDC_LA(2, false);
   } else {
