@@ -41,6 +41,7 @@ class BoundedLloydEngine(LloydEngine):
     # the totals are fp64 (gbuf) and the per-step deltas small: plain [sums | counts] buffer
     exact_counts_ok = False
     rsag_ok = False
+    warmup_ok = False  # the bounds and running totals are incremental
     oom_guard_ok = False
     slack = 1e-3     # relative margin on ub (bf16 distance arithmetic)
     refresh = 64     # iterations between full recomputations of the totals

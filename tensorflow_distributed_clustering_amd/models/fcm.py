@@ -125,7 +125,7 @@ class FcmEngine(OomGuard):
     def step(self):
         self.buf.zero_()
         try:
-            if self.oom_guard:
+            if self.oom_guard and not self._warming:
                 faults.maybe_fail(str(self.n_iter + 1), self.comm.rank, kinds=("oom",))
             self._local_step()
         except Exception as e:  # noqa: BLE001 - filtered right below
@@ -267,6 +267,8 @@ class FuzzyCMeans:
         eng = self._build_engine(first, x_local, dev, comm, n_global, row_offset, n_local,
                                  init_centers_, start_iter, m)
         self.engine_ = eng
+        if cfg.max_iter > eng.n_iter:
+            eng.warmup()
         sync(dev)
         setup_time = time.perf_counter() - t1
 

@@ -140,6 +140,30 @@ class OomGuard:
             self._checked = n
         return None
 
+    # ------------------------------------------------------------ untimed warm-up step
+    _warming = False
+    warmup_ok = True  # engines with incremental state a discarded step would corrupt: off
+
+    def warmup(self):
+        """One step whose result is discarded (the centroids and the iteration count are
+        restored): the first launch of each step kernel loads its code object and sizes
+        its grid (~2.5 ms at the reference's N=25M, K=3 -- more than ten iterations), a
+        setup cost that belongs in setup_time, not in the timed iterations.  Resident,
+        replicated-centroid engines on a GPU only (a streamed pass would cost a full
+        transfer; rsag state is sliced across ranks)."""
+        if (not self.warmup_ok or self.streamed or getattr(self, "rsag", False)
+                or self.device.type != "cuda" or getattr(self, "_graph", None) is not None):
+            return
+        c0, n0 = self.C.clone(), self.n_iter
+        self._warming = True
+        try:
+            self.step()
+        finally:
+            self._warming = False
+        self.C.copy_(c0)
+        self.local.prepare(self.C)
+        self.n_iter = n0
+
     def rollback(self, step: int) -> np.ndarray:
         """Centroids at the start of ``step`` (replicated, host fp64); resets n_iter."""
         slot = step % len(self._ring)
@@ -335,7 +359,7 @@ class LloydEngine(OomGuard):
         self.buf.zero_()
         mind = self.mind if (with_inertia and self.mind is not None) else None
         try:
-            if self.oom_guard:
+            if self.oom_guard and not self._warming:
                 faults.maybe_fail(str(self.n_iter + 1), self.comm.rank, kinds=("oom",))
             self._local_step(mind)
         except Exception as e:  # noqa: BLE001 - filtered right below
@@ -619,6 +643,8 @@ class KMeans:
                                  init_centers_, start_iter)
         if cfg.graph and eng.graphable() and comm.world_size == 1:
             eng.capture()
+        if cfg.max_iter > eng.n_iter:
+            eng.warmup()
         sync(dev)
         setup_time = time.perf_counter() - t_setup0
 
