@@ -144,7 +144,7 @@ class OomGuard:
     _warming = False
     warmup_ok = True  # engines with incremental state a discarded step would corrupt: off
 
-    def warmup(self):
+    def warmup(self, force: bool = False):
         """One step whose result is discarded (the centroids and the iteration count are
         restored): the first launch of each step kernel loads its code object and sizes
         its grid (~2.5 ms at the reference's N=25M, K=3 -- more than ten iterations), a
@@ -152,7 +152,8 @@ class OomGuard:
         replicated-centroid engines on a GPU only (a streamed pass would cost a full
         transfer; rsag state is sliced across ranks)."""
         if (not self.warmup_ok or self.streamed or getattr(self, "rsag", False)
-                or self.device.type != "cuda" or getattr(self, "_graph", None) is not None):
+                or getattr(self, "_graph", None) is not None
+                or (self.device.type != "cuda" and not force)):
             return
         c0, n0 = self.C.clone(), self.n_iter
         self._warming = True

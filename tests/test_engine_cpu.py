@@ -172,3 +172,25 @@ def test_fcm_predict_and_memberships_match_fit():
     torch.testing.assert_close(u.sum(1), torch.ones(4000, dtype=torch.float64))
     assert torch.equal(u.argmax(1).to(torch.int32), lab)
 
+
+
+@pytest.mark.parametrize("method", ["kmeans", "fcm"])
+def test_warmup_step_leaves_no_trace(method):
+    """The untimed warm-up step (setup) restores the centroids and the iteration count:
+    the steps after it match an engine that never warmed up."""
+    from tensorflow_distributed_clustering_amd.models.fcm import FcmEngine
+    from tensorflow_distributed_clustering_amd.models.kmeans import LloydEngine
+    from tensorflow_distributed_clustering_amd.parallel.dist import init_comm
+    comm = init_comm("cpu")
+    x = gaussian_blobs(3000, 4, 6, seed=5, dtype=torch.float64)
+    cfg = tdc.ClusterConfig(n_clusters=6, max_iter=5, dtype="fp64", seed=3, fuzzifier=2.0,
+                            empty_cluster="reseed" if method == "kmeans" else "keep")
+    Eng = LloydEngine if method == "kmeans" else FcmEngine
+    a, b = Eng(x, cfg, comm, 3000, 0), Eng(x, cfg, comm, 3000, 0)
+    c0 = a.C.clone()
+    a.warmup(force=True)
+    assert torch.equal(a.C, c0) and a.n_iter == 0
+    for _ in range(3):
+        a.step()
+        b.step()
+    assert torch.equal(a.C, b.C) and a.n_iter == b.n_iter == 3
