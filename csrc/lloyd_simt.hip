@@ -11,6 +11,8 @@
 // * assign_simt: difference-form argmin for larger K (centroids staged through LDS).
 // * update_lds: per-block LDS histogram of sum(x) and count, sliced over D so that
 //   K x D_slice fits LDS; one flush of global atomics per block.
+#include <type_traits>
+
 #include "tdc_common.h"
 #include "kernels.h"
 
@@ -368,75 +370,133 @@ int tdc_lloyd_small(int dtype, int acc_dtype, const void* X, int64_t N, int64_t 
 
 // ------------------------------------------------------------------------------------
 // exact assignment for ANY D (fp32 / fp64, difference form like the reference's
-// Sub/Square/Sum, `scripts/distribuitedClustering.py:228-230`): 64-row x 64-centroid block
-// tiles, 16 x 16 threads with a 4 x 4 register micro-tile, rows and centroids staged
-// through LDS in 16-feature chunks (LDS use independent of D), argmin kept per row and
-// merged over the 16 centroid lanes at the end.  Replaces the library-GEMM fallback for
-// fp32 D > 64 / fp64 D > 32 (the GEMM expansion loses the exact-difference precision).
+// Sub/Square/Sum, `scripts/distribuitedClustering.py:228-230`): (16 MR)-row x 128-centroid
+// block tiles, 16 x 16 threads with an MR-row x 8-centroid register micro-tile, rows and centroids
+// staged through LDS feature-major in 32-feature chunks (LDS use independent of D), so a
+// thread's MR rows / 8 centroids of one feature are ds_read_b128 pieces; fp32 runs
+// on packed math (v_pk_add_f32 / v_pk_fma_f32: two centroids per instruction).  The argmin
+// is kept per row and merged over the 16 centroid lanes at the end.  Replaces the
+// library-GEMM fallback for fp32 D > 64 / fp64 D > 32 (the GEMM expansion loses the
+// exact-difference precision).
 // ------------------------------------------------------------------------------------
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// x - c for a centroid pair c with x broadcast from one half of a row pair (VOP3P op_sel:
+// no register copy to build the (x, x) pair, which cost more moves than the math)
+__device__ __forceinline__ f32x2 pk_sub_lo(f32x2 xp, f32x2 c) {
+  f32x2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel_hi:[0,1] neg_lo:[0,1] neg_hi:[0,1]"
+      : "=v"(r) : "v"(xp), "v"(c));
+  return r;
+}
+__device__ __forceinline__ f32x2 pk_sub_hi(f32x2 xp, f32x2 c) {
+  f32x2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1] neg_lo:[0,1] neg_hi:[0,1]"
+      : "=v"(r) : "v"(xp), "v"(c));
+  return r;
+}
+
+// MR rows x 8 centroids per thread: fp32 MR = 8 (packed pairs, 64 accumulators), fp64 MR = 4
+template <typename T> struct ExactCfg { static constexpr int MR = 8; };
+template <> struct ExactCfg<double> { static constexpr int MR = 4; };
+
 template <typename T>
 __global__ __launch_bounds__(256) void assign_exact_kernel(const T* __restrict__ X, int64_t N,
                                                            int64_t ldx, int D,
                                                            const T* __restrict__ C, int K,
                                                            int32_t* __restrict__ labels,
                                                            T* __restrict__ mind) {
-  constexpr int R = 64, KT = 64, DC = 16;
-  __shared__ T s_x[R][DC + 1];
-  __shared__ T s_c[KT][DC + 1];
+  constexpr int MR = ExactCfg<T>::MR;
+  constexpr int R = 16 * MR, KT = 128, DC = 32;
+  constexpr int PX = R + 4, PC = KT + 4;  // row pitch (16-B aligned, spreads the store banks)
+  __shared__ __attribute__((aligned(16))) T s_x[DC][PX];
+  __shared__ __attribute__((aligned(16))) T s_c[DC][PC];
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  constexpr bool F32 = sizeof(T) == 4;
   for (int64_t r0 = (int64_t)blockIdx.x * R; r0 < N; r0 += (int64_t)gridDim.x * R) {
-    T best[4];
-    int bk[4];
+    T best[MR];
+    int bk[MR];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < MR; ++i) {
       best[i] = (T)INFINITY;
       bk[i] = 0;
     }
     for (int k0 = 0; k0 < K; k0 += KT) {
-      T acc[4][4];
+      // fp32: MR x 4 packed centroid pairs; fp64: MR x 8 scalars
+      typename std::conditional<F32, f32x2[MR][4], double[MR][8]>::type acc;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MR; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = (T)0;
+        for (int j = 0; j < (F32 ? 4 : 8); ++j) {
+          if constexpr (F32) acc[i][j] = f32x2{0.f, 0.f};
+          else acc[i][j] = 0.0;
+        }
       for (int dc = 0; dc < D; dc += DC) {
         __syncthreads();
+        // coalesced along the features, stored feature-major (transposed)
         for (int e = tid; e < R * DC; e += 256) {
           const int r = e / DC, d = e % DC;
-          s_x[r][d] = (r0 + r < N && dc + d < D) ? X[(r0 + r) * ldx + dc + d] : (T)0;
-          s_c[r][d] = (k0 + r < K && dc + d < D) ? C[(int64_t)(k0 + r) * D + dc + d] : (T)0;
+          s_x[d][r] = (r0 + r < N && dc + d < D) ? X[(r0 + r) * ldx + dc + d] : (T)0;
+        }
+        for (int e = tid; e < KT * DC; e += 256) {
+          const int r = e / DC, d = e % DC;
+          s_c[d][r] = (k0 + r < K && dc + d < D) ? C[(int64_t)(k0 + r) * D + dc + d] : (T)0;
         }
         __syncthreads();
-#pragma unroll 4
+#pragma unroll 2
         for (int d = 0; d < DC; ++d) {
-          T xv[4], cv[4];
+          if constexpr (F32) {
+            const f32x2* xs = reinterpret_cast<const f32x2*>(&s_x[d][ty * MR]);
+            const f32x2* cs = reinterpret_cast<const f32x2*>(&s_c[d][tx * 8]);
+            f32x2 xp[MR / 2], c2[4];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) xv[i] = s_x[ty + 16 * i][d];
+            for (int m = 0; m < MR / 2; ++m) xp[m] = xs[m];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) cv[j] = s_c[tx + 16 * j][d];
+            for (int j = 0; j < 4; ++j) c2[j] = cs[j];
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+            for (int m = 0; m < MR / 2; ++m)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const T df = xv[i] - cv[j];
-              acc[i][j] = fma(df, df, acc[i][j]);
-            }
+              for (int j = 0; j < 4; ++j) {
+                const f32x2 d0 = pk_sub_lo(xp[m], c2[j]);
+                const f32x2 d1 = pk_sub_hi(xp[m], c2[j]);
+                acc[2 * m][j] = __builtin_elementwise_fma(d0, d0, acc[2 * m][j]);
+                acc[2 * m + 1][j] = __builtin_elementwise_fma(d1, d1, acc[2 * m + 1][j]);
+              }
+          } else {
+            T xv[MR], cv[8];
+#pragma unroll
+            for (int i = 0; i < MR; ++i) xv[i] = s_x[d][ty * MR + i];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) cv[j] = s_c[d][tx * 8 + j];
+#pragma unroll
+            for (int i = 0; i < MR; ++i)
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const T df = xv[i] - cv[j];
+                acc[i][j] = fma(df, df, acc[i][j]);
+              }
+          }
         }
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = k0 + tx + 16 * j;  // ascending per thread: strict < keeps the first
+      for (int j = 0; j < 8; ++j) {
+        const int k = k0 + tx * 8 + j;  // ascending per thread: strict < keeps the first
         if (k < K) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (acc[i][j] < best[i]) {
-              best[i] = acc[i][j];
+          for (int i = 0; i < MR; ++i) {
+            T v;
+            if constexpr (F32) v = acc[i][j >> 1][j & 1];
+            else v = acc[i][j];
+            if (v < best[i]) {
+              best[i] = v;
               bk[i] = k;
             }
+          }
         }
       }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < MR; ++i) {
 #pragma unroll
       for (int o = 1; o < 16; o <<= 1) {
         const T ob = __shfl_xor(best[i], o, 64);
@@ -446,7 +506,7 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(const T* __restrict__
           bk[i] = ok;
         }
       }
-      const int64_t row = r0 + ty + 16 * i;
+      const int64_t row = r0 + ty * MR + i;
       if (tx == 0 && row < N) {
         labels[row] = bk[i];
         if (mind) mind[row] = best[i];
@@ -459,8 +519,9 @@ int tdc_assign_exact(int dtype, const void* X, int64_t N, int64_t ldx, int D, co
                      int32_t* labels, void* mind, int num_cus, hipStream_t s) {
   if (N <= 0) return 0;
   (void)num_cus;
-  int64_t blocks = (N + 63) / 64;
-  // grid-stride over 64-row tiles with the blocks resident at once (no partial 2nd round)
+  const int64_t rows_per_tile = 16 * (dtype == TDC_F64 ? ExactCfg<double>::MR : ExactCfg<float>::MR);
+  int64_t blocks = (N + rows_per_tile - 1) / rows_per_tile;
+  // grid-stride over row tiles with the blocks resident at once (no partial 2nd round)
   static const int res32 = resident_blocks(assign_exact_kernel<float>, 256);
   static const int res64 = resident_blocks(assign_exact_kernel<double>, 256);
   const int64_t resident = dtype == TDC_F64 ? res64 : res32;
