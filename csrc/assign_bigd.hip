@@ -1,4 +1,4 @@
-// N1/N8 for wide embeddings: fused distance + argmin for D in (256, 512] (bf16) and for
+// N1/N8 for wide embeddings: fused distance + argmin for D in (256, 768] (bf16) and for
 // block-scaled fp8 (OCP e4m3 + E8M0 scales, D a multiple of 256 up to 1024), plus the
 // fp8 row quantiser.  BASELINE config 5: N=50M, D=768, K=65536.
 //
@@ -485,9 +485,10 @@ int launch_bigd(const void* X, const void* Xs, int64_t N, int64_t ldx_bytes, con
 }  // namespace
 
 int tdc_assign_bigd_supported(int dtype, int DP) {
-  // (bf16 D > 512 would need > 256 VGPRs of resident point fragments: spills)
+  // (bf16 D > 512: one wave per SIMD, the point fragments spill into AGPRs; D > 768 would
+  // not fit at all)
   if (dtype == TDC_FP8) return DP == 256 || DP == 512 || DP == 768 || DP == 1024;
-  if (dtype == TDC_BF16) return DP == 384 || DP == 512;
+  if (dtype == TDC_BF16) return DP == 384 || DP == 512 || DP == 640 || DP == 768;
   return 0;
 }
 
@@ -535,6 +536,10 @@ int tdc_assign_bigd(int dtype, const void* X, const void* Xs, int64_t N, int64_t
     switch (DP) {
       case 384: return launch_bigd<OpBf16, 384, 8, 4>(X, nullptr, N, ldb, Cm2, nullptr, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
       case 512: return launch_bigd<OpBf16, 512, 8, 4>(X, nullptr, N, ldb, Cm2, nullptr, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
+      // D > 512: the point fragments (D/4 VGPRs) need one wave per SIMD (4-wave groups,
+      // accumulators in AGPRs); 48 KiB stages, 3 deep
+      case 640: return launch_bigd<OpBf16, 640, 4, 3>(X, nullptr, N, ldb, Cm2, nullptr, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
+      case 768: return launch_bigd<OpBf16, 768, 4, 3>(X, nullptr, N, ldb, Cm2, nullptr, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
     }
   }
   return (int)hipErrorInvalidValue;

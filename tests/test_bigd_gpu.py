@@ -109,7 +109,8 @@ def test_assign_fp8_vs_dequantised_reference(gpu, d, dp, k, kg):
         assert torch.equal(lab, lab2)
 
 
-@pytest.mark.parametrize("d,dp,k,kg", [(300, 384, 777, 0), (512, 512, 3000, 16), (384, 384, 64, 1)])
+@pytest.mark.parametrize("d,dp,k,kg", [(300, 384, 777, 0), (512, 512, 3000, 16), (384, 384, 64, 1),
+                                       (600, 640, 300, 0), (768, 768, 1000, 0), (700, 768, 130, 8)])
 def test_assign_wide_bf16(gpu, d, dp, k, kg):
     torch.manual_seed(2)
     n = 15000
