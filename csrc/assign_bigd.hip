@@ -1,4 +1,4 @@
-// N1/N8 for wide embeddings: fused distance + argmin for D in (256, 768] (bf16) and for
+// N1/N8 for wide embeddings: fused distance + argmin for D in (256, 1024] (bf16) and for
 // block-scaled fp8 (OCP e4m3 + E8M0 scales, D a multiple of 256 up to 1024), plus the
 // fp8 row quantiser.  BASELINE config 5: N=50M, D=768, K=65536.
 //
@@ -485,10 +485,11 @@ int launch_bigd(const void* X, const void* Xs, int64_t N, int64_t ldx_bytes, con
 }  // namespace
 
 int tdc_assign_bigd_supported(int dtype, int DP) {
-  // (bf16 D > 512: one wave per SIMD, the point fragments spill into AGPRs; D > 768 would
-  // not fit at all)
+  // (bf16 D > 512: one wave per SIMD, the point fragments spill into AGPRs; 56-64 KiB
+  // stages 2 deep above D=768; D > 1024 would not fit the register file)
   if (dtype == TDC_FP8) return DP == 256 || DP == 512 || DP == 768 || DP == 1024;
-  if (dtype == TDC_BF16) return DP == 384 || DP == 512 || DP == 640 || DP == 768;
+  if (dtype == TDC_BF16)
+    return DP == 384 || DP == 512 || DP == 640 || DP == 768 || DP == 896 || DP == 1024;
   return 0;
 }
 
@@ -540,6 +541,8 @@ int tdc_assign_bigd(int dtype, const void* X, const void* Xs, int64_t N, int64_t
       // accumulators in AGPRs); 48 KiB stages, 3 deep
       case 640: return launch_bigd<OpBf16, 640, 4, 3>(X, nullptr, N, ldb, Cm2, nullptr, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
       case 768: return launch_bigd<OpBf16, 768, 4, 3>(X, nullptr, N, ldb, Cm2, nullptr, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
+      case 896: return launch_bigd<OpBf16, 896, 4, 2>(X, nullptr, N, ldb, Cm2, nullptr, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
+      case 1024: return launch_bigd<OpBf16, 1024, 4, 2>(X, nullptr, N, ldb, Cm2, nullptr, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
     }
   }
   return (int)hipErrorInvalidValue;

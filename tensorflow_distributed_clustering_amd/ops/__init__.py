@@ -11,7 +11,7 @@ Variants (picked by :func:`make_lloyd_ops`):
 
 ========================  =====================================================
 ``HipBf16Lloyd``          bf16 MFMA distance+argmin (N1) + LDS update (N2) + N3
-``HipWideBf16Lloyd``      bf16, 256 < D <= 768: K-grouped wide-D MFMA kernel
+``HipWideBf16Lloyd``      bf16, 256 < D <= 1024: K-grouped wide-D MFMA kernel
 ``HipFp8Lloyd``           fp8 e4m3 + E8M0 block scales (N8), scaled-MFMA assign,
                           update from the full-precision shard
 ``HipSmallLloyd``         fused fp32/fp64 assign+accumulate (reference configs)
@@ -36,7 +36,7 @@ POLICY_CODES = {"keep": 0, "reseed": 0, "nan": 1, "nan_any": 1, "zero": 2}
 TORCH_DTYPES = {"fp64": torch.float64, "fp32": torch.float32, "bf16": torch.bfloat16,
                 "fp8": torch.bfloat16}
 MFMA_DIMS = (32, 64, 128, 256)
-WIDE_BF16_DIMS = (384, 512, 640, 768)
+WIDE_BF16_DIMS = (384, 512, 640, 768, 896, 1024)
 FP8_DIMS = (256, 512, 768, 1024)
 # centroid bytes one K-group may occupy (0 = one group over all of K).  Grouping keeps a
 # group L2-resident per XCD, but measured slower than one group (the 256 MiB MALL serves
@@ -406,9 +406,9 @@ class _GroupedAssign:
 
 
 class HipWideBf16Lloyd(_GroupedAssign, _LocalOpsBase):
-    """bf16 shard [N, DP], 256 < D <= 768 (DP = 384 / 512 / 640 / 768): assign_bigd bf16
-    kernel (8-wave groups up to 512, one wave per SIMD above: the point fragments are D/4
-    registers)."""
+    """bf16 shard [N, DP], 256 < D <= 1024 (DP = 384 ... 1024 in steps of 128): assign_bigd
+    bf16 kernel (8-wave groups up to 512, one wave per SIMD above: the point fragments are
+    D/4 registers)."""
     name = "hip_bf16_wide"
     c_dtype = torch.float32
 
@@ -699,7 +699,7 @@ def _make_lloyd_ops(x, k, dtype, backend, empty_cluster, deterministic):
             return HipBf16Lloyd(x, k, empty_cluster)
         if wide_bf16_dim(d) is not None:
             return HipWideBf16Lloyd(x, k, empty_cluster)
-        return HipExactLloyd(x, k, "fp32", empty_cluster)  # bf16 D > 768: exact fp32 tiles
+        return HipExactLloyd(x, k, "fp32", empty_cluster)  # bf16 D > 1024: exact fp32 tiles
     tdt = TORCH_DTYPES[dtype]
     ops = _native.require()
     if ops.lloyd_small_supported(tdt, k, d) and not deterministic:

@@ -110,7 +110,8 @@ def test_assign_fp8_vs_dequantised_reference(gpu, d, dp, k, kg):
 
 
 @pytest.mark.parametrize("d,dp,k,kg", [(300, 384, 777, 0), (512, 512, 3000, 16), (384, 384, 64, 1),
-                                       (600, 640, 300, 0), (768, 768, 1000, 0), (700, 768, 130, 8)])
+                                       (600, 640, 300, 0), (768, 768, 1000, 0), (700, 768, 130, 8),
+                                       (896, 896, 200, 0), (1000, 1024, 500, 0)])
 def test_assign_wide_bf16(gpu, d, dp, k, kg):
     torch.manual_seed(2)
     n = 15000

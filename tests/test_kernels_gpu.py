@@ -564,10 +564,11 @@ def test_assign_exact_wide_d(gpu, dt, n, d, k):
 @pytest.mark.parametrize("dtype,d,backend", [("fp64", 48, "hip_exact_tiled"),
                                              ("fp32", 96, "hip_exact_tiled"),
                                              ("bf16", 768, "hip_bf16_wide"),
-                                             ("bf16", 900, "hip_exact_tiled")])
+                                             ("bf16", 900, "hip_bf16_wide"),
+                                             ("bf16", 1100, "hip_exact_tiled")])
 def test_wide_d_lloyd_is_native(gpu, dtype, d, backend):
-    """fp64 D > 32 and fp32 D > 64 run the native exact kernels (no GEMM); bf16 up to D=768
-    the wide MFMA kernel, above it the exact tiles."""
+    """fp64 D > 32 and fp32 D > 64 run the native exact kernels (no GEMM); bf16 runs
+    the wide MFMA kernel up to D=1024, above it the exact tiles."""
     import tensorflow_distributed_clustering_amd as tdc
     from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs
     x = gaussian_blobs(20000, d, 20, seed=3, dtype=torch.float64, device=gpu)
