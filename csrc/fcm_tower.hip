@@ -35,13 +35,14 @@ struct FcmParam {
   int pmode, mint, nz;
 };
 
-template <typename T>
+// FM: compile-time fuzzifier form (fcm_math.h fm_t / fm_w; 2, 5 or any m)
+template <int FM, typename T>
 __device__ __forceinline__ T fcm_weight(T d2, T info, const FcmParam<T>& p) {
   T u;
-  if (info > (T)0) u = fcm_t(d2, p.expo, p.pmode) * info;
+  if (info > (T)0) u = fm_t<FM>(d2, p.expo) * info;
   else if (info == (T)0) return (T)0;
   else u = (d2 == (T)0) ? (T)-1 / info : (T)0;
-  return u > (T)0 ? fcm_w(u, p.m, p.mint) : (T)0;
+  return u > (T)0 ? fm_w<FM>(u, p.m) : (T)0;
 }
 
 // d2 of the block's R rows (s_x, staged) against centroids [k0, k0 + 64): acc[i][j] is row
@@ -92,7 +93,7 @@ __device__ __forceinline__ void stage_x(const T* __restrict__ X, int64_t N, int6
   }
 }
 
-template <typename T, int DMAX, int R>
+template <typename T, int DMAX, int R, int FM>
 __global__ __launch_bounds__(256) void fcm_stats_kernel(const T* __restrict__ X, int64_t N,
                                                         int64_t ldx, int D,
                                                         const T* __restrict__ C, int K,
@@ -125,7 +126,8 @@ __global__ __launch_bounds__(256) void fcm_stats_kernel(const T* __restrict__ X,
 #pragma unroll
         for (int i = 0; i < RM; ++i) {
           const T d2 = acc[i][j];
-          S[i] += d2 == (T)0 ? inf : fcm_t(d2, p.expo, p.pmode);
+          const T t = fm_t<FM>(d2, p.expo);
+          S[i] += d2 == (T)0 ? inf : t;
           nzc[i] += d2 == (T)0;
           if (d2 < best[i]) {  // ascending k per thread: the first minimum wins
             best[i] = d2;
@@ -158,7 +160,7 @@ __global__ __launch_bounds__(256) void fcm_stats_kernel(const T* __restrict__ X,
   }
 }
 
-template <typename T, typename ACC, int DMAX, int R>
+template <typename T, typename ACC, int DMAX, int R, int FM>
 __global__ __launch_bounds__(256) void fcm_accum_kernel(const T* __restrict__ X, int64_t N,
                                                         int64_t ldx, int D,
                                                         const T* __restrict__ C, int K,
@@ -197,7 +199,7 @@ __global__ __launch_bounds__(256) void fcm_accum_kernel(const T* __restrict__ X,
       const T info = s_info[ty + 16 * i];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const T w = (k0 + tx + 16 * j < K) ? fcm_weight(acc[i][j], info, p) : (T)0;
+        const T w = (k0 + tx + 16 * j < K) ? fcm_weight<FM>(acc[i][j], info, p) : (T)0;
         s_w[ty + 16 * i][tx + 16 * j] = w;
         wsp[j] += w;
       }
@@ -254,9 +256,16 @@ int launch_stats(const void* X, int64_t N, int64_t ldx, int D, const void* C, in
   constexpr int R = (sizeof(T) == 8 && DMAX > 128) ? 16 : 32;
   int64_t tiles = (N + R - 1) / R;
   int64_t blocks = tiles < (int64_t)num_cus * 8 ? tiles : (int64_t)num_cus * 8;
-  hipLaunchKernelGGL((fcm_stats_kernel<T, DMAX, R>), dim3((unsigned)blocks), dim3(256), 0, s,
-                     (const T*)X, N, ldx, D, (const T*)C, K, make_param<T>(m, nz), labels,
-                     (T*)rowinfo);
+#define TDC_LS(FMV)                                                                            \
+  hipLaunchKernelGGL((fcm_stats_kernel<T, DMAX, R, FMV>), dim3((unsigned)blocks), dim3(256), 0, s, \
+                     (const T*)X, N, ldx, D, (const T*)C, K, make_param<T>(m, nz), labels,       \
+                     (T*)rowinfo)
+  switch (fcm_fm(m)) {
+    case 2: TDC_LS(2); break;
+    case 5: TDC_LS(5); break;
+    default: TDC_LS(0);
+  }
+#undef TDC_LS
   TDC_CHECK_LAUNCH();
   return 0;
 }
@@ -272,9 +281,16 @@ int launch_accum(const void* X, int64_t N, int64_t ldx, int D, const void* C, in
   if (splits < 1) splits = 1;
   const int64_t rps = ((tiles + splits - 1) / splits) * R;
   splits = (N + rps - 1) / rps;
-  hipLaunchKernelGGL((fcm_accum_kernel<T, ACC, DMAX, R>), dim3((unsigned)(splits * nkt)), dim3(256),
-                     0, s, (const T*)X, N, ldx, D, (const T*)C, K, make_param<T>(m, nz),
-                     (const T*)rowinfo, rps, nkt, (ACC*)wx, (ACC*)ws);
+#define TDC_LA(FMV)                                                                            \
+  hipLaunchKernelGGL((fcm_accum_kernel<T, ACC, DMAX, R, FMV>), dim3((unsigned)(splits * nkt)),   \
+                     dim3(256), 0, s, (const T*)X, N, ldx, D, (const T*)C, K,                   \
+                     make_param<T>(m, nz), (const T*)rowinfo, rps, nkt, (ACC*)wx, (ACC*)ws)
+  switch (fcm_fm(m)) {
+    case 2: TDC_LA(2); break;
+    case 5: TDC_LA(5); break;
+    default: TDC_LA(0);
+  }
+#undef TDC_LA
   TDC_CHECK_LAUNCH();
   return 0;
 }
