@@ -43,7 +43,7 @@ __global__ __launch_bounds__(256) void lloyd_small_kernel(
   const T* sc = s_c + part * KL * DMAX;
 
   T acc[KL][DMAX];
-  int cnt[KL];
+  T cnt[KL];  // counted with the one-hot selector itself: one add instead of cmp + select + add
 #pragma unroll
   for (int k = 0; k < KL; ++k) {
     cnt[k] = 0;
@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void lloyd_small_kernel(
       const int k = part * KL + j;
       if (LPR > 1 || k < K) {
         const T sel = (k == best) ? (T)1 : (T)0;
-        cnt[j] += (k == best);
+        cnt[j] += sel;
 #pragma unroll
         for (int d = 0; d < DMAX; ++d) acc[j][d] = fma(sel, x[d], acc[j][d]);
       }
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) void lloyd_small_kernel(
   for (int j = 0; j < KL; ++j) {
 #pragma unroll
     for (int d = 0; d <= DMAX; ++d) {
-      T v = (d < DMAX) ? acc[j][d] : (T)cnt[j];
+      T v = (d < DMAX) ? acc[j][d] : cnt[j];
 #pragma unroll
       for (int o = 32; o >= LPR; o >>= 1) v += __shfl_xor(v, o, 64);
       if (lane < LPR) s_red[w][(lane * KL + j) * (DMAX + 1) + d] = v;
