@@ -204,6 +204,8 @@ int dispatch_fcm(const void* X, int64_t N, int64_t ldx, int D, const void* C, in
     TDC_FCM(4, 5, 2)
     TDC_FCM(6, 5, 2)
     TDC_FCM(8, 5, 2)
+    TDC_FCM(8, 5, 4)  // K <= 32: four lanes per row (the tower took 8.7x longer at K=32)
+    TDC_FCM(8, 5, 8)  // K <= 64: eight
   }
   TDC_FCM(4, 8, 1)
   TDC_FCM(8, 4, 1)
@@ -222,8 +224,8 @@ int dispatch_fcm(const void* X, int64_t N, int64_t ldx, int D, const void* C, in
 using namespace tdc;
 
 int tdc_fcm_small_supported(int dtype, int K, int D) {
-  if (dtype == TDC_F32) return (K <= 16 && D <= 8) || (K <= 32 && D <= 4);
-  if (dtype == TDC_F64) return (K <= 8 && D <= 8) || (K <= 16 && D <= 5);
+  if (dtype == TDC_F32) return (K <= 16 && D <= 8) || (K <= 32 && D <= 4) || (K <= 64 && D == 5);
+  if (dtype == TDC_F64) return (K <= 8 && D <= 8) || (K <= 16 && D <= 5) || (K <= 64 && D == 5);
   return 0;
 }
 

@@ -27,7 +27,9 @@ namespace tdc {
 namespace {
 
 constexpr int KT = 64;   // centroids per tile
-constexpr int DC = 16;   // feature chunk of the centroid staging
+// feature chunk of the centroid staging: 16, or DMAX itself for the narrow tiles (a fixed
+// 16 made the D <= 8 tiles do twice the work of their feature count)
+template <int DMAX> struct Chunk { static constexpr int DC = DMAX < 16 ? DMAX : 16; };
 
 template <typename T>
 struct FcmParam {
@@ -49,10 +51,11 @@ __device__ __forceinline__ T fcm_weight(T d2, T info, const FcmParam<T>& p) {
 // ty + 16 i, centroid k0 + tx + 16 j.  Ends with a barrier-free read of s_c, so callers
 // sync before the next staging.
 template <typename T, int DMAX, int R>
-__device__ __forceinline__ void tile_d2(T (*s_x)[DMAX + 1], T (*s_c)[DC + 1],
+__device__ __forceinline__ void tile_d2(T (*s_x)[DMAX + 1], T (*s_c)[Chunk<DMAX>::DC + 1],
                                         const T* __restrict__ C, int K, int D, int k0,
                                         T (&acc)[R / 16][4]) {
   constexpr int RM = R / 16;
+  constexpr int DC = Chunk<DMAX>::DC;
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
 #pragma unroll
   for (int i = 0; i < RM; ++i)
@@ -101,7 +104,7 @@ __global__ __launch_bounds__(256) void fcm_stats_kernel(const T* __restrict__ X,
                                                         T* __restrict__ rowinfo) {
   constexpr int RM = R / 16;
   __shared__ T s_x[R][DMAX + 1];
-  __shared__ T s_c[KT][DC + 1];
+  __shared__ T s_c[KT][Chunk<DMAX>::DC + 1];
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
   const T inf = (T)INFINITY;
   for (int64_t r0 = (int64_t)blockIdx.x * R; r0 < N; r0 += (int64_t)gridDim.x * R) {
@@ -171,7 +174,7 @@ __global__ __launch_bounds__(256) void fcm_accum_kernel(const T* __restrict__ X,
   constexpr int RM = R / 16;
   constexpr int QD = DMAX >= 16 ? DMAX / 16 : 1;
   __shared__ T s_x[R][DMAX + 1];
-  __shared__ T s_c[KT][DC + 1];
+  __shared__ T s_c[KT][Chunk<DMAX>::DC + 1];
   __shared__ T s_w[R][KT + 1];
   __shared__ T s_info[R];
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;

@@ -80,7 +80,9 @@ def test_fcm_mfma_matches_oracle(gpu, k, d, m, nz):
     assert torch.equal(lab, lab2)
 
 
-@pytest.mark.parametrize("dtype,d,k,backend", [("fp64", 5, 32, "hip_fcm_tower"),
+@pytest.mark.parametrize("dtype,d,k,backend", [("fp64", 5, 32, "hip_fcm_small"),
+                                               ("fp64", 5, 40, "hip_fcm_small"),
+                                               ("fp64", 6, 40, "hip_fcm_tower"),
                                                ("fp64", 64, 100, "hip_fcm_tower"),
                                                ("fp32", 12, 64, "hip_fcm_tower"),
                                                ("fp32", 128, 256, "hip_fcm_mfma")])

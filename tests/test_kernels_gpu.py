@@ -192,7 +192,9 @@ def test_assign_simt(gpu, dt, k, d):
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.float64])
 @pytest.mark.parametrize("k,d,m", [(3, 5, 5.0), (6, 5, 5.0), (9, 5, 5.0), (12, 5, 2.0),
-                                   (15, 5, 5.0), (16, 5, 1.5), (3, 3, 2.0), (8, 2, 2.0),
+                                   (15, 5, 5.0), (16, 5, 1.5), (24, 5, 5.0), (32, 5, 2.0),
+                                   (48, 5, 5.0), (64, 5, 2.0),
+                                   (3, 3, 2.0), (8, 2, 2.0),
                                    (6, 4, 1.7), (5, 3, 3.0), (4, 4, 4.0), (7, 2, 2.5)])
 @pytest.mark.parametrize("nan_to_zero", [True, False])
 def test_fcm_small(gpu, dt, k, d, m, nan_to_zero):
