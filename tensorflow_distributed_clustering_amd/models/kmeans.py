@@ -151,9 +151,14 @@ class OomGuard:
         setup cost that belongs in setup_time, not in the timed iterations.  Resident,
         replicated-centroid engines on a GPU only (a streamed pass would cost a full
         transfer; rsag state is sliced across ranks)."""
-        if (not self.warmup_ok or self.streamed or getattr(self, "rsag", False)
+        skip = (not self.warmup_ok or self.streamed or getattr(self, "rsag", False)
                 or getattr(self, "_graph", None) is not None
-                or (self.device.type != "cuda" and not force)):
+                or (self.device.type != "cuda" and not force))
+        if self.comm.world_size > 1:
+            # the step is collective: warm up only if every rank can (a rank whose planner
+            # chose streaming would otherwise leave the others waiting in the all-reduce)
+            skip = self.comm.max_scalar(1.0 if skip else 0.0) > 0.0
+        if skip:
             return
         c0, n0 = self.C.clone(), self.n_iter
         self._warming = True

@@ -252,3 +252,45 @@ def test_large_k_kmeanspp_is_sampled_kmeans_parallel_world_invariant(monkeypatch
     _, _, _, _, i2, _ = run_world(2, init="kmeans++", k=24, iters=1)
     np.testing.assert_allclose(i2, i1, rtol=1e-12, atol=1e-12)
     assert len(np.unique(i1, axis=0)) == 24
+
+
+def _warmup_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    import tensorflow_distributed_clustering_amd as tdc
+    from tensorflow_distributed_clustering_amd.data.stream import PlainHostSource
+    from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs
+    from tensorflow_distributed_clustering_amd.models.kmeans import LloydEngine
+    from tensorflow_distributed_clustering_amd.parallel import dist as D
+    D._COMM = None
+    comm = D.init_comm("cpu")
+    s, e = comm.shard(4000)
+    x = gaussian_blobs(e - s, 3, 4, seed=1, row_offset=s, dtype=torch.float64)
+    cfg = tdc.ClusterConfig(n_clusters=4, max_iter=3, dtype="fp64", seed=2, init="first_k")
+    # rank 1 streams its shard (a planner may pick that for one rank only), rank 0 is resident
+    src = PlainHostSource(x.numpy(), (torch.float64, 3), torch.device("cpu"), s) if rank else x
+    eng = LloydEngine(src, cfg, comm, 4000, s, chunk_rows=500 if rank else 0)
+    c0 = eng.C.clone()
+    eng.warmup(force=True)  # collective decision: rank 1 cannot, so neither warms up
+    same = bool(torch.equal(eng.C, c0)) and eng.n_iter == 0
+    for _ in range(2):
+        eng.step()
+    q.put((rank, same, eng.C.numpy().copy()))
+    D.destroy_comm()
+
+
+def test_warmup_is_skipped_on_every_rank_when_one_rank_streams():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_warmup_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (a, b)) for r, a, b in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][0] and res[1][0]
+    np.testing.assert_array_equal(res[0][1], res[1][1])
