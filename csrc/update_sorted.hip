@@ -421,14 +421,21 @@ template <typename XT, typename ACC, int VEC>
 int launch_segsum(const void* X, int64_t ldx, int D, const int32_t* perm, const int* offsets,
                   int K, int64_t N, void* sums, int num_cus, hipStream_t s) {
   const int lanes_needed = (D + VEC - 1) / VEC;
-  int64_t waves = (int64_t)num_cus * 32;  // ~8 resident 256-thread blocks per CU
-  int64_t rpw = (N + waves - 1) / waves;
-  if (rpw < 64) rpw = 64;  // small N (mini-batches, moved rows): keep ~8K waves in flight
-  waves = (N + rpw - 1) / rpw;
-  const dim3 grid((unsigned)((waves + 3) / 4));
+  (void)num_cus;
+  // every wave gets the same row count, so the grid is exactly the waves resident at once
+  // (8 blocks per CU asked for 8 waves per SIMD where the kernel fits 5: a second, partial
+  // round of blocks)
 #define TDC_SEG(TPRV)                                                                       \
-  hipLaunchKernelGGL((segsum_kernel<XT, ACC, VEC, TPRV>), grid, dim3(256), 0, s, (const XT*)X, \
-                     ldx, D, perm, offsets, K, N, (ACC*)sums, rpw)
+  do {                                                                                      \
+    static const int64_t res = resident_blocks(segsum_kernel<XT, ACC, VEC, TPRV>, 256);     \
+    int64_t waves = res * 4;                                                                \
+    int64_t rpw = (N + waves - 1) / waves;                                                  \
+    if (rpw < 64) rpw = 64; /* small N (mini-batches, moved rows) */                        \
+    waves = (N + rpw - 1) / rpw;                                                            \
+    const dim3 grid((unsigned)((waves + 3) / 4));                                           \
+    hipLaunchKernelGGL((segsum_kernel<XT, ACC, VEC, TPRV>), grid, dim3(256), 0, s,          \
+                       (const XT*)X, ldx, D, perm, offsets, K, N, (ACC*)sums, rpw);         \
+  } while (0)
   if (lanes_needed <= 4) TDC_SEG(4);
   else if (lanes_needed <= 8) TDC_SEG(8);
   else if (lanes_needed <= 16) TDC_SEG(16);
