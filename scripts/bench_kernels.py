@@ -72,8 +72,17 @@ def main():
         ms = timeit(lambda: ops.assign_bf16(loc.x, loc.cm2, loc.cnorm, labels, None))
         res["assign_ms"] = ms
         res["assign_tflops"] = 2.0 * a.n * a.k * loc.dp / ms / 1e9
+    if only is not None and "assign_idx" in only:
+        # cost of the point loads: the indexed kernel over rows in order, over a 4096-row
+        # (1 MiB, L2-resident) window, and over one row (timing only; labels are discarded)
+        for name, ri in (("arange", torch.arange(a.n, device=dev, dtype=torch.int32)),
+                         ("l2win", torch.arange(a.n, device=dev, dtype=torch.int32) % 4096),
+                         ("row0", torch.zeros(a.n, device=dev, dtype=torch.int32))):
+            ms = timeit(lambda: ops.assign_bf16_indexed(loc.x, ri, loc.cm2, loc.cnorm, labels,
+                                                        None))
+            res[f"assign_idx_{name}_ms"] = ms
     ops.assign_bf16(loc.x, loc.cm2, loc.cnorm, labels, None)
-    sums = torch.zeros(a.k, a.d, dtype=torch.float32, device=dev)
+    sums =torch.zeros(a.k, a.d, dtype=torch.float32, device=dev)
     counts = torch.zeros(a.k, dtype=torch.float32, device=dev)
     if only is None or "update" in only:
         up = NativeUpdate(ops, a.n, a.k, a.d, torch.bfloat16, dev)
