@@ -341,6 +341,10 @@ int dispatch_small(const void* X, int64_t N, int64_t ldx, int D, const void* C, 
     TDC_SMALL(32, 4, 1)
   } else {
     TDC_SMALL(16, 6, 1)
+    // fp64 K <= 16 x D <= 8 and K <= 32 x D <= 4: two lanes per row (a one-lane tile
+    // would hold 128 fp64 accumulators = 256 VGPRs)
+    TDC_SMALL(8, 8, 2)
+    TDC_SMALL(16, 4, 2)
   }
 #undef TDC_SMALL
   return (int)hipErrorInvalidValue;
@@ -350,7 +354,8 @@ int dispatch_small(const void* X, int64_t N, int64_t ldx, int D, const void* C, 
 
 int tdc_lloyd_small_supported(int dtype, int K, int D) {
   if (dtype == TDC_F32) return (K <= 16 && D <= 8) || (K <= 8 && D <= 16) || (K <= 32 && D <= 4);
-  if (dtype == TDC_F64) return (K <= 8 && D <= 8) || (K <= 16 && D <= 6) || (K <= 4 && D <= 16);
+  if (dtype == TDC_F64)
+    return (K <= 16 && D <= 8) || (K <= 4 && D <= 16) || (K <= 32 && D <= 4);
   return 0;
 }
 
@@ -573,9 +578,11 @@ int launch_update(const void* X, int64_t N, int64_t ldx, int D, int DS, const in
   if (chunks < 1) chunks = 1;
   const int64_t rpb = (N + chunks - 1) / chunks;
   chunks = (N + rpb - 1) / rpb;
-  if (lds > 64 * 1024)
-    hipFuncSetAttribute((const void*)update_lds_kernel<XT, ACC, VEC>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute((const void*)update_lds_kernel<XT, ACC, VEC>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
   hipLaunchKernelGGL((update_lds_kernel<XT, ACC, VEC>), dim3((unsigned)(chunks * nslices)),
                      dim3(256), lds, s, (const XT*)X, N, ldx, D, DS, labels, K, (ACC*)sums,
                      (ACC*)counts, nslices, rpb);
