@@ -81,7 +81,7 @@ int tdc_assign_mfma_bf16(const void* X, int64_t N, int64_t ldx, int DP, const vo
                        c, cnorm, Kp / (16 * QTV), labels, mind);                                   \
   }
     TDC_R3(4, 4, 2, 3) TDC_R3(4, 4, 8, 2) TDC_R3(4, 2, 4, 3) TDC_R3(4, 8, 4, 3)
-    TDC_R3(8, 4, 4, 3) TDC_R3(4, 4, 4, 2) TDC_R3(4, 4, 2, 4)
+    TDC_R3(8, 4, 4, 3) TDC_R3(4, 4, 4, 2) TDC_R3(4, 4, 2, 4) TDC_R3(6, 4, 4, 3)
 #undef TDC_R3
     TDC_CHECK_LAUNCH();
     return 0;

@@ -593,7 +593,7 @@ void assign_mfma_bf16_ring2_kernel(const __bf16* __restrict__ X, int64_t N, int6
 // TOP2: also track the second-smallest distance (mind2): one v_med3 + one v_min per
 // score instead of half a v_min3 (bounds-based pruning, models/bounded.py).
 template <int DP, int P, int NST, int WAVES, int QT, bool TOP2 = false>
-__global__ __launch_bounds__(WAVES * 64, (WAVES % 4 == 0 ? (WAVES / 4 > 1 ? WAVES / 4 : 3) : 2))
+__global__ __launch_bounds__(WAVES * 64, (WAVES == 6 ? 3 : (WAVES % 4 == 0 ? (WAVES / 4 > 1 ? WAVES / 4 : 3) : 2)))
 void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
                                    const __bf16* __restrict__ Cm2, const float* __restrict__ cnorm,
                                    int ntiles, int32_t* __restrict__ labels,
@@ -607,11 +607,15 @@ void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int6
   constexpr int NORM_B = BNL * 4;
   constexpr int STAGE_B = TILE_B + NORM_B;
   constexpr int PIECES = TILE_B / 1024;
-  constexpr int PPW = PIECES / WAVES;
+  // pieces / norm chunks per wave, rounded up: with a wave count that does not divide
+  // them (6 waves) the last waves re-load pieces another wave also loads (identical bytes
+  // to the same LDS slot), so every wave issues the same VPS DMAs per stage and the
+  // stage-end vmcnt wait is exact for all of them
+  constexpr int PPW = (PIECES + WAVES - 1) / WAVES;
   constexpr int NCH = NORM_B / 16;
-  constexpr int NPW = NCH / WAVES;
+  constexpr int NPW = (NCH + WAVES - 1) / WAVES;
   constexpr int VPS = PPW + 1;
-  static_assert(PIECES % WAVES == 0 && NCH % WAVES == 0 && NPW >= 1, "stage split");
+  static_assert(NPW >= 1 && NPW <= NCH && PPW >= 1, "stage split");
   static_assert(KS >= 1, "DP >= 32");
   constexpr unsigned EMB = QT * 4 <= 16 ? 15u : 31u;  // (q, reg) id bits in the mantissa
   __shared__ __attribute__((aligned(16))) char smem[NST * STAGE_B];
@@ -658,7 +662,7 @@ void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int6
   auto issue = [&](int t, int slot) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
-      const int piece = w * PPW + i;
+      const int piece = (w * PPW + i) % PIECES;
       const int L = piece * 64 + lane;
       const int row = L / CPR, cp = L % CPR;
       const int csrc = swz<DP>(row, cp);
@@ -667,11 +671,13 @@ void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int6
           (const void*)src,
           (__attribute__((address_space(3))) void*)(smem + slot * STAGE_B + piece * 1024), 16, 0, 0);
     }
+    // contiguous chunk run per wave (the DMA writes lane l at base + 16 l)
+    const int nb = w * NPW < NCH - NPW ? w * NPW : NCH - NPW;
     if (lane < NPW) {
-      const float* src = cnorm + (int64_t)t * BNL + (w * NPW + lane) * 4;
+      const float* src = cnorm + (int64_t)t * BNL + (nb + lane) * 4;
       __builtin_amdgcn_global_load_lds(
           (const void*)src,
-          (__attribute__((address_space(3))) void*)(smem + slot * STAGE_B + TILE_B + w * NPW * 16),
+          (__attribute__((address_space(3))) void*)(smem + slot * STAGE_B + TILE_B + nb * 16),
           16, 0, 0);
     }
   };
