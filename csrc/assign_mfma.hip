@@ -48,19 +48,23 @@ int tdc_assign_mfma_bf16(const void* X, int64_t N, int64_t ldx, int DP, const vo
   static const int r2cfg = getenv("TDC_RING2_CFG") ? atoi(getenv("TDC_RING2_CFG")) : 0;
   if (DP == 128 && ring == 2 && r2cfg != 0) {  // schedule experiments: QT*10 + NST
     dim3 grid((unsigned)((N + 255) / 256));
+    bool launched = false;
 #define TDC_R2(QTV, NSTV)                                                                          \
   if (r2cfg == QTV * 10 + NSTV) {                                                                  \
     if (Kp % (32 * QTV) != 0) return (int)hipErrorInvalidValue;                                    \
+    launched = true;                                                                               \
     hipLaunchKernelGGL((assign_mfma_bf16_ring2_kernel<128, 2, NSTV, 4, QTV>), grid, dim3(256), 0,  \
                        stream, x, N, ldx, c, cnorm, Kp / (32 * QTV), labels, mind);                \
   }
     TDC_R2(2, 4) TDC_R2(1, 4) TDC_R2(1, 5) TDC_R2(1, 6) TDC_R2(1, 3)
 #undef TDC_R2
+    if (!launched) return (int)hipErrorInvalidValue;
     TDC_CHECK_LAUNCH();
     return 0;
   }
   if (DP == 128 && ring == 2 && abl != 0) {  // timing ablations (tools only; results invalid)
     dim3 grid((unsigned)((N + 255) / 256));
+    if (abl != 1 && abl != 2 && abl != 4 && abl != 7 && abl != 8) return (int)hipErrorInvalidValue;
 #define TDC_ABL(A)                                                                                \
   if (abl == A)                                                                                   \
     hipLaunchKernelGGL((assign_mfma_bf16_ring2_kernel<128, 2, 3, 4, 2, A>), grid, dim3(256), 0,   \
@@ -72,17 +76,21 @@ int tdc_assign_mfma_bf16(const void* X, int64_t N, int64_t ldx, int DP, const vo
   }
   static const int r3cfg = getenv("TDC_RING3_CFG") ? atoi(getenv("TDC_RING3_CFG")) : 0;
   if (ring == 3 && DP == 128 && r3cfg != 0) {  // schedule experiments: WAVES*1000+P*100+QT*10+NST
+    bool launched = false;
 #define TDC_R3(WV, PV, QTV, NSTV)                                                                  \
   if (r3cfg == WV * 1000 + PV * 100 + QTV * 10 + NSTV) {                                           \
     if (Kp % (16 * QTV) != 0) return (int)hipErrorInvalidValue;                                    \
+    launched = true;                                                                               \
     const int64_t per = WV * PV * 16;                                                              \
     hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<128, PV, NSTV, WV, QTV>),                    \
                        dim3((unsigned)((N + per - 1) / per)), dim3(WV * 64), 0, stream, x, N, ldx, \
                        c, cnorm, Kp / (16 * QTV), labels, mind);                                   \
   }
-    TDC_R3(4, 4, 2, 3) TDC_R3(4, 4, 8, 2) TDC_R3(4, 2, 4, 3) TDC_R3(4, 8, 4, 3)
-    TDC_R3(8, 4, 4, 3) TDC_R3(4, 4, 4, 2) TDC_R3(4, 4, 2, 4) TDC_R3(6, 4, 4, 3)
+    TDC_R3(4, 4, 4, 3) TDC_R3(4, 4, 2, 3) TDC_R3(4, 4, 8, 2) TDC_R3(4, 2, 4, 3)
+    TDC_R3(4, 8, 4, 3) TDC_R3(8, 4, 4, 3) TDC_R3(4, 4, 4, 2) TDC_R3(4, 4, 2, 4)
+    TDC_R3(6, 4, 4, 3) TDC_R3(4, 8, 4, 2) TDC_R3(8, 8, 4, 2)
 #undef TDC_R3
+    if (!launched) return (int)hipErrorInvalidValue;  // not a compiled schedule: fail loudly
     TDC_CHECK_LAUNCH();
     return 0;
   }
@@ -100,10 +108,19 @@ int tdc_assign_mfma_bf16(const void* X, int64_t N, int64_t ldx, int DP, const vo
       else
         hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<64, 8, 3, 4, 4>), grid8, dim3(256), 0,
                            stream, x, N, ldx, c, cnorm, Kp / 64, labels, mind);
-    } else if (DP == 128)
+    } else if (DP == 128 && N >= (1 << 20)) {
+      // large shards: P=8 point tiles per wave (512 points per workgroup, 256 VGPRs, two
+      // waves per SIMD) halve the ring refill per point; NST=2.  1.93-1.95 -> 1.91 ms at
+      // the headline shape (profiles/assign_ring3_ablation_r02.txt).  Small launches keep
+      // P=4 (twice the workgroups for a short request).
+      const int64_t per8 = 4 * 8 * 16;
+      hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<128, 8, 2, 4, 4>),
+                         dim3((unsigned)((N + per8 - 1) / per8)), dim3(256), 0, stream, x, N, ldx,
+                         c, cnorm, Kp / 64, labels, mind);
+    } else if (DP == 128) {
       hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<128, 4, 3, 4, 4>), grid, dim3(256), 0,
                          stream, x, N, ldx, c, cnorm, Kp / 64, labels, mind);
-    else
+    } else
       hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<256, 4, 2, 4, 4>), grid, dim3(256), 0,
                          stream, x, N, ldx, c, cnorm, Kp / 64, labels, mind);
     TDC_CHECK_LAUNCH();

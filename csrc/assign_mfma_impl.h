@@ -593,7 +593,7 @@ void assign_mfma_bf16_ring2_kernel(const __bf16* __restrict__ X, int64_t N, int6
 // TOP2: also track the second-smallest distance (mind2): one v_med3 + one v_min per
 // score instead of half a v_min3 (bounds-based pruning, models/bounded.py).
 template <int DP, int P, int NST, int WAVES, int QT, bool TOP2 = false>
-__global__ __launch_bounds__(WAVES * 64, (WAVES == 6 ? 3 : (WAVES % 4 == 0 ? (WAVES / 4 > 1 ? WAVES / 4 : 3) : 2)))
+__global__ __launch_bounds__(WAVES * 64, ((DP >= 128 && P >= 8) ? 2 : WAVES == 6 ? 3 : (WAVES % 4 == 0 ? (WAVES / 4 > 1 ? WAVES / 4 : 3) : 2)))
 void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
                                    const __bf16* __restrict__ Cm2, const float* __restrict__ cnorm,
                                    int ntiles, int32_t* __restrict__ labels,

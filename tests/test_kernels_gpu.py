@@ -368,6 +368,32 @@ def test_indexed_assign_and_update(gpu, n, b, d, k):
     torch.testing.assert_close(s_i.double(), s_ref, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("d,k", [(128, 1024), (128, 64), (100, 300)])
+def test_assign_large_shard_tiles(gpu, d, k):
+    """Shards of >= 2^20 rows take the P=8 point-tile launch at D=128: labels and distances
+    equal the indexed (P=4) kernel's bit for bit, and the tail rows are at the fp64
+    oracle's (near-)minimum."""
+    import tensorflow_distributed_clustering_amd.ops as ops_mod
+    from tensorflow_distributed_clustering_amd import _native
+    ops = _native.require()
+    n = (1 << 20) + 12345
+    x, c = _bf16_case(n, d, k, gpu, seed=d + k)
+    lo = ops_mod.make_lloyd_ops(x, k, "bf16", "hip")
+    C = c.float().contiguous()
+    lo.prepare(C)
+    lab = torch.full((n,), -1, dtype=torch.int32, device=gpu)
+    md = torch.zeros(n, dtype=torch.float32, device=gpu)
+    ops.assign_bf16(lo.x, lo.cm2, lo.cnorm, lab, md)
+    idx = torch.arange(n, device=gpu, dtype=torch.int32)
+    lab_i = torch.full((n,), -1, dtype=torch.int32, device=gpu)
+    md_i = torch.zeros(n, dtype=torch.float32, device=gpu)
+    ops.assign_bf16_indexed(lo.x, idx, lo.cm2, lo.cnorm, lab_i, md_i)
+    assert torch.equal(lab, lab_i)
+    assert torch.equal(md, md_i)
+    sl = slice(n - 30000, n)
+    _check_labels(x[sl].double(), C.to(torch.bfloat16).double(), lab[sl])
+
+
 @pytest.mark.parametrize("cdt", [torch.float32, torch.float64])
 def test_sculley_update(gpu, cdt):
     from tensorflow_distributed_clustering_amd import _native
