@@ -154,7 +154,7 @@ class OomGuard:
         skip = (not self.warmup_ok or self.streamed or getattr(self, "rsag", False)
                 or getattr(self, "_graph", None) is not None
                 or (self.device.type != "cuda" and not force))
-        if self.comm.world_size > 1:
+        if self.comm.collective:
             # the step is collective: warm up only if every rank can (a rank whose planner
             # chose streaming would otherwise leave the others waiting in the all-reduce)
             skip = self.comm.max_scalar(1.0 if skip else 0.0) > 0.0
@@ -309,7 +309,7 @@ class LloydEngine(OomGuard):
     RSAG_MIN_BYTES = 32 << 20
 
     def _use_rsag(self, comm: Comm, cfg: ClusterConfig, sums_bytes: int) -> bool:
-        if comm.world_size <= 1 or not self.rsag_ok:
+        if not comm.collective or not self.rsag_ok:
             return False
         if cfg.comm_mode == "rsag":
             return True
@@ -447,8 +447,9 @@ class LloydEngine(OomGuard):
         graph capture requires."""
         if not self.graphable():
             raise RuntimeError("this engine configuration cannot be captured")
-        if self.comm.world_size > 1 and not include_collectives:
-            raise RuntimeError("capture with world_size > 1 needs include_collectives=True")
+        if self.comm.collective and not include_collectives:
+            raise RuntimeError("capture with collectives (world_size > 1 or forced) needs "
+                               "include_collectives=True")
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         snapshot = (self.C.clone(), self.n_iter)
@@ -647,7 +648,7 @@ class KMeans:
         first = [first]  # handed over: _build_engine drops it before any retry
         eng = self._build_engine(first, x_local, dev, comm, n_global, row_offset, n_local,
                                  init_centers_, start_iter)
-        if cfg.graph and eng.graphable() and comm.world_size == 1:
+        if cfg.graph and eng.graphable() and not comm.collective:
             eng.capture()
         if cfg.max_iter > eng.n_iter:
             eng.warmup()

@@ -57,13 +57,18 @@ class Comm:
     """Thin handle over the default process group (or a single-process no-op)."""
 
     def __init__(self, device: torch.device, rank: int = 0, world_size: int = 1,
-                 local_rank: int = 0, group=None, backend: str = ""):
+                 local_rank: int = 0, group=None, backend: str = "",
+                 force_collectives: bool = False):
         self.device = device
         self.backend = backend
         self.rank = rank
         self.world_size = world_size
         self.local_rank = local_rank
         self.group = group
+        # collectives are issued (not short-circuited) on more than one rank, or on a
+        # world-1 process group when forced: TDC_FORCE_COLLECTIVES=1 runs every RCCL call
+        # of the production path on a single GPU (tests/test_rccl_gpu.py)
+        self.collective = world_size > 1 or force_collectives
 
     # ------------------------------------------------------------------ props
     @property
@@ -79,7 +84,7 @@ class Comm:
 
     # ------------------------------------------------------------ collectives
     def allreduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
-        if self.world_size > 1:
+        if self.collective:
             rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
                    "min": dist.ReduceOp.MIN}[op]
             dist.all_reduce(t, op=rop, group=self.group)
@@ -97,7 +102,7 @@ class Comm:
         buffer); the large-K*D bandwidth win is :meth:`reduce_scatter_` +
         :meth:`all_gather_` (``ClusterConfig.comm_mode='rsag'``).
         """
-        if self.world_size <= 1:
+        if not self.collective:
             return flat
         nbytes = flat.numel() * flat.element_size()
         if bucket_bytes <= 0 or nbytes <= bucket_bytes:
@@ -111,7 +116,7 @@ class Comm:
     def reduce_scatter_(self, out: torch.Tensor, flat: torch.Tensor) -> torch.Tensor:
         """SUM reduce-scatter: rank r receives block r of ``flat`` (``flat.numel() ==
         world * out.numel()``), summed over ranks."""
-        if self.world_size <= 1:
+        if not self.collective:
             out.copy_(flat.view_as(out))
             return out
         dist.reduce_scatter_tensor(out, flat, group=self.group)
@@ -120,7 +125,7 @@ class Comm:
     def all_gather_(self, out: torch.Tensor, part: torch.Tensor) -> torch.Tensor:
         """``out`` = concatenation over ranks of ``part`` (``out.numel() == world *
         part.numel()``; ``part`` must not alias ``out``)."""
-        if self.world_size <= 1:
+        if not self.collective:
             out.copy_(part.view_as(out))
             return out
         if out.dtype in (torch.float8_e4m3fn, torch.float8_e5m2):
@@ -130,33 +135,33 @@ class Comm:
         return out
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
-        if self.world_size > 1:
+        if self.collective:
             dist.broadcast(t, src=src, group=self.group)
         return t
 
     def barrier(self):
-        if self.world_size > 1:
+        if self.collective:
             if self.device.type == "cuda" and self.backend == "nccl":
                 dist.barrier(group=self.group, device_ids=[self.device.index])
             else:
                 dist.barrier(group=self.group)
 
     def max_scalar(self, v: float) -> float:
-        if self.world_size <= 1:
+        if not self.collective:
             return v
         t = torch.tensor([v], dtype=torch.float64, device=self.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return float(t.item())
 
     def sum_scalar(self, v: float) -> float:
-        if self.world_size <= 1:
+        if not self.collective:
             return v
         t = torch.tensor([v], dtype=torch.float64, device=self.device)
         dist.all_reduce(t, group=self.group)
         return float(t.item())
 
     def all_gather_sizes(self, n_local: int) -> List[int]:
-        if self.world_size <= 1:
+        if not self.collective:
             return [n_local]
         t = torch.zeros(self.world_size, dtype=torch.int64, device=self.device)
         t[self.rank] = n_local
@@ -165,7 +170,7 @@ class Comm:
 
     def gather_rows_to_root(self, local: torch.Tensor) -> Optional[torch.Tensor]:
         """Concatenate every rank's rows on rank 0 (variable sizes; for outputs only)."""
-        if self.world_size <= 1:
+        if not self.collective:
             return local
         sizes = self.all_gather_sizes(local.shape[0])
         mx = max(sizes)
@@ -218,7 +223,8 @@ def init_comm(device_type: Optional[str] = None, timeout_s: float = 600.0,
     # TDC_DIST_BACKEND=gloo runs GPU ranks over gloo (host-staged collectives): rehearses the
     # multi-rank GPU path with several ranks on ONE GPU, which RCCL does not allow
     backend = os.environ.get("TDC_DIST_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
-    if world > 1 and not dist.is_initialized():
+    force = os.environ.get("TDC_FORCE_COLLECTIVES", "0") == "1"
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = dict(backend=backend, init_method="env://", world_size=world, rank=rank,
                   timeout=datetime.timedelta(seconds=timeout_s))
@@ -227,7 +233,8 @@ def init_comm(device_type: Optional[str] = None, timeout_s: float = 600.0,
         dist.init_process_group(**kw)
     if dist.is_initialized():
         backend = str(dist.get_backend())
-    _COMM = Comm(device, rank, world, local_rank, group, backend if world > 1 else "")
+    _COMM = Comm(device, rank, world, local_rank, group,
+                 backend if (world > 1 or force) else "", force_collectives=force)
     return _COMM
 
 

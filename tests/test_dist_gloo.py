@@ -294,3 +294,19 @@ def test_warmup_is_skipped_on_every_rank_when_one_rank_streams():
         assert p.exitcode == 0
     assert res[0][0] and res[1][0]
     np.testing.assert_array_equal(res[0][1], res[1][1])
+
+
+def test_forced_collectives_world1_equals_local(monkeypatch):
+    """TDC_FORCE_COLLECTIVES=1: a world-1 process group that issues every collective (the
+    single-GPU RCCL rehearsal of tests/test_rccl_gpu.py) gives the no-group result; rsag
+    engages at world 1 only when forced."""
+    c0, l0, in0, it0, i0, f0 = run_world(1, extra={"comm_mode": "rsag"})
+    monkeypatch.setenv("TDC_FORCE_COLLECTIVES", "1")
+    c1, l1, in1, it1, i1, f1 = run_world(1)
+    np.testing.assert_array_equal(c1, c0)
+    np.testing.assert_array_equal(l1, l0)
+    assert it1 == it0
+    c2, l2, _, _, _, f2 = run_world(1, extra={"comm_mode": "rsag"})
+    assert f2["rsag"] and not f0["rsag"]
+    np.testing.assert_allclose(c2, c0, rtol=1e-12, atol=1e-12)
+    np.testing.assert_array_equal(l2, l0)
