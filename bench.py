@@ -229,6 +229,8 @@ def main(argv=None):
             out["config"]["fuzzifier"] = a.fuzzifier if a.fuzzifier is not None else a.dim
             out["active_frac_last_step"] = getattr(eng, "active_frac", None)
         print(json.dumps(out), flush=True)
+    from tensorflow_distributed_clustering_amd.parallel.dist import destroy_comm
+    destroy_comm()  # a clean process-group teardown (RCCL warns otherwise)
 
 
 def host_shard(a, n_rows, row_offset, dev, torch):

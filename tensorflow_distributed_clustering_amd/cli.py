@@ -337,7 +337,14 @@ def main(argv=None) -> int:
         return subprocess.call(cmd, env=env)
     if _under_launcher() and int(os.environ["WORLD_SIZE"]) != args.n_GPUs:
         parser.error("WORLD_SIZE does not match --n_GPUs")
-    return run(args)
+    try:
+        return run(args)
+    finally:
+        # tear the process group down before interpreter exit: a gloo group left to the
+        # exit-time destructors intermittently aborted rank 0 ("terminate called without
+        # an active exception") after its outputs were written
+        from .parallel.dist import destroy_comm
+        destroy_comm()
 
 
 if __name__ == "__main__":
