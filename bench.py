@@ -1,16 +1,22 @@
 #!/usr/bin/env python3
-"""Flagship benchmark: distributed Lloyd K-Means, N=10M points per GPU, D=128, K=1024, bf16.
+"""Flagship benchmark: distributed Lloyd K-Means, N=10M points, D=128, K=1024, bf16.
 
-Metric (BASELINE.json): points assigned / s (whole job) and iters / s.  One *step* is one
-full Lloyd iteration on every rank: bf16 MFMA distance + fused argmin (HIP), LDS centroid
-update (HIP), ONE packed RCCL all-reduce of [sums | counts], centroid finalize (HIP).
-Nothing is skipped inside the timed region.
+Metric (BASELINE.json): points assigned / s (whole job) and iters / s of "K-Means N=10M
+D=128 K=1024 at 1/2/4/8 MI355X".  One *step* is one full Lloyd iteration on every rank:
+bf16 MFMA distance + fused argmin (HIP), LDS centroid update (HIP), ONE packed RCCL
+all-reduce of [sums | counts], centroid finalize (HIP).  Nothing is skipped inside the
+timed region.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N
 
 Data: synthetic Gaussian blobs generated on each GPU (counter-based, world-size
-invariant), random-row centroid init.  Weak scaling: each GPU owns ``--n-per-gpu`` points.
+invariant), random-row centroid init.  The default ``headline`` preset is STRONG scaling:
+N = 10M points in total, split over the ranks (1.25M rows per GPU at N=8), exactly the
+BASELINE.json metric; ``headline_weak`` keeps 10M points per GPU.  ``--n-per-gpu`` is the
+rows per GPU under ``--scaling weak`` and the TOTAL rows under ``--scaling strong``.  At
+world > 1 the JSON carries ``phase_ms`` (assign / update / all-reduce / finalize device
+time of one step, max over ranks).
 ``vs_baseline`` compares only like with like: it is set for the reference's own configs
 (``--preset ref25m_kmeans`` / ``ref25m_fcm``: N=25M, D=5, K=3, fp64) against the
 executions_log.csv row with the same method and GPU count, and is null otherwise -- the
@@ -38,7 +44,8 @@ REF25M_K3 = {
 
 # BASELINE.json configs (the default is the headline metric/config)
 PRESETS = {
-    "headline": dict(n_per_gpu=10_000_000, dim=128, k=1024, scaling="weak", mode="lloyd"),
+    "headline": dict(n_per_gpu=10_000_000, dim=128, k=1024, scaling="strong", mode="lloyd"),
+    "headline_weak": dict(n_per_gpu=10_000_000, dim=128, k=1024, scaling="weak", mode="lloyd"),
     "dp100m": dict(n_per_gpu=100_000_000, dim=128, k=1024, scaling="strong", mode="lloyd"),
     "minibatch1b": dict(n_per_gpu=1_000_000_000, dim=64, k=4096, scaling="strong",
                         mode="minibatch", batch_size=1 << 20),
@@ -65,10 +72,13 @@ def parse(argv=None):
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--k", type=int, default=1024)
     ap.add_argument("--dtype", default="bf16", choices=["fp8", "bf16", "fp32", "fp64"])
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="strong: --n-per-gpu is the total N split over the ranks; weak: "
+                         "every rank owns --n-per-gpu rows")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--preset", default="headline", choices=sorted(PRESETS),
-                    help="BASELINE config: headline (N=10M/GPU D=128 K=1024, default), "
+                    help="BASELINE config: headline (N=10M total D=128 K=1024, strong "
+                         "scaling, default), headline_weak (10M per GPU), "
                          "dp100m (N=100M total), minibatch1b (mini-batch N=1B D=64 K=4096), "
                          "embed50m_fp8 (N=50M D=768 K=65536, fp8 block-scaled MFMA), "
                          "ref25m_kmeans / ref25m_fcm (the reference's own N=25M D=5 K=3 fp64)")
@@ -92,7 +102,10 @@ def parse(argv=None):
     ap.add_argument("--graph", action="store_true",
                     help="replay the step from a captured HIP graph (1 GPU; RCCL capture for N>1)")
     ap.add_argument("--profile-steps", action="store_true",
-                    help="print a per-phase breakdown after the timed region")
+                    help="add a per-phase breakdown (phase_ms) after the timed region "
+                         "(always on at world > 1)")
+    ap.add_argument("--centers-out", default=None,
+                    help="rank 0 writes the final centroids (.npy, fp64) here")
     a = ap.parse_args(argv)
     p = PRESETS[a.preset]
     given = set(x.split("=")[0].lstrip("-").replace("-", "_") for x in (argv or sys.argv[1:]))
@@ -190,8 +203,14 @@ def main(argv=None):
     ms = elapsed / max(1, a.steps) * 1e3
     pps = points_per_step * a.steps / elapsed
     breakdown = None
-    if a.profile_steps and dev.type == "cuda" and a.mode == "lloyd" and a.method == "kmeans":
+    if ((a.profile_steps or world > 1) and a.mode == "lloyd" and a.method == "kmeans"
+            and a.algorithm == "lloyd" and not getattr(eng, "streamed", False)):
         breakdown = phase_breakdown(eng, torch, dev)
+    if a.centers_out:
+        c = eng.centers() if hasattr(eng, "centers") else eng.C
+        if rank == 0:
+            import numpy as np
+            np.save(a.centers_out, c.double().cpu().numpy())
     if rank == 0:
         out = {
             "metric": "points_assigned_per_sec",
@@ -273,27 +292,52 @@ def vs_baseline(a, world, pps):
 
 
 def phase_breakdown(eng, torch, dev, reps: int = 5):
-    """Per-phase device time of one step (events; diagnostic only, after the timed run)."""
+    """Per-phase time of one step, max over ranks (diagnostic, after the timed run; the
+    phases run eagerly with an event -- or a host clock on CPU -- between them, so their
+    sum is a little above a graph-replayed step).  The all-reduce phase includes the
+    wait for the slowest rank.  rsag engines: "allreduce" is reduce-scatter + all-gather."""
     from tensorflow_distributed_clustering_amd.ops import NativeUpdate
-    ev = lambda: torch.cuda.Event(enable_timing=True)
+    cuda = dev.type == "cuda"
+    if cuda:
+        mark = lambda: torch.cuda.Event(enable_timing=True)
+    else:
+        mark = lambda: None
     names = ["zero", "assign", "update", "allreduce", "finalize"]
     tot = {n: 0.0 for n in names}
     loc = eng.local
+    c_keep = eng.C.clone()
+    eng.comm.barrier()
     for _ in range(reps):
-        e = [ev() for _ in range(len(names) + 1)]
-        e[0].record()
-        eng.buf.zero_(); e[1].record()
+        e, t = [], []
+
+        def rec():
+            ev = mark()
+            if ev is not None:
+                ev.record()
+            e.append(ev)
+            t.append(time.perf_counter())
+        rec()
+        eng.buf.zero_(); rec()
         if isinstance(getattr(loc, "update", None), NativeUpdate):
-            loc.assign(eng.C, eng.labels, None); e[2].record()
-            loc.update(loc.x, eng.labels, eng.sums, eng.counts); e[3].record()
+            loc.assign(eng.C, eng.labels, None); rec()
+            loc.update(loc.x, eng.labels, eng.sums, eng.counts); rec()
         else:
-            loc.step(eng.C, eng.labels, None, eng.sums, eng.counts); e[2].record(); e[3].record()
-        eng.comm.allreduce_bucketed_(eng.buf, eng.bucket_bytes); e[4].record()
-        loc.finalize(eng.sums, eng.counts, eng.C, None); e[5].record()
-        torch.cuda.synchronize(dev)
+            loc.step(eng.C, eng.labels, None, eng.sums, eng.counts); rec(); rec()
+        if getattr(eng, "rsag", False):
+            eng._reduce_scatter_finalize(); rec(); rec()
+        else:
+            eng.comm.allreduce_bucketed_(eng.buf, eng.bucket_bytes); rec()
+            loc.finalize(eng.sums, eng.counts, eng.C, None); rec()
+        if cuda:
+            torch.cuda.synchronize(dev)
         for i, n in enumerate(names):
-            tot[n] += e[i].elapsed_time(e[i + 1]) / reps
-    return {k: round(v, 4) for k, v in tot.items()}
+            dt = e[i].elapsed_time(e[i + 1]) if cuda else (t[i + 1] - t[i]) * 1e3
+            tot[n] += dt / reps
+    eng.C.copy_(c_keep)  # leave the engine as the timed run left it
+    loc.prepare(eng.C)
+    vals = torch.tensor([tot[n] for n in names], dtype=torch.float64, device=dev)
+    eng.comm.allreduce_(vals, "max")
+    return {n: round(float(v), 4) for n, v in zip(names, vals.tolist())}
 
 
 if __name__ == "__main__":

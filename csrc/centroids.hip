@@ -113,6 +113,7 @@ int launch_finalize(const void* sums, const void* counts, int K, int D, void* C,
                     float* shift, void* Cm2, float* cnorm, int Kp, int DP, hipStream_t s,
                     float* drift, float* maxdrift) {
   const int rows = Cm2 ? (Kp > K ? Kp : K) : K;
+  if (rows <= 0) return 0;  // an rsag rank with no centroid rows of its own: nothing to do
   const int blocks = std::min((rows + 3) / 4, MAX_BLOCKS);
   hipLaunchKernelGGL((finalize_kernel<ACC, CT>), dim3((unsigned)blocks), dim3(256), 0,
                      s, (const ACC*)sums, (const ACC*)counts, K, D, (CT*)C, policy, shift,

@@ -5,8 +5,8 @@
 // A RowStreamer reads row ranges of a host matrix (typically a memory-mapped .npy member
 // of the input NPZ, float64 or float32, any row stride) and converts them -- in a pool of
 // worker threads, off the Python thread -- into a caller-owned destination buffer
-// (typically a pinned tensor) in the kernel layout: bf16 or fp32, zero-padded to `dp`
-// columns.  submit() is asynchronous; wait() blocks until that slot is filled.  The
+// (typically a pinned tensor) in the kernel layout: bf16, fp32 or fp64, zero-padded to
+// `dp` columns.  submit() is asynchronous; wait() blocks until that slot is filled.  The
 // Python side (data/stream.py) rings these pinned slots and overlaps their H2D copies with
 // compute on a separate HIP stream.
 #include <torch/custom_class.h>
@@ -41,7 +41,8 @@ class RowStreamer : public torch::CustomClassHolder {
     TORCH_CHECK(start >= 0 && rows >= 0 && start + rows <= core_->rows(),
                 "RowStreamer: range out of bounds");
     TORCH_CHECK((core_->dst_type() == tdc::DST_BF16 && dst.scalar_type() == at::kBFloat16) ||
-                    (core_->dst_type() == tdc::DST_F32 && dst.scalar_type() == at::kFloat),
+                    (core_->dst_type() == tdc::DST_F32 && dst.scalar_type() == at::kFloat) ||
+                    (core_->dst_type() == tdc::DST_F64 && dst.scalar_type() == at::kDouble),
                 "RowStreamer: dst dtype mismatch");
     return core_->submit(dst.data_ptr(), start, rows);
   }

@@ -1,7 +1,8 @@
 // Torch-free core of the native host-side row streamer (see loader.cpp for the role it
 // plays): a pool of worker threads converting row ranges of a host matrix (f64 / f32, any
-// row stride) into a caller-owned buffer in the kernel layout (bf16 RNE or f32, zero-padded
-// to dp columns).  submit() is asynchronous and returns a ticket; wait(ticket) blocks until
+// row stride) into a caller-owned buffer in the kernel layout (bf16 RNE, f32 or f64,
+// zero-padded to dp columns; f64 -> f64 is a row copy, so the exact fp64 kernels stream
+// through the same pinned ring as the bf16 ones).  submit() is asynchronous and returns a ticket; wait(ticket) blocks until
 // every piece of that submission is converted.  Kept free of torch so the thread pool can
 // be built and stress-tested on its own under ThreadSanitizer / AddressSanitizer
 // (tests/native/row_streamer_test.cpp, tests/test_native_sanitizers.py).
@@ -30,7 +31,7 @@ inline uint16_t f32_to_bf16_rne(float f) {
 }
 
 enum SrcType { SRC_F64 = 0, SRC_F32 = 1 };
-enum DstType { DST_BF16 = 0, DST_F32 = 1 };
+enum DstType { DST_BF16 = 0, DST_F32 = 1, DST_F64 = 2 };
 
 class RowStreamerCore {
  public:
@@ -41,8 +42,8 @@ class RowStreamerCore {
     if (src == nullptr) throw std::invalid_argument("RowStreamer: null source");
     if (src_type != SRC_F64 && src_type != SRC_F32)
       throw std::invalid_argument("RowStreamer: src must be f64/f32");
-    if (dst_type != DST_BF16 && dst_type != DST_F32)
-      throw std::invalid_argument("RowStreamer: dst must be bf16/f32");
+    if (dst_type != DST_BF16 && dst_type != DST_F32 && dst_type != DST_F64)
+      throw std::invalid_argument("RowStreamer: dst must be bf16/f32/f64");
     if (dp < n_cols) throw std::invalid_argument("RowStreamer: padded width smaller than the row");
     const int64_t nt = n_threads > 0 ? n_threads : 4;
     for (int64_t i = 0; i < nt; ++i) workers_.emplace_back([this] { loop(); });
@@ -106,6 +107,15 @@ class RowStreamerCore {
           for (int64_t c = 0; c < n_cols_; ++c) drow[c] = f32_to_bf16_rne(s[c]);
         }
         for (int64_t c = n_cols_; c < dp_; ++c) drow[c] = 0;
+      } else if (dst_type_ == DST_F64) {
+        double* drow = reinterpret_cast<double*>(out) + (size_t)r * dp_;
+        if (src_type_ == SRC_F64) {
+          std::memcpy(drow, srow, (size_t)n_cols_ * 8);
+        } else {
+          const float* s = reinterpret_cast<const float*>(srow);
+          for (int64_t c = 0; c < n_cols_; ++c) drow[c] = (double)s[c];
+        }
+        for (int64_t c = n_cols_; c < dp_; ++c) drow[c] = 0.0;
       } else {
         float* drow = reinterpret_cast<float*>(out) + (size_t)r * dp_;
         if (src_type_ == SRC_F64) {

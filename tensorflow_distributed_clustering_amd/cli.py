@@ -168,6 +168,10 @@ def build_parser():
     parser.add_argument("--algorithm", default="lloyd", choices=["lloyd", "bounded"],
                         help="bounded: exact Lloyd that re-assigns only the rows its Hamerly "
                              "bounds cannot settle (resident bf16 MFMA path)")
+    parser.add_argument("--no_warmup", action="store_true",
+                        help="time the first iteration too (the reference's computation_time "
+                             "includes its first sess.run); by default one discarded step "
+                             "runs before the timer, its first-launch cost counted in setup_time")
     parser.add_argument("--num_batches", type=int, default=1,
                         help="reference batch mode: cluster N array_split batches independently, "
                              "sum the phase times and average the centers (default 1: one "
@@ -234,7 +238,7 @@ def run(args) -> int:
                             hbm_budget_gb=args.hbm_budget_gb, deterministic=args.deterministic,
                             graph=args.graph, log_every=args.log_every,
                             spherical=args.spherical, algorithm=args.algorithm,
-                            fp8_recheck=args.fp8_recheck)
+                            fp8_recheck=args.fp8_recheck, warmup=not args.no_warmup)
 
         def make_model():
             if args.method_name == "distributedKMeans":
@@ -307,6 +311,7 @@ def run(args) -> int:
                         "n_iter": n_iter, "computation_time": comp, "backend": result.backend,
                         "points_per_sec": result.n_global * n_iter / comp if comp > 0 else None,
                         "iters_per_sec": n_iter / comp if comp > 0 else None,
+                        "warmup_step": not args.no_warmup,
                         "inertia": result.inertia, "history": result.history}) + "\n")
         print("log_file =", args.log_file)
     return status

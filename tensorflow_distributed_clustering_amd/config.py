@@ -50,6 +50,16 @@ class ClusterConfig:
                     centroids and preps their assign operands -> all-gather of the
                     operands), 'auto' (rsag when the sums buffer >= 32 MiB and G > 1)
     bucket_kb       split the all-reduce into calls of this many KiB (0: one call)
+    warmup          one discarded step before the timer starts (first-launch code-object
+                    load and grid sizing go to setup_time).  The reference's
+                    computation_time includes its first sess.run
+                    (`distribuitedClustering.py:164-166`): set False for like-for-like
+    kgroup_bytes    wide-D / fp8 assign: centroid bytes per K-group (0: one group)
+    kpp_max_k       init='kmeans++' above this K seeds with sampled k-means|| instead of
+                    greedy k-means++ (K dependent sweeps would take hours at K=65536)
+    kpp_sample_per_k greedy k-means++ runs on a uniform world-invariant sample of
+                    max(kpp_sample_min, kpp_sample_per_k * K) rows when N is over 4x that
+                    (0: always the full data).  The root rank logs whenever a sample is used.
     """
 
     n_clusters: int
@@ -80,6 +90,11 @@ class ClusterConfig:
     comm_mode: str = "auto"     # 'allreduce' | 'rsag' | 'auto' (parallel/dist.py)
     bucket_kb: int = 0          # all-reduce bucket size (0: one call per iteration)
     oom_recovery: bool = True   # mid-run OOM on any rank -> roll back one step, go streamed
+    warmup: bool = True         # discarded first step before the timed loop (see above)
+    kgroup_bytes: int = 0       # wide-D / fp8 assign K-group size in bytes (0: one group)
+    kpp_max_k: int = 2048       # greedy k-means++ up to this K, sampled k-means|| above
+    kpp_sample_per_k: int = 256 # greedy k-means++ sample rows per centre (0: full data)
+    kpp_sample_min: int = 50_000  # ... and at least this many rows
 
     def __post_init__(self):
         if self.n_clusters <= 0:

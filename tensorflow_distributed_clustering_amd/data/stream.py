@@ -5,7 +5,7 @@ already in the kernel layout (``layout = (torch dtype, padded width)``):
 
 * :class:`ResidentSource`  -- the shard is on the device; chunks are row views.
 * :class:`HostSource`      -- the shard is in host memory (numpy array / NPZ memory map).
-  A native :class:`RowStreamer` (csrc/loader.cpp) converts rows (f64/f32 -> bf16/f32,
+  A native :class:`RowStreamer` (csrc/loader.cpp) converts rows (f64/f32 -> bf16/f32/f64,
   zero-padded) into a ring of pinned buffers on worker threads; H2D copies run on a
   separate HIP stream into two device slots, so conversion, PCIe transfer and compute
   of consecutive chunks overlap.  This is what the reference attempted with
@@ -96,9 +96,10 @@ class HostSource:
         self.device = torch.device(device)
         self.row_offset = row_offset
         self.n_pinned = max(2, n_pinned)
-        dst_type = 0 if layout[0] == torch.bfloat16 else 1
-        if layout[0] not in (torch.bfloat16, torch.float32):
-            raise ValueError("HostSource streams to bf16 or fp32 layouts")
+        dst_codes = {torch.bfloat16: 0, torch.float32: 1, torch.float64: 2}
+        if layout[0] not in dst_codes:
+            raise ValueError("HostSource streams to bf16, fp32 or fp64 layouts")
+        dst_type = dst_codes[layout[0]]
         _native.require()
         ld = x_host.strides[0] // x_host.itemsize
         self.streamer = torch.classes.tdc.RowStreamer(
@@ -175,25 +176,16 @@ class HostSource:
         torch.cuda.current_stream(self.device).synchronize()
 
 
-class PlainHostSource:
-    """Host-resident shard streamed as plain row slices (any dtype, e.g. fp64 FCM, which
-    the bf16/fp32 RowStreamer does not produce): pinned staging + one H2D per chunk."""
+class PlainHostSource(HostSource):
+    """Host-resident fp32 / fp64 rows streamed as they are (no bf16 conversion): the same
+    pinned ring, worker-thread row copies and copy-stream H2D as :class:`HostSource`
+    (the fp64 kernels' layout is the source's own rows)."""
 
-    def __init__(self, x_host: np.ndarray, layout: Layout, device, row_offset: int = 0):
-        self.x = x_host
-        self.n_rows, self.d = x_host.shape
-        self.layout = layout
-        self.device = torch.device(device)
-        self.row_offset = row_offset
-
-    def chunks(self, chunk_rows: int) -> Iterator[Tuple[int, torch.Tensor]]:
-        chunk_rows = min(chunk_rows or self.n_rows, self.n_rows)
-        dt, width = self.layout
-        for s in range(0, self.n_rows, chunk_rows):
-            part = torch.from_numpy(np.ascontiguousarray(self.x[s:s + chunk_rows])).to(dt)
-            if self.device.type == "cuda":
-                part = part.pin_memory().to(self.device, non_blocking=True)
-            yield self.row_offset + s, to_layout(part, (dt, width))
+    def __init__(self, x_host: np.ndarray, layout: Layout, device, row_offset: int = 0,
+                 n_pinned: int = 3, n_threads: int = 8, resident_rows: int = 0):
+        if layout[0] not in (torch.float32, torch.float64):
+            raise ValueError("PlainHostSource streams fp32 / fp64 rows")
+        super().__init__(x_host, layout, device, row_offset, n_pinned, n_threads, resident_rows)
 
     def rows(self, idx: torch.Tensor) -> torch.Tensor:
         sel = torch.from_numpy(np.ascontiguousarray(self.x[idx.cpu().numpy()]))

@@ -49,7 +49,8 @@ def _shared_init(model, x_batch0: torch.Tensor, row_offset: int, n_batch0: int) 
     dev = comm.device
     method = cfg.init if cfg.init != "given" else "first_k"
     c = init_centers(method, x_batch0.to(dev), row_offset, n_batch0, cfg.n_clusters, comm,
-                     cfg.seed)
+                     cfg.seed, kpp_max_k=cfg.kpp_max_k, kpp_sample_per_k=cfg.kpp_sample_per_k,
+                     kpp_sample_min=cfg.kpp_sample_min)
     return c.double().cpu().numpy()
 
 

@@ -17,21 +17,22 @@ reference doubled its batch count and restarted on ResourceExhaustedError, `:331
 from __future__ import annotations
 
 import time
+import weakref
 from typing import Optional
 
 import numpy as np
 import torch
 
 from ..config import ClusterConfig
-from ..data.stream import (HostSource, PlainHostSource, ResidentSource, plan_chunk_rows,
-                           plan_resident_rows)
+from ..data.stream import HostSource, ResidentSource, plan_chunk_rows, plan_resident_rows
 from ..ops import make_fcm_ops
 from ..parallel.dist import Comm, local_comm
 from ..utils import faults
 from ..utils.checkpoint import RunCheckpointer
 from ..utils.timers import DeviceTimer, sync
 from .init import init_centers, init_centers_from_source
-from .kmeans import ClusterResult, OomGuard, _shard_geometry
+from .kmeans import (ClusterResult, OomGuard, _release, _retry_chunk, _shard_geometry,
+                     build_engine_collective)
 
 
 def fcm_dtype(cfg: ClusterConfig) -> torch.dtype:
@@ -100,11 +101,15 @@ class FcmEngine(OomGuard):
         cfg = self.cfg
         if self._x0 is not None:
             c0 = init_centers(cfg.init, self._x0, self.row_offset, self.n_global, self.k,
-                              self.comm, cfg.seed, given=self._init_given)
+                              self.comm, cfg.seed, given=self._init_given,
+                              kpp_max_k=cfg.kpp_max_k, kpp_sample_per_k=cfg.kpp_sample_per_k,
+                              kpp_sample_min=cfg.kpp_sample_min)
         else:
             c0 = init_centers_from_source(cfg.init, self.source, self.row_offset, self.n_global,
                                           self.k, self.comm, cfg.seed, given=self._init_given,
-                                          d=self.d)
+                                          d=self.d, kpp_max_k=cfg.kpp_max_k,
+                                          kpp_sample_per_k=cfg.kpp_sample_per_k,
+                                          kpp_sample_min=cfg.kpp_sample_min)
         self.c0 = c0
         self.C.copy_(c0.to(self.local.c_dtype))
         self._x0 = None
@@ -174,7 +179,8 @@ class FuzzyCMeans:
 
     def _make_source(self, x_local, dev, row_offset, chunk_override: int = 0):
         """(source, chunk_rows): the resident shard, or a host source streamed in chunks
-        when it does not fit the HBM budget (or cfg.chunk_rows / an OOM retry asks)."""
+        (native RowStreamer, pinned ring, copy stream; fp32 or fp64 rows) when it does not
+        fit the HBM budget (or cfg.chunk_rows / an OOM retry asks)."""
         cfg = self.cfg
         want = chunk_override or cfg.chunk_rows
         if hasattr(x_local, "chunks"):
@@ -184,6 +190,7 @@ class FuzzyCMeans:
             return x_local.to(dev), want
         xn = x_local.numpy() if isinstance(x_local, torch.Tensor) else np.asarray(x_local)
         n, d = xn.shape
+        layout = (tdt, d)
         if dev.type == "cuda":
             es = 8 if tdt == torch.float64 else 4
             # MFMA tower keeps hi/lo bf16 rows + norms + row info next to the chunk
@@ -191,52 +198,22 @@ class FuzzyCMeans:
             chunk = want or plan_chunk_rows(n, row_bytes, cfg.n_clusters, d, dev,
                                             cfg.hbm_budget_gb)
             if chunk:
-                layout = (tdt, d)
-                if tdt == torch.float32:
-                    resident = 0 if want else plan_resident_rows(n, d * es, chunk, cfg.n_clusters,
-                                                                 d, dev, cfg.hbm_budget_gb)
-                    return HostSource(xn, layout, dev, row_offset, resident_rows=resident), chunk
-                return PlainHostSource(xn, layout, dev, row_offset), chunk
+                resident = 0 if want else plan_resident_rows(n, row_bytes, chunk, cfg.n_clusters,
+                                                             d, dev, cfg.hbm_budget_gb)
+                return HostSource(xn, layout, dev, row_offset, resident_rows=resident), chunk
         elif want:
-            return PlainHostSource(xn, (tdt, d), dev, row_offset), want
+            return HostSource(xn, layout, dev, row_offset), want
         return torch.as_tensor(xn).to(dev), want
 
-    def _build_engine(self, first, x_local, dev, comm, n_global, row_offset, n_local, init_c,
-                      start_iter, m):
-        """FcmEngine with the collective setup-OOM agreement (see KMeans._build_engine);
-        ``first`` is a one-element list that is emptied here."""
+    def _build_engine(self, x_local, dev, comm, n_global, row_offset, n_local, init_c,
+                      start_iter, m, chunk: int = 0):
+        """FcmEngine under the collective OOM agreement (see KMeans._build_engine)."""
         cfg = self.cfg
-        chunk = 0
-        err = None
-        for attempt in range(cfg.max_oom_retries + 1):
-            err = None
-            eng = source = None
-            try:
-                if first:
-                    source, chunk_rows = first.pop()
-                else:
-                    source, chunk_rows = self._make_source(x_local, dev, row_offset, chunk)
-                chunk = chunk_rows or chunk
-                faults.maybe_fail("setup", comm.rank)
-                eng = FcmEngine(source, cfg, comm, n_global, row_offset, init_c, m, chunk_rows,
-                                defer_init=True)
-            except Exception as e:  # noqa: BLE001 - filtered right below
-                if not faults.is_oom(e):
-                    raise
-                err = e
-            if comm.max_scalar(1.0 if err is not None else 0.0) == 0.0:
-                eng.init_centroids()
-                eng.n_iter = start_iter
-                return eng
-            del eng, source
-            if dev.type == "cuda":
-                torch.cuda.empty_cache()
-            chunk = max(1024, (chunk or n_local) // 2)
-            if comm.is_root:
-                print(f"[fcm] out of memory while building the engine "
-                      f"({type(err).__name__ if err else 'peer rank'}); retrying streamed with "
-                      f"chunk_rows={chunk}", flush=True)
-        raise err if err is not None else faults.oom_error("out of memory on a peer rank")
+        return build_engine_collective(
+            "fcm", cfg, comm, dev, n_local, start_iter, chunk,
+            lambda c: self._make_source(x_local, dev, row_offset, c),
+            lambda source, chunk_rows: FcmEngine(source, cfg, comm, n_global, row_offset, init_c,
+                                                 m, chunk_rows, defer_init=True))
 
     def fit(self, x_local, init_centers_=None, n_global=None, row_offset=None) -> "FuzzyCMeans":
         cfg = self.cfg
@@ -253,25 +230,21 @@ class FuzzyCMeans:
         d = int(x_local.d if hasattr(x_local, "d") else x_local.shape[1])
         if n_global is None or row_offset is None:
             n_global, row_offset = _shard_geometry(n_local, comm)
-        first = [self._make_source(x_local, dev, row_offset)]
-        sync(dev)
-        initialization_time = time.perf_counter() - t0
-
-        t1 = time.perf_counter()
         ckpt = RunCheckpointer(cfg, comm, "distributedFuzzyCMeans")
         resumed = ckpt.load_for_resume(cfg.n_clusters, d)
         start_iter = 0
         if resumed is not None:
             init_centers_, start_iter = resumed.centers, resumed.n_iter
         m = self.fuzzifier(d)
-        eng = self._build_engine(first, x_local, dev, comm, n_global, row_offset, n_local,
-                                 init_centers_, start_iter, m)
+        eng, initialization_time = self._build_engine(x_local, dev, comm, n_global, row_offset,
+                                                      n_local, init_centers_, start_iter, m)
         self.engine_ = eng
-        if cfg.max_iter > eng.n_iter:
+        if cfg.warmup and cfg.max_iter > eng.n_iter:
             eng.warmup()
         sync(dev)
-        setup_time = time.perf_counter() - t1
+        setup_time = time.perf_counter() - t0 - initialization_time
 
+        self._retired = []  # weak references to engines replaced after an OOM
         timer = DeviceTimer(dev)
         timer.start()
         history = []
@@ -282,17 +255,15 @@ class FuzzyCMeans:
                 if bad is not None:
                     c_host, c0 = eng.rollback(bad), eng.c0
                     n_back = eng.n_iter
-                    chunk = max(1024, (eng.chunk_rows or n_local) // 2)
-                    del eng
-                    self.engine_ = None
-                    if dev.type == "cuda":
-                        torch.cuda.empty_cache()
+                    chunk = _retry_chunk(eng.chunk_rows, n_local)
+                    self._retired.append(weakref.ref(eng))
+                    eng = self.engine_ = None
+                    _release(dev)
                     if comm.is_root:
                         print(f"[fcm] out of memory in iteration {n_back + 1}; continuing "
                               f"streamed with chunk_rows={chunk}", flush=True)
-                    eng = self._build_engine([self._make_source(x_local, dev, row_offset, chunk)],
-                                             x_local, dev, comm, n_global, row_offset, n_local,
-                                             c_host, n_back, m)
+                    eng, _ = self._build_engine(x_local, dev, comm, n_global, row_offset, n_local,
+                                                c_host, n_back, m, chunk)
                     eng.c0 = c0
                     self.engine_ = eng
                     continue

@@ -241,17 +241,17 @@ def weighted_kmeanspp(c: torch.Tensor, w: torch.Tensor, k: int, seed: int,
 
 
 # Greedy k-means++ is K dependent sweeps over the shard (~3 kernels + 4 small collectives
-# per centre); above this K, init='kmeans++' runs the sampled k-means|| below instead
-# (override: TDC_KPP_MAX_K).  K = 65536 greedy would be ~131K full sweeps -- hours.
-KPP_MAX_K = int(__import__("os").environ.get("TDC_KPP_MAX_K", 2048))
+# per centre); above ClusterConfig.kpp_max_k (default 2048), init='kmeans++' runs the
+# sampled k-means|| below instead.  K = 65536 greedy would be ~131K full sweeps -- hours.
+KPP_MAX_K = 2048
 # k-means|| on a uniform sample of this many rows per centre (sampled mode)
 KPAR_SAMPLE_PER_K = 8
-# greedy k-means++ sweeps a uniform sample of max(KPP_SAMPLE_MIN, KPP_SAMPLE_PER_K * K)
+# greedy k-means++ sweeps a uniform sample of max(KPP_SAMPLE_MIN, kpp_sample_per_k * K)
 # rows when the data has more than 4x that many (K sweeps of 100M rows at K = 1024 took
-# 76 s on one MI355X; of the 262K-row sample, well under a second).  TDC_KPP_SAMPLE=0:
-# always sweep the full shards.
+# 76 s on one MI355X; of the 262K-row sample, well under a second).
+# ClusterConfig.kpp_sample_per_k = 0: always sweep the full shards.
 KPP_SAMPLE_MIN = 50_000
-KPP_SAMPLE_PER_K = int(__import__("os").environ.get("TDC_KPP_SAMPLE", 256))
+KPP_SAMPLE_PER_K = 256
 # weighted k-means++ recluster up to this many centres; above it the K centres are drawn
 # from the candidates by weight without replacement (Python-level greedy is O(K) steps)
 RECLUSTER_MAX_K = 2048
@@ -311,9 +311,21 @@ def init_kmeans_parallel(x_local, row_offset, n_global, k, comm: Comm, seed,
     return weighted_kmeanspp(C, w, k, seed)
 
 
+def _note(comm: Comm, msg: str):
+    if comm.is_root:
+        print(f"[init] {msg}", flush=True)
+
+
 def init_centers(method: str, x_local: torch.Tensor, row_offset: int, n_global: int, k: int,
-                 comm: Comm, seed: int = 0, given: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """[K, D] float64 on the shard's device, identical on every rank."""
+                 comm: Comm, seed: int = 0, given: Optional[torch.Tensor] = None,
+                 kpp_max_k: int = KPP_MAX_K, kpp_sample_per_k: int = KPP_SAMPLE_PER_K,
+                 kpp_sample_min: int = KPP_SAMPLE_MIN) -> torch.Tensor:
+    """[K, D] float64 on the shard's device, identical on every rank.
+
+    init='kmeans++' is exact greedy k-means++ over all rows only while K <= kpp_max_k and
+    N <= 4 * max(kpp_sample_min, kpp_sample_per_k * K); otherwise it seeds on a uniform
+    world-invariant sample (greedy k-means++ on the sample, or sampled k-means|| above
+    kpp_max_k).  Either approximation is logged on the root rank."""
     if given is None and method != "given" and k > n_global:
         raise ValueError(f"K={k} is larger than the number of points N={n_global}")
     if given is not None or method == "given":
@@ -327,10 +339,12 @@ def init_centers(method: str, x_local: torch.Tensor, row_offset: int, n_global: 
         return init_random(x_local, row_offset, n_global, k, comm, seed)
     if method == "first_k":
         return init_first_k(x_local, row_offset, n_global, k, comm, seed)
-    if method == "kmeans++" and k <= KPP_MAX_K:
-        m = max(KPP_SAMPLE_MIN, KPP_SAMPLE_PER_K * k)
-        if KPP_SAMPLE_PER_K > 0 and n_global > 4 * m:
+    if method == "kmeans++" and k <= kpp_max_k:
+        m = max(kpp_sample_min, kpp_sample_per_k * k)
+        if kpp_sample_per_k > 0 and n_global > 4 * m:
             # world-invariant uniform sample, replicated; greedy seeding on it
+            _note(comm, f"kmeans++ seeds on a uniform sample of {m} of {n_global} rows "
+                        f"(kpp_sample_per_k={kpp_sample_per_k}; 0 = all rows)")
             idx = floyd_sample(n_global, m, seed + 1)
             xs = gather_global_rows(x_local, row_offset, idx, comm,
                                     dtype=torch.float32 if x_local.device.type == "cuda"
@@ -339,7 +353,10 @@ def init_centers(method: str, x_local: torch.Tensor, row_offset: int, n_global: 
             return init_kmeanspp(xs, 0, m, k, local_comm(xs.device), seed)
         return init_kmeanspp(x_local, row_offset, n_global, k, comm, seed)
     if method in ("kmeans++", "kmeans||"):
-        sample = KPAR_SAMPLE_PER_K * k if k > KPP_MAX_K else 0
+        sample = KPAR_SAMPLE_PER_K * k if k > kpp_max_k else 0
+        if sample and sample < n_global:
+            _note(comm, f"{method} with K={k} > kpp_max_k={kpp_max_k}: sampled k-means|| on "
+                        f"{sample} of {n_global} rows, centres drawn by cluster mass")
         return init_kmeans_parallel(x_local, row_offset, n_global, k, comm, seed,
                                     sample=min(sample, n_global) if sample else 0)
     raise ValueError(f"unknown init {method!r}")
@@ -381,7 +398,9 @@ def gather_rows_from_source(source, row_offset: int, idx, comm: Comm, d: int) ->
 
 def init_centers_from_source(method: str, source, row_offset: int, n_global: int, k: int,
                              comm: Comm, seed: int = 0, given=None, d: int = None,
-                             rows=None) -> torch.Tensor:
+                             rows=None, kpp_max_k: int = KPP_MAX_K,
+                             kpp_sample_per_k: int = KPP_SAMPLE_PER_K,
+                             kpp_sample_min: int = KPP_SAMPLE_MIN) -> torch.Tensor:
     """Init for streamed / generated shards (rows are gathered from the source).
 
     k-means++ on a source that is not device-resident runs on a uniform random sample of
@@ -402,9 +421,13 @@ def init_centers_from_source(method: str, source, row_offset: int, n_global: int
     if method == "first_k":
         return gather_rows_from_source(source, row_offset, range(k), comm, d)
     if method in ("kmeans++", "kmeans||"):
-        m = min(n_global, max(50_000, 256 * k))
+        m = min(n_global, max(kpp_sample_min, (kpp_sample_per_k or KPP_SAMPLE_PER_K) * k))
+        if m < n_global:
+            _note(comm, f"{method} on a streamed shard seeds on a uniform sample of {m} of "
+                        f"{n_global} rows")
         sample = gather_rows_from_source(source, row_offset, floyd_sample(n_global, m, seed + 1),
                                          comm, d)
         from ..parallel.dist import local_comm
-        return init_centers(method, sample, 0, m, k, local_comm(sample.device), seed)
+        return init_centers(method, sample, 0, m, k, local_comm(sample.device), seed,
+                            kpp_max_k=kpp_max_k, kpp_sample_per_k=0)
     raise ValueError(f"unknown init {method!r}")

@@ -23,8 +23,10 @@ the *final* centroids (what the reference returns as ``cluster_idx``) runs untim
 """
 from __future__ import annotations
 
+import gc
 import math
 import time
+import weakref
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -33,7 +35,7 @@ import torch
 
 from ..config import ClusterConfig
 from ..data.stream import HostSource, ResidentSource, plan_chunk_rows, plan_resident_rows
-from ..ops import acc_dtype_for, make_lloyd_ops, padded_dim
+from ..ops import acc_dtype_for, lloyd_layout, make_lloyd_ops
 from ..parallel.dist import Comm, join_counts, local_comm
 from ..utils import faults
 from ..utils.checkpoint import RunCheckpointer
@@ -64,6 +66,20 @@ class ClusterResult:
     @property
     def iters_per_sec(self) -> float:
         return self.n_iter / self.computation_time if self.computation_time > 0 else 0.0
+
+
+def _release(dev: torch.device):
+    """Return the memory of dropped engines / sources to the device before a retry
+    (reference cycles through exception frames are collected first)."""
+    gc.collect()
+    if dev.type == "cuda":
+        torch.cuda.empty_cache()
+
+
+def _retry_chunk(chunk: int, n_local: int) -> int:
+    """Streamed chunk rows after an OOM: half the previous chunk; from a resident shard,
+    a quarter of it (the stream holds two device slots, so they take half the shard)."""
+    return max(1024, (chunk or n_local // 2) // 2)
 
 
 def _shard_geometry(n_local: int, comm: Comm):
@@ -208,9 +224,7 @@ class LloydEngine(OomGuard):
                 source = (source.float() / n).to(source.dtype)
             x0 = source
             self.local = make_lloyd_ops(source, k, cfg.dtype, cfg.backend, cfg.empty_cluster,
-                                        cfg.deterministic)
-            if cfg.fp8_recheck > 0 and hasattr(self.local, "RECHECK_TAU"):
-                self.local.RECHECK_TAU = cfg.fp8_recheck
+                                        cfg.deterministic, cfg.kgroup_bytes, cfg.fp8_recheck)
             self.source = ResidentSource(self.local.x, self.local.layout, row_offset)
             self.local.x = self.source.x
             self.device = source.device
@@ -225,7 +239,7 @@ class LloydEngine(OomGuard):
             self.n_local = int(source.n_rows)
             probe = torch.zeros(1, self.d, dtype=torch.float32, device=self.device)
             self.local = make_lloyd_ops(probe, k, cfg.dtype, cfg.backend, cfg.empty_cluster,
-                                        cfg.deterministic)
+                                        cfg.deterministic, cfg.kgroup_bytes, cfg.fp8_recheck)
             if tuple(self.local.layout) != tuple(source.layout):
                 raise ValueError(f"source layout {source.layout} != kernel layout {self.local.layout}")
             x0 = None
@@ -335,10 +349,15 @@ class LloydEngine(OomGuard):
         cfg, comm, k = self.cfg, self.comm, self.k
         if self._x0 is not None:
             c0 = init_centers(cfg.init, self._x0, self.row_offset, self.n_global, k, comm,
-                              cfg.seed, given=self._init_given)
+                              cfg.seed, given=self._init_given, kpp_max_k=cfg.kpp_max_k,
+                              kpp_sample_per_k=cfg.kpp_sample_per_k,
+                              kpp_sample_min=cfg.kpp_sample_min)
         else:
             c0 = init_centers_from_source(cfg.init, self.source, self.row_offset, self.n_global,
-                                          k, comm, cfg.seed, given=self._init_given, d=self.d)
+                                          k, comm, cfg.seed, given=self._init_given, d=self.d,
+                                          kpp_max_k=cfg.kpp_max_k,
+                                          kpp_sample_per_k=cfg.kpp_sample_per_k,
+                                          kpp_sample_min=cfg.kpp_sample_min)
         if cfg.spherical:
             c0 = c0 / c0.norm(dim=1, keepdim=True).clamp_min(1e-30)
         self.c0 = c0
@@ -493,6 +512,52 @@ class LloydEngine(OomGuard):
         return self.comm.sum_scalar(float(self.mind.double().sum()))
 
 
+def build_engine_collective(tag: str, cfg: ClusterConfig, comm: Comm, dev, n_local: int,
+                            start_iter: int, chunk: int, make_source, make_engine):
+    """Build an engine with collective OOM handling; returns (engine, seconds spent in
+    ``make_source``, i.e. loading / uploading the shard).
+
+    The source (the device upload of a resident shard) is created inside the agreement:
+    if any rank runs out of memory while uploading or building, every rank frees what it
+    holds and retries with the shard streamed from host memory in halved chunks.  The
+    reference doubled its batch count on ResourceExhaustedError
+    (`scripts/distribuitedClustering.py:331-360`) but clustered the batches independently;
+    here the streamed pass is still the exact step.  ``chunk`` > 0 (a mid-run OOM retry)
+    streams from the start."""
+    t_src = 0.0
+    err = None
+    for attempt in range(cfg.max_oom_retries + 1):
+        err = None
+        eng = source = None
+        try:
+            faults.maybe_fail("setup", comm.rank)  # an injected OOM of the upload
+            t = time.perf_counter()
+            source, chunk_rows = make_source(chunk)
+            sync(dev)
+            t_src += time.perf_counter() - t
+            chunk = chunk_rows or chunk
+            eng = make_engine(source, chunk_rows)
+        except Exception as e:  # noqa: BLE001 - filtered right below
+            if not faults.is_oom(e):
+                raise
+            err = e
+        if err is not None:
+            # the traceback's frames hold the half-built engine and the device copy
+            err.__traceback__ = None
+        if comm.max_scalar(1.0 if err is not None else 0.0) == 0.0:
+            eng.init_centroids()
+            eng.n_iter = start_iter
+            return eng, t_src
+        del eng, source
+        _release(dev)
+        chunk = _retry_chunk(chunk, n_local)
+        if comm.is_root:
+            print(f"[{tag}] out of memory while building the engine "
+                  f"({type(err).__name__ if err else 'peer rank'}); retrying streamed with "
+                  f"chunk_rows={chunk}", flush=True)
+    raise err if err is not None else faults.oom_error("out of memory on a peer rank")
+
+
 class KMeans:
     """sklearn-like front end over the distributed engine.
 
@@ -530,100 +595,56 @@ class KMeans:
         return torch.device(getattr(x, "device", "cpu"))
 
     def _make_source(self, x_local, dev, row_offset, chunk_override: int = 0):
-        """(source, chunk_rows): resident tensor, or a HostSource when the shard stays on
-        the host (does not fit the HBM budget, or cfg.chunk_rows / an OOM retry forces
-        streaming)."""
+        """(source, chunk_rows): the resident device shard, or a HostSource when the shard
+        stays in host memory (it does not fit the HBM budget, or cfg.chunk_rows / an OOM
+        retry asks for streaming).  Every dtype streams: the native RowStreamer converts
+        host rows into the kernel layout (bf16 / fp32, or fp64 rows as they are) in a
+        pinned ring with H2D on a copy stream; the planner keeps the leading rows that fit
+        next to the streaming buffers resident."""
         cfg = self.cfg
         want = chunk_override or cfg.chunk_rows
         if hasattr(x_local, "chunks"):
             return x_local, want or (1 << 22)
         if isinstance(x_local, torch.Tensor) and x_local.device.type != "cpu":
+            # device data stays where the caller put it: a retry can only re-chunk it
             return x_local.to(dev), want
         xn = x_local.numpy() if isinstance(x_local, torch.Tensor) else np.asarray(x_local)
-        if dev.type == "cuda" and cfg.dtype in ("bf16", "fp32"):
+        if dev.type == "cuda" and cfg.backend != "torch":
             d = xn.shape[1]
-            width = padded_dim(d) if cfg.dtype == "bf16" else d
-            if width is not None:
-                es = 2 if cfg.dtype == "bf16" else 4
-                chunk = want or plan_chunk_rows(xn.shape[0], width * es, cfg.n_clusters, d, dev,
-                                                cfg.hbm_budget_gb)
-                if chunk:
-                    layout = (torch.bfloat16 if cfg.dtype == "bf16" else torch.float32, width)
-                    resident = 0
-                    if not want:  # planner-driven streaming: keep what fits in HBM resident
-                        resident = plan_resident_rows(xn.shape[0], width * es, chunk,
-                                                      cfg.n_clusters, d, dev, cfg.hbm_budget_gb)
-                    return HostSource(xn, layout, dev, row_offset, resident_rows=resident), chunk
+            layout = lloyd_layout(cfg.dtype, d)
+            es = torch.tensor([], dtype=layout[0]).element_size()
+            row_bytes = layout[1] * es
+            chunk = want or plan_chunk_rows(xn.shape[0], row_bytes, cfg.n_clusters, d, dev,
+                                            cfg.hbm_budget_gb)
+            if chunk:
+                resident = 0
+                if not want:  # planner-driven streaming: keep what fits in HBM resident
+                    resident = plan_resident_rows(xn.shape[0], row_bytes, chunk, cfg.n_clusters,
+                                                  d, dev, cfg.hbm_budget_gb)
+                return HostSource(xn, layout, dev, row_offset, resident_rows=resident), chunk
         return torch.as_tensor(xn).to(dev), want
 
-    def _build_engine(self, first, x_local, dev, comm, n_global, row_offset, n_local,
-                      init_centers_, start_iter):
-        """``first``: a one-element list holding the first (source, chunk_rows); it is
-        emptied here, so a retry after an OOM does not keep the failed device copy alive."""
-        """LloydEngine with collective OOM handling: if any rank runs out of memory while
-        building the engine, every rank halves the streamed chunk and retries (the
-        reference doubled its batch count on ResourceExhaustedError,
-        `scripts/distribuitedClustering.py:331-360`, but clustered batches independently)."""
+    def _build_engine(self, x_local, dev, comm, n_global, row_offset, n_local,
+                      init_centers_, start_iter, chunk: int = 0):
+        """LloydEngine under the collective OOM agreement (:func:`build_engine_collective`);
+        returns (engine, seconds spent creating the data source)."""
         cfg = self.cfg
-        chunk = 0
-        for attempt in range(cfg.max_oom_retries + 1):
-            err = None
-            eng = source = None
-            try:
-                if first:
-                    source, chunk_rows = first.pop()
-                else:
-                    source, chunk_rows = self._make_source(x_local, dev, row_offset, chunk)
-                faults.maybe_fail("setup", comm.rank)
-                cls = LloydEngine
-                if cfg.algorithm == "bounded":
-                    from .bounded import BoundedLloydEngine as cls
-                eng = cls(source, cfg, comm, n_global, row_offset, init_centers_,
-                          chunk_rows, defer_init=True)
-            except Exception as e:  # noqa: BLE001 - filtered right below
-                if not faults.is_oom(e):
-                    raise
-                err = e
-            if comm.max_scalar(1.0 if err is not None else 0.0) == 0.0:
-                eng.init_centroids()
-                eng.n_iter = start_iter
-                return eng
-            del eng, source
-            if dev.type == "cuda":
-                torch.cuda.empty_cache()
-            chunk = max(1024, (chunk or n_local) // 2)
-            if comm.is_root:
-                print(f"[kmeans] out of memory while building the engine "
-                      f"({type(err).__name__ if err else 'peer rank'}); retrying streamed with "
-                      f"chunk_rows={chunk}", flush=True)
-        raise err if err is not None else faults.oom_error("out of memory on a peer rank")
 
-    def _recover_oom(self, eng, step, x_local, dev, comm, n_global, row_offset, n_local):
-        """A rank ran out of memory inside the last step (flag in the all-reduce buffer):
-        every rank rolls back to the pre-step centroids and continues from the same
-        iteration on a streamed engine with half the chunk (the reference restarted the
-        whole run with twice the batches, `scripts/distribuitedClustering.py:357-360`)."""
-        c_host = eng.rollback(step)
-        n_back = eng.n_iter
-        chunk = max(1024, (eng.chunk_rows or n_local) // 2)
-        c0 = eng.c0
-        del eng
-        self.engine_ = None
-        if dev.type == "cuda":
-            torch.cuda.empty_cache()
-        if comm.is_root:
-            print(f"[kmeans] out of memory in iteration {n_back + 1}; continuing streamed with "
-                  f"chunk_rows={chunk}", flush=True)
-        eng = self._build_engine([self._make_source(x_local, dev, row_offset, chunk)], x_local,
-                                 dev, comm, n_global, row_offset, n_local, c_host, n_back)
-        eng.c0 = c0
-        self.engine_ = eng
-        return eng
+        def make_engine(source, chunk_rows):
+            cls = LloydEngine
+            if cfg.algorithm == "bounded":
+                from .bounded import BoundedLloydEngine as cls
+            return cls(source, cfg, comm, n_global, row_offset, init_centers_, chunk_rows,
+                       defer_init=True)
+
+        return build_engine_collective(
+            "kmeans", cfg, comm, dev, n_local, start_iter, chunk,
+            lambda c: self._make_source(x_local, dev, row_offset, c), make_engine)
 
     def fit(self, x_local, init_centers_: Optional[np.ndarray] = None,
             n_global: Optional[int] = None, row_offset: Optional[int] = None) -> "KMeans":
         cfg = self.cfg
-        t_init0 = time.perf_counter()
+        t_setup0 = time.perf_counter()
         dev = self._target_device(x_local)
         if self.comm is None:
             self.comm = local_comm(dev)
@@ -631,11 +652,7 @@ class KMeans:
         n_local = int(x_local.n_rows if hasattr(x_local, "n_rows") else x_local.shape[0])
         if n_global is None or row_offset is None:
             n_global, row_offset = _shard_geometry(n_local, comm)
-        first = self._make_source(x_local, dev, row_offset)
-        sync(dev)
-        initialization_time = time.perf_counter() - t_init0
 
-        t_setup0 = time.perf_counter()
         ckpt = RunCheckpointer(cfg, comm, "distributedKMeans")
         d = int(x_local.d if hasattr(x_local, "d") else x_local.shape[1])
         resumed = ckpt.load_for_resume(cfg.n_clusters, d)
@@ -645,28 +662,45 @@ class KMeans:
             if comm.is_root:
                 print(f"[kmeans] resuming from {cfg.checkpoint_path} at iteration {start_iter}",
                       flush=True)
-        first = [first]  # handed over: _build_engine drops it before any retry
-        eng = self._build_engine(first, x_local, dev, comm, n_global, row_offset, n_local,
-                                 init_centers_, start_iter)
+        eng, initialization_time = self._build_engine(x_local, dev, comm, n_global, row_offset,
+                                                      n_local, init_centers_, start_iter)
         if cfg.graph and eng.graphable() and not comm.collective:
             eng.capture()
-        if cfg.max_iter > eng.n_iter:
+        if cfg.warmup and cfg.max_iter > eng.n_iter:
             eng.warmup()
         sync(dev)
-        setup_time = time.perf_counter() - t_setup0
+        # initialization_time: the shard load / H2D (the reference's variable init with the
+        # data feed, `:273`); setup_time: the rest (init, kernels' first launch, graph)
+        setup_time = time.perf_counter() - t_setup0 - initialization_time
 
         # ------------------------------------------------------------ timed loop
         history = []
         centers_host = lambda: self.engine_.centers().double().cpu().numpy()
         self.engine_ = eng
+        self._retired = []  # weak references to engines replaced after an OOM
         timer = DeviceTimer(dev)
         timer.start()
         while True:
             if eng.oom_guard:
                 bad = eng.failed_step(final=eng.n_iter >= cfg.max_iter)
                 if bad is not None:
-                    eng = self._recover_oom(eng, bad, x_local, dev, comm, n_global, row_offset,
-                                            n_local)
+                    # every rank rolls back to the pre-step centroids and continues from the
+                    # same iteration on a streamed engine with half the chunk (the reference
+                    # restarted the whole run with twice the batches, `:357-360`).  The old
+                    # engine (device shard, operand tables, graph pool) is released first.
+                    c_host = eng.rollback(bad)
+                    n_back, c0 = eng.n_iter, eng.c0
+                    chunk = _retry_chunk(eng.chunk_rows, n_local)
+                    self._retired.append(weakref.ref(eng))
+                    eng = self.engine_ = None
+                    _release(dev)
+                    if comm.is_root:
+                        print(f"[kmeans] out of memory in iteration {n_back + 1}; continuing "
+                              f"streamed with chunk_rows={chunk}", flush=True)
+                    eng, _ = self._build_engine(x_local, dev, comm, n_global, row_offset, n_local,
+                                                c_host, n_back, chunk)
+                    eng.c0 = c0
+                    self.engine_ = eng
                     continue
             if eng.n_iter >= cfg.max_iter:
                 break

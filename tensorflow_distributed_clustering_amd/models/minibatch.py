@@ -51,7 +51,9 @@ class MiniBatchStepper:
             self.source = ResidentSource(self.local.x, self.local.layout, row_offset)
             self.d = int(source.shape[1])
             self.c0 = init_centers(cfg.init, source, row_offset, n_global, k, comm, cfg.seed,
-                                   given=init_centers_)
+                                   given=init_centers_, kpp_max_k=cfg.kpp_max_k,
+                                   kpp_sample_per_k=cfg.kpp_sample_per_k,
+                                   kpp_sample_min=cfg.kpp_sample_min)
         else:
             dev = torch.device(getattr(source, "device", "cpu"))
             self.source = source
@@ -59,7 +61,10 @@ class MiniBatchStepper:
             self.local = make_lloyd_ops(torch.zeros(1, self.d, device=dev), k, cfg.dtype,
                                         cfg.backend, cfg.empty_cluster, cfg.deterministic)
             self.c0 = init_centers_from_source(cfg.init, source, row_offset, n_global, k, comm,
-                                               cfg.seed, given=init_centers_, d=self.d)
+                                               cfg.seed, given=init_centers_, d=self.d,
+                                               kpp_max_k=cfg.kpp_max_k,
+                                               kpp_sample_per_k=cfg.kpp_sample_per_k,
+                                               kpp_sample_min=cfg.kpp_sample_min)
         self.device = dev
         self.n_local = int(self.source.n_rows)
         d = self.d

@@ -16,8 +16,7 @@ Variants (picked by :func:`make_lloyd_ops`):
                           update from the full-precision shard
 ``HipSmallLloyd``         fused fp32/fp64 assign+accumulate (reference configs)
 ``HipSimtLloyd``          fp32/fp64 exact SIMT assign + LDS update
-``HipExactLloyd``         fp32/fp64 large-D (and bf16 D > 512): tiled exact assign
-``HipGemmLloyd``          fp32/fp64 large-D via library GEMM (comparisons only)
+``HipExactLloyd``         fp32/fp64 large-D (and bf16 D > 1024): tiled exact assign
 ``TorchLloyd``            plain PyTorch (CPU ranks, oracle)
 ========================  =====================================================
 """
@@ -38,16 +37,6 @@ TORCH_DTYPES = {"fp64": torch.float64, "fp32": torch.float32, "bf16": torch.bflo
 MFMA_DIMS = (32, 64, 128, 256)
 WIDE_BF16_DIMS = (384, 512, 640, 768, 896, 1024)
 FP8_DIMS = (256, 512, 768, 1024)
-# centroid bytes one K-group may occupy (0 = one group over all of K).  Grouping keeps a
-# group L2-resident per XCD, but measured slower than one group (the 256 MiB MALL serves
-# the 48 MiB fp8 table): N=5M D=768 K=65536 fp8, 3 MiB groups 206.5 ms vs one group
-# 197.3 ms (docs/PERF_NOTES.md).  Kept as a tunable (TDC_KGROUP_BYTES).
-KGROUP_BYTES = int(__import__("os").environ.get("TDC_KGROUP_BYTES", 0))
-# assign/update overlap: the resident bf16 step runs in this many row slices; slice i's
-# (memory-bound) update runs on a side stream while slice i+1's (MFMA-bound) assign runs
-OVERLAP_SLICES = int(__import__("os").environ.get("TDC_OVERLAP_SLICES", 1))
-OVERLAP_PRIO = int(__import__("os").environ.get("TDC_OVERLAP_PRIO", 0))  # side stream
-OVERLAP_MIN_ROWS = 1 << 20  # per slice: below this the assign grid no longer fills 256 CUs
 
 
 def acc_dtype_for(dtype: str, k: int, d: int) -> torch.dtype:
@@ -86,18 +75,21 @@ def fp8_dim(d: int) -> Optional[int]:
 KGROUP_MIN_ITEMS = 2048
 
 
-def kgroup_tiles(row_bytes: int, kp: int, n: Optional[int] = None) -> int:
+def kgroup_tiles(row_bytes: int, kp: int, n: Optional[int] = None,
+                 group_bytes: int = 0) -> int:
     """Centroid tiles (of 32) per K-group (0 = one group over all of K).
 
-    With ``TDC_KGROUP_BYTES`` > 0: groups of that many centroid bytes (L2 residency).
-    Otherwise one group, unless the point count is too small to fill the chip (serving
-    requests, small chunks): then K is split so that (N/256 point blocks) x groups reaches
-    KGROUP_MIN_ITEMS work items (1024 rows x K=65536 fp8: 4 items -> 2.2 ms; the groups'
-    winners merge through the 64-bit key atomics).  Groups are a whole number of 64-row
-    stages."""
+    ``group_bytes`` > 0 (``ClusterConfig.kgroup_bytes``): groups of that many centroid
+    bytes, for L2 residency per XCD.  Measured slower than one group (the 256 MiB MALL
+    serves the 48 MiB fp8 table: N=5M D=768 K=65536, 3 MiB groups 206.5 ms vs one group
+    197.3 ms, docs/PERF_NOTES.md), so the default is 0.  Otherwise one group, unless the
+    point count is too small to fill the chip (serving requests, small chunks): then K is
+    split so that (N/256 point blocks) x groups reaches KGROUP_MIN_ITEMS work items (1024
+    rows x K=65536 fp8: 4 items -> 2.2 ms; the groups' winners merge through the 64-bit
+    key atomics).  Groups are a whole number of 64-row stages."""
     ntiles = kp // 32
-    if KGROUP_BYTES > 0:
-        tiles = max(1, KGROUP_BYTES // (32 * row_bytes))
+    if group_bytes > 0:
+        tiles = max(1, group_bytes // (32 * row_bytes))
         return 0 if tiles * 32 >= kp else int(tiles)
     if n is None:
         return 0
@@ -315,38 +307,9 @@ class HipBf16Lloyd(_LocalOpsBase):
     def prepare(self, C):
         self.ops.finalize(None, None, C, 0, None, self.cm2, self.cnorm)
 
-    def _slices(self):
-        n = self.n
-        s = max(1, min(OVERLAP_SLICES, n // OVERLAP_MIN_ROWS))
-        if s <= 1 or self.update.kind != "sorted" or self.update.deterministic:
-            return None
-        b = [(n * i // s) // 256 * 256 for i in range(s)] + [n]
-        return list(zip(b[:-1], b[1:]))
-
     def step(self, C, labels, mind, sums, counts):
-        sl = self._slices()
-        if sl is None:
-            self.ops.assign_bf16(self.x, self.cm2, self.cnorm, labels, mind)
-            self.update(self.x, labels, sums, counts)
-            return
-        # fork/join over a side stream (also valid under hipGraph capture): the update of
-        # slice i (gather-bound, ~5 TB/s) overlaps the assign of slice i+1 (MFMA-bound).
-        # Updates stay ordered on the side stream, so one workspace and the accumulating
-        # sums/counts are safe.
-        main = torch.cuda.current_stream(self.device)
-        side = getattr(self, "_side", None)
-        if side is None:
-            side = self._side = torch.cuda.Stream(device=self.device, priority=OVERLAP_PRIO)
-        side.wait_stream(main)
-        for s, e in sl:
-            self.ops.assign_bf16(self.x[s:e], self.cm2, self.cnorm, labels[s:e],
-                                 None if mind is None else mind[s:e])
-            ev = torch.cuda.Event()
-            ev.record(main)
-            side.wait_event(ev)
-            with torch.cuda.stream(side):
-                self.update(self.x[s:e], labels[s:e], sums, counts)
-        main.wait_stream(side)
+        self.ops.assign_bf16(self.x, self.cm2, self.cnorm, labels, mind)
+        self.update(self.x, labels, sums, counts)
 
     def assign(self, C, labels, mind):
         self.ops.assign_bf16(self.x, self.cm2, self.cnorm, labels, mind)
@@ -387,14 +350,18 @@ class HipBf16Lloyd(_LocalOpsBase):
 class _GroupedAssign:
     """Shared state of the K-grouped wide-D kernels: point norms + merge keys."""
 
+    # ClusterConfig.kgroup_bytes (0: one K-group unless the launch is too small to fill
+    # the chip); set by the engine after construction
+    kgroup_bytes = 0
+
     def _init_grouped(self, row_bytes: int):
         self._row_bytes = row_bytes
-        self.kg = kgroup_tiles(row_bytes, self.kp)
+        self.kg = kgroup_tiles(row_bytes, self.kp, group_bytes=self.kgroup_bytes)
         self._keys = None
 
     def _kg_for(self, n: int) -> int:
         """K-group size for an n-row launch (splits K when n alone cannot fill the chip)."""
-        self.kg = kgroup_tiles(self._row_bytes, self.kp, n)
+        self.kg = kgroup_tiles(self._row_bytes, self.kp, n, self.kgroup_bytes)
         return self.kg
 
     def _keys_for(self, n):
@@ -469,7 +436,7 @@ class HipWideBf16Lloyd(_GroupedAssign, _LocalOpsBase):
             self.kp = kpad
             self.cm2 = torch.zeros(kpad, self.dp, dtype=torch.bfloat16, device=self.device)
             self.cnorm = torch.zeros(kpad, dtype=torch.float32, device=self.device)
-            self.kg = kgroup_tiles(self._row_bytes, self.kp)
+            self.kg = kgroup_tiles(self._row_bytes, self.kp, group_bytes=self.kgroup_bytes)
 
     def gather_operands(self):
         return [self.cm2, self.cnorm]
@@ -539,8 +506,8 @@ class HipFp8Lloyd(_GroupedAssign, _LocalOpsBase):
     # distances are recomputed in fp32 from the full-precision rows.
     # Off by default: the top-2 epilogue costs ~8 % of the assignment (embed50m_fp8:
     # 1.93 -> 2.14 s/iter) for labels that only differ on near ties.  Needs one K-group
-    # (N >= KGROUP_MIN_ITEMS * 256 rows per launch).
-    RECHECK_TAU = float(__import__("os").environ.get("TDC_FP8_RECHECK_TAU", 0.0))
+    # (N >= KGROUP_MIN_ITEMS * 256 rows per launch).  Set from ClusterConfig.fp8_recheck.
+    RECHECK_TAU = 0.0
 
     def _top2_buffers(self, n):
         b = getattr(self, "_t2", None)
@@ -590,13 +557,17 @@ class HipFp8Lloyd(_GroupedAssign, _LocalOpsBase):
             self.cm2 = torch.zeros(kpad, self.dp, dtype=torch.float8_e4m3fn, device=dev)
             self.cs = torch.zeros(kpad, self.dp // 32, dtype=torch.uint8, device=dev)
             self.cnorm = torch.zeros(kpad, dtype=torch.float32, device=dev)
-            self.kg = kgroup_tiles(self._row_bytes, self.kp)
+            self.kg = kgroup_tiles(self._row_bytes, self.kp, group_bytes=self.kgroup_bytes)
 
     def gather_operands(self):
         return [self.cm2, self.cs, self.cnorm]
 
     def finalize_rows(self, sums, counts, C, shift, r0, kr):
-        self.ops.finalize(sums, counts, C, self.policy, shift, None, None)
+        # a rank whose rsag slice holds only padding rows (K small next to lcm(32, world))
+        # finalises nothing but still writes its padding operands (quant of 0 rows: zeros
+        # and the BIG pad norm)
+        if C.shape[0]:
+            self.ops.finalize(sums, counts, C, self.policy, shift, None, None)
         self.ops.quant_fp8(C, C.shape[0], 1, self.cm2[r0:r0 + kr], self.cs[r0:r0 + kr],
                            self.cnorm[r0:r0 + kr])
 
@@ -660,29 +631,32 @@ class HipExactLloyd(_HipExactBase):
         self.ops.assign_exact(self.x, C, labels, mind)
 
 
-class HipGemmLloyd(_HipExactBase):
-    """Large-D fp32/fp64 via the vendor GEMM expansion (library GEMM), native update:
-    faster than the exact kernel at very large K*D but not difference-form exact
-    (``backend`` never selects it automatically; kept for comparisons)."""
-    name = "hip_gemm"
-
-    def step(self, C, labels, mind, sums, counts):
-        self.assign(C, labels, mind)
-        self.update(self.x, labels, sums, counts)
-
-    def assign(self, C, labels, mind):
-        lab, md = ref.assign(self.x, C, exact=False)
-        labels.copy_(lab)
-        if mind is not None:
-            mind.copy_(md.to(mind.dtype))
+def lloyd_layout(dtype: str, d: int):
+    """(torch dtype, width) of the rows the GPU Lloyd ops for ``dtype`` consume (the
+    layout a streamed source must produce; mirrors :func:`_make_lloyd_ops`)."""
+    if dtype == "fp8" and fp8_dim(d) is not None:
+        return (torch.float32, d)  # fp8 ops quantise each chunk they are bound to
+    if dtype in ("bf16", "fp8"):
+        w = padded_dim(d) or wide_bf16_dim(d)
+        return (torch.bfloat16, w) if w is not None else (torch.float32, d)
+    return (TORCH_DTYPES[dtype], d)
 
 
 def make_lloyd_ops(x: torch.Tensor, k: int, dtype: str = "bf16", backend: str = "auto",
-                   empty_cluster: str = "keep", deterministic: bool = False):
-    """Pick the fastest local implementation for (device, dtype, K, D)."""
+                   empty_cluster: str = "keep", deterministic: bool = False,
+                   kgroup_bytes: int = 0, fp8_recheck: float = 0.0):
+    """Pick the fastest local implementation for (device, dtype, K, D).
+
+    ``kgroup_bytes`` / ``fp8_recheck``: ClusterConfig tunables of the wide-D / fp8 assign
+    (K-group size; near-tie re-check margin), applied to the ops that have them."""
     ops = _make_lloyd_ops(x, k, dtype, backend, empty_cluster, deterministic)
     if deterministic and isinstance(getattr(ops, "update", None), NativeUpdate):
         ops.update.deterministic = True
+    if isinstance(ops, _GroupedAssign) and kgroup_bytes:
+        ops.kgroup_bytes = int(kgroup_bytes)
+        ops.kg = kgroup_tiles(ops._row_bytes, ops.kp, group_bytes=ops.kgroup_bytes)
+    if isinstance(ops, HipFp8Lloyd) and fp8_recheck > 0:
+        ops.RECHECK_TAU = float(fp8_recheck)
     return ops
 
 

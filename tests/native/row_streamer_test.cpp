@@ -5,7 +5,7 @@
 //
 // Several caller threads submit overlapping-in-time conversions of random row ranges into
 // their own buffers, wait for them in a shuffled order and check every converted value
-// (bf16 round-to-nearest-even and f32, zero padding up to dp).  Exit code 0 = pass.
+// (bf16 round-to-nearest-even, f32 and the exact f64 copy, zero padding up to dp).  Exit code 0 = pass.
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -31,6 +31,9 @@ static int check(const std::vector<double>& src, int64_t ld, int64_t cols, int64
       if (dst_type == tdc::DST_BF16) {
         got = bf16_to_f32(reinterpret_cast<const uint16_t*>(out.data())[(size_t)r * dp + c]);
         if (std::fabs(got - want) > std::fabs(want) * (1.0 / 256) + 1e-30) return 1;
+      } else if (dst_type == tdc::DST_F64) {
+        got = reinterpret_cast<const double*>(out.data())[(size_t)r * dp + c];
+        if (got != want) return 1;
       } else {
         got = reinterpret_cast<const float*>(out.data())[(size_t)r * dp + c];
         if (got != (double)(float)want) return 1;
@@ -46,8 +49,8 @@ int main() {
   std::normal_distribution<double> nd(0.0, 3.0);
   for (auto& v : src) v = nd(rng);
   int failures = 0;
-  for (int dst_type : {tdc::DST_BF16, tdc::DST_F32}) {
-    const size_t es = dst_type == tdc::DST_BF16 ? 2 : 4;
+  for (int dst_type : {tdc::DST_BF16, tdc::DST_F32, tdc::DST_F64}) {
+    const size_t es = dst_type == tdc::DST_BF16 ? 2 : dst_type == tdc::DST_F64 ? 8 : 4;
     for (int round = 0; round < 3; ++round) {
       tdc::RowStreamerCore rs(src.data(), tdc::SRC_F64, n, cols, ld, dst_type, dp, 4);
       std::vector<std::thread> callers;

@@ -5,6 +5,7 @@ import os
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -22,15 +23,36 @@ def _run(args, timeout=600):
 
 
 @pytest.mark.parametrize("gpus", [1, 2])
-def test_bench_json_contract(gpus):
+@pytest.mark.parametrize("scaling", ["strong", "weak"])
+def test_bench_json_contract(gpus, scaling):
     d = _run(["--gpus", str(gpus), "--steps", "3", "--warmup", "1", "--n-per-gpu", "20000",
-              "--k", "16", "--dim", "8", "--dtype", "fp32"])
+              "--k", "16", "--dim", "8", "--dtype", "fp32", "--scaling", scaling])
     assert KEYS <= set(d)
+    n = 20000 * gpus if scaling == "weak" else 20000
     assert d["n_gpus"] == gpus and d["steps"] == 3 and d["warmup"] == 1
-    assert d["config"]["global_batch"] == 20000 * gpus and d["config"]["parallelism"] == f"dp{gpus}"
-    assert d["scaling"] == "weak" and d["higher_is_better"] is True
+    assert d["config"]["global_batch"] == n and d["config"]["parallelism"] == f"dp{gpus}"
+    assert d["scaling"] == scaling and d["higher_is_better"] is True
     # whole-job value = global points per step / step time
-    assert d["value"] == pytest.approx(20000 * gpus / (d["ms_per_step"] / 1e3), rel=1e-6)
+    assert d["value"] == pytest.approx(n / (d["ms_per_step"] / 1e3), rel=1e-6)
+    if gpus > 1:  # per-phase times (max over ranks) ride along at world > 1
+        assert set(d["phase_ms"]) == {"zero", "assign", "update", "allreduce", "finalize"}
+
+
+def test_bench_headline_is_strong_scaling_at_10m(tmp_path):
+    """The default preset measures BASELINE.json's metric: N = 10M points in TOTAL, split
+    over the ranks (strong scaling), so --gpus 1/2/4 time the same problem and reach the
+    same centroids (gloo ranks on CPU; D and K reduced so the CPU fp32 path is quick)."""
+    cs = {}
+    for g in (1, 2, 4):
+        out = tmp_path / f"c{g}.npy"
+        d = _run(["--gpus", str(g), "--steps", "2", "--warmup", "1", "--k", "16", "--dim", "8",
+                  "--dtype", "fp32", "--centers-out", str(out)], timeout=900)
+        assert d["scaling"] == "strong" and d["preset"] == "headline"
+        assert d["config"]["N"] == 10_000_000 and d["config"]["global_batch"] == 10_000_000
+        assert d["config"]["points_per_gpu"] == 10_000_000 // g
+        cs[g] = np.load(out)
+    for g in (2, 4):
+        np.testing.assert_allclose(cs[g], cs[1], rtol=1e-4, atol=1e-4)
 
 
 def test_bench_fcm_and_minibatch_presets():

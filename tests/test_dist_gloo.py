@@ -247,11 +247,30 @@ def test_dist_debug_detects_collective_mismatch():
 def test_large_k_kmeanspp_is_sampled_kmeans_parallel_world_invariant(monkeypatch):
     """Above KPP_MAX_K, init='kmeans++' seeds with k-means|| on a world-invariant uniform
     sample (greedy k-means++ would be K dependent sweeps): same centres at world 1 and 2."""
-    monkeypatch.setenv("TDC_KPP_MAX_K", "8")
-    _, _, _, _, i1, _ = run_world(1, init="kmeans++", k=24, iters=1)
-    _, _, _, _, i2, _ = run_world(2, init="kmeans++", k=24, iters=1)
+    _, _, _, _, i1, _ = run_world(1, init="kmeans++", k=24, iters=1, extra=dict(kpp_max_k=8))
+    _, _, _, _, i2, _ = run_world(2, init="kmeans++", k=24, iters=1, extra=dict(kpp_max_k=8))
     np.testing.assert_allclose(i2, i1, rtol=1e-12, atol=1e-12)
     assert len(np.unique(i1, axis=0)) == 24
+
+
+def test_sampled_greedy_kmeanspp_world_invariant_and_sound():
+    """N > 4 * max(min sample, kpp_sample_per_k * K): greedy k-means++ runs on a uniform
+    world-invariant sample.  Same seeds at world 1 and 2, every seed is a data row, and the
+    seeding is as good as greedy k-means++ over all rows (potential within 2x; the blobs are
+    well separated, so both find one seed per blob)."""
+    extra = dict(kpp_sample_per_k=200, kpp_sample_min=1000)
+    n, k = 30011, 6
+    c1, _, in1, _, i1, _ = run_world(1, init="kmeans++", n=n, k=k, iters=0, extra=extra)
+    _, _, _, _, i2, _ = run_world(2, init="kmeans++", n=n, k=k, iters=0, extra=extra)
+    np.testing.assert_allclose(i2, i1, rtol=1e-12, atol=1e-12)
+    from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs
+    x = gaussian_blobs(n, 3, k, seed=11, dtype=torch.float64)
+    d = torch.cdist(torch.as_tensor(i1), x).min(1).values
+    assert float(d.max()) < 1e-9  # seeds are data rows
+    _, _, _, _, full, _ = run_world(1, init="kmeans++", n=n, k=k, iters=0,
+                                    extra=dict(kpp_sample_per_k=0))
+    pot = lambda c: float(torch.cdist(x, torch.as_tensor(c)).min(1).values.pow(2).sum())
+    assert pot(i1) < 2.0 * pot(full)
 
 
 def _warmup_worker(rank, world, port, q):

@@ -90,7 +90,7 @@ def test_setup_oom_retries_streamed(monkeypatch, capsys):
     monkeypatch.setenv("TDC_FAULT", "oom@setup")
     res = tdc.KMeans(cfg).fit(x).result_
     assert res.streamed  # the retry streams the shard in halved chunks
-    assert "retrying streamed with chunk_rows=2500" in capsys.readouterr().out
+    assert "retrying streamed with chunk_rows=1250" in capsys.readouterr().out
     np.testing.assert_allclose(res.centers, ref_run.centers, rtol=1e-12, atol=1e-12)
 
 
@@ -322,3 +322,21 @@ def test_distributed_crash_and_resume(tmp_path):
     x = gaussian_blobs(6001, 3, 5, seed=4, dtype=torch.float64)
     full = tdc.KMeans(tdc.ClusterConfig(n_clusters=5, max_iter=8, dtype="fp64", seed=2)).fit(x)
     np.testing.assert_allclose(centers, full.result_.centers, rtol=1e-10, atol=1e-10)
+
+
+@pytest.mark.parametrize("model", ["kmeans", "fcm"])
+def test_mid_run_oom_releases_the_old_engine(monkeypatch, capsys, model):
+    """After a mid-run OOM the engine that failed (its device shard, operand tables, graph
+    pool) is garbage before the streamed engine is built: fit keeps only weak references
+    to it, and those are dead once the fit returns."""
+    x = gaussian_blobs(3000, 3, 4, seed=5, dtype=torch.float64)
+    cfg = tdc.ClusterConfig(n_clusters=4, max_iter=6, dtype="fp64", init="first_k",
+                            fuzzifier=2.0)
+    cls = tdc.KMeans if model == "kmeans" else tdc.FuzzyCMeans
+    ref_run = cls(cfg).fit(x.numpy()).result_
+    monkeypatch.setenv("TDC_FAULT", "oom@3")
+    m = cls(cfg)
+    r = m.fit(x.numpy()).result_
+    assert r.streamed and "continuing streamed" in capsys.readouterr().out
+    assert len(m._retired) == 1 and all(w() is None for w in m._retired)
+    np.testing.assert_allclose(r.centers, ref_run.centers, rtol=1e-10, atol=1e-10)

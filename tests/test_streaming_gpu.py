@@ -184,3 +184,60 @@ def test_fcm_hbm_budget_streams_and_matches_resident(gpu, dtype, backend):
     tol = 1e-9 if dtype == "fp64" else 2e-4
     np.testing.assert_allclose(st.centers, res.centers, rtol=tol, atol=tol)
     assert (st.labels == res.labels).float().mean().item() > 0.999
+
+
+def _fp64_shard(n=2_000_000, d=16, k=16):
+    x = gaussian_blobs(n, d, k, seed=12, dtype=torch.float64).numpy()
+    return x, x[:k] + 0.25
+
+
+def test_fp64_kmeans_larger_than_budget_streams_from_host(gpu):
+    """fp64 K-Means (the reference's dtype) with an HBM budget below the shard: the rows
+    stay in host memory and stream through the RowStreamer's pinned ring (f64 rows as they
+    are) into the fused fp64 kernel; same centres as the resident fit to 1e-9, and the
+    device never holds the shard (peak allocation < the shard's bytes)."""
+    x, c0 = _fp64_shard()
+    cfg = tdc.ClusterConfig(n_clusters=16, max_iter=5, dtype="fp64", init="given")
+    res = tdc.KMeans(cfg, device=gpu).fit(x, init_centers_=c0).result_
+    del_labels = res.labels
+    res.labels = None
+    del del_labels
+    torch.cuda.synchronize(gpu)
+    torch.cuda.empty_cache()
+    torch.cuda.reset_peak_memory_stats(gpu)
+    base = torch.cuda.memory_allocated(gpu)
+    st = tdc.KMeans(cfg.replace(hbm_budget_gb=0.1), device=gpu).fit(x, init_centers_=c0).result_
+    peak = torch.cuda.max_memory_allocated(gpu) - base
+    assert st.streamed and not res.streamed and st.backend == res.backend
+    np.testing.assert_allclose(st.centers, res.centers, rtol=1e-9, atol=1e-9)
+    assert peak < x.nbytes // 2, (peak, x.nbytes)
+
+
+@pytest.mark.parametrize("fault", ["oom@setup", "oom@3"])
+def test_fp64_kmeans_oom_falls_back_to_host_streaming(gpu, monkeypatch, fault):
+    """TDC_FAULT=oom@setup (the upload of the fp64 shard fails) and oom@3 (iteration 3
+    fails): the run continues streamed from host memory and matches the undisturbed fit;
+    afterwards the device holds no copy of the shard (the failed engine was released)."""
+    from tensorflow_distributed_clustering_amd.utils import faults
+    x, c0 = _fp64_shard()
+    cfg = tdc.ClusterConfig(n_clusters=16, max_iter=5, dtype="fp64", init="given")
+    ref_c = tdc.KMeans(cfg, device=gpu).fit(x, init_centers_=c0).result_.centers
+    torch.cuda.synchronize(gpu)
+    torch.cuda.empty_cache()
+    torch.cuda.reset_peak_memory_stats(gpu)
+    base = torch.cuda.memory_allocated(gpu)
+    faults._FIRED.clear()
+    monkeypatch.setenv("TDC_FAULT", fault)
+    m = tdc.KMeans(cfg, device=gpu)
+    r = m.fit(x, init_centers_=c0).result_
+    monkeypatch.delenv("TDC_FAULT")
+    faults._FIRED.clear()
+    assert r.streamed
+    np.testing.assert_allclose(r.centers, ref_c, rtol=1e-9, atol=1e-9)
+    torch.cuda.synchronize(gpu)
+    now = torch.cuda.memory_allocated(gpu) - base
+    assert now < x.nbytes // 2, (now, x.nbytes)
+    if fault == "oom@setup":
+        assert torch.cuda.max_memory_allocated(gpu) - base < x.nbytes // 2
+    else:
+        assert all(w() is None for w in m._retired)
