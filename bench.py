@@ -182,7 +182,7 @@ def main(argv=None):
         init_s = comm.max_scalar(time.perf_counter() - t_i)
     if a.mode == "lloyd" and a.method == "kmeans" and a.algorithm == "lloyd" and a.graph \
             and dev.type == "cuda":
-        eng.capture(include_collectives=world > 1)
+        eng.capture(include_collectives=comm.collective)
 
     for _ in range(a.warmup):
         eng.step()

@@ -184,7 +184,8 @@ void check_split(const std::optional<at::Tensor>& hi, const std::optional<at::Te
 
 void update_sorted(const at::Tensor& X, const at::Tensor& labels, at::Tensor& sums,
                    at::Tensor& counts, at::Tensor& work, const std::optional<at::Tensor>& cnt_hi,
-                   const std::optional<at::Tensor>& cnt_lo) {
+                   const std::optional<at::Tensor>& cnt_lo,
+                   const std::optional<at::Tensor>& zero_first) {
   check_cuda(X, "X");
   check_rows(X, "X");
   TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous() && labels.numel() >= X.size(0),
@@ -197,13 +198,20 @@ void update_sorted(const at::Tensor& X, const at::Tensor& labels, at::Tensor& su
                   work.numel() >= tdc_update_sorted_workspace(X.size(0), (int)sums.size(0)),
               "tdc.update_sorted: workspace too small");
   check_split(cnt_hi, cnt_lo, sums.size(0), "update_sorted");
+  int64_t zbytes = 0;
+  if (zero_first.has_value() && zero_first->defined()) {
+    TORCH_CHECK(zero_first->is_contiguous() && zero_first->device() == X.device() &&
+                    (zero_first->numel() * zero_first->element_size()) % 4 == 0,
+                "tdc.update_sorted: zero_first must be a contiguous device buffer of 4-byte words");
+    zbytes = zero_first->numel() * zero_first->element_size();
+  }
   const DevGuard guard(X.device());
   check(tdc_update_sorted(dcode(X.scalar_type()), dcode(sums.scalar_type()), X.data_ptr(),
                           X.size(0), X.stride(0), (int)sums.size(1), labels.data_ptr<int32_t>(),
                           (int)sums.size(0), sums.data_ptr(), counts.data_ptr(),
                           work.data_ptr<int>(), num_cus(X.device().index()), cur_stream(),
                           nullptr, static_cast<float*>(opt_ptr(cnt_hi)),
-                          static_cast<float*>(opt_ptr(cnt_lo))),
+                          static_cast<float*>(opt_ptr(cnt_lo)), opt_ptr(zero_first), zbytes),
         "update_sorted");
 }
 
@@ -771,7 +779,7 @@ TORCH_LIBRARY(tdc, m) {
   m.def("lloyd_small(Tensor X, Tensor C, Tensor(a!)? labels, Tensor(b!)? mind, Tensor(c!) sums, Tensor(d!) counts) -> ()");
   m.def("update(Tensor X, Tensor labels, Tensor(a!) sums, Tensor(b!) counts) -> ()");
   m.def("update_sorted_workspace(int N, int K) -> int", &update_sorted_workspace);
-  m.def("update_sorted(Tensor X, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work, Tensor(d!)? cnt_hi=None, Tensor(e!)? cnt_lo=None) -> ()");
+  m.def("update_sorted(Tensor X, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work, Tensor(d!)? cnt_hi=None, Tensor(e!)? cnt_lo=None, Tensor(f!)? zero_first=None) -> ()");
   m.def("fcm_small_supported(ScalarType dtype, int K, int D) -> bool", &fcm_small_supported);
   m.def("fcm_small(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!)? labels, Tensor(b!) wx, Tensor(c!) ws) -> ()");
   m.def("fcm_tower_stats(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) rowinfo) -> ()");

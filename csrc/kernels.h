@@ -61,8 +61,11 @@ int tdc_update_lds(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t
                    hipStream_t stream);
 
 // N2 (large K x D): counting sort by label + segmented row gather-sum.  work: int32
-// workspace of tdc_update_sorted_workspace(N, K) elements.  sums/counts are accumulated
-// (caller zeroes them once per pass).
+// workspace of tdc_update_sorted_workspace(N, K) elements, ZERO-FILLED when allocated (its
+// histogram part is left zeroed by every call).  sums/counts are accumulated (caller
+// zeroes them once per pass); zero_first (nullable, zero_bytes a multiple of 4) is cleared
+// by the first kernel before anything accumulates -- the caller's zero fill of the
+// all-reduce buffer without a launch of its own.
 // rowidx (nullable): labels[i] belongs to row rowidx[i] of X (N = number of labels).
 // cnt_hi / cnt_lo (nullable, fp32 [K]): the exact count split of an fp32 all-reduce
 // buffer, hi += c >> 12, lo += c & 4095 (each term stays an integer below 2^24, so the
@@ -70,7 +73,8 @@ int tdc_update_lds(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t
 int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
                       const int32_t* labels, int K, void* sums, void* counts, int* work,
                       int num_cus, hipStream_t stream, const int32_t* rowidx = nullptr,
-                      float* cnt_hi = nullptr, float* cnt_lo = nullptr);
+                      float* cnt_hi = nullptr, float* cnt_lo = nullptr,
+                      void* zero_first = nullptr, int64_t zero_bytes = 0);
 int64_t tdc_update_sorted_workspace(int64_t N, int K);
 
 // N4/N5  fused small-K Fuzzy C-Means tower: sum_i w_ki x_i, sum_i w_ki, argmax labels.

@@ -31,9 +31,15 @@ constexpr int LDS_HIST_MAX_K = 16384;
 template <int NT>
 __global__ __launch_bounds__(NT) void hist_kernel(const int32_t* __restrict__ labels, int64_t N,
                                                   int K, int* __restrict__ cnt,
-                                                  int64_t per_block) {
+                                                  int64_t per_block, uint32_t* __restrict__ zero,
+                                                  int64_t zero_words) {
   extern __shared__ int s_h[];
   const int tid = threadIdx.x;
+  // the caller's accumulation buffer (the all-reduce buffer of the step), cleared here
+  // instead of by a separate fill launch: scan / segsum accumulate into it only after
+  // this kernel has finished
+  for (int64_t w = (int64_t)blockIdx.x * NT + tid; w < zero_words; w += (int64_t)gridDim.x * NT)
+    zero[w] = 0u;
   const int64_t r0 = (int64_t)blockIdx.x * per_block;
   const int64_t r1 = min(N, r0 + per_block);
   const bool lds = K <= LDS_HIST_MAX_K;
@@ -69,7 +75,7 @@ __global__ __launch_bounds__(NT) void hist_kernel(const int32_t* __restrict__ la
 
 // single block, 1024 threads: offsets[0..K] (exclusive), cursor = offsets, counts_acc = cnt
 template <typename ACC>
-__global__ __launch_bounds__(1024) void scan_kernel(const int* __restrict__ cnt, int K,
+__global__ __launch_bounds__(1024) void scan_kernel(int* __restrict__ cnt, int K,
                                                     int* __restrict__ offsets,
                                                     int* __restrict__ cursor,
                                                     ACC* __restrict__ counts_acc,
@@ -93,6 +99,7 @@ __global__ __launch_bounds__(1024) void scan_kernel(const int* __restrict__ cnt,
   int run = s_part[tid] - s;  // exclusive prefix of this thread's range
   for (int k = k0; k < k1; ++k) {
     const int c = cnt[k];
+    cnt[k] = 0;  // the histogram is left zeroed for the next call (no memset launch)
     offsets[k] = run;
     cursor[k] = run;
     if (counts_acc) counts_acc[k] += (ACC)c;  // accumulate: streamed chunks add up
@@ -473,15 +480,21 @@ int dispatch_segsum(int x_dtype, const void* X, int64_t ldx, int D, const int32_
 int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
                       const int32_t* labels, int K, void* sums, void* counts, int* work,
                       int num_cus, hipStream_t s, const int32_t* rowidx, float* cnt_hi,
-                      float* cnt_lo) {
-  if (N <= 0) return 0;
+                      float* cnt_lo, void* zero_first, int64_t zero_bytes) {
+  if (zero_bytes % 4 != 0 || (zero_bytes > 0 && zero_first == nullptr))
+    return (int)hipErrorInvalidValue;
+  if (N <= 0) {
+    if (zero_bytes && hipMemsetAsync(zero_first, 0, (size_t)zero_bytes, s) != hipSuccess)
+      return (int)hipErrorUnknown;
+    return 0;
+  }
   if (N >= (int64_t)1 << 31) return (int)hipErrorInvalidValue;
-  // workspace layout (ints): cnt[K] | offsets[K+1] | cursor[K] | perm[N]
+  // workspace layout (ints): cnt[K] | offsets[K+1] | cursor[K] | perm[N]; cnt is zero on
+  // entry (a zero-filled workspace) and the scan leaves it zero
   int* cnt = work;
   int* offsets = cnt + K;
   int* cursor = offsets + K + 1;
   int32_t* perm = cursor + K;
-  if (hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)K, s) != hipSuccess) return (int)hipErrorUnknown;
   {
     // one 1024-thread block per CU: a quarter of the global flush atomics of 4 x 256-thread
     // blocks per CU (each block adds its whole LDS histogram into cnt)
@@ -491,12 +504,14 @@ int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int6
     if (per < 4096) per = 4096;
     blocks = (N + per - 1) / per;
     const size_t lds = K <= LDS_HIST_MAX_K ? sizeof(int) * (size_t)K : 0;
+    uint32_t* zw = static_cast<uint32_t*>(zero_first);
+    const int64_t nzw = zero_bytes / 4;
     if (hnt == 1024)
       hipLaunchKernelGGL(hist_kernel<1024>, dim3((unsigned)blocks), dim3(1024), lds, s, labels, N,
-                         K, cnt, per);
+                         K, cnt, per, zw, nzw);
     else
       hipLaunchKernelGGL(hist_kernel<256>, dim3((unsigned)blocks), dim3(256), lds, s, labels, N, K,
-                         cnt, per);
+                         cnt, per, zw, nzw);
     TDC_CHECK_LAUNCH();
   }
   if (acc_dtype == TDC_F64)
@@ -514,9 +529,13 @@ int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int6
       const char* e = getenv("TDC_BSCATTER_THREADS");
       return (e && atoi(e) == 256) ? 256 : 1024;
     }();
+    static const int64_t min_per_k = getenv("TDC_BSCATTER_MINPER_K") ? atoi(getenv("TDC_BSCATTER_MINPER_K")) : 4;
     int64_t blocks = nt == 1024 ? (int64_t)num_cus : (int64_t)num_cus * 2;
     int64_t per = (N + blocks - 1) / blocks;
+    // every block pays K-bin LDS passes and up to K returning reservation atomics (all
+    // blocks hit the same K cursors): at small N keep at least min_per_k labels per bin
     if (per < 4096) per = 4096;
+    if (per < min_per_k * K) per = min_per_k * K;
     blocks = (N + per - 1) / per;
     if (nt == 1024)
       hipLaunchKernelGGL(bscatter_kernel<1024>, dim3((unsigned)blocks), dim3(1024),

@@ -16,6 +16,7 @@ reference doubled its batch count and restarted on ResourceExhaustedError, `:331
 """
 from __future__ import annotations
 
+import math
 import time
 import weakref
 from typing import Optional
@@ -35,9 +36,23 @@ from .kmeans import (ClusterResult, OomGuard, _release, _retry_chunk, _shard_geo
                      build_engine_collective)
 
 
-def fcm_dtype(cfg: ClusterConfig) -> torch.dtype:
-    """Memberships need exact-difference-grade distances: bf16/fp8 configs run fp32."""
-    return torch.float64 if cfg.dtype == "fp64" else torch.float32
+# log2 of the smallest typical weight w = u^m (u ~ 1/K) that fp32 carries with headroom
+# (smallest normal fp32: 2^-126)
+FCM_FP32_MIN_LOG2_W = -100.0
+
+
+def fcm_dtype(cfg: ClusterConfig, m: Optional[float] = None) -> torch.dtype:
+    """Memberships need exact-difference-grade distances: bf16/fp8 configs run fp32.
+
+    With the reference's fuzzifier m = D (`distribuitedClustering.py:121,129`) the weights
+    u^m of a point's typical memberships u ~ 1/K fall to K^-m: 2^-144 at K=64, D=24, below
+    fp32's range, where every sum over them flushes to zero and the centroids become 0/0.
+    The reference ran fp64 throughout; such configurations are promoted to fp64 here."""
+    if cfg.dtype == "fp64":
+        return torch.float64
+    if m is not None and -m * math.log2(max(2, cfg.n_clusters)) < FCM_FP32_MIN_LOG2_W:
+        return torch.float64
+    return torch.float32
 
 
 class FcmEngine(OomGuard):
@@ -51,8 +66,6 @@ class FcmEngine(OomGuard):
         self.cfg, self.comm = cfg, comm
         self.n_global, self.row_offset = n_global, row_offset
         k = cfg.n_clusters
-        tdt = fcm_dtype(cfg)
-        dt_name = "fp64" if tdt == torch.float64 else "fp32"
         if isinstance(source, torch.Tensor):
             d = int(source.shape[1])
             dev = source.device
@@ -66,6 +79,11 @@ class FcmEngine(OomGuard):
         self.k, self.d, self.device = k, d, dev
         self.m = float(m) if m is not None else (float(cfg.fuzzifier) if cfg.fuzzifier is not None
                                                  else float(d))
+        tdt = fcm_dtype(cfg, self.m)
+        dt_name = "fp64" if tdt == torch.float64 else "fp32"
+        if tdt == torch.float64 and cfg.dtype != "fp64" and comm.is_root:
+            print(f"[fcm] fuzzifier m={self.m:g} with K={k}: weights u^m ~ K^-m underflow fp32; "
+                  f"computing in fp64", flush=True)
         if isinstance(source, torch.Tensor) and not chunk_rows:
             self.local = make_fcm_ops(source, k, dt_name, self.m, cfg.fcm_nan_to_zero, cfg.backend)
             self.source = None
@@ -126,6 +144,7 @@ class FcmEngine(OomGuard):
             s = start - self.row_offset
             self.local.bind(chunk).step(self.C, self.labels[s:s + chunk.shape[0]], self.wx,
                                         self.ws)
+        self.local.unbind()
 
     def step(self):
         self.buf.zero_()
@@ -156,6 +175,7 @@ class FcmEngine(OomGuard):
         for start, chunk in self._chunks():
             s = start - self.row_offset
             self.local.bind(chunk).assign(self.C, self.labels[s:s + chunk.shape[0]])
+        self.local.unbind()
 
 
 class FuzzyCMeans:
@@ -185,7 +205,8 @@ class FuzzyCMeans:
         want = chunk_override or cfg.chunk_rows
         if hasattr(x_local, "chunks"):
             return x_local, want or (1 << 22)
-        tdt = fcm_dtype(cfg)
+        tdt = fcm_dtype(cfg, self.fuzzifier(int(x_local.d if hasattr(x_local, "d")
+                                                else x_local.shape[1])))
         if isinstance(x_local, torch.Tensor) and x_local.device.type != "cpu":
             return x_local.to(dev), want
         xn = x_local.numpy() if isinstance(x_local, torch.Tensor) else np.asarray(x_local)

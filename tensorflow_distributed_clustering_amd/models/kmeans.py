@@ -35,7 +35,7 @@ import torch
 
 from ..config import ClusterConfig
 from ..data.stream import HostSource, ResidentSource, plan_chunk_rows, plan_resident_rows
-from ..ops import acc_dtype_for, lloyd_layout, make_lloyd_ops
+from ..ops import NativeUpdate, acc_dtype_for, lloyd_layout, make_lloyd_ops
 from ..parallel.dist import Comm, join_counts, local_comm
 from ..utils import faults
 from ..utils.checkpoint import RunCheckpointer
@@ -307,6 +307,13 @@ class LloydEngine(OomGuard):
         self.need_shift = cfg.tol > 0 or cfg.log_every > 0
         self.shift = torch.zeros(1, dtype=torch.float32, device=dev) if self.need_shift else None
         self.bucket_bytes = cfg.bucket_kb << 10
+        # resident sorted update: the step's zero fill of buf rides in the update's first
+        # kernel (one launch less per step; the small-shard step is launch-bound)
+        upd = getattr(self.local, "update", None)
+        self._zero_fused = (isinstance(upd, NativeUpdate) and upd.fuses_zero()
+                            and not self.streamed and type(self) is LloydEngine)
+        if self._zero_fused:
+            upd.zero_buf = self.buf
         self.n_iter = 0
         self.c0 = None
         if self.oom_guard:
@@ -381,7 +388,8 @@ class LloydEngine(OomGuard):
         return self._eager_step(with_inertia)
 
     def _eager_step(self, with_inertia: bool = False) -> Optional[float]:
-        self.buf.zero_()
+        if not self._zero_fused:
+            self.buf.zero_()
         mind = self.mind if (with_inertia and self.mind is not None) else None
         try:
             if self.oom_guard and not self._warming:
@@ -426,6 +434,7 @@ class LloydEngine(OomGuard):
                 self.local.bind(chunk).step(self.C, self.labels[s:e],
                                             None if mind is None else mind[s:e],
                                             self.sums, self.counts)
+            self.local.unbind()
 
     def _reduce_scatter_finalize(self):
         """rsag mode: reduce-scatter the sums (rank r gets centroid rows [r0, r0 + kr)),
@@ -507,6 +516,7 @@ class LloydEngine(OomGuard):
                 e = s + chunk.shape[0]
                 self.local.bind(chunk).assign(self.C, self.labels[s:e],
                                               None if self.mind is None else self.mind[s:e])
+            self.local.unbind()
         if self.mind is None:
             return None
         return self.comm.sum_scalar(float(self.mind.double().sum()))

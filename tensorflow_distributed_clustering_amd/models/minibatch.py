@@ -164,6 +164,7 @@ class MiniBatchStepper:
             s = start - self.source.row_offset
             e = s + chunk.shape[0]
             self.local.bind(chunk).assign(self.C, labels[s:e], mind[s:e])
+        self.local.unbind()
         return labels, self.comm.sum_scalar(float(mind.double().sum()))
 
 

@@ -123,13 +123,24 @@ class NativeUpdate:
         self.kind = "lds" if k * (d + 1) * es + 4 * k <= self.LDS_BUDGET else "sorted"
         self.work = None
         if self.kind == "sorted":
-            self.work = torch.empty(int(ops.update_sorted_workspace(n, k)), dtype=torch.int32,
-                                    device=device)
+            self.work = self._workspace(n, k, device)
+
+    @staticmethod
+    def _workspace(n, k, device):
+        # zero-filled once: the kernels leave its histogram part zeroed after every call
+        return torch.zeros(int(_native.require().update_sorted_workspace(n, k)),
+                           dtype=torch.int32, device=device)
 
     deterministic = False
     # (hi, lo) fp32 [K] views of the all-reduce buffer: exact count halves
     # (parallel/dist.split_counts), accumulated by the scan kernel of the sorted update
     count_split = None
+    # the engine's all-reduce buffer when the step's zero fill rides in the first update
+    # kernel (resident sorted path); consumed by the next call only
+    zero_buf = None
+
+    def fuses_zero(self) -> bool:
+        return self.kind == "sorted" and not self.deterministic
 
     def __call__(self, x, labels, sums, counts):
         if self.deterministic or self.kind == "lds":
@@ -142,9 +153,9 @@ class NativeUpdate:
                              *self.count_split)
             return
         if self.work.numel() < int(self.ops.update_sorted_workspace(x.shape[0], sums.shape[0])):
-            self.work = torch.empty(int(self.ops.update_sorted_workspace(x.shape[0], sums.shape[0])),
-                                    dtype=torch.int32, device=x.device)
-        self.ops.update_sorted(x, labels, sums, counts, self.work, *(self.count_split or (None, None)))
+            self.work = self._workspace(x.shape[0], sums.shape[0], x.device)
+        self.ops.update_sorted(x, labels, sums, counts, self.work, *(self.count_split or (None, None)),
+                               self.zero_buf)
 
 
     def supports_indexed(self) -> bool:
@@ -154,7 +165,7 @@ class NativeUpdate:
         """Partials of the rows ``x[rowidx]`` without gathering them (mini-batches)."""
         need = int(self.ops.update_sorted_workspace(rowidx.shape[0], sums.shape[0]))
         if self.work is None or self.work.numel() < need:
-            self.work = torch.empty(need, dtype=torch.int32, device=x.device)
+            self.work = self._workspace(rowidx.shape[0], sums.shape[0], x.device)
         self.ops.update_sorted_indexed(x, rowidx, labels, sums, counts, self.work,
                                        *(self.count_split or (None, None)))
 
@@ -200,6 +211,14 @@ class _LocalOpsBase:
         self.x = x
         self.n = x.shape[0]
         return self
+
+    def unbind(self):
+        """Drop the reference to the last streamed chunk: it is a view of the source's
+        device slot, which would otherwise stay allocated next to the next pass's slots."""
+        x = getattr(self, "x", None)
+        if isinstance(x, torch.Tensor) and x.numel():
+            self.x = x.new_empty((0,) + tuple(x.shape[1:]))
+            self.n = 0
 
     def prepare(self, C: torch.Tensor):
         """(Re)derive kernel operands from C (called after init / external edits)."""

@@ -226,6 +226,12 @@ def init_comm(device_type: Optional[str] = None, timeout_s: float = 600.0,
     force = os.environ.get("TDC_FORCE_COLLECTIVES", "0") == "1"
     if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1 and "MASTER_PORT" not in os.environ:
+            # a forced world-1 group (no launcher): any free local port
+            import socket
+            with socket.socket() as so:
+                so.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(so.getsockname()[1])
         kw = dict(backend=backend, init_method="env://", world_size=world, rank=rank,
                   timeout=datetime.timedelta(seconds=timeout_s))
         if device_type == "cuda" and backend == "nccl":

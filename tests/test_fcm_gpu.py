@@ -80,6 +80,44 @@ def test_fcm_mfma_matches_oracle(gpu, k, d, m, nz):
     assert torch.equal(lab, lab2)
 
 
+@pytest.mark.parametrize("k,d,m", [(32, 20, 8.0), (64, 24, 12.0), (48, 33, 10.0)])
+@pytest.mark.parametrize("nz", [True, False])
+def test_fcm_mfma_large_fuzzifier(gpu, k, d, m, nz):
+    """Large fuzzifiers on the MFMA tower: the bf16x3 distance error enters
+    t = d^(-2/(m-1)) scaled by 2/(m-1), so w = u^m carries ~2m/(m-1) ~ 2x the distance
+    error however large m is -- the m = 2 tolerance holds (no m-proportional slack)."""
+    from tensorflow_distributed_clustering_amd.ops import HipMfmaFCM
+    n = 20001
+    x, c = _data(n, k, d, 3 * k + d)
+    xg, cg = x.float().to(gpu), c.float().to(gpu)
+    ops = HipMfmaFCM(xg, k, m, nz)
+    lab = torch.empty(n, dtype=torch.int32, device=gpu)
+    wx = torch.zeros(k, d, dtype=torch.float64, device=gpu)
+    ws = torch.zeros(k, dtype=torch.float64, device=gpu)
+    ops.step(cg, lab, wx, ws)
+    _check(wx.cpu(), ws.cpu(), lab, xg.cpu(), cg.cpu(), m, nz, 4e-3, 0.998)
+
+
+@pytest.mark.parametrize("d,k,backend", [(20, 32, "hip_fcm_mfma"), (24, 40, "hip_fcm_tower")])
+def test_fcm_fit_reference_fuzzifier_m_equals_d(gpu, d, k, backend):
+    """fuzzifier=None (the reference's m = D) with dtype fp32: while the typical weight
+    K^-m stays in fp32's range (D=20, K=32: 2^-100) the fit runs on the MFMA tower; past it
+    (D=24, K=40: 2^-128, where every fp32 sum of u^m flushes to 0) the engine computes in
+    fp64 (exact tower).  Both follow the fp64 torch fit."""
+    import tensorflow_distributed_clustering_amd as tdc
+    from tensorflow_distributed_clustering_amd.data.synth import blob_centers, gaussian_blobs
+    x = gaussian_blobs(30000, d, k, seed=4, dtype=torch.float64, device=gpu)
+    c0 = blob_centers(k, d, 4) + 0.3
+    cfg = tdc.ClusterConfig(n_clusters=k, max_iter=4, dtype="fp32", init="given")
+    r = tdc.FuzzyCMeans(cfg).fit(x, init_centers_=c0).result_
+    assert r.backend == backend
+    o = tdc.FuzzyCMeans(cfg.replace(dtype="fp64", backend="torch"),
+                        device="cpu").fit(x.cpu(), init_centers_=c0).result_
+    tol = 3e-3 if backend == "hip_fcm_mfma" else 1e-8
+    torch.testing.assert_close(torch.as_tensor(r.centers), torch.as_tensor(o.centers),
+                               rtol=tol, atol=tol)
+
+
 @pytest.mark.parametrize("dtype,d,k,backend", [("fp64", 5, 32, "hip_fcm_small"),
                                                ("fp64", 5, 40, "hip_fcm_small"),
                                                ("fp64", 6, 40, "hip_fcm_tower"),

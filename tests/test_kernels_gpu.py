@@ -106,7 +106,7 @@ def test_update_sorted(gpu, xdt, n, d, k):
     x = torch.randn(n, d, generator=g).to(xdt).to(gpu)
     lab = torch.randint(0, k, (n,), generator=g, dtype=torch.int32).to(gpu)
     lab[: n // 3] = 1  # one long segment spanning many waves
-    work = torch.empty(int(ops.update_sorted_workspace(n, k)), dtype=torch.int32, device=gpu)
+    work = torch.zeros(int(ops.update_sorted_workspace(n, k)), dtype=torch.int32, device=gpu)
     s_ref, c_ref = ref.cluster_sums(x.double(), lab, k, acc_dtype=torch.float64)
     for acc in (torch.float32, torch.float64):
         sums = torch.zeros(k, d, dtype=acc, device=gpu)
@@ -116,6 +116,29 @@ def test_update_sorted(gpu, xdt, n, d, k):
         assert torch.equal(counts.double(), 2 * c_ref)
         tol = 1e-3 if acc == torch.float32 or xdt != torch.float64 else 1e-9
         torch.testing.assert_close(sums.double(), 2 * s_ref, rtol=tol, atol=tol * 10)
+
+
+@pytest.mark.parametrize("n,k", [(1_250_000, 1024), (40_000, 4096), (3000, 64)])
+def test_update_sorted_zero_first_and_clean_workspace(gpu, n, k):
+    """zero_first: the all-reduce buffer [sums | counts | tail] full of garbage is cleared by
+    the update's first kernel before anything accumulates (the engine's step needs no fill
+    launch); the workspace histogram is left zeroed for the next call."""
+    from tensorflow_distributed_clustering_amd import _native
+    ops = _native.require()
+    d = 128
+    g = torch.Generator().manual_seed(n + k)
+    x = torch.randn(n, d, generator=g).to(torch.bfloat16).to(gpu)
+    lab = torch.randint(0, k, (n,), generator=g, dtype=torch.int32).to(gpu)
+    work = torch.zeros(int(ops.update_sorted_workspace(n, k)), dtype=torch.int32, device=gpu)
+    buf = torch.full((k * d + k + 7,), 123.0, dtype=torch.float32, device=gpu)
+    sums, counts = buf[: k * d].view(k, d), buf[k * d: k * d + k]
+    ops.update_sorted(x, lab, sums, counts, work, None, None, buf)
+    torch.cuda.synchronize()
+    assert int(work[:k].abs().sum()) == 0
+    s_ref, c_ref = ref.cluster_sums(x.double(), lab, k, acc_dtype=torch.float64)
+    assert torch.equal(counts.double(), c_ref)
+    assert torch.equal(buf[k * d + k:], torch.zeros(7, device=gpu))
+    torch.testing.assert_close(sums.double(), s_ref, rtol=1e-3, atol=1e-2)
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.float64])
@@ -285,57 +308,6 @@ def test_native_kmeanspp_matches_torch_path(gpu):
     torch.testing.assert_close(native.cpu(), torch_path, rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("slices", [2, 4])
-def test_bf16_step_sliced_overlap(gpu, slices, monkeypatch):
-    """The resident bf16 step split into row slices, with each slice's update on a side
-    stream overlapping the next slice's assign, gives the same labels / counts / sums as
-    the unsliced step (and the fp64 oracle), eagerly and under hipGraph capture."""
-    import tensorflow_distributed_clustering_amd.ops as ops_mod
-    n, d, k = 2_100_000 + 77, 128, 1024
-    monkeypatch.setattr(ops_mod, "OVERLAP_MIN_ROWS", 1 << 18)
-    x, c = _bf16_case(n, d, k, gpu, seed=5)
-    lo = ops_mod.make_lloyd_ops(x, k, "bf16", "hip")
-    assert isinstance(lo, ops_mod.HipBf16Lloyd) and lo.update.kind == "sorted"
-    C = c.float().contiguous()
-    lo.prepare(C)
-    outs = []
-    for s in (1, slices):
-        monkeypatch.setattr(ops_mod, "OVERLAP_SLICES", s)
-        assert (lo._slices() is None) == (s == 1)
-        lab = torch.zeros(n, dtype=torch.int32, device=gpu)
-        sums = torch.zeros(k, d, dtype=torch.float32, device=gpu)
-        cnt = torch.zeros(k, dtype=torch.float32, device=gpu)
-        lo.step(C, lab, None, sums, cnt)
-        torch.cuda.synchronize()
-        outs.append((lab, sums, cnt))
-    (l1, s1, c1), (l2, s2, c2) = outs
-    assert torch.equal(l1, l2)
-    assert torch.equal(c1, c2) and int(c1.sum()) == n
-    torch.testing.assert_close(s2, s1, rtol=1e-4, atol=1e-2)
-    s_ref, c_ref = ref.cluster_sums(x.double(), l1, k, acc_dtype=torch.float64)
-    assert torch.equal(c1.double(), c_ref)
-    torch.testing.assert_close(s2.double(), s_ref, rtol=1e-4, atol=1e-2)
-    # the same sliced step captured into a hipGraph and replayed
-    lab = torch.zeros(n, dtype=torch.int32, device=gpu)
-    sums = torch.zeros(k, d, dtype=torch.float32, device=gpu)
-    cnt = torch.zeros(k, dtype=torch.float32, device=gpu)
-    side = torch.cuda.Stream(device=gpu)
-    side.wait_stream(torch.cuda.current_stream(gpu))
-    with torch.cuda.stream(side):
-        lo.step(C, lab, None, sums, cnt)  # warm-up outside capture
-    torch.cuda.current_stream(gpu).wait_stream(side)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        sums.zero_()
-        cnt.zero_()
-        lo.step(C, lab, None, sums, cnt)
-    lab.zero_()
-    g.replay()
-    torch.cuda.synchronize()
-    assert torch.equal(lab, l1) and torch.equal(cnt, c1)
-    torch.testing.assert_close(sums, s1, rtol=1e-4, atol=1e-2)
-
-
 @pytest.mark.parametrize("n,b,d,k", [(50000, 20000, 128, 1024), (30000, 7777, 64, 4096),
                                      (20000, 5000, 256, 300)])
 def test_indexed_assign_and_update(gpu, n, b, d, k):
@@ -359,7 +331,7 @@ def test_indexed_assign_and_update(gpu, n, b, d, k):
     ops.assign_bf16(xb, lo.cm2, lo.cnorm, lab_g, md_g)
     assert torch.equal(lab_i, lab_g)
     assert torch.equal(md_i, md_g)
-    work = torch.empty(int(ops.update_sorted_workspace(b, k)), dtype=torch.int32, device=gpu)
+    work = torch.zeros(int(ops.update_sorted_workspace(b, k)), dtype=torch.int32, device=gpu)
     s_i = torch.zeros(k, d, dtype=torch.float32, device=gpu)
     c_i = torch.zeros(k, dtype=torch.float32, device=gpu)
     ops.update_sorted_indexed(lo.x, idx, lab_i, s_i, c_i, work)
