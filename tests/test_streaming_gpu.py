@@ -195,7 +195,7 @@ def test_fp64_kmeans_larger_than_budget_streams_from_host(gpu):
     """fp64 K-Means (the reference's dtype) with an HBM budget below the shard: the rows
     stay in host memory and stream through the RowStreamer's pinned ring (f64 rows as they
     are) into the fused fp64 kernel; same centres as the resident fit to 1e-9, and the
-    device never holds the shard (peak allocation < the shard's bytes)."""
+    device never holds the shard (peak allocation well below the shard's bytes)."""
     x, c0 = _fp64_shard()
     cfg = tdc.ClusterConfig(n_clusters=16, max_iter=5, dtype="fp64", init="given")
     res = tdc.KMeans(cfg, device=gpu).fit(x, init_centers_=c0).result_
@@ -210,7 +210,7 @@ def test_fp64_kmeans_larger_than_budget_streams_from_host(gpu):
     peak = torch.cuda.max_memory_allocated(gpu) - base
     assert st.streamed and not res.streamed and st.backend == res.backend
     np.testing.assert_allclose(st.centers, res.centers, rtol=1e-9, atol=1e-9)
-    assert peak < x.nbytes // 2, (peak, x.nbytes)
+    assert peak < 0.7 * x.nbytes, (peak, x.nbytes)
 
 
 @pytest.mark.parametrize("fault", ["oom@setup", "oom@3"])
@@ -235,9 +235,11 @@ def test_fp64_kmeans_oom_falls_back_to_host_streaming(gpu, monkeypatch, fault):
     assert r.streamed
     np.testing.assert_allclose(r.centers, ref_c, rtol=1e-9, atol=1e-9)
     torch.cuda.synchronize(gpu)
+    # the retry streams quarter-shard chunks through two device slots (half the shard)
+    # next to the per-row labels / min distances (12 of the 128 bytes per row)
     now = torch.cuda.memory_allocated(gpu) - base
-    assert now < x.nbytes // 2, (now, x.nbytes)
+    assert now < 0.7 * x.nbytes, (now, x.nbytes)
     if fault == "oom@setup":
-        assert torch.cuda.max_memory_allocated(gpu) - base < x.nbytes // 2
+        assert torch.cuda.max_memory_allocated(gpu) - base < 0.7 * x.nbytes
     else:
         assert all(w() is None for w in m._retired)
