@@ -284,6 +284,44 @@ void fcm_tower_accum(const at::Tensor& X, const at::Tensor& C, double m, bool na
         "fcm_tower_accum");
 }
 
+// pass 0: G = d2 of the chunk X against C; 1: labels + G <- w; 3: labels only; 2: wx/ws +=
+void fcm_wide(int64_t pass, const at::Tensor& X, const at::Tensor& C, double m, bool nan_to_zero,
+              at::Tensor& G, const std::optional<at::Tensor>& labels,
+              const std::optional<at::Tensor>& wx, const std::optional<at::Tensor>& ws) {
+  check_cuda(X, "X");
+  check_rows(X, "X");
+  TORCH_CHECK(X.scalar_type() == at::kFloat || X.scalar_type() == at::kDouble,
+              "tdc.fcm_wide: X fp32/fp64");
+  TORCH_CHECK(C.scalar_type() == X.scalar_type() && C.is_contiguous() && C.dim() == 2 &&
+                  C.size(1) == X.size(1), "tdc.fcm_wide: C [K, D] in the X dtype");
+  const int64_t M = X.size(0), K = C.size(0);
+  TORCH_CHECK(G.scalar_type() == X.scalar_type() && G.is_contiguous() && G.numel() >= M * K,
+              "tdc.fcm_wide: G [M, K] in the X dtype");
+  TORCH_CHECK(m > 1.0, "tdc.fcm_wide: fuzzifier must be > 1");
+  int32_t* lab = nullptr;
+  if (pass == 1 || pass == 3) {
+    TORCH_CHECK(labels.has_value() && labels->defined() && labels->scalar_type() == at::kInt &&
+                    labels->is_contiguous() && labels->numel() >= M,
+                "tdc.fcm_wide: labels int32 [M]");
+    lab = labels->data_ptr<int32_t>();
+  }
+  double *pwx = nullptr, *pws = nullptr;
+  if (pass == 2) {
+    TORCH_CHECK(wx.has_value() && ws.has_value() && wx->scalar_type() == at::kDouble &&
+                    ws->scalar_type() == at::kDouble && wx->is_contiguous() &&
+                    ws->is_contiguous() && wx->numel() == C.numel() && ws->numel() == K,
+                "tdc.fcm_wide: wx [K, D] / ws [K] fp64");
+    pwx = wx->data_ptr<double>();
+    pws = ws->data_ptr<double>();
+  }
+  TORCH_CHECK(pass >= 0 && pass <= 3, "tdc.fcm_wide: pass 0..3");
+  const DevGuard guard(X.device());
+  check(tdc_fcm_wide((int)pass, dcode(X.scalar_type()), X.data_ptr(), M, X.stride(0),
+                     (int)X.size(1), C.data_ptr(), (int)K, m, nan_to_zero ? 1 : 0, G.data_ptr(),
+                     lab, pwx, pws, num_cus(X.device().index()), cur_stream()),
+        "fcm_wide");
+}
+
 void fcm_split_rows(const at::Tensor& src, int64_t valid, int64_t neg2, at::Tensor& hi,
                     at::Tensor& lo, const std::optional<at::Tensor>& norm,
                     const std::optional<at::Tensor>& shift) {
@@ -376,29 +414,6 @@ void fcm_mfma_accum(const at::Tensor& Xh, const at::Tensor& Xl, const at::Tensor
 
 int64_t fcm_mfma_workspace(const at::Tensor& like, int64_t N, int64_t K, int64_t Kp, int64_t DP) {
   return tdc_fcm_mfma_workspace(N, (int)K, (int)Kp, (int)DP, num_cus(like.device().index()));
-}
-
-void fcm_rows(at::Tensor& G, const at::Tensor& xx, const std::optional<at::Tensor>& cc, double m,
-              bool nan_to_zero, at::Tensor& labels, const std::optional<at::Tensor>& colsum) {
-  check_cuda(G, "G");
-  TORCH_CHECK(G.scalar_type() == at::kFloat && G.dim() == 2 && G.is_contiguous(),
-              "tdc.fcm_rows: G fp32 contiguous [rows, K]");
-  const int64_t rows = G.size(0), K = G.size(1);
-  TORCH_CHECK(xx.scalar_type() == at::kFloat && xx.is_contiguous() && xx.numel() == rows,
-              "tdc.fcm_rows: xx fp32 [rows]");
-  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous() && labels.numel() == rows,
-              "tdc.fcm_rows: labels int32 [rows]");
-  for (const auto* t : {&cc, &colsum})
-    if (t->has_value() && (*t)->defined())
-      TORCH_CHECK((*t)->scalar_type() == at::kFloat && (*t)->is_contiguous() && (*t)->numel() == K,
-                  "tdc.fcm_rows: cc/colsum fp32 [K]");
-  TORCH_CHECK(m > 1.0, "tdc.fcm_rows: fuzzifier must be > 1");
-  const DevGuard guard(G.device());
-  check(tdc_fcm_rows(G.data_ptr<float>(), rows, (int)K, xx.data_ptr<float>(),
-                     static_cast<const float*>(opt_ptr(cc)), (float)m, nan_to_zero ? 1 : 0,
-                     labels.data_ptr<int32_t>(), static_cast<float*>(opt_ptr(colsum)),
-                     cur_stream()),
-        "fcm_rows");
 }
 
 void finalize(const std::optional<at::Tensor>& sums, const std::optional<at::Tensor>& counts,
@@ -784,11 +799,11 @@ TORCH_LIBRARY(tdc, m) {
   m.def("fcm_small(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!)? labels, Tensor(b!) wx, Tensor(c!) ws) -> ()");
   m.def("fcm_tower_stats(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) rowinfo) -> ()");
   m.def("fcm_tower_accum(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor rowinfo, Tensor(a!) wx, Tensor(b!) ws) -> ()");
+  m.def("fcm_wide(int stage, Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!) G, Tensor(b!)? labels=None, Tensor(c!)? wx=None, Tensor(d!)? ws=None) -> ()");
   m.def("fcm_split_rows(Tensor src, int valid, int neg2, Tensor(a!) hi, Tensor(b!) lo, Tensor(c!)? norm, Tensor? shift=None) -> ()");
   m.def("fcm_mfma_stats(Tensor Xh, Tensor Xl, Tensor xx, Tensor Ch, Tensor Cl, Tensor cc, int K, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) rowinfo) -> ()");
   m.def("fcm_mfma_accum(Tensor Xh, Tensor Xl, Tensor xx, Tensor rowinfo, Tensor Ch, Tensor Cl, Tensor cc, int K, float m, bool nan_to_zero, Tensor(a!) wx, Tensor(b!) ws, Tensor(c!) work, Tensor? shift=None) -> ()");
   m.def("fcm_mfma_workspace(Tensor like, int N, int K, int Kp, int DP) -> int");
-  m.def("fcm_rows(Tensor(a!) G, Tensor xx, Tensor? cc, float m, bool nan_to_zero, Tensor(b!) labels, Tensor(c!)? colsum=None) -> ()");
   m.def("assign_bigd_supported(ScalarType dtype, int DP) -> bool", &assign_bigd_supported);
   m.def("assign_bigd(Tensor X, Tensor? Xs, Tensor xnorm, Tensor Cm2, Tensor? Cs, Tensor cnorm, int kg_tiles, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!)? keys, Tensor(d!)? labels2=None, Tensor(e!)? mind2=None) -> ()");
   m.def("recheck_top2(Tensor X, Tensor C, Tensor(a!) labels, Tensor labels2, Tensor d1, Tensor d2, float tau) -> int");
@@ -811,13 +826,13 @@ TORCH_LIBRARY_IMPL(tdc, CUDA, m) {
   m.impl("update", &update);
   m.impl("update_sorted", &update_sorted);
   m.impl("fcm_small", &fcm_small);
-  m.impl("fcm_rows", &fcm_rows);
   m.impl("fcm_tower_stats", &fcm_tower_stats);
   m.impl("fcm_split_rows", &fcm_split_rows);
   m.impl("fcm_mfma_stats", &fcm_mfma_stats);
   m.impl("fcm_mfma_accum", &fcm_mfma_accum);
   m.impl("fcm_mfma_workspace", &fcm_mfma_workspace);
   m.impl("fcm_tower_accum", &fcm_tower_accum);
+  m.impl("fcm_wide", &fcm_wide);
   m.impl("finalize", &finalize);
   m.impl("assign_bigd", &assign_bigd);
   m.impl("recheck_top2", &recheck_top2);

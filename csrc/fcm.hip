@@ -242,141 +242,3 @@ int tdc_fcm_small(int dtype, int acc_dtype, const void* X, int64_t N, int64_t ld
     return dispatch_fcm<double, double>(X, N, ldx, D, C, K, m, nan_to_zero, labels, wx, ws, s);
   return (int)hipErrorInvalidValue;
 }
-
-// ------------------------------------------------------------------------------------
-// N4 for large K*D (HipGemmFCM, ops/__init__.py): the GEMM terms run on hipBLASLt and this
-// kernel is the whole elementwise middle of the FCM tower (`distribuitedClustering.py:
-// 117-148`), one wave per row, in place on G = ||c||^2 - 2 x.c [rows, K] (fp32):
-//   d2 = max(G + ||x||^2, 0);  t = d2^(-1/(m-1)) (= d^(-2/(m-1)));  u = t / sum_k t
-//   nan_to_zero: NaN (a row on a centroid: inf/inf) -> 0, else the one-hot of the zero
-//   distances;  G <- w = u^m;  labels = argmax_k u (first index on ties).
-// Two sweeps over the row (t is stored in G by the first); the row stays in L2.
-// ------------------------------------------------------------------------------------
-namespace tdc {
-
-// NV > 0: the row is held in registers (NV values per lane, K <= 64*NV): one read and one
-// write of G.  NV == 0: any K, t is stored in G between the two sweeps.
-// cc (nullable): ||c||^2 added here (G then holds only -2 x.c, so the GEMM needs no
-// broadcast bias copy).  colsum (nullable, zeroed by the caller): += sum over rows of w
-// (the FCM denominators); a lane owns columns lane + 64v across all the rows its wave
-// visits, so NV > 0 flushes one atomic per column per wave.
-template <int NV>
-__global__ __launch_bounds__(256) void fcm_rows_kernel(float* __restrict__ G, int64_t rows, int K,
-                                                       const float* __restrict__ xx,
-                                                       const float* __restrict__ cc, float m,
-                                                       int nan_to_zero,
-                                                       int32_t* __restrict__ labels,
-                                                       float* __restrict__ colsum) {
-  const int lane = threadIdx.x & 63;
-  const float e = -1.0f / (m - 1.0f);
-  constexpr int NR = NV > 0 ? NV : 1;
-  float ccr[NR], csum[NR];
-#pragma unroll
-  for (int v = 0; v < NR; ++v) {
-    const int k = v * 64 + lane;
-    ccr[v] = (NV > 0 && cc && k < K) ? cc[k] : 0.f;
-    csum[v] = 0.f;
-  }
-  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows;
-       row += (int64_t)gridDim.x * 4) {  // wave-uniform
-    float* g = G + row * (int64_t)K;
-    const float x2 = xx[row];
-    float sum = 0.f, best = INFINITY;
-    int bk = 0, nzero = 0;
-    float tr[NR];
-    auto visit = [&](int k, float gv) __attribute__((always_inline)) {
-      const float d2 = fmaxf(gv + x2, 0.f);
-      const float t = exp2f(log2f(d2) * e);  // d2 = 0 -> +inf
-      sum += t;
-      nzero += d2 == 0.f;
-      if (d2 < best) { best = d2; bk = k; }  // lane-local: ascending k, first wins
-      return t;
-    };
-    if constexpr (NV > 0) {
-#pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        const int k = v * 64 + lane;
-        tr[v] = k < K ? g[k] : 0.f;
-      }
-#pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        const int k = v * 64 + lane;
-        if (k < K) tr[v] = visit(k, tr[v] + ccr[v]);
-      }
-    } else {
-      for (int k = lane; k < K; k += 64) g[k] = visit(k, g[k] + (cc ? cc[k] : 0.f));
-    }
-    sum = wave_sum(sum);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ob = __shfl_xor(best, o, 64);
-      const int ok = __shfl_xor(bk, o, 64);
-      if (ob < best || (ob == best && ok < bk)) { best = ob; bk = ok; }
-      nzero += __shfl_xor(nzero, o, 64);
-    }
-    // on-centroid row (sum = inf): u = inf/inf = NaN on the zero distances, 0 elsewhere
-    const bool oncen = nzero > 0;
-    const float inv = 1.0f / sum;
-    const float onehot = oncen ? 1.0f / (float)nzero : 0.f;
-    auto weight = [&](float t) __attribute__((always_inline)) {
-      float u;
-      if (!oncen) u = t * inv;
-      else if (nan_to_zero) u = 0.f;
-      else u = isinf(t) ? onehot : 0.f;
-      return u > 0.f ? exp2f(log2f(u) * m) : 0.f;
-    };
-    if constexpr (NV > 0) {
-#pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        const int k = v * 64 + lane;
-        if (k < K) {
-          const float w = weight(tr[v]);
-          g[k] = w;
-          csum[v] += w;
-        }
-      }
-    } else {
-      for (int k = lane; k < K; k += 64) {
-        const float w = weight(g[k]);
-        g[k] = w;
-        if (colsum && w != 0.f) atomicAdd(colsum + k, w);
-      }
-    }
-    // argmax u = argmin d2; an all-zero row (nan_to_zero on a centroid) -> index 0
-    if (lane == 0) labels[row] = (oncen && nan_to_zero) ? 0 : bk;
-  }
-  if constexpr (NV > 0) {
-    if (colsum) {
-#pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        const int k = v * 64 + lane;
-        if (k < K && csum[v] != 0.f) atomicAdd(colsum + k, csum[v]);
-      }
-    }
-  }
-}
-
-}  // namespace tdc
-
-int tdc_fcm_rows(float* G, int64_t rows, int K, const float* xx, const float* cc, float m,
-                 int nan_to_zero, int32_t* labels, float* colsum, hipStream_t s) {
-  if (rows <= 0) return 0;
-  // persistent waves, exactly the blocks resident at once (every block the same row
-  // count, so a larger grid would leave a partial second round); the column-sum flush is
-  // one atomic per column per block
-  const int64_t want = (rows + 3) / 4;
-#define TDC_FR(NVV)                                                                           \
-  do {                                                                                        \
-    static const int res = resident_blocks(tdc::fcm_rows_kernel<NVV>, 256);                   \
-    const dim3 grid((unsigned)(want < res ? want : res));                                     \
-    hipLaunchKernelGGL(tdc::fcm_rows_kernel<NVV>, grid, dim3(256), 0, s, G, rows, K, xx, cc,  \
-                       m, nan_to_zero, labels, colsum);                                       \
-  } while (0)
-  if (K <= 256) TDC_FR(4);
-  else if (K <= 1024) TDC_FR(16);
-  else if (K <= 2048) TDC_FR(32);
-  else TDC_FR(0);
-#undef TDC_FR
-  TDC_CHECK_LAUNCH();
-  return 0;
-}

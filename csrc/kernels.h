@@ -82,11 +82,6 @@ int tdc_fcm_small(int dtype, int acc_dtype, const void* X, int64_t N, int64_t ld
                   const void* C, int K, double m, int nan_to_zero, int32_t* labels, void* wx,
                   void* ws, hipStream_t stream);
 int tdc_fcm_small_supported(int dtype, int K, int D);
-// FCM memberships for large K*D, in place on G = -2 x.c (+ ||c||^2 if cc is null) (fp32
-// [rows, K]): G <- w = u^m, labels = argmax u, colsum (nullable, [K]) += sum_rows w.
-// xx = ||x||^2 [rows], cc = ||c||^2 [K] (nullable).
-int tdc_fcm_rows(float* G, int64_t rows, int K, const float* xx, const float* cc, float m,
-                 int nan_to_zero, int32_t* labels, float* colsum, hipStream_t stream);
 
 // N4/N5 for any K and D <= 256 (fp32 / fp64, exact difference-form distances), two passes:
 // pass 0 (stats): labels = argmax_k u, rowinfo [N] (X dtype) = 1/sum_k t (> 0), 0 (all
@@ -95,6 +90,14 @@ int tdc_fcm_rows(float* G, int64_t rows, int K, const float* xx, const float* cc
 int tdc_fcm_tower(int pass, int dtype, const void* X, int64_t N, int64_t ldx, int D, const void* C,
                   int K, double m, int nan_to_zero, int32_t* labels, void* rowinfo, void* wx,
                   void* ws, int num_cus, hipStream_t stream);
+
+// N4/N5 for any D (fp32 / fp64, exact difference form) over a row chunk of M rows with the
+// [M, K] block G (X dtype) in HBM: pass 0: G = d2; pass 1: labels = argmax u and G <- w =
+// u^m in place (rowinfo semantics as tdc_fcm_tower); pass 3: labels only (G keeps d2);
+// pass 2: wx [K, D] += W^T X, ws [K] += sum W (fp64, accumulated).
+int tdc_fcm_wide(int pass, int dtype, const void* X, int64_t M, int64_t ldx, int D, const void* C,
+                 int K, double m, int nan_to_zero, void* G, int32_t* labels, double* wx, double* ws,
+                 int num_cus, hipStream_t stream);
 
 // N4/N5 on MFMA (fp32 FCM, large K x D): hi/lo bf16 operands.  split_rows: fp32 rows
 // [rows, ld] (d valid columns, rows >= valid are zero padding) -> hi/lo bf16 [rows, DP]

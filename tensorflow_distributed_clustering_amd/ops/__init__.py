@@ -901,71 +901,49 @@ class HipMfmaFCM(_LocalOpsBase):
         self.ops.finalize(sums, counts, C, 0, shift, None, None)
 
 
-class HipGemmFCM(_LocalOpsBase):
-    """FCM for large K*D: fp32 library GEMMs (hipBLASLt) for ``-2 X C^T`` and ``W^T X``
-    around the fused ``fcm_rows`` HIP kernel (distances -> memberships -> u^m -> labels in
-    place, no host syncs), in row chunks of up to ``chunk_elems`` [rows, K] elements."""
-    name = "hip_fcm_gemm"
-    chunk_elems = 1 << 28  # 1 GiB fp32 membership block per chunk
+class HipWideFCM(_LocalOpsBase):
+    """FCM for any D in fp32 / fp64 (csrc/fcm_wide.hip): exact difference-form distances of a
+    row chunk into the [rows, K] block G (the only intermediate, up to ``chunk_elems``
+    elements), memberships w = u^m in place, then W^T X and sum W -- three native kernels
+    per chunk, no library GEMM.  Takes over from fcm_tower (D <= 256) and the MFMA tower
+    (fp32, D <= 128) past their register / LDS budgets."""
+    name = "hip_fcm_wide"
+    chunk_elems = 1 << 27
 
-    def __init__(self, x, k, m=2.0, nan_to_zero=True):
+    def __init__(self, x, k, dtype="fp64", m=2.0, nan_to_zero=True):
         super().__init__(x, k, "keep")
         self.ops = _native.require()
-        self.x = x.to(torch.float32).contiguous()
-        self.c_dtype = torch.float32
+        tdt = torch.float64 if dtype == "fp64" else torch.float32
+        self.x = x.to(tdt).contiguous()
+        self.c_dtype = tdt
         self.m = float(m)
         self.nan_to_zero = bool(nan_to_zero)
-        self.xx = (self.x * self.x).sum(1)
-        self.rows = max(1, min(self.n, self.chunk_elems // max(1, k)))
-        self.G = torch.empty(self.rows, k, dtype=torch.float32, device=self.device)
-        self.wx32 = torch.empty(k, self.d, dtype=torch.float32, device=self.device)
-        self.ws32 = torch.empty(k, dtype=torch.float32, device=self.device)
-        # W^T X has a [K, D] output and a reduction over the chunk's rows: as one GEMM it
-        # is a handful of output tiles (887 us per 256K x 1024 x 128 chunk).  Split the rows
-        # into S batched GEMMs (partials <= 64 MiB) and sum the partials.
-        self.splits = max(1, min(64, (1 << 24) // max(1, k * self.d)))
-        self.part = (torch.empty(self.splits, k, self.d, dtype=torch.float32, device=self.device)
-                     if self.splits > 1 else None)
+        self.G = None
 
-    def _wtx(self, w, xs):
-        r, S = w.shape[0], self.splits
-        q = r // S if S > 1 else 0
-        if q < 1024:
-            torch.mm(w.t(), xs, out=self.wx32)
-            return
-        body = S * q
-        torch.bmm(w[:body].view(S, q, self.k).transpose(1, 2), xs[:body].view(S, q, self.d),
-                  out=self.part)
-        torch.sum(self.part, 0, out=self.wx32)
-        if body < r:
-            self.wx32.addmm_(w[body:].t(), xs[body:])
-
-    def _memberships(self, C, s, e, labels, colsum=None):
-        xs, g = self.x[s:e], self.G[: e - s]
-        torch.mm(xs, C.t(), out=g)
-        self.ops.fcm_rows(g, self.xx[s:e], self.cc, self.m, self.nan_to_zero, labels[s:e],
-                          colsum)
-        return xs, g
-
-    def _prep(self, C):
-        C = C.to(torch.float32)
-        self.cc = (C * C).sum(1)
-        return (-2.0 * C).contiguous()  # G = x.(-2c): the GEMM writes -2 x.c directly
+    def _block(self):
+        rows = max(1, min(self.n, self.chunk_elems // max(1, self.k)))
+        if self.G is None or self.G.shape[0] < rows:
+            self.G = torch.empty(rows, self.k, dtype=self.c_dtype, device=self.device)
+        return rows
 
     def step(self, C, labels, wx, ws):
-        C2 = self._prep(C)
-        for s in range(0, self.n, self.rows):
-            e = min(self.n, s + self.rows)
-            self.ws32.zero_()
-            xs, w = self._memberships(C2, s, e, labels, self.ws32)  # + sum_i w_ki (fp32)
-            self._wtx(w, xs)                     # sum_i w_ki x_i of the chunk (fp32)
-            wx.add_(self.wx32)                   # fp64 totals across chunks / ranks
-            ws.add_(self.ws32)
+        C = C.to(self.c_dtype).contiguous()
+        rows = self._block()
+        for s in range(0, self.n, rows):
+            e = min(self.n, s + rows)
+            xs, g = self.x[s:e], self.G[: e - s]
+            self.ops.fcm_wide(0, xs, C, self.m, self.nan_to_zero, g)
+            self.ops.fcm_wide(1, xs, C, self.m, self.nan_to_zero, g, labels[s:e])
+            self.ops.fcm_wide(2, xs, C, self.m, self.nan_to_zero, g, None, wx, ws)
 
     def assign(self, C, labels):
-        C2 = self._prep(C)
-        for s in range(0, self.n, self.rows):
-            self._memberships(C2, s, min(self.n, s + self.rows), labels)
+        C = C.to(self.c_dtype).contiguous()
+        rows = self._block()
+        for s in range(0, self.n, rows):
+            e = min(self.n, s + rows)
+            xs, g = self.x[s:e], self.G[: e - s]
+            self.ops.fcm_wide(0, xs, C, self.m, self.nan_to_zero, g)
+            self.ops.fcm_wide(3, xs, C, self.m, self.nan_to_zero, g, labels[s:e])
 
     def finalize(self, sums, counts, C, shift):
         self.ops.finalize(sums, counts, C, 0, shift, None, None)
@@ -985,6 +963,4 @@ def make_fcm_ops(x: torch.Tensor, k: int, dtype: str = "fp64", m: float = 2.0,
         return HipMfmaFCM(x, k, m, nan_to_zero)
     if d <= 256:
         return HipTowerFCM(x, k, dtype, m, nan_to_zero)
-    if dtype == "fp32":
-        return HipGemmFCM(x, k, m, nan_to_zero)
-    return TorchFCM(x, k, dtype, m, nan_to_zero)
+    return HipWideFCM(x, k, dtype, m, nan_to_zero)

@@ -118,8 +118,47 @@ def test_fcm_fit_reference_fuzzifier_m_equals_d(gpu, d, k, backend):
                                rtol=tol, atol=tol)
 
 
+@pytest.mark.parametrize("dt", [torch.float64, torch.float32])
+@pytest.mark.parametrize("k,d", [(100, 384), (257, 768), (40, 300), (1030, 1024)])
+@pytest.mark.parametrize("nz", [True, False])
+def test_fcm_wide_matches_oracle(gpu, dt, k, d, nz):
+    """D > 256 (past the register towers): the native wide tower -- exact difference-form
+    distances of a row chunk into [rows, K], memberships in place, W^T X -- against the fp64
+    oracle, over several chunks with a ragged tail (a point exactly on a centroid included)."""
+    from tensorflow_distributed_clustering_amd.ops import HipWideFCM, make_fcm_ops
+    n = 6001
+    m = 2.0 if d != 300 else 3.0
+    x, c = _data(n, k, d, k * 3 + d)
+    xg, cg = x.to(dt).to(gpu), c.to(dt).to(gpu)
+    ops = make_fcm_ops(xg, k, "fp64" if dt == torch.float64 else "fp32", m, nz)
+    assert isinstance(ops, HipWideFCM)
+    ops.chunk_elems = 2500 * k  # 3 chunks, the last ragged
+    lab = torch.empty(n, dtype=torch.int32, device=gpu)
+    wx = torch.zeros(k, d, dtype=torch.float64, device=gpu)
+    ws = torch.zeros(k, dtype=torch.float64, device=gpu)
+    ops.step(cg, lab, wx, ws)
+    rtol = 1e-9 if dt == torch.float64 else 2e-4 * m
+    _check(wx.cpu(), ws.cpu(), lab, xg.cpu(), cg.cpu(), m, nz, rtol,
+           0.99999 if dt == torch.float64 else 0.999)
+    lab2 = torch.full_like(lab, -1)
+    ops.assign(cg, lab2)
+    assert torch.equal(lab, lab2)
+
+
+def test_fcm_dispatch_native_up_to_1024(gpu):
+    """No GPU FCM shape up to D = 1024 falls back to a library GEMM or plain PyTorch."""
+    from tensorflow_distributed_clustering_amd.ops import make_fcm_ops
+    for dtype in ("fp32", "fp64"):
+        for d in (3, 17, 100, 200, 256, 300, 512, 768, 1024):
+            for k in (3, 40, 300):
+                ops = make_fcm_ops(torch.zeros(64, d, device=gpu), k, dtype, 2.0)
+                assert ops.name.startswith("hip_fcm_"), (dtype, d, k, ops.name)
+
+
 @pytest.mark.parametrize("dtype,d,k,backend", [("fp64", 5, 32, "hip_fcm_small"),
                                                ("fp64", 5, 40, "hip_fcm_small"),
+                                               ("fp64", 384, 50, "hip_fcm_wide"),
+                                               ("fp32", 512, 64, "hip_fcm_wide"),
                                                ("fp64", 6, 40, "hip_fcm_tower"),
                                                ("fp64", 64, 100, "hip_fcm_tower"),
                                                ("fp32", 12, 64, "hip_fcm_tower"),

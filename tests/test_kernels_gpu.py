@@ -475,72 +475,6 @@ def test_bounds_filter_and_scatter(gpu, off):
     torch.testing.assert_close(ub[act.long()], d1.sqrt())
 
 
-@pytest.mark.parametrize("m", [2.0, 5.0, 64.0])
-@pytest.mark.parametrize("nan_to_zero", [True, False])
-@pytest.mark.parametrize("k", [200, 777, 2100])  # register rows (NV=4, 16) and the G-resident sweep
-def test_fcm_rows_kernel(gpu, m, nan_to_zero, k):
-    """fused FCM membership rows (HipGemmFCM) vs the fp64 formula on the same distances,
-    incl. a row on a centroid (exact zero distances) for both NaN policies."""
-    from tensorflow_distributed_clustering_amd import _native
-    ops = _native.require()
-    g = torch.Generator().manual_seed(3)
-    rows = 1000  # K not a multiple of 64
-    d2 = torch.rand(rows, k, generator=g, dtype=torch.float64) * 4 + 0.01
-    d2[7, 5] = 0.0
-    d2[9, 3] = d2[9, k - 100] = 0.0
-    xx = torch.rand(rows, generator=g, dtype=torch.float64)
-    xx[7] = xx[9] = 0.0
-    G = (d2 - xx[:, None]).float()
-    G[7], G[9] = d2[7].float(), d2[9].float()  # exact zeros survive the fp32 round trip
-    d2f = (G.double() + xx.float().double()[:, None]).clamp_min(0)
-    t = d2f.pow(-1.0 / (m - 1.0))
-    u = t / t.sum(1, keepdim=True)
-    bad = torch.isnan(u)
-    if nan_to_zero:
-        u = torch.where(bad, torch.zeros_like(u), u)
-    else:
-        z = d2f == 0
-        oh = z.double() / z.sum(1, keepdim=True).clamp_min(1)
-        u = torch.where(z.any(1, keepdim=True), oh, u)
-    want_w, want_lab = u.pow(m), u.argmax(1).to(torch.int32)
-    Gd, lab = G.to(gpu), torch.empty(rows, dtype=torch.int32, device=gpu)
-    colsum = torch.zeros(k, dtype=torch.float32, device=gpu)
-    ops.fcm_rows(Gd, xx.float().to(gpu), None, m, nan_to_zero, lab, colsum)
-    torch.testing.assert_close(Gd.double().cpu(), want_w, rtol=2e-4 * m, atol=1e-6)
-    torch.testing.assert_close(colsum.double().cpu(), want_w.sum(0), rtol=2e-4 * m, atol=1e-4)
-    assert torch.equal(lab.cpu(), want_lab)
-    # ||c||^2 passed separately: same result from G - cc
-    cc = torch.rand(k, generator=g, dtype=torch.float64).float()
-    G2, lab2 = (G - cc[None, :]).to(gpu), torch.empty(rows, dtype=torch.int32, device=gpu)
-    G2[7], G2[9] = (G[7] - cc).to(gpu), (G[9] - cc).to(gpu)
-    ops.fcm_rows(G2, xx.float().to(gpu), cc.to(gpu), m, nan_to_zero, lab2)
-    ok = torch.ones(rows, dtype=torch.bool)
-    ok[7] = ok[9] = False  # G - cc + cc need not be exactly 0 again
-    torch.testing.assert_close(G2.double().cpu()[ok], want_w[ok], rtol=2e-4 * m, atol=1e-5)
-
-
-@pytest.mark.parametrize("m", [2.0, 32.0])
-def test_hip_gemm_fcm_step_matches_reference(gpu, m):
-    from tensorflow_distributed_clustering_amd.ops import HipGemmFCM
-    g = torch.Generator().manual_seed(5)
-    n, d, k = 30000, 32, 300
-    x = torch.randn(n, d, generator=g, dtype=torch.float64)
-    c = x[torch.randperm(n, generator=g)[:k]] + 0.01
-    x32, c32 = x.float().to(gpu), c.float().to(gpu)
-    ops = HipGemmFCM(x32, k, m)  # the library-GEMM FCM (selected for D > 128 fp32 only)
-    ops.rows = 17001  # several chunks incl. a ragged tail
-    assert ops.splits > 1  # batched W^T X with a remainder (17001 = 16 * 1062 + 9)
-    ops.splits, ops.part = 16, ops.part[:16]
-    labels = torch.empty(n, dtype=torch.int32, device=gpu)
-    wx = torch.zeros(k, d, dtype=torch.float64, device=gpu)
-    ws = torch.zeros(k, dtype=torch.float64, device=gpu)
-    ops.step(c32, labels, wx, ws)
-    a, b, lr = ref.fcm_partial(x32.double(), c32.double(), m, True)
-    torch.testing.assert_close(ws, b, rtol=5e-4 * m, atol=1e-6 * n)
-    torch.testing.assert_close(wx, a, rtol=5e-4 * m, atol=1e-5 * n)
-    assert (labels == lr).double().mean().item() > 0.999
-
-
 @pytest.mark.parametrize("dt", [torch.float32, torch.float64])
 @pytest.mark.parametrize("n,d,k", [(5000, 96, 100), (4001, 128, 1000), (3000, 256, 130),
                                    (2000, 768, 257), (1500, 33, 65)])
