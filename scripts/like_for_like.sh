@@ -6,6 +6,7 @@
 # rocprofv3 trace per run -- the like-for-like of scripts/executions_log.csv.
 #
 #   scripts/like_for_like.sh OUTDIR [GPU counts...]      (default: 1 2 3 4 5 6 7 8)
+#   DTYPES=fp32 scripts/like_for_like.sh OUTDIR 1         (one dtype pass only)
 #
 # --no_warmup: the reference's computation_time includes its first sess.run.  Re-runnable:
 # --skip_done keeps the rows already in the logs.  Compile and compare afterwards with
@@ -17,7 +18,7 @@ OUT=${1:-results/like_for_like}
 shift || true
 GPUS=${*:-1 2 3 4 5 6 7 8}
 mkdir -p "$OUT"
-for DT in fp64 fp32; do
+for DT in ${DTYPES:-fp64 fp32}; do
   python scripts/new_experiment.py --gpus $GPUS --skip_unavailable --skip_done \
       --log_file "$OUT/executions_log_mi355x_$DT.csv" --log_dir "$OUT/rocprof_$DT" \
       --data_file "${TMPDIR:-/tmp}/class-data.npz" --timeout 900 -- --dtype "$DT" --no_warmup \
