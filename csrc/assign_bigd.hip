@@ -517,18 +517,11 @@ int tdc_assign_bigd(int dtype, const void* X, const void* Xs, int64_t N, int64_t
       case 256: return launch_bigd<OpFp8, 256, 8, 4>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
       case 512: return launch_bigd<OpFp8, 512, 8, 4>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
       case 768: {
-        static const int abl = getenv("TDC_BIGD_ABL") ? atoi(getenv("TDC_BIGD_ABL")) : 0;
-        // 64-row stages: 206.5 vs 211.8 ms (grouped), 197.3 vs 200.8 ms (one group) at N=5M
-        static const int qh = getenv("TDC_BIGD_QH") ? atoi(getenv("TDC_BIGD_QH")) : 2;
-        if (abl == 0 && qh == 2 && Kp % 64 == 0)  // 64-row stages
+        // 64-row stages (QH=2): 206.5 vs 211.8 ms (grouped), 197.3 vs 200.8 ms (one group)
+        // at N=5M.  The ablations (ABL) are instantiated by tools harnesses only.
+        if (Kp % 64 == 0)
           return launch_bigd<OpFp8, 768, 8, 3, 0, 2>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
-        switch (abl) {  // timing ablations (tools only)
-          case 1: return launch_bigd<OpFp8, 768, 8, 4, 1>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
-          case 2: return launch_bigd<OpFp8, 768, 8, 4, 2>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
-          case 4: return launch_bigd<OpFp8, 768, 8, 4, 4>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
-          case 7: return launch_bigd<OpFp8, 768, 8, 4, 7>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
-          default: return launch_bigd<OpFp8, 768, 8, 4>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
-        }
+        return launch_bigd<OpFp8, 768, 8, 4>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
       }
       case 1024: return launch_bigd<OpFp8, 1024, 8, 4>(X, Xs, N, ldx, Cm2, Cs, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
     }

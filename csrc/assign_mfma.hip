@@ -41,60 +41,11 @@ int tdc_assign_mfma_bf16(const void* X, int64_t N, int64_t ldx, int DP, const vo
   const int ntiles = Kp / BN;
   const __bf16* x = (const __bf16*)X;
   const __bf16* c = (const __bf16*)Cm2;
-  // LDS-DMA ring, 4 waves x P x 32 points per workgroup, 64-centroid stages.
-  // TDC_ASSIGN_RING=1 selects the first ring variant (kept for A/B timing).
-  static const int ring = getenv("TDC_ASSIGN_RING") ? atoi(getenv("TDC_ASSIGN_RING")) : 3;
-  static const int abl = getenv("TDC_ASSIGN_ABL") ? atoi(getenv("TDC_ASSIGN_ABL")) : 0;
-  static const int r2cfg = getenv("TDC_RING2_CFG") ? atoi(getenv("TDC_RING2_CFG")) : 0;
-  if (DP == 128 && ring == 2 && r2cfg != 0) {  // schedule experiments: QT*10 + NST
-    dim3 grid((unsigned)((N + 255) / 256));
-    bool launched = false;
-#define TDC_R2(QTV, NSTV)                                                                          \
-  if (r2cfg == QTV * 10 + NSTV) {                                                                  \
-    if (Kp % (32 * QTV) != 0) return (int)hipErrorInvalidValue;                                    \
-    launched = true;                                                                               \
-    hipLaunchKernelGGL((assign_mfma_bf16_ring2_kernel<128, 2, NSTV, 4, QTV>), grid, dim3(256), 0,  \
-                       stream, x, N, ldx, c, cnorm, Kp / (32 * QTV), labels, mind);                \
-  }
-    TDC_R2(2, 4) TDC_R2(1, 4) TDC_R2(1, 5) TDC_R2(1, 6) TDC_R2(1, 3)
-#undef TDC_R2
-    if (!launched) return (int)hipErrorInvalidValue;
-    TDC_CHECK_LAUNCH();
-    return 0;
-  }
-  if (DP == 128 && ring == 2 && abl != 0) {  // timing ablations (tools only; results invalid)
-    dim3 grid((unsigned)((N + 255) / 256));
-    if (abl != 1 && abl != 2 && abl != 4 && abl != 7 && abl != 8) return (int)hipErrorInvalidValue;
-#define TDC_ABL(A)                                                                                \
-  if (abl == A)                                                                                   \
-    hipLaunchKernelGGL((assign_mfma_bf16_ring2_kernel<128, 2, 3, 4, 2, A>), grid, dim3(256), 0,   \
-                       stream, x, N, ldx, c, cnorm, ntiles, labels, mind);
-    TDC_ABL(1) TDC_ABL(2) TDC_ABL(4) TDC_ABL(7) TDC_ABL(8)
-#undef TDC_ABL
-    TDC_CHECK_LAUNCH();
-    return 0;
-  }
-  static const int r3cfg = getenv("TDC_RING3_CFG") ? atoi(getenv("TDC_RING3_CFG")) : 0;
-  if (ring == 3 && DP == 128 && r3cfg != 0) {  // schedule experiments: WAVES*1000+P*100+QT*10+NST
-    bool launched = false;
-#define TDC_R3(WV, PV, QTV, NSTV)                                                                  \
-  if (r3cfg == WV * 1000 + PV * 100 + QTV * 10 + NSTV) {                                           \
-    if (Kp % (16 * QTV) != 0) return (int)hipErrorInvalidValue;                                    \
-    launched = true;                                                                               \
-    const int64_t per = WV * PV * 16;                                                              \
-    hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<128, PV, NSTV, WV, QTV>),                    \
-                       dim3((unsigned)((N + per - 1) / per)), dim3(WV * 64), 0, stream, x, N, ldx, \
-                       c, cnorm, Kp / (16 * QTV), labels, mind);                                   \
-  }
-    TDC_R3(4, 4, 4, 3) TDC_R3(4, 4, 2, 3) TDC_R3(4, 4, 8, 2) TDC_R3(4, 2, 4, 3)
-    TDC_R3(4, 8, 4, 3) TDC_R3(8, 4, 4, 3) TDC_R3(4, 4, 4, 2) TDC_R3(4, 4, 2, 4)
-    TDC_R3(6, 4, 4, 3) TDC_R3(4, 8, 4, 2) TDC_R3(8, 8, 4, 2)
-#undef TDC_R3
-    if (!launched) return (int)hipErrorInvalidValue;  // not a compiled schedule: fail loudly
-    TDC_CHECK_LAUNCH();
-    return 0;
-  }
-  if (ring == 3 && (DP == 64 || DP == 128 || DP == 256)) {  // 16x16x32 MFMA variant
+  // LDS-DMA ring, 4 waves x P x 16 points per workgroup (ring3: 16x16x32 MFMA, tag-in-
+  // mantissa argmin).  The schedule variants measured against it (ring / ring2 schedules,
+  // ablations, WAVES/P/QT/NST sweeps: docs/PERF_NOTES.md) are instantiated by the harnesses
+  // in tools/, not selectable here.
+  if (DP == 64 || DP == 128 || DP == 256) {
     const int64_t per = 4 * 4 * 16;
     dim3 grid((unsigned)((N + per - 1) / per));
     if (DP == 64) {
@@ -126,27 +77,11 @@ int tdc_assign_mfma_bf16(const void* X, int64_t N, int64_t ldx, int DP, const vo
     TDC_CHECK_LAUNCH();
     return 0;
   }
-  switch (DP) {
-#define TDC_CASE(DPV, PV, NSTV)                                                              \
-  case DPV: {                                                                                \
-    const int64_t per = 4 * PV * 32;                                                         \
-    dim3 grid((unsigned)((N + per - 1) / per));                                              \
-    if (ring == 1)                                                                           \
-      hipLaunchKernelGGL((assign_mfma_bf16_ring_kernel<DPV, PV, NSTV, 4, 2>), grid, dim3(256), \
-                         0, stream, x, N, ldx, c, cnorm, ntiles, labels, mind);              \
-    else                                                                                     \
-      hipLaunchKernelGGL((assign_mfma_bf16_ring2_kernel<DPV, PV, NSTV, 4, 2>), grid,         \
-                         dim3(256), 0, stream, x, N, ldx, c, cnorm, ntiles, labels, mind);   \
-    break;                                                                                   \
-  }
-    TDC_CASE(32, 4, 3)
-    TDC_CASE(64, 2, 3)
-    TDC_CASE(128, 2, 3)
-    TDC_CASE(256, 1, 2)
-#undef TDC_CASE
-    default:
-      return (int)hipErrorInvalidValue;
-  }
+  if (DP != 32) return (int)hipErrorInvalidValue;
+  // D <= 32: the 32x32x16 ring2 schedule, 4 waves x 4 tiles of 32 points
+  const int64_t per = 4 * 4 * 32;
+  hipLaunchKernelGGL((assign_mfma_bf16_ring2_kernel<32, 4, 3, 4, 2>), dim3((unsigned)((N + per - 1) / per)),
+                     dim3(256), 0, stream, x, N, ldx, c, cnorm, ntiles, labels, mind);
   TDC_CHECK_LAUNCH();
   return 0;
 }

@@ -37,10 +37,6 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-#ifndef TDC_FCM_SCHED
-#define TDC_FCM_SCHED 0
-#endif
-
 constexpr float ZERO_FLOOR = 1.52587890625e-05f;  // 2^-16 (an exact hit computes ~2^-17 |x|^2)
 
 struct MParam {
@@ -479,15 +475,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
 #undef TDC_LOADQ
 #undef TDC_WTX
 #undef TDC_TRLD
-#if TDC_FCM_SCHED
-    // interleave: one MFMA, then ~5 VALU and a DS read (the membership arithmetic of one
-    // half beside the MFMAs of the other; one wave per SIMD cannot hide it otherwise)
-#pragma unroll
-    for (int i = 0; i < 96; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-    }
-#endif
     if (more) TDC_TILE_STORE(buf ^ 1)
     __syncthreads();
     buf ^= 1;
@@ -638,18 +625,13 @@ int launch_maccum(const void* Xh, const void* Xl, const float* xx, const float* 
   const int xcd = (nb % 8 == 0) ? 1 : 0;
   float* part_ws = part + splits * (int64_t)Kp * DP;
   const MParam p = make_mparam(m, nz);
-  static const int waves = getenv("TDC_FCM_WAVES") ? atoi(getenv("TDC_FCM_WAVES")) : 8;
+  // 8 waves (2 per SIMD): one wave's epilogue VALU runs beside the other's MFMAs; the
+  // one-wave software-pipelined WAVES=4 form measured slower (docs/PERF_NOTES.md)
 #define TDC_LA(MODE, NZV)                                                                     \
-  if (waves == 4)                                                                             \
-    hipLaunchKernelGGL((fcm_mfma_accum_kernel<DP, MODE, NZV, 4>), dim3((unsigned)nb), dim3(256), \
-                       0, s, (const __bf16*)Xh, (const __bf16*)Xl, xx, rowinfo, N,             \
-                       (const __bf16*)Ch, (const __bf16*)Cl, cc, K, nkt, rps, xcd, p, part,    \
-                       part_ws, Kp);                                                          \
-  else                                                                                        \
-    hipLaunchKernelGGL((fcm_mfma_accum_kernel<DP, MODE, NZV, 8>), dim3((unsigned)nb), dim3(512), \
-                       0, s, (const __bf16*)Xh, (const __bf16*)Xl, xx, rowinfo, N,             \
-                       (const __bf16*)Ch, (const __bf16*)Cl, cc, K, nkt, rps, xcd, p, part,    \
-                       part_ws, Kp)
+  hipLaunchKernelGGL((fcm_mfma_accum_kernel<DP, MODE, NZV, 8>), dim3((unsigned)nb), dim3(512),   \
+                     0, s, (const __bf16*)Xh, (const __bf16*)Xl, xx, rowinfo, N,               \
+                     (const __bf16*)Ch, (const __bf16*)Cl, cc, K, nkt, rps, xcd, p, part,      \
+                     part_ws, Kp)
   if (m == 2.0) {
     if (nz) TDC_LA(2, true); else TDC_LA(2, false);
   } else {

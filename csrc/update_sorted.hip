@@ -498,20 +498,13 @@ int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int6
   {
     // one 1024-thread block per CU: a quarter of the global flush atomics of 4 x 256-thread
     // blocks per CU (each block adds its whole LDS histogram into cnt)
-    static const int hnt = getenv("TDC_HIST_THREADS") ? atoi(getenv("TDC_HIST_THREADS")) : 1024;
-    int64_t blocks = hnt == 1024 ? (int64_t)num_cus : (int64_t)num_cus * 4;
+    int64_t blocks = (int64_t)num_cus;
     int64_t per = (N + blocks - 1) / blocks;
     if (per < 4096) per = 4096;
     blocks = (N + per - 1) / per;
     const size_t lds = K <= LDS_HIST_MAX_K ? sizeof(int) * (size_t)K : 0;
-    uint32_t* zw = static_cast<uint32_t*>(zero_first);
-    const int64_t nzw = zero_bytes / 4;
-    if (hnt == 1024)
-      hipLaunchKernelGGL(hist_kernel<1024>, dim3((unsigned)blocks), dim3(1024), lds, s, labels, N,
-                         K, cnt, per, zw, nzw);
-    else
-      hipLaunchKernelGGL(hist_kernel<256>, dim3((unsigned)blocks), dim3(256), lds, s, labels, N, K,
-                         cnt, per, zw, nzw);
+    hipLaunchKernelGGL(hist_kernel<1024>, dim3((unsigned)blocks), dim3(1024), lds, s, labels, N, K,
+                       cnt, per, static_cast<uint32_t*>(zero_first), zero_bytes / 4);
     TDC_CHECK_LAUNCH();
   }
   if (acc_dtype == TDC_F64)
@@ -525,22 +518,14 @@ int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int6
     // one 1024-thread block per CU: 16 waves keep the LDS-rank -> store chains in flight
     // (2 x 256-thread blocks per CU measured 122 us at N=10M, K=1024); still one
     // reservation atomic per non-empty bin per block
-    static const int nt = [] {
-      const char* e = getenv("TDC_BSCATTER_THREADS");
-      return (e && atoi(e) == 256) ? 256 : 1024;
-    }();
     // (fewer, fuller blocks at small N -- 1, 4, 8 or 16 labels per bin per block at
     // N=1.25M, K=1024 -- measured the same: the per-block K-bin passes are not the cost)
-    int64_t blocks = nt == 1024 ? (int64_t)num_cus : (int64_t)num_cus * 2;
+    int64_t blocks = (int64_t)num_cus;
     int64_t per = (N + blocks - 1) / blocks;
     if (per < 4096) per = 4096;
     blocks = (N + per - 1) / per;
-    if (nt == 1024)
-      hipLaunchKernelGGL(bscatter_kernel<1024>, dim3((unsigned)blocks), dim3(1024),
-                         2 * sizeof(int) * (size_t)K, s, labels, N, K, cursor, perm, per, rowidx);
-    else
-      hipLaunchKernelGGL(bscatter_kernel<256>, dim3((unsigned)blocks), dim3(256),
-                         2 * sizeof(int) * (size_t)K, s, labels, N, K, cursor, perm, per, rowidx);
+    hipLaunchKernelGGL(bscatter_kernel<1024>, dim3((unsigned)blocks), dim3(1024),
+                       2 * sizeof(int) * (size_t)K, s, labels, N, K, cursor, perm, per, rowidx);
     TDC_CHECK_LAUNCH();
   } else {
     int64_t blocks = (int64_t)num_cus * 4;
