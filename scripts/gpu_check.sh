@@ -6,6 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
 OUT="$PWD/gpurun_out"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
+export TMPDIR=/tmp
 step() {  # step <seconds> <logname> <cmd...>
   local secs=$1 log=$2; shift 2
   echo "== $(date +%T) $*" | tee -a "$OUT/steps.log"
