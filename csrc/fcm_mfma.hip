@@ -165,17 +165,19 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats_kernel(
       const f32x4 n4 = *reinterpret_cast<const f32x4*>(&ns[(Q) * 32 + 8 * g4 + 4 * h]);   \
       _Pragma("unroll") for (int e = 0; e < 4; ++e) init[4 * g4 + e] = n4[e];             \
     }                                                                                     \
-    bf16x8 ah = as_bf16x8(*reinterpret_cast<const uint4*>(cb + coff<DP>(crow, h * (CPR / 2)))); \
-    bf16x8 al = as_bf16x8(*reinterpret_cast<const uint4*>(cb + IMGB + coff<DP>(crow, h * (CPR / 2)))); \
+    /* every fragment of the half is read up front: with a one-step prefetch the        \
+       compiler re-used the registers and waited for each pair right before its MFMAs,    \
+       exposing the LDS latency on every k-step */                                        \
+    bf16x8 ah[KS], al[KS];                                                                \
     _Pragma("unroll") for (int kk = 0; kk < KS; ++kk) {                                   \
-      const int kn = kk + 1 < KS ? kk + 1 : kk;                                           \
-      const bf16x8 ahn = as_bf16x8(*reinterpret_cast<const uint4*>(cb + coff<DP>(crow, h * (CPR / 2) + kn))); \
-      const bf16x8 aln = as_bf16x8(*reinterpret_cast<const uint4*>(cb + IMGB + coff<DP>(crow, h * (CPR / 2) + kn))); \
-      ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[kk], kk == 0 ? init : ACC, 0, 0, 0); \
-      ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[kk], ACC, 0, 0, 0);           \
-      ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[kk], ACC, 0, 0, 0);           \
-      ah = ahn;                                                                           \
-      al = aln;                                                                           \
+      ah[kk] = as_bf16x8(*reinterpret_cast<const uint4*>(cb + coff<DP>(crow, h * (CPR / 2) + kk))); \
+      al[kk] = as_bf16x8(*reinterpret_cast<const uint4*>(cb + IMGB + coff<DP>(crow, h * (CPR / 2) + kk))); \
+    }                                                                                     \
+    __builtin_amdgcn_sched_barrier(0); /* keep the reads ahead of the MFMAs */            \
+    _Pragma("unroll") for (int kk = 0; kk < KS; ++kk) {                                   \
+      ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[kk], bh[kk], kk == 0 ? init : ACC, 0, 0, 0); \
+      ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[kk], bl[kk], ACC, 0, 0, 0);       \
+      ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[kk], bh[kk], ACC, 0, 0, 0);       \
     }                                                                                     \
   }
   // epilogue of half Q of stage T_: register i = centroid (i&3)+8(i>>2)+4h (ascending);

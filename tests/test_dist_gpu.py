@@ -67,7 +67,11 @@ def _run(world, dtype, n, d, k, iters=4, method="kmeans", algorithm="lloyd", com
 
 
 @pytest.mark.parametrize("world,dtype,d,k", [(2, "bf16", 128, 1000), (3, "bf16", 128, 1000),
-                                             (2, "fp8", 256, 500), (2, "fp32", 96, 700)])
+                                             (2, "fp8", 256, 500), (2, "fp32", 96, 700),
+                                             # K=40 over 3 ranks of 32-row slices: rank 2's
+                                             # slice has no real centroid (fp8 finalize of
+                                             # an empty slice, padding rows only)
+                                             (3, "fp8", 256, 40)])
 def test_rsag_matches_one_rank(gpu, world, dtype, d, k):
     """comm_mode='rsag': reduce-scatter of the fp32 sums, each rank finalises + preps the
     operand rows of its K/G slice, all-gather of the bf16/fp8 operand tables (fp32 path:
@@ -77,7 +81,8 @@ def test_rsag_matches_one_rank(gpu, world, dtype, d, k):
     c1, l1, b1, i1 = _run(1, dtype, n, d, k, full=True)
     c2, l2, b2, i2 = _run(world, dtype, n, d, k, comm_mode="rsag", full=True)
     assert b1 == b2 and i2["rsag"] and not i1["rsag"]
-    assert i1["split"] and i2["split"]
+    if k * (d + 1) > 65536:  # fp32 partial sums (smaller buffers travel in fp64)
+        assert i1["split"] and i2["split"]
     assert i2["counts"].sum() == n and np.all(i2["counts"] == np.round(i2["counts"]))
     if dtype == "fp32":
         np.testing.assert_allclose(c2, c1, rtol=1e-4, atol=1e-4)
