@@ -70,6 +70,13 @@ static void ring3(const Bufs& b, hipStream_t s) {
                      (int64_t)DP, b.c, b.cn, b.kp / 64, b.lab, nullptr);
 }
 
+static void ring3p4(const Bufs& b, hipStream_t s) {  // the short-launch schedule
+  const int64_t per = 4 * 4 * 16;
+  hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<128, 4, 3, 4, 4>),
+                     dim3((unsigned)((b.n + per - 1) / per)), dim3(256), 0, s, b.x, b.n,
+                     (int64_t)DP, b.c, b.cn, b.kp / 64, b.lab, nullptr);
+}
+
 template <int P, int WAVES, bool PF, bool R3 = false>
 static void kres(const Bufs& b, hipStream_t s, int cus) {
   constexpr int R = KresGeom<DP>::R;
@@ -174,7 +181,13 @@ int main(int argc, char** argv) {
   kres<4, 8, false, true>(b1, 0, cus);
   CK(hipDeviceSynchronize());
   check("kres r3 P4 W8");
+  CK(hipMemset(l1, 0xff, N * 4));
+  ring3p4(b1, 0);
+  CK(hipDeviceSynchronize());
+  check("ring3 P4 (short-launch)");
   for (int round = 0; round < 3; ++round) {
+    const float tp4 = timeit([&] { ring3p4(b1, 0); }, reps);
+    printf("round %d: ring3 P4 NST3 %.3f ms\n", round, tp4);
     const float t0 = timeit([&] { ring3(b0, 0); }, reps);
     const float t1 = timeit([&] { kres<8, 8, false, true>(b1, 0, cus); }, reps);
     const float t2 = timeit([&] { kres<4, 12, false, true>(b1, 0, cus); }, reps);
