@@ -659,17 +659,31 @@ void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int6
     }
   }
 
+  // Per-lane byte offsets of this wave's pieces inside a stage image: loop invariant, one
+  // VGPR each.  The pieces are issued by inline asm in the saddr + voffset form (stage base
+  // in SGPRs, M0 = LDS destination): with the builtin, hipcc kept a 64-bit VGPR address
+  // per piece and recomputed it every stage -- 256 VGPRs at P=8 against 235 this way, and
+  // 1.5 % (10M rows) to 5 % (1.25M rows) more time (tools/ring3_ab.hip,
+  // profiles/ring3_ab_r03.txt).  The compiler does not count these loads in its vmcnt
+  // bookkeeping; the explicit stage-end waits below do (extra outstanding loads only
+  // make the compiler's own vmcnt waits more conservative).
+  unsigned voff[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int piece = (w * PPW + i) % PIECES;
+    const int L = piece * 64 + lane;
+    const int row = L / CPR, cp = L % CPR;
+    voff[i] = (unsigned)((row * DP + swz<DP>(row, cp) * 8) * 2);
+  }
   auto issue = [&](int t, int slot) __attribute__((always_inline)) {
+    const __bf16* base = Cm2 + (int64_t)t * BNL * DP;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int piece = (w * PPW + i) % PIECES;
-      const int L = piece * 64 + lane;
-      const int row = L / CPR, cp = L % CPR;
-      const int csrc = swz<DP>(row, cp);
-      const __bf16* src = Cm2 + ((int64_t)t * BNL + row) * DP + csrc * 8;
-      __builtin_amdgcn_global_load_lds(
-          (const void*)src,
-          (__attribute__((address_space(3))) void*)(smem + slot * STAGE_B + piece * 1024), 16, 0, 0);
+      const unsigned dst = lds0 + slot * STAGE_B + piece * 1024;
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
+                   :: "s"(__builtin_amdgcn_readfirstlane(dst)), "v"(voff[i]), "s"(base)
+                   : "memory", "m0");
     }
     // contiguous chunk run per wave (the DMA writes lane l at base + 16 l)
     const int nb = w * NPW < NCH - NPW ? w * NPW : NCH - NPW;
