@@ -11,6 +11,7 @@
 //      ~60 cycles per piece among bare MFMAs, 100-185 inside a phase already carrying
 //      pieces and fragment reads)
 //   2: s_setprio(1) around every MFMA cluster (guide T5)
+//   4: index tags carry the stage within a super-stage of 16 (8 tag bits)
 // Data: Gaussian blobs around K uniform(-10,10) centres (splitmix64 + Box-Muller).
 #include <hip/hip_runtime.h>
 
@@ -54,7 +55,13 @@ void ring3x_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
   constexpr bool SPREAD = (VAR & 1) != 0;
   constexpr bool PRIO = (VAR & 2) != 0;
   static_assert(!SPREAD || PPW <= QT, "one piece per phase");
-  constexpr unsigned EMB = QT * 4 <= 16 ? 15u : 31u;
+  // VAR 4: the tag also carries the stage within a super-stage of 16 stages (8 tag bits for
+  // QT=4), so the per-stage compare / select of the running best becomes one v_min_f32
+  // per point tile, and the compare / select runs once per super-stage
+  constexpr bool STAGETAG = (VAR & 4) != 0;
+  static_assert(!STAGETAG || QT == 4, "stage tags: 4 (q, reg) bits + 4 stage bits");
+  if (STAGETAG && ntiles > 16) return;  // experiment covers K <= 1024
+  constexpr unsigned EMB = STAGETAG ? 255u : (QT * 4 <= 16 ? 15u : 31u);
   __shared__ __attribute__((aligned(16))) char smem[NST * STAGE_B];
 
   const int tid = threadIdx.x;
@@ -126,6 +133,8 @@ void ring3x_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
 #pragma unroll
   for (int kk = 0; kk < KS; ++kk) aoff[kk] = lds0 + r * (DP * 2) + swz<DP>(r, kk * 4 + g) * 16;
   const unsigned noff = lds0 + TILE_B + 16 * g;
+  unsigned vmask = ~EMB;
+  asm volatile("" : "+v"(vmask));  // keep the non-inline mask in one VGPR
 
   auto stage = [&](int t, auto slot_c) __attribute__((always_inline)) {
     constexpr int slot = decltype(slot_c)::value;
@@ -135,7 +144,8 @@ void ring3x_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
     if constexpr (!SPREAD) issue(tn, nslot);
     float m[P];
 #pragma unroll
-    for (int p = 0; p < P; ++p) m[p] = INFINITY;
+    for (int p = 0; p < P; ++p) m[p] = STAGETAG ? best[p] : INFINITY;
+    const unsigned stag = STAGETAG ? (unsigned)((t & 15) << 4) : 0u;
 #pragma unroll
     for (int q = 0; q < QT; ++q) {
       auto afrag = [&](int kk) __attribute__((always_inline)) {
@@ -176,16 +186,30 @@ void ring3x_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
       for (int p = 0; p < P; ++p) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float v = __uint_as_float((__float_as_uint(acc[p][i]) & ~EMB) | (unsigned)(q * 4 + i));
+          float v;
+          if constexpr (STAGETAG) {  // one v_and_or_b32: mask in a VGPR, tag in an SGPR
+            const unsigned tg = __builtin_amdgcn_readfirstlane(stag | (unsigned)(q * 4 + i));
+            v = __uint_as_float((__float_as_uint(acc[p][i]) & vmask) | tg);
+          } else {
+            v = __uint_as_float((__float_as_uint(acc[p][i]) & ~EMB) | (unsigned)(q * 4 + i));
+          }
           m[p] = __builtin_fminf(m[p], v);
         }
       }
     }
+    if constexpr (STAGETAG) {
+#pragma unroll
+      for (int p = 0; p < P; ++p) best[p] = m[p];
+    }
 #pragma unroll
     for (int p = 0; p < P; ++p) {
-      const bool up = m[p] < best[p];
-      best[p] = up ? m[p] : best[p];
-      bt[p] = up ? t : bt[p];
+      if constexpr (STAGETAG) {
+        // experiment: one super-stage (ntiles <= 16, K <= 1024): best is a plain minimum
+      } else {
+        const bool up = m[p] < best[p];
+        best[p] = up ? m[p] : best[p];
+        bt[p] = up ? t : bt[p];
+      }
     }
     asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * VPS) : "memory");
     __builtin_amdgcn_s_barrier();
@@ -202,7 +226,8 @@ void ring3x_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
 #pragma unroll
   for (int p = 0; p < P; ++p) {
     const unsigned e = __float_as_uint(best[p]) & EMB;
-    int lab = bt[p] * BNL + (int)(e >> 2) * 16 + 4 * g + (int)(e & 3);
+    int lab = STAGETAG ? (bt[p] * 16 + (int)(e >> 4)) * BNL + (int)((e & 15) >> 2) * 16 + 4 * g + (int)(e & 3)
+                       : bt[p] * BNL + (int)(e >> 2) * 16 + 4 * g + (int)(e & 3);
     float v = __uint_as_float(__float_as_uint(best[p]) & ~EMB);
 #pragma unroll
     for (int o = 16; o <= 32; o <<= 1) {
@@ -347,15 +372,17 @@ int main(int argc, char** argv) {
   TRY("spread+setprio", var<8, 2, 4, 3>)
   TRY("P4 NST3 spread", var<4, 3, 4, 1>)
   TRY("prod P4 NST3", prod4)
+  TRY("stage tags P8", var<8, 2, 4, 4>)
+  TRY("stage tags P4 NST3", var<4, 3, 4, 4>)
   const double flop = 2.0 * (double)N * Kp * DP;
   for (int round = 0; round < 3; ++round) {
     const float t0 = timeit([&] { prod(b0, 0); }, reps);
     const float t1 = timeit([&] { var<8, 2, 4, 0>(b1, 0); }, reps);
-    const float t3 = timeit([&] { var<8, 2, 4, 2>(b1, 0); }, reps);
+    const float t3 = timeit([&] { var<8, 2, 4, 4>(b1, 0); }, reps);
     const float t5 = timeit([&] { prod4(b1, 0); }, reps);
-    const float t6 = timeit([&] { var<4, 3, 4, 1>(b1, 0); }, reps);
-    printf("round %d: prod P8 %.3f ms (%.0f TF/s) | copy P8 %.3f | setprio %.3f | "
-           "prod P4N3 %.3f | P4N3 spread %.3f\n",
+    const float t6 = timeit([&] { var<4, 3, 4, 4>(b1, 0); }, reps);
+    printf("round %d: prod P8 %.3f ms (%.0f TF/s) | copy P8 %.3f | stagetag P8 %.3f | "
+           "prod P4N3 %.3f | stagetag P4N3 %.3f\n",
            round, t0, flop / t0 / 1e9, t1, t3, t5, t6);
     fflush(stdout);
   }
