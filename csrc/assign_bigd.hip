@@ -77,11 +77,13 @@ __device__ __forceinline__ float unord_bits(unsigned o) {
 // [0,16), and supplies the scale of block 2kk + h.
 __device__ __forceinline__ int fp8_off(int kk, int h, int u) { return 64 * kk + 32 * u + 16 * h; }
 
-template <class OP>
+// SEL: the byte of the scale registers the MFMA applies (its op_sel; probed with
+// tools/probe_mfma_scale_opsel.hip: SEL = byte index 0..3 of the 32-bit scale operand)
+template <class OP, int SEL = 0>
 __device__ __forceinline__ f32x16 mma(const typename OP::frag& a, const typename OP::frag& b,
                                       const f32x16& c, int sa, int sb) {
   if constexpr (OP::SCALED) {
-    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, SEL, sa, SEL, sb);
   } else {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
   }
@@ -161,13 +163,29 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
     for (int kk = 0; kk < NK; ++kk)
       bq[kk] = *reinterpret_cast<const typename OP::frag*>(src + kk * OP::FB);
   }
+  // E8M0 scales: lane half h applies the scale of block 2kk + h, byte 2(kk & 1) + h of
+  // scale dword kk >> 1.  The dwords are shifted right by 8h once, so the byte is
+  // 2(kk & 1) for both halves and the MFMA's byte select (op_sel) picks it: no per-MFMA
+  // shift / mask (it was ~2 VALU per MFMA).
+  const int hsh = 8 * h;
   int xs[NSW];
   if constexpr (OP::SCALED) {
     const int* s = reinterpret_cast<const int*>(Xs + xrow * SB);
 #pragma unroll
-    for (int i = 0; i < NSW; ++i) xs[i] = s[i];
+    for (int i = 0; i < NSW; ++i) xs[i] = (int)((unsigned)s[i] >> hsh);
   }
-  const int hsh = 8 * h;  // byte of the lane half inside a scale dword pair
+  // fp8 A fragments: per-lane LDS byte offsets inside a 32-row tile, one VGPR per
+  // distinct (chunk & 15): chunk 4kk + 2u + h of row r sits at swizzled chunk
+  // 16 (kk >> 2) + ((4 (kk & 3) + 2u + h) ^ (r & 15)) (swz with 16 chunk groups), so the
+  // kk >> 2 part is a ds_read immediate offset.  The per-read address arithmetic of the
+  // generic form was ~3 VALU per MFMA.
+  unsigned aoff8[8];
+  if constexpr (OP::SCALED) {
+    static_assert(RB >= 256 && NK % 4 == 0 || NK < 4, "fp8 swizzle: 16-chunk groups");
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+      aoff8[m] = (unsigned)(r * RB + 16 * ((2 * m + h) ^ (r & 15)));
+  }
   const unsigned lds_base =
       (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
 
@@ -215,10 +233,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
     // scale row of centroid row qh*32 + r; issued before the fragments, so the first
     // counted lgkmcnt wait below also covers them
     f32x16 acc;
+    const unsigned nbase = xbase + (qh * 32 + 4 * h) * 4;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       f32x4 v;
-      asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(xbase + (qh * 32 + 8 * j + 4 * h) * 4));
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(nbase), "i"(32 * j));
       acc[4 * j + 0] = v[0];
       acc[4 * j + 1] = v[1];
       acc[4 * j + 2] = v[2];
@@ -226,10 +245,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
     }
     int sa_row[NSW];
     if constexpr (OP::SCALED) {
+      const unsigned sbase = xbase + NRM_B + (qh * 32 + r) * SB;
 #pragma unroll
       for (int j = 0; j < NSW; ++j)
-        asm volatile("ds_read_b32 %0, %1" : "=v"(sa_row[j]) : "v"(xbase + NRM_B + (qh * 32 + r) * SB + 4 * j));
+        asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(sa_row[j]) : "v"(sbase), "i"(4 * j));
     }
+    const unsigned qbase = lds_base + slot * STAGE_B + qh * 32 * RB;
     // A fragments via inline-asm ds_read_b128: the compiler cannot prove they do not
     // alias the in-flight LDS-DMA ring refill, so compiler-visible LDS reads get a
     // vmcnt(0) in front of them (= waiting for the refill just issued, every stage).
@@ -241,8 +262,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
         asm volatile("ds_read_b128 %0, %1" : "=v"(lo) : "v"(rbase + swz<RB>(r, h * (CPR / 2) + kk) * 16));
         a = __builtin_bit_cast(typename OP::frag, lo);
       } else {
-        asm volatile("ds_read_b128 %0, %1" : "=v"(lo) : "v"(rbase + swz<RB>(r, fp8_off(kk, h, 0) / 16) * 16));
-        asm volatile("ds_read_b128 %0, %1" : "=v"(hi) : "v"(rbase + swz<RB>(r, fp8_off(kk, h, 1) / 16) * 16));
+        asm volatile("ds_read_b128 %0, %1 offset:%2"
+                     : "=v"(lo) : "v"(qbase + aoff8[2 * (kk & 3)]), "i"(256 * (kk >> 2)));
+        asm volatile("ds_read_b128 %0, %1 offset:%2"
+                     : "=v"(hi) : "v"(qbase + aoff8[2 * (kk & 3) + 1]), "i"(256 * (kk >> 2)));
         a = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
       return a;
@@ -259,12 +282,19 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
       else if (kk + 1 < NK) asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(PER) : "memory");
       else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      int sa = 0, sb = 0;
-      if constexpr (OP::SCALED) {  // block 2kk+h: dword kk>>1, byte 2(kk&1)+h
-        sa = (sa_row[kk >> 1] >> (16 * (kk & 1) + hsh)) & 0xff;
-        sb = (xs[kk >> 1] >> (16 * (kk & 1) + hsh)) & 0xff;
+      if constexpr (OP::SCALED) {
+        // the scale row was read before the fragments, so it has landed by the first wait
+        if (kk == 0) {
+#pragma unroll
+          for (int j = 0; j < NSW; ++j) sa_row[j] = (int)((unsigned)sa_row[j] >> hsh);
+        }
       }
-      acc = mma<OP>(a0, bq[kk], acc, sa, sb);
+      if constexpr (OP::SCALED) {  // block 2kk+h: dword kk>>1, byte 2(kk&1) after >> 8h
+        if ((kk & 1) == 0) acc = mma<OP, 0>(a0, bq[kk], acc, sa_row[kk >> 1], xs[kk >> 1]);
+        else acc = mma<OP, 2>(a0, bq[kk], acc, sa_row[kk >> 1], xs[kk >> 1]);
+      } else {
+        acc = mma<OP>(a0, bq[kk], acc, 0, 0);
+      }
       __builtin_amdgcn_sched_barrier(0);
       a0 = a1;
       a1 = a2;
