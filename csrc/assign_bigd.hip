@@ -189,16 +189,27 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
   const unsigned lds_base =
       (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
 
+  // ring refill: per-lane byte offsets of this wave's pieces inside a stage (loop
+  // invariant), issued by inline asm in the saddr + voffset form with M0 = the LDS
+  // destination (the builtin made hipcc rebuild a 64-bit VGPR address per piece every
+  // stage; the same change measured 1-5 % on the D <= 256 kernel, assign_mfma_impl.h).
+  // The compiler does not count these loads; the explicit stage-end vmcnt waits do.
+  unsigned voff[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int L = (w * PPW + i) * 64 + lane;  // 16-B chunk index inside the stage
+    const int row = L / CPR, cp = L % CPR;
+    voff[i] = (unsigned)(row * RB + swz<RB>(row, cp) * 16);
+  }
   auto issue = [&](int t, int slot) __attribute__((always_inline)) {
+    const uint8_t* base = Cm2 + (int64_t)t * (32 * QH) * RB;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int piece = w * PPW + i;
-      const int L = piece * 64 + lane;  // 16-B chunk index inside the stage
-      const int row = L / CPR, cp = L % CPR;
-      const uint8_t* src = Cm2 + ((int64_t)t * (32 * QH) + row) * RB + swz<RB>(row, cp) * 16;
-      __builtin_amdgcn_global_load_lds(
-          (const void*)src,
-          (__attribute__((address_space(3))) void*)(smem + slot * STAGE_B + piece * 1024), 16, 0, 0);
+      const unsigned dst = lds_base + slot * STAGE_B + piece * 1024;
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
+                   :: "s"(__builtin_amdgcn_readfirstlane(dst)), "v"(voff[i]), "s"(base)
+                   : "memory", "m0");
     }
     if (lane < LPW) {
       const int c = w * LPW + lane;  // 16-B chunk of the side region
