@@ -201,11 +201,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
     const int row = L / CPR, cp = L % CPR;
     voff[i] = (unsigned)(row * RB + swz<RB>(row, cp) * 16);
   }
+  const int wu = __builtin_amdgcn_readfirstlane(w);  // wave index in SGPRs (DMA destinations)
   auto issue = [&](int t, int slot) __attribute__((always_inline)) {
     const uint8_t* base = Cm2 + (int64_t)t * (32 * QH) * RB;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
-      const int piece = w * PPW + i;
+      const int piece = wu * PPW + i;
       const unsigned dst = lds_base + slot * STAGE_B + piece * 1024;
       asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
                    :: "s"(__builtin_amdgcn_readfirstlane(dst)), "v"(voff[i]), "s"(base)

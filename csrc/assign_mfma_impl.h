@@ -675,11 +675,12 @@ void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int6
     const int row = L / CPR, cp = L % CPR;
     voff[i] = (unsigned)((row * DP + swz<DP>(row, cp) * 8) * 2);
   }
+  const int wu = __builtin_amdgcn_readfirstlane(w);  // wave index in SGPRs (DMA destinations)
   auto issue = [&](int t, int slot) __attribute__((always_inline)) {
     const __bf16* base = Cm2 + (int64_t)t * BNL * DP;
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
-      const int piece = (w * PPW + i) % PIECES;
+      const int piece = (wu * PPW + i) % PIECES;
       const unsigned dst = lds0 + slot * STAGE_B + piece * 1024;
       asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
                    :: "s"(__builtin_amdgcn_readfirstlane(dst)), "v"(voff[i]), "s"(base)

@@ -102,9 +102,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats_kernel(
   constexpr int KS = DP / 16;
   constexpr int HALF = DP / 2;
   constexpr int IMGB = BN * DP * 2;           // bytes of one (hi or lo) stage image
-  constexpr int CHUNKS = 2 * BN * CPR;        // 16-byte chunks per stage
-  constexpr int CPT = CHUNKS / NT;
-  static_assert(CHUNKS % NT == 0, "stage chunks must split over the block");
   __shared__ __attribute__((aligned(16))) char s_c[2][2 * IMGB];
   __shared__ __attribute__((aligned(16))) float s_n[2][BN];
 
@@ -127,30 +124,49 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats_kernel(
     zf = ZERO_FLOOR * xn;
   }
 
-  uint4 pre[CPT];
-  float npre = 0.f;
-#define TDC_STAGE_LOAD(T_)                                                                \
-  {                                                                                       \
-    _Pragma("unroll") for (int i = 0; i < CPT; ++i) {                                     \
-      const int q = tid + i * NT;                                                         \
-      const int hl = q / (BN * CPR), rem = q % (BN * CPR);                                \
-      const __bf16* src = (hl ? Cl : Ch) + ((int64_t)(T_) * BN + rem / CPR) * DP + (rem % CPR) * 8; \
-      TDC_GLOAD16(pre[i], src);                                                           \
-    }                                                                                     \
-    if (tid < BN) npre = cc[(T_) * BN + tid];                                             \
+  // Centroid stages arrive by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction,
+  // lane l -> M0 + 16 l): the XOR swizzle of the stage image is applied on the source side
+  // (coff is an involution in the chunk index), so no staging registers, no ds_write and
+  // no vmcnt wait in the middle of the stage.  Issued by inline asm in the saddr + voffset
+  // form (stage base in SGPRs); the compiler does not count these loads, the explicit
+  // vmcnt(0) before each stage's barrier does.
+  constexpr int PPI = IMGB / 1024;              // 1-KiB pieces per (hi or lo) image
+  constexpr int PPW = 2 * PPI / WAVES;          // pieces per wave per stage
+  static_assert(IMGB % 1024 == 0 && (2 * PPI) % WAVES == 0 && PPI % PPW == 0, "stage pieces");
+  constexpr int G = CPR < 16 ? CPR : 16;
+  constexpr int RPB = 16 / G;
+  const int wu = __builtin_amdgcn_readfirstlane(w);  // wave index in SGPRs (DMA destinations)
+  const int hlw = (wu * PPW) / PPI;             // this wave's image
+  unsigned voff[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int q = ((w * PPW + i) % PPI) * 64 + lane;  // destination chunk in the image
+    const int row = q / CPR, cs = q % CPR;
+    voff[i] = (unsigned)(row * DP * 2 + 16 * (cs ^ ((row / RPB) & (G - 1))));
   }
-#define TDC_STAGE_STORE(B_)                                                               \
+  const unsigned lds_c = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)&s_c[0][0];
+  const unsigned lds_n = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)&s_n[0][0];
+#define TDC_STAGE_LOAD(T_, B_)                                                            \
   {                                                                                       \
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                      \
-    _Pragma("unroll") for (int i = 0; i < CPT; ++i) {                                     \
-      const int q = tid + i * NT;                                                         \
-      const int hl = q / (BN * CPR), rem = q % (BN * CPR);                                \
-      *reinterpret_cast<uint4*>(&s_c[B_][hl * IMGB + coff<DP>(rem / CPR, rem % CPR)]) = pre[i]; \
+    const __bf16* base_ = (hlw ? Cl : Ch) + (int64_t)(T_) * BN * DP;                      \
+    _Pragma("unroll") for (int i = 0; i < PPW; ++i) {                                     \
+      const int pc_ = wu * PPW + i;                                                       \
+      const unsigned dst_ = lds_c + (B_) * 2 * IMGB + (pc_ / PPI) * IMGB + (pc_ % PPI) * 1024; \
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"                  \
+                   :: "s"(__builtin_amdgcn_readfirstlane(dst_)), "v"(voff[i]),             \
+                      "s"(uniform_ptr(base_))                                             \
+                   : "memory", "m0");                                                     \
     }                                                                                     \
-    if (tid < BN) s_n[B_][tid] = npre;                                                    \
+    if (wu == 0 && lane < BN / 4) {                                                        \
+      const float* nb_ = cc + (int64_t)(T_) * BN;                                         \
+      const unsigned nd_ = lds_n + (B_) * BN * 4;                                         \
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"                  \
+                   :: "s"(__builtin_amdgcn_readfirstlane(nd_)), "v"((unsigned)(lane * 16)), \
+                      "s"(uniform_ptr(nb_)) : "memory", "m0");                            \
+    }                                                                                     \
   }
-  TDC_STAGE_LOAD(0)
-  TDC_STAGE_STORE(0)
+  TDC_STAGE_LOAD(0, 0)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   float S = 0.f, best = INFINITY;
@@ -211,21 +227,21 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats_kernel(
   f32x16 acc0, acc1;
   for (int t = 0; t < nstages; ++t) {
     const int buf = t & 1;
-    if (t + 1 < nstages) TDC_STAGE_LOAD(t + 1)
+    // buffer buf ^ 1 was last read in stage t - 1, before that stage's barrier
+    if (t + 1 < nstages) TDC_STAGE_LOAD(t + 1, buf ^ 1)
     const char* cb = s_c[buf];
     const float* ns = s_n[buf];
     TDC_PHASE(acc0, 0)
     if (t > 0) TDC_EPI(acc1, 1, t - 1)
     TDC_PHASE(acc1, 1)
     TDC_EPI(acc0, 0, t)
-    if (t + 1 < nstages) TDC_STAGE_STORE(buf ^ 1)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage t + 1 landed (this wave's part)
     __syncthreads();
   }
   TDC_EPI(acc1, 1, nstages - 1)
 #undef TDC_PHASE
 #undef TDC_EPI
 #undef TDC_STAGE_LOAD
-#undef TDC_STAGE_STORE
 
   S += __shfl_xor(S, 32, 64);
   const unsigned e0 = __float_as_uint(best) & 15u;
@@ -266,9 +282,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
   constexpr int NDT = DP / 32;            // 32-feature output tiles
   constexpr int IMG = TP * DP * 2;        // bytes of one hi (or lo) image
   constexpr int NT = WAVES * 64;
-  constexpr int CHUNKS = 2 * TP * CPR;
-  constexpr int CPT = CHUNKS / NT;
-  static_assert(CHUNKS % NT == 0, "tile chunks must split over the block's threads");
   static_assert(WAVES == 4 || WAVES == 8, "4 or 8 waves");
   __shared__ __attribute__((aligned(16))) char s_x[2][2 * IMG];
   __shared__ __attribute__((aligned(16))) float s_xx[2][TP];
@@ -310,17 +323,38 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     for (int i = 0; i < 16; ++i) out[dt][i] = 0.f;
   float wsum = 0.f;
 
-  uint4 pre[CPT];
+  // X tiles arrive by LDS-DMA (as the stats pass's centroid stages): source-side XOR
+  // swizzle (xoff is an involution in the chunk index), rows past the range clamped to its
+  // last row through the per-lane offset, inline asm in the saddr + voffset form.  Only
+  // the 2 x 64 row statistics still go through registers (padded rows get special
+  // values).
+  constexpr int PPI = IMG / 1024;               // 1-KiB pieces per (hi or lo) image
+  constexpr int PPW = 2 * PPI / WAVES;          // pieces per wave per tile
+  static_assert(IMG % 1024 == 0 && (2 * PPI) % WAVES == 0 && PPI % PPW == 0, "tile pieces");
+  const int wu = __builtin_amdgcn_readfirstlane(w);  // wave index in SGPRs (DMA destinations)
+  const int hlw = (wu * PPW) / PPI;             // this wave's image
+  int prow[PPW];
+  unsigned pcol[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int q = ((w * PPW + i) % PPI) * 64 + lane;  // destination chunk in the image
+    prow[i] = q / CPR;
+    pcol[i] = (unsigned)(xoff<DP>(prow[i], q % CPR) - prow[i] * DP * 2);  // = source chunk
+  }
+  const unsigned lds_x = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)&s_x[0][0];
   float pv = 0.f;
-#define TDC_TILE_LOAD(R0_)                                                                \
+#define TDC_TILE_LOAD(R0_, B_)                                                            \
   {                                                                                       \
-    _Pragma("unroll") for (int i = 0; i < CPT; ++i) {                                     \
-      const int q = tid + i * NT;                                                         \
-      const int hl = q / (TP * CPR), rem = q % (TP * CPR);                                \
-      int64_t gr = (R0_) + rem / CPR;                                                     \
-      gr = gr < b ? gr : b - 1;                                                           \
-      const __bf16* src = (hl ? Xl : Xh) + gr * DP + (rem % CPR) * 8;                     \
-      TDC_GLOAD16(pre[i], src);                                                           \
+    const __bf16* base_ = (hlw ? Xl : Xh) + (R0_) * DP;                                   \
+    const int last_ = (int)(b - 1 - (R0_));                                               \
+    _Pragma("unroll") for (int i = 0; i < PPW; ++i) {                                     \
+      const int pc_ = wu * PPW + i;                                                       \
+      const int rr_ = prow[i] < last_ ? prow[i] : last_;                                  \
+      const unsigned dst_ = lds_x + (B_) * 2 * IMG + (pc_ / PPI) * IMG + (pc_ % PPI) * 1024; \
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"                  \
+                   :: "s"(__builtin_amdgcn_readfirstlane(dst_)),                          \
+                      "v"((unsigned)(rr_ * DP * 2) + pcol[i]), "s"(uniform_ptr(base_))    \
+                   : "memory", "m0");                                                     \
     }                                                                                     \
     if (tid < 2 * TP) {                                                                   \
       const int64_t gr = (R0_) + (tid & (TP - 1));                                        \
@@ -331,16 +365,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
 #define TDC_TILE_STORE(B_)                                                                \
   {                                                                                       \
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                      \
-    _Pragma("unroll") for (int i = 0; i < CPT; ++i) {                                     \
-      const int q = tid + i * NT;                                                         \
-      const int hl = q / (TP * CPR), rem = q % (TP * CPR);                                \
-      *reinterpret_cast<uint4*>(&s_x[B_][hl * IMG + xoff<DP>(rem / CPR, rem % CPR)]) = pre[i]; \
-    }                                                                                     \
     if (tid < TP) s_xx[B_][tid] = pv;                                                     \
     else if (tid < 2 * TP) s_in[B_][tid - TP] = pv;                                       \
   }
   if (a < b) {
-    TDC_TILE_LOAD(a)
+    TDC_TILE_LOAD(a, 0)
     TDC_TILE_STORE(0)
   }
   __syncthreads();
@@ -350,7 +379,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
   int buf = 0;
   for (int64_t r0 = a; r0 < b; r0 += TP) {
     const bool more = r0 + TP < b;
-    if (more) TDC_TILE_LOAD(r0 + TP)
+    // buffer buf ^ 1 was last read in the previous tile, before its barrier
+    if (more) TDC_TILE_LOAD(r0 + TP, buf ^ 1)
     const char* xh = s_x[buf];
     const char* xl = s_x[buf] + IMG;
     // Software pipeline over the two 32-point halves, written out explicitly so that the

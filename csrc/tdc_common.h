@@ -45,6 +45,15 @@ template <typename T, typename A> __device__ __forceinline__ A to_acc(T v) { ret
 __device__ __forceinline__ void atomic_add(float* p, float v) { atomicAdd(p, v); }
 __device__ __forceinline__ void atomic_add(double* p, double v) { atomicAdd(p, v); }
 
+// A wave-uniform pointer in SGPRs (readfirstlane of both halves): the saddr operand of
+// an inline-asm global / LDS-DMA load, when the compiler cannot prove the value uniform.
+__device__ __forceinline__ const void* uniform_ptr(const void* p) {
+  const uint64_t v = (uint64_t)(uintptr_t)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return (const void*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+
 // Stage rows [r0, r0 + 256) of a CONTIGUOUS row-major X (ldx == D, 16-B aligned base)
 // into LDS with 16-byte loads.  Returns the number of valid rows; the caller syncs before
 // reading s_x[row * D + d].
