@@ -666,7 +666,11 @@ void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int6
   // 1.5 % (10M rows) to 5 % (1.25M rows) more time (tools/ring3_ab.hip,
   // profiles/ring3_ab_r03.txt).  The compiler does not count these loads in its vmcnt
   // bookkeeping; the explicit stage-end waits below do (extra outstanding loads only
-  // make the compiler's own vmcnt waits more conservative).
+  // make the compiler's own vmcnt waits more conservative).  M0 is a reserved register
+  // to hipcc (-Winline-asm notes the clobber): it sets M0 immediately before each of its
+  // own LDS-DMA instructions (checked in the ISA: the norm DMA below), so the value this
+  // asm leaves in M0 is never relied on.  The builtin with a uniform base + 32-bit offset
+  // still fell back to 64-bit VGPR addresses inside the ring loop.
   unsigned voff[PPW];
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
