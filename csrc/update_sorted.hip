@@ -172,7 +172,8 @@ template <int NT>
 __global__ __launch_bounds__(NT) void bscatter_kernel(const int32_t* __restrict__ labels, int64_t N,
                                                        int K, int* __restrict__ cursor,
                                                        int32_t* __restrict__ perm, int64_t per_block,
-                                                       const int32_t* __restrict__ rowidx) {
+                                                       const int32_t* __restrict__ rowidx,
+                                                       int parts) {
   // perm holds X row numbers: i itself, or rowidx[i] for an indexed (mini-batch) pass
 #define TDC_ROW(ii) (rowidx ? rowidx[ii] : (int32_t)(ii))
   extern __shared__ int s_mem[];
@@ -201,17 +202,25 @@ __global__ __launch_bounds__(NT) void bscatter_kernel(const int32_t* __restrict_
     s_cur[k] = c ? atomicAdd(cursor + k, c) : 0;
   }
   __syncthreads();
-  i = r0 + tid;
-  for (; i + 3 * NT < r1; i += 4 * NT) {
-    const int a0 = labels[i], a1 = labels[i + NT], a2 = labels[i + 2 * NT], a3 = labels[i + 3 * NT];
-    if ((unsigned)a0 < (unsigned)K) perm[atomicAdd(s_cur + a0, 1)] = TDC_ROW(i);
-    if ((unsigned)a1 < (unsigned)K) perm[atomicAdd(s_cur + a1, 1)] = TDC_ROW(i + NT);
-    if ((unsigned)a2 < (unsigned)K) perm[atomicAdd(s_cur + a2, 1)] = TDC_ROW(i + 2 * NT);
-    if ((unsigned)a3 < (unsigned)K) perm[atomicAdd(s_cur + a3, 1)] = TDC_ROW(i + 3 * NT);
-  }
-  for (; i < r1; i += NT) {
-    const int a0 = labels[i];
-    if ((unsigned)a0 < (unsigned)K) perm[atomicAdd(s_cur + a0, 1)] = TDC_ROW(i);
+  // The scatter runs in `parts` passes over bin ranges [p K / parts, (p + 1) K / parts):
+  // the block re-reads its (L2-resident) labels, and the perm lines it is writing at any
+  // time span 1/parts of the bins, so the partial-line stores of the XCD's blocks combine
+  // in its L2 instead of thrashing it.
+  for (int part = 0; part < parts; ++part) {
+    const unsigned lo = (unsigned)((int64_t)K * part / parts);
+    const unsigned n = (unsigned)((int64_t)K * (part + 1) / parts) - lo;
+    i = r0 + tid;
+    for (; i + 3 * NT < r1; i += 4 * NT) {
+      const int a0 = labels[i], a1 = labels[i + NT], a2 = labels[i + 2 * NT], a3 = labels[i + 3 * NT];
+      if ((unsigned)a0 - lo < n) perm[atomicAdd(s_cur + a0, 1)] = TDC_ROW(i);
+      if ((unsigned)a1 - lo < n) perm[atomicAdd(s_cur + a1, 1)] = TDC_ROW(i + NT);
+      if ((unsigned)a2 - lo < n) perm[atomicAdd(s_cur + a2, 1)] = TDC_ROW(i + 2 * NT);
+      if ((unsigned)a3 - lo < n) perm[atomicAdd(s_cur + a3, 1)] = TDC_ROW(i + 3 * NT);
+    }
+    for (; i < r1; i += NT) {
+      const int a0 = labels[i];
+      if ((unsigned)a0 - lo < n) perm[atomicAdd(s_cur + a0, 1)] = TDC_ROW(i);
+    }
   }
 #undef TDC_ROW
 }
@@ -524,8 +533,12 @@ int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int6
     int64_t per = (N + blocks - 1) / blocks;
     if (per < 4096) per = 4096;
     blocks = (N + per - 1) / per;
+    // bin-range passes: the XCD's 32 blocks each write ~per/K entries into each of K perm
+    // segments; with K=1024 at N=10M that is ~5 MB of lines in flight per XCD (4 MB L2)
+    const int parts = K >= 512 && per >= 8 * (int64_t)K ? 2 : 1;
     hipLaunchKernelGGL(bscatter_kernel<1024>, dim3((unsigned)blocks), dim3(1024),
-                       2 * sizeof(int) * (size_t)K, s, labels, N, K, cursor, perm, per, rowidx);
+                       2 * sizeof(int) * (size_t)K, s, labels, N, K, cursor, perm, per, rowidx,
+                       parts);
     TDC_CHECK_LAUNCH();
   } else {
     int64_t blocks = (int64_t)num_cus * 4;
