@@ -59,13 +59,16 @@ int tdc_assign_mfma_bf16(const void* X, int64_t N, int64_t ldx, int DP, const vo
       else
         hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<64, 8, 3, 4, 4>), grid8, dim3(256), 0,
                            stream, x, N, ldx, c, cnorm, Kp / 64, labels, mind);
-    } else if (DP == 128 && N >= (1 << 22)) {
-      // large shards: P=8 point tiles per wave (512 points per workgroup, 256 VGPRs, two
-      // waves per SIMD) halve the ring refill per point; NST=2.  1.93-1.95 -> 1.91 ms at
-      // the headline shape (profiles/assign_ring3_ablation_r02.txt).  Below ~4M rows P=4
-      // (twice the workgroups, three waves per SIMD) wins: 0.248 vs 0.256-0.276 ms at
-      // 1.25M (the 8-GPU share of the headline), 0.486-0.497 vs 0.494-0.509 at 2.5M, even
-      // at 5M (profiles/ring3_p4_vs_p8_*_r03.txt).
+    } else if (DP == 128 && N >= (1 << 20)) {
+      // shards from 1M rows: P=8 point tiles per wave (512 points per workgroup, two waves
+      // per SIMD) halve the ring refill per point; NST=2.  1.93-1.95 -> 1.91 ms at the
+      // headline shape (profiles/assign_ring3_ablation_r02.txt).  With the builtin LDS-DMA
+      // (256 VGPRs) P=4 had won below ~4M rows (profiles/ring3_p4_vs_p8_*_r03.txt); with
+      // the saddr-form DMA (244 VGPRs) P=8 wins at every strong-scaling shard size:
+      // 0.247-0.251 vs 0.254-0.255 ms at 1.25M (the 8-GPU share of the headline),
+      // 0.484-0.493 vs 0.498-0.502 at 2.5M, 0.948-0.959 vs 0.978-0.989 at 5M
+      // (profiles/ring3_p8_threshold_r03.txt).  Below 1M rows P=4 keeps twice the
+      // workgroups.
       const int64_t per8 = 4 * 8 * 16;
       hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<128, 8, 2, 4, 4>),
                          dim3((unsigned)((N + per8 - 1) / per8)), dim3(256), 0, stream, x, N, ldx,
