@@ -81,22 +81,34 @@ __global__ __launch_bounds__(1024) void scan_kernel(int* __restrict__ cnt, int K
                                                     ACC* __restrict__ counts_acc,
                                                     float* __restrict__ cnt_hi,
                                                     float* __restrict__ cnt_lo) {
-  __shared__ int s_part[1024];
-  const int tid = threadIdx.x;
+  __shared__ int s_wave[16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int per = (K + 1023) / 1024;
   const int k0 = tid * per, k1 = min(K, k0 + per);
   int s = 0;
   for (int k = k0; k < k1; ++k) s += cnt[k];
-  s_part[tid] = s;
-  __syncthreads();
-  // Hillis-Steele inclusive scan over 1024 partials
-  for (int o = 1; o < 1024; o <<= 1) {
-    const int v = tid >= o ? s_part[tid - o] : 0;
-    __syncthreads();
-    s_part[tid] += v;
-    __syncthreads();
+  // inclusive scan: within each wave by shuffles (no barrier), then over the 16 wave
+  // totals by wave 0 (two barriers in all; the Hillis-Steele form over LDS took 20)
+  int inc = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += v;
   }
-  int run = s_part[tid] - s;  // exclusive prefix of this thread's range
+  if (lane == 63) s_wave[wv] = inc;
+  __syncthreads();
+  if (wv == 0) {
+    int t = lane < 16 ? s_wave[lane] : 0;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const int v = __shfl_up(t, o, 64);
+      if (lane >= o) t += v;
+    }
+    if (lane < 16) s_wave[lane] = t;  // inclusive totals of waves 0..lane
+  }
+  __syncthreads();
+  inc += wv > 0 ? s_wave[wv - 1] : 0;
+  int run = inc - s;  // exclusive prefix of this thread's range
   for (int k = k0; k < k1; ++k) {
     const int c = cnt[k];
     cnt[k] = 0;  // the histogram is left zeroed for the next call (no memset launch)
@@ -109,7 +121,7 @@ __global__ __launch_bounds__(1024) void scan_kernel(int* __restrict__ cnt, int K
     }
     run += c;
   }
-  if (tid == 1023) offsets[K] = s_part[1023];
+  if (tid == 1023) offsets[K] = inc;
 }
 
 // block-aggregated counting-sort scatter: perm[offset[label] + rank] = i
