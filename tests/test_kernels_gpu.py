@@ -118,6 +118,31 @@ def test_update_sorted(gpu, xdt, n, d, k):
         torch.testing.assert_close(sums.double(), 2 * s_ref, rtol=tol, atol=tol * 10)
 
 
+@pytest.mark.parametrize("n,k", [(2_500_000, 1024), (1_250_000, 1024)])
+def test_update_sorted_scatter_passes(gpu, n, k):
+    """Large per-block label ranges (>= 8 labels per bin per block) scatter in two bin-range
+    passes: the permutation in the workspace is still every row exactly once, grouped by
+    label, and the sums / counts match the fp64 oracle (1.25M rows: the one-pass form)."""
+    from tensorflow_distributed_clustering_amd import _native
+    ops = _native.require()
+    d = 128
+    g = torch.Generator().manual_seed(n + 7)
+    x = torch.randn(n, d, generator=g).to(torch.bfloat16).to(gpu)
+    lab = torch.randint(0, k, (n,), generator=g, dtype=torch.int32).to(gpu)
+    lab[: n // 5] = 3  # one hot bin
+    work = torch.zeros(int(ops.update_sorted_workspace(n, k)), dtype=torch.int32, device=gpu)
+    sums = torch.zeros(k, d, dtype=torch.float32, device=gpu)
+    counts = torch.zeros(k, dtype=torch.float32, device=gpu)
+    ops.update_sorted(x, lab, sums, counts, work)
+    perm = work[3 * k + 1: 3 * k + 1 + n].long()
+    assert torch.equal(torch.sort(perm).values, torch.arange(n, device=gpu))
+    grouped = lab[perm]
+    assert bool((grouped[1:] >= grouped[:-1]).all())
+    s_ref, c_ref = ref.cluster_sums(x.double(), lab, k, acc_dtype=torch.float64)
+    assert torch.equal(counts.double(), c_ref)
+    torch.testing.assert_close(sums.double(), s_ref, rtol=1e-3, atol=1e-2)
+
+
 @pytest.mark.parametrize("n,k", [(1_250_000, 1024), (40_000, 4096), (3000, 64)])
 def test_update_sorted_zero_first_and_clean_workspace(gpu, n, k):
     """zero_first: the all-reduce buffer [sums | counts | tail] full of garbage is cleared by
