@@ -106,6 +106,15 @@ def parse(argv=None):
                          "(always on at world > 1)")
     ap.add_argument("--centers-out", default=None,
                     help="rank 0 writes the final centroids (.npy, fp64) here")
+    ap.add_argument("--update", default="auto", choices=["auto", "full", "delta"],
+                    help="K-Means centroid update: delta moves only the rows whose label "
+                         "changed between fp64 running totals (with a full re-sum every "
+                         "--delta-refresh steps and after steps that moved > 40%% of the rows); "
+                         "full re-sums every row every step; auto = delta where supported")
+    ap.add_argument("--delta-refresh", type=int, default=32,
+                    help="delta update: full re-sum every this many steps (0: never)")
+    ap.add_argument("--no-check", action="store_true",
+                    help="skip the correctness witness after the timed region")
     a = ap.parse_args(argv)
     p = PRESETS[a.preset]
     given = set(x.split("=")[0].lstrip("-").replace("-", "_") for x in (argv or sys.argv[1:]))
@@ -149,7 +158,8 @@ def main(argv=None):
         x = gaussian_blobs(e - s, a.dim, a.k, seed=a.seed, row_offset=s, dtype=dt, device=dev)
     cfg = tdc.ClusterConfig(n_clusters=a.k, max_iter=a.steps, dtype=a.dtype, init=a.init,
                             seed=a.seed, compute_inertia=False, algorithm=a.algorithm,
-                            fuzzifier=a.fuzzifier)
+                            fuzzifier=a.fuzzifier, update=a.update,
+                            delta_refresh=a.delta_refresh)
     if a.mode == "minibatch":
         from tensorflow_distributed_clustering_amd.models.minibatch import MiniBatchStepper
         eng = MiniBatchStepper(x, cfg.replace(batch_size=a.batch_size or (1 << 20)), comm,
@@ -190,6 +200,7 @@ def main(argv=None):
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     h2d0 = getattr(x, "bytes_h2d", 0) if src_info is not None else 0
+    upd0 = eng.update_stats() if hasattr(eng, "update_stats") else None
     t0 = time.perf_counter()
     for _ in range(a.steps):
         eng.step()
@@ -202,6 +213,21 @@ def main(argv=None):
 
     ms = elapsed / max(1, a.steps) * 1e3
     pps = points_per_step * a.steps / elapsed
+    # ---- everything below runs after the timed region ----
+    update_info = None
+    if hasattr(eng, "update_stats"):
+        update_info = {"mode": eng.update_mode}
+        upd1 = eng.update_stats()
+        if upd0 is not None and upd1 is not None:
+            dm = upd1["moved_rows"] - upd0["moved_rows"]
+            ds = upd1["moved_steps"] - upd0["moved_steps"]
+            update_info.update({
+                "moved_frac_mean": dm / max(1.0, ds) / max(1, n_global),
+                "full_steps_timed": int(upd1["full_steps"] - upd0["full_steps"]),
+                "refresh_every": a.delta_refresh})
+    check = None
+    if not a.no_check and src_info is None:
+        check = witness(eng, x, n_global, s, e, comm, torch, a)
     breakdown = None
     if ((a.profile_steps or world > 1) and a.mode == "lloyd" and a.method == "kmeans"
             and a.algorithm == "lloyd" and not getattr(eng, "streamed", False)):
@@ -237,6 +263,10 @@ def main(argv=None):
                        "K": a.k, "D": a.dim, "points_per_gpu": e - s,
                        "parallelism": f"dp{world}"},
         }
+        if update_info is not None:
+            out["update"] = update_info
+        if check is not None:
+            out["check"] = check
         if breakdown:
             out["phase_ms"] = breakdown
         if src_info is not None:
@@ -293,51 +323,89 @@ def vs_baseline(a, world, pps):
 
 def phase_breakdown(eng, torch, dev, reps: int = 5):
     """Per-phase time of one step, max over ranks (diagnostic, after the timed run; the
-    phases run eagerly with an event -- or a host clock on CPU -- between them, so their
-    sum is a little above a graph-replayed step).  The all-reduce phase includes the
-    wait for the slowest rank.  rsag engines: "allreduce" is reduce-scatter + all-gather."""
-    from tensorflow_distributed_clustering_amd.ops import NativeUpdate
+    phases (``LloydEngine.phase_fns``: buffer fill, assign, local update -- the delta update
+    when the engine uses it --, all-reduce, finalize) run eagerly with an event -- or a host
+    clock on CPU -- between them, so their sum is a little above a graph-replayed step).
+    The all-reduce phase includes the wait for the slowest rank.  rsag engines:
+    "allreduce" is reduce-scatter + all-gather + the slice finalize, "finalize" is empty."""
     cuda = dev.type == "cuda"
-    if cuda:
-        mark = lambda: torch.cuda.Event(enable_timing=True)
-    else:
-        mark = lambda: None
-    names = ["zero", "assign", "update", "allreduce", "finalize"]
+    phases = eng.phase_fns()
+    if getattr(eng, "rsag", False):
+        phases = phases[:3] + [("allreduce", eng._reduce_scatter_finalize),
+                               ("finalize", lambda: None)]
+    names = [n for n, _ in phases]
     tot = {n: 0.0 for n in names}
-    loc = eng.local
     c_keep = eng.C.clone()
     eng.comm.barrier()
     for _ in range(reps):
         e, t = [], []
 
         def rec():
-            ev = mark()
+            ev = torch.cuda.Event(enable_timing=True) if cuda else None
             if ev is not None:
                 ev.record()
             e.append(ev)
             t.append(time.perf_counter())
         rec()
-        eng.buf.zero_(); rec()
-        if isinstance(getattr(loc, "update", None), NativeUpdate):
-            loc.assign(eng.C, eng.labels, None); rec()
-            loc.update(loc.x, eng.labels, eng.sums, eng.counts); rec()
-        else:
-            loc.step(eng.C, eng.labels, None, eng.sums, eng.counts); rec(); rec()
-        if getattr(eng, "rsag", False):
-            eng._reduce_scatter_finalize(); rec(); rec()
-        else:
-            eng.comm.allreduce_bucketed_(eng.buf, eng.bucket_bytes); rec()
-            loc.finalize(eng.sums, eng.counts, eng.C, None); rec()
+        for _, fn in phases:
+            fn()
+            rec()
         if cuda:
             torch.cuda.synchronize(dev)
         for i, n in enumerate(names):
             dt = e[i].elapsed_time(e[i + 1]) if cuda else (t[i + 1] - t[i]) * 1e3
             tot[n] += dt / reps
-    eng.C.copy_(c_keep)  # leave the engine as the timed run left it
-    loc.prepare(eng.C)
+    eng.C.copy_(c_keep)  # leave the engine's centroids as the timed run left them
+    eng.local.prepare(eng.C)
     vals = torch.tensor([tot[n] for n in names], dtype=torch.float64, device=dev)
     eng.comm.allreduce_(vals, "max")
     return {n: round(float(v), 4) for n, v in zip(names, vals.tolist())}
+
+
+WITNESS_ROWS = 65536
+
+
+def witness(eng, x, n_global, s, e, comm, torch, a):
+    """Correctness witness, computed after the timed region (never inside it): a label pass
+    against the final centroids, then (1) the global inertia sum_i ||x_i - c_{label_i}||^2
+    in fp64 over every row, and (2) the agreement of the kernel labels with an exact fp64
+    argmin on a fixed sample of WITNESS_ROWS global rows (evenly spaced,
+    world-size invariant).  The oracle sees the same rows the kernels see (the bf16 shard
+    upcast), so disagreements are near ties of the bf16 / fp8 distance arithmetic;
+    ``agree_tie_tol`` also counts a label whose exact distance is within 1e-5 (relative)
+    of the exact minimum."""
+    from tensorflow_distributed_clustering_amd.ops import reference as ref
+    dev = comm.device
+    C = (eng.centers() if hasattr(eng, "centers") else eng.C).double()
+    if hasattr(eng, "blabels"):  # mini-batch stepper: labels from its own label pass
+        labels, _ = eng.label_pass()
+    else:
+        eng.label_pass()
+        labels = eng.labels
+    xs = x[:, : C.shape[1]]
+    inertia = 0.0
+    step = max(1, (1 << 26) // max(1, C.shape[1]))
+    for r0 in range(0, xs.shape[0], step):
+        r1 = min(xs.shape[0], r0 + step)
+        diff = xs[r0:r1].double() - C.index_select(0, labels[r0:r1].long())
+        inertia += float(diff.pow_(2).sum())
+    g = torch.arange(WITNESS_ROWS, dtype=torch.float64) * (n_global / WITNESS_ROWS)
+    g = torch.unique(g.floor().long())
+    loc = g[(g >= s) & (g < e)] - s
+    agree = near = 0.0
+    if loc.numel():
+        idx = loc.to(dev)
+        xsm = xs.index_select(0, idx).double()
+        lab_o, d_o = ref.assign(xsm, C, exact=False)  # fp64 GEMM form
+        lab_k = labels.index_select(0, idx).long()
+        d_k = (xsm - C.index_select(0, lab_k)).pow_(2).sum(1)
+        agree = float((lab_o.long() == lab_k).sum())
+        near = float((d_k <= d_o.double() * (1 + 1e-5) + 1e-12).sum())
+    tot = comm.sum_scalar(float(loc.numel()))
+    return {"inertia": comm.sum_scalar(inertia),
+            "agree_fp64_sample": comm.sum_scalar(agree) / max(1.0, tot),
+            "agree_tie_tol": comm.sum_scalar(near) / max(1.0, tot),
+            "sample_rows": int(tot)}
 
 
 if __name__ == "__main__":

@@ -534,6 +534,109 @@ void update_sorted_indexed(const at::Tensor& X, const at::Tensor& rowidx, const 
         "update_sorted_indexed");
 }
 
+// ---- delta update of plain Lloyd (kernels.h tdc_delta_*) ----
+int64_t delta_workspace(int64_t N, int64_t K) { return tdc_delta_workspace(N, (int)K); }
+
+void check_ctrl(const at::Tensor& ctrl, const at::Tensor& like, const char* op) {
+  TORCH_CHECK(ctrl.scalar_type() == at::kInt && ctrl.is_contiguous() &&
+                  ctrl.numel() >= TDC_DC_WORDS && ctrl.device() == like.device(),
+              "tdc.", op, ": ctrl must be int32 [", (int)TDC_DC_WORDS, "] on the data's device");
+}
+
+void delta_update(const at::Tensor& X, const at::Tensor& labels, at::Tensor& prev, at::Tensor& sums,
+                  at::Tensor& counts, at::Tensor& work, at::Tensor& ctrl,
+                  const std::optional<at::Tensor>& cnt_hi, const std::optional<at::Tensor>& cnt_lo,
+                  const std::optional<at::Tensor>& moved, const std::optional<at::Tensor>& zero_first) {
+  check_cuda(X, "X");
+  check_rows(X, "X");
+  const int64_t N = X.size(0);
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous() && labels.numel() >= N,
+              "tdc.delta_update: labels int32 [N]");
+  TORCH_CHECK(prev.scalar_type() == at::kInt && prev.is_contiguous() && prev.numel() >= N,
+              "tdc.delta_update: prev int32 [N]");
+  TORCH_CHECK(sums.dim() == 2 && sums.is_contiguous() && counts.is_contiguous(),
+              "tdc.delta_update: sums");
+  TORCH_CHECK(sums.scalar_type() == counts.scalar_type() && counts.numel() >= sums.size(0),
+              "tdc.delta_update: counts");
+  TORCH_CHECK(X.size(1) >= sums.size(1), "tdc.delta_update: X narrower than sums");
+  const int K = (int)sums.size(0);
+  TORCH_CHECK(K <= TDC_DELTA_MAX_K, "tdc.delta_update: K > ", TDC_DELTA_MAX_K);
+  TORCH_CHECK(N < ((int64_t)1 << 30), "tdc.delta_update: shard has >= 2^30 rows");
+  TORCH_CHECK(work.scalar_type() == at::kInt && work.is_contiguous() &&
+                  work.numel() >= tdc_delta_workspace(N, K),
+              "tdc.delta_update: workspace too small");
+  check_ctrl(ctrl, X, "delta_update");
+  check_split(cnt_hi, cnt_lo, K, "delta_update");
+  if (moved.has_value() && moved->defined())
+    TORCH_CHECK(moved->scalar_type() == sums.scalar_type() && moved->numel() >= 1,
+                "tdc.delta_update: moved must be one element of the sums dtype");
+  int64_t zbytes = 0;
+  if (zero_first.has_value() && zero_first->defined()) {
+    TORCH_CHECK(zero_first->is_contiguous() && zero_first->device() == X.device() &&
+                    (zero_first->numel() * zero_first->element_size()) % 4 == 0,
+                "tdc.delta_update: zero_first must be a contiguous device buffer of 4-byte words");
+    zbytes = zero_first->numel() * zero_first->element_size();
+  }
+  const DevGuard guard(X.device());
+  check(tdc_delta_update(dcode(X.scalar_type()), dcode(sums.scalar_type()), X.data_ptr(), N,
+                         X.stride(0), (int)sums.size(1), labels.data_ptr<int32_t>(),
+                         prev.data_ptr<int32_t>(), K, sums.data_ptr(), counts.data_ptr(),
+                         work.data_ptr<int>(), ctrl.data_ptr<int>(), num_cus(X.device().index()),
+                         cur_stream(), static_cast<float*>(opt_ptr(cnt_hi)),
+                         static_cast<float*>(opt_ptr(cnt_lo)), opt_ptr(moved), opt_ptr(zero_first),
+                         zbytes),
+        "delta_update");
+}
+
+void delta_finalize(const at::Tensor& sums, const at::Tensor& counts,
+                    const std::optional<at::Tensor>& cnt_hi, const std::optional<at::Tensor>& cnt_lo,
+                    const std::optional<at::Tensor>& moved, at::Tensor& G, at::Tensor& C,
+                    int64_t policy, const std::optional<at::Tensor>& shift,
+                    const std::optional<at::Tensor>& Cm2, const std::optional<at::Tensor>& cnorm,
+                    at::Tensor& ctrl, const std::optional<at::Tensor>& stats, int64_t refresh,
+                    double theta_n) {
+  check_cuda(C, "C");
+  TORCH_CHECK(C.is_contiguous() && C.dim() == 2, "tdc.delta_finalize: C");
+  const int K = (int)C.size(0), D = (int)C.size(1);
+  TORCH_CHECK(sums.is_contiguous() && sums.numel() == (int64_t)K * D, "tdc.delta_finalize: sums");
+  TORCH_CHECK(counts.scalar_type() == sums.scalar_type() && counts.is_contiguous() &&
+                  counts.numel() >= K, "tdc.delta_finalize: counts");
+  TORCH_CHECK(G.scalar_type() == at::kDouble && G.is_contiguous() &&
+                  G.numel() >= (int64_t)K * D + K, "tdc.delta_finalize: G fp64 [K*D + K]");
+  check_split(cnt_hi, cnt_lo, K, "delta_finalize");
+  if (moved.has_value() && moved->defined())
+    TORCH_CHECK(moved->scalar_type() == sums.scalar_type() && moved->numel() >= 1,
+                "tdc.delta_finalize: moved");
+  int Kp = K, DP = D;
+  if (Cm2.has_value() && Cm2->defined()) {
+    TORCH_CHECK(Cm2->scalar_type() == at::kBFloat16 && Cm2->is_contiguous(), "tdc.delta_finalize: Cm2");
+    TORCH_CHECK(cnorm.has_value() && cnorm->defined(), "tdc.delta_finalize: cnorm required with Cm2");
+    Kp = (int)Cm2->size(0);
+    DP = (int)Cm2->size(1);
+    TORCH_CHECK(Kp >= K && DP >= D, "tdc.delta_finalize: Cm2 smaller than C");
+  }
+  float* sh = nullptr;
+  if (shift.has_value() && shift->defined()) {
+    TORCH_CHECK(shift->scalar_type() == at::kFloat, "tdc.delta_finalize: shift fp32");
+    sh = shift->data_ptr<float>();
+  }
+  double* st = nullptr;
+  if (stats.has_value() && stats->defined()) {
+    TORCH_CHECK(stats->scalar_type() == at::kDouble && stats->numel() >= 4 && stats->is_contiguous(),
+                "tdc.delta_finalize: stats fp64 [4]");
+    st = stats->data_ptr<double>();
+  }
+  check_ctrl(ctrl, C, "delta_finalize");
+  const DevGuard guard(C.device());
+  check(tdc_delta_finalize(dcode(sums.scalar_type()), dcode(C.scalar_type()), sums.data_ptr(),
+                           counts.data_ptr(), static_cast<const float*>(opt_ptr(cnt_hi)),
+                           static_cast<const float*>(opt_ptr(cnt_lo)), opt_ptr(moved),
+                           G.data_ptr<double>(), K, D, C.data_ptr(), (int)policy, sh, opt_ptr(Cm2),
+                           static_cast<float*>(opt_ptr(cnorm)), Kp, DP, ctrl.data_ptr<int>(), st,
+                           (int)refresh, theta_n, cur_stream()),
+        "delta_finalize");
+}
+
 void sculley_update(const at::Tensor& sums, const at::Tensor& counts, at::Tensor& C, at::Tensor& v,
                     const std::optional<at::Tensor>& shift, const std::optional<at::Tensor>& Cm2,
                     const std::optional<at::Tensor>& cnorm) {
@@ -815,6 +918,9 @@ TORCH_LIBRARY(tdc, m) {
   m.def("assign_bf16_top2(Tensor X, Tensor? rowidx, Tensor Cm2, Tensor cnorm, Tensor(a!) labels, Tensor(b!) mind, Tensor(c!) mind2) -> ()");
   m.def("bounds_filter(Tensor labels, Tensor(a!) ub, Tensor(b!) lb, Tensor drift, Tensor maxdrift, float slack, Tensor(c!) active, Tensor(d!) count) -> ()");
   m.def("bounds_scatter(Tensor active, Tensor count, Tensor blab, Tensor d1, Tensor d2, Tensor(a!) labels, Tensor(b!) ub, Tensor(c!) lb, Tensor(d!) moved_idx, Tensor(e!) moved_old, Tensor(f!) moved_new, Tensor(g!) mcount) -> ()");
+  m.def("delta_workspace(int N, int K) -> int", &delta_workspace);
+  m.def("delta_update(Tensor X, Tensor labels, Tensor(a!) prev, Tensor(b!) sums, Tensor(c!) counts, Tensor(d!) work, Tensor(e!) ctrl, Tensor(f!)? cnt_hi=None, Tensor(g!)? cnt_lo=None, Tensor(h!)? moved=None, Tensor(i!)? zero_first=None) -> ()");
+  m.def("delta_finalize(Tensor sums, Tensor counts, Tensor? cnt_hi, Tensor? cnt_lo, Tensor? moved, Tensor(a!) G, Tensor(b!) C, int policy, Tensor(c!)? shift, Tensor(d!)? Cm2, Tensor(e!)? cnorm, Tensor(f!) ctrl, Tensor(g!)? stats, int refresh, float theta_n) -> ()");
   m.def("sculley_update(Tensor sums, Tensor counts, Tensor(a!) C, Tensor(b!) v, Tensor(c!)? shift, Tensor(d!)? Cm2, Tensor(e!)? cnorm) -> ()");
 }
 
@@ -834,6 +940,8 @@ TORCH_LIBRARY_IMPL(tdc, CUDA, m) {
   m.impl("fcm_tower_accum", &fcm_tower_accum);
   m.impl("fcm_wide", &fcm_wide);
   m.impl("finalize", &finalize);
+  m.impl("delta_update", &delta_update);
+  m.impl("delta_finalize", &delta_finalize);
   m.impl("assign_bigd", &assign_bigd);
   m.impl("recheck_top2", &recheck_top2);
   m.impl("quant_fp8", &quant_fp8);

@@ -166,3 +166,38 @@ int tdc_quant_fp8(int src_dtype, const void* X, int64_t rows, int64_t valid, int
 int tdc_kpp_step(int x_dtype, int d_dtype, const void* X, int64_t N, int64_t ldx, int D,
                  const void* cand, int T, void* closest, int mode, double* pots, int num_cus,
                  hipStream_t s);
+
+// ---- delta update of plain Lloyd (update_sorted.hip delta_*, centroids.hip) ----
+// ctrl: int32 [TDC_DC_WORDS] device words shared by the step's kernels and the host.
+enum TdcDeltaCtrl {
+  TDC_DC_NEXT = 0,    // mode of the upcoming step: 0 delta, 1 full (finalize; host on reset)
+  TDC_DC_MODE = 1,    // mode of the running step (set by the scan for the kernels after it)
+  TDC_DC_MOVED = 2,   // rows whose label changed in the running step (diff kernel)
+  TDC_DC_EVENTS = 3,  // perm entries of the running step
+  TDC_DC_PREVOK = 4,  // prev[] holds the previous step's labels (host reset: 0)
+  TDC_DC_ITER = 5,    // steps since the last reset
+  TDC_DC_WORDS = 16
+};
+constexpr int TDC_DELTA_MAX_K = 8192;       // two K-int LDS histograms per block (64 KiB)
+constexpr int TDC_DELTA_MAX_BLOCKS = 1024;  // per-block moved-list slots in the workspace
+// One local update of a Lloyd step in the mode ctrl[NEXT] says: labels (this step's
+// assignment) vs prev (the previous one; prev = labels on return) -> sums / counts (the
+// step's all-reduce buffer views: deltas of the moved rows, or full partials), the exact
+// count split as tdc_update_sorted (signed), moved (nullable, acc dtype [1]) += rows that
+// changed label.  work: int32 [tdc_delta_workspace(N, K)], zero-filled once.  K <=
+// TDC_DELTA_MAX_K, N < 2^30.
+int tdc_delta_update(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
+                     const int32_t* labels, int32_t* prev, int K, void* sums, void* counts,
+                     int* work, int* ctrl, int num_cus, hipStream_t stream, float* cnt_hi,
+                     float* cnt_lo, void* moved, void* zero_first, int64_t zero_bytes);
+int64_t tdc_delta_workspace(int64_t N, int K);
+// The step's finalize: G (fp64 [K*D + K] totals) += or = the all-reduced buffer (by
+// ctrl[MODE]), C = G means (policy as tdc_finalize), optional bf16 operand prep, shift;
+// picks ctrl[NEXT] (full every `refresh` steps (0: never) or when moved > theta_n) and
+// accumulates stats (nullable, fp64 [4]: moved rows, steps with a valid prev, full steps,
+// steps).
+int tdc_delta_finalize(int acc_dtype, int c_dtype, const void* dsums, const void* dcounts,
+                       const float* cnt_hi, const float* cnt_lo, const void* moved, double* G,
+                       int K, int D, void* C, int policy, float* shift, void* Cm2, float* cnorm,
+                       int Kp, int DP, int* ctrl, double* stats, int refresh, double theta_n,
+                       hipStream_t stream);

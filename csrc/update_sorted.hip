@@ -73,22 +73,12 @@ __global__ __launch_bounds__(NT) void hist_kernel(const int32_t* __restrict__ la
   }
 }
 
-// single block, 1024 threads: offsets[0..K] (exclusive), cursor = offsets, counts_acc = cnt
-template <typename ACC>
-__global__ __launch_bounds__(1024) void scan_kernel(int* __restrict__ cnt, int K,
-                                                    int* __restrict__ offsets,
-                                                    int* __restrict__ cursor,
-                                                    ACC* __restrict__ counts_acc,
-                                                    float* __restrict__ cnt_hi,
-                                                    float* __restrict__ cnt_lo) {
+// Inclusive prefix sum of one value per thread over a 1024-thread block: within each
+// wave by shuffles (no barrier), then over the 16 wave totals by wave 0 (two barriers in
+// all; the Hillis-Steele form over LDS took 20).
+__device__ __forceinline__ int block_inclusive_scan_1024(int s) {
   __shared__ int s_wave[16];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int per = (K + 1023) / 1024;
-  const int k0 = tid * per, k1 = min(K, k0 + per);
-  int s = 0;
-  for (int k = k0; k < k1; ++k) s += cnt[k];
-  // inclusive scan: within each wave by shuffles (no barrier), then over the 16 wave
-  // totals by wave 0 (two barriers in all; the Hillis-Steele form over LDS took 20)
   int inc = s;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -107,7 +97,23 @@ __global__ __launch_bounds__(1024) void scan_kernel(int* __restrict__ cnt, int K
     if (lane < 16) s_wave[lane] = t;  // inclusive totals of waves 0..lane
   }
   __syncthreads();
-  inc += wv > 0 ? s_wave[wv - 1] : 0;
+  return inc + (wv > 0 ? s_wave[wv - 1] : 0);
+}
+
+// single block, 1024 threads: offsets[0..K] (exclusive), cursor = offsets, counts_acc = cnt
+template <typename ACC>
+__global__ __launch_bounds__(1024) void scan_kernel(int* __restrict__ cnt, int K,
+                                                    int* __restrict__ offsets,
+                                                    int* __restrict__ cursor,
+                                                    ACC* __restrict__ counts_acc,
+                                                    float* __restrict__ cnt_hi,
+                                                    float* __restrict__ cnt_lo) {
+  const int tid = threadIdx.x;
+  const int per = (K + 1023) / 1024;
+  const int k0 = tid * per, k1 = min(K, k0 + per);
+  int s = 0;
+  for (int k = k0; k < k1; ++k) s += cnt[k];
+  const int inc = block_inclusive_scan_1024(s);
   int run = inc - s;  // exclusive prefix of this thread's range
   for (int k = k0; k < k1; ++k) {
     const int c = cnt[k];
@@ -291,25 +297,68 @@ template <> struct RowRaw<double, 2> {
   __device__ static void add(const raw_t& t, double (&a)[2]) { a[0] += t.x; a[1] += t.y; }
 };
 
+// signed accumulation (delta updates): sg is 0 or 0x80000000, XOR-ed into the sign bit of
+// every element -- one VALU per element on top of the conversion, no multiply
+template <typename XT, int VEC> struct RowRawSigned;
+template <> struct RowRawSigned<__bf16, 8> {
+  __device__ static void add(const uint4& t, unsigned sg, float (&a)[8]) {
+    a[0] += __uint_as_float((t.x << 16) ^ sg); a[1] += __uint_as_float((t.x & 0xffff0000u) ^ sg);
+    a[2] += __uint_as_float((t.y << 16) ^ sg); a[3] += __uint_as_float((t.y & 0xffff0000u) ^ sg);
+    a[4] += __uint_as_float((t.z << 16) ^ sg); a[5] += __uint_as_float((t.z & 0xffff0000u) ^ sg);
+    a[6] += __uint_as_float((t.w << 16) ^ sg); a[7] += __uint_as_float((t.w & 0xffff0000u) ^ sg);
+  }
+};
+template <> struct RowRawSigned<float, 4> {
+  __device__ static void add(const float4& t, unsigned sg, float (&a)[4]) {
+    a[0] += __uint_as_float(__float_as_uint(t.x) ^ sg);
+    a[1] += __uint_as_float(__float_as_uint(t.y) ^ sg);
+    a[2] += __uint_as_float(__float_as_uint(t.z) ^ sg);
+    a[3] += __uint_as_float(__float_as_uint(t.w) ^ sg);
+  }
+};
+template <> struct RowRawSigned<double, 2> {
+  __device__ static void add(const double2& t, unsigned sg, double (&a)[2]) {
+    const long long s = (long long)sg << 32;
+    a[0] += __longlong_as_double(__double_as_longlong(t.x) ^ s);
+    a[1] += __longlong_as_double(__double_as_longlong(t.y) ^ s);
+  }
+};
+
 template <typename XT> struct RowLoad1 {
   typedef typename std::conditional<sizeof(XT) == 8, double, float>::type acc_t;
   __device__ static void add(const XT* p, acc_t (&a)[1]) { a[0] += (acc_t)p[0]; }
+  __device__ static void add(const XT* p, unsigned sg, acc_t (&a)[1]) {
+    a[0] += sg ? -(acc_t)p[0] : (acc_t)p[0];
+  }
 };
 
+// perm entries of a delta update carry the sign in bit 31 (row numbers are < 2^31)
+constexpr unsigned PERM_NEG = 0x80000000u;
+
 // each wave: rows [a, b) of the sorted permutation; TPR lanes per row, G = 64/TPR rows
-// in flight per wave-instruction, columns [c0, c0 + TPR*VEC) per pass
-template <typename XT, typename ACC, int VEC, int TPR>
+// in flight per wave-instruction, columns [c0, c0 + TPR*VEC) per pass.
+// SIGNED (delta updates): a perm entry with PERM_NEG set subtracts its row.  nptr
+// (nullable): the entry count lives on the device (delta updates decide it there); the
+// waves then split it evenly themselves (at least 64 entries each, the rest exit).
+template <typename XT, typename ACC, int VEC, int TPR, bool SIGNED = false>
 __global__ __launch_bounds__(256) void segsum_kernel(const XT* __restrict__ X, int64_t ldx, int D,
                                                      const int32_t* __restrict__ perm,
                                                      const int* __restrict__ offsets, int K,
                                                      int64_t N, ACC* __restrict__ sums,
-                                                     int64_t rows_per_wave) {
+                                                     int64_t rows_per_wave,
+                                                     const int* __restrict__ nptr = nullptr) {
   typedef typename RowLoad1<XT>::acc_t AT;  // fp64 data -> fp64 partials, else fp32
   constexpr int G = 64 / TPR;
   constexpr int U = 8;  // rows per group in flight
   const int lane = threadIdx.x & 63;
   const int g = lane / TPR, t = lane % TPR;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (nptr) {
+    N = *nptr;
+    const int64_t waves = (int64_t)gridDim.x * 4;
+    rows_per_wave = (N + waves - 1) / waves;
+    if (rows_per_wave < 64) rows_per_wave = 64;
+  }
   const int64_t a = wave * rows_per_wave;
   if (a >= N) return;
   const int64_t b = min(N, a + rows_per_wave);
@@ -356,10 +405,14 @@ __global__ __launch_bounds__(256) void segsum_kernel(const XT* __restrict__ X, i
       }
       while (p < b) {
         raw_t xv[U];
+        unsigned sg[U];
         if (colok) {
 #pragma unroll
-          for (int u = 0; u < U; ++u)
-            if (p + g + u * G < pe) xv[u] = RowRaw<XT, VEC>::load(X + (int64_t)nidx[u] * ldx + col);
+          for (int u = 0; u < U; ++u) {
+            sg[u] = SIGNED ? (unsigned)nidx[u] & PERM_NEG : 0u;
+            const int64_t row = SIGNED ? (int64_t)((unsigned)nidx[u] & ~PERM_NEG) : (int64_t)nidx[u];
+            if (p + g + u * G < pe) xv[u] = RowRaw<XT, VEC>::load(X + row * ldx + col);
+          }
         }
         const bool closes = pe == kend || pe == b;  // wave-uniform
         int kn = k;
@@ -381,7 +434,10 @@ __global__ __launch_bounds__(256) void segsum_kernel(const XT* __restrict__ X, i
         if (colok) {
 #pragma unroll
           for (int u = 0; u < U; ++u)
-            if (p + g + u * G < pe) RowRaw<XT, VEC>::add(xv[u], acc);
+            if (p + g + u * G < pe) {
+              if constexpr (SIGNED) RowRawSigned<XT, VEC>::add(xv[u], sg[u], acc);
+              else RowRaw<XT, VEC>::add(xv[u], acc);
+            }
         }
         if (closes) {
 #pragma unroll
@@ -419,7 +475,13 @@ __global__ __launch_bounds__(256) void segsum_kernel(const XT* __restrict__ X, i
           for (int u = 0; u < U; ++u) idx[u] = perm[j + u * G];
           if (colok) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) RowLoad1<XT>::add(X + (int64_t)idx[u] * ldx + col, acc);
+            for (int u = 0; u < U; ++u) {
+              if constexpr (SIGNED)
+                RowLoad1<XT>::add(X + (int64_t)((unsigned)idx[u] & ~PERM_NEG) * ldx + col,
+                                  (unsigned)idx[u] & PERM_NEG, acc);
+              else
+                RowLoad1<XT>::add(X + (int64_t)idx[u] * ldx + col, acc);
+            }
           }
           j += U * G;
         } else {
@@ -429,7 +491,13 @@ __global__ __launch_bounds__(256) void segsum_kernel(const XT* __restrict__ X, i
             kend = offsets[k + 1];
           }
           const int32_t idx = perm[j];
-          if (colok) RowLoad1<XT>::add(X + (int64_t)idx * ldx + col, acc);
+          if (colok) {
+            if constexpr (SIGNED)
+              RowLoad1<XT>::add(X + (int64_t)((unsigned)idx & ~PERM_NEG) * ldx + col,
+                                (unsigned)idx & PERM_NEG, acc);
+            else
+              RowLoad1<XT>::add(X + (int64_t)idx * ldx + col, acc);
+          }
           j += G;
         }
       }
@@ -439,30 +507,230 @@ __global__ __launch_bounds__(256) void segsum_kernel(const XT* __restrict__ X, i
 #undef TDC_FLUSH
 }
 
+
+// ---- delta update (plain Lloyd after its first step; models/kmeans.py) ----
+//
+// Between two Lloyd steps only the rows whose label changed move their contribution from
+// one cluster total to another.  The engine keeps the totals G (fp64, replicated) and the
+// previous step's labels prev[]; a delta step sums +x into the new and -x out of the old
+// cluster of every moved row (a counting sort of 2M signed events + the signed segmented
+// gather-sum), all-reduces those deltas, and the finalize adds them to G.  A full step
+// (the first one, every `refresh` steps, or after a step that moved more than theta N
+// rows) sums every row instead and the finalize replaces G.  The choice is made ON THE
+// DEVICE by the previous step's finalize (from the all-reduced moved count, so every rank
+// makes the same one): no host sync, and the step stays capturable in a hipGraph.  Both
+// modes run the same four kernels; each reads the mode from ctrl (kernels.h TDC_DC_*).
+//
+//   diff    : labels vs prev -> prev = labels; per-block list of moved rows (idx, old|new),
+//             LDS-appended (no global atomic per row); LDS histograms of the events
+//             (delta: +1 at new, +1 at old; full: +1 at every label) and signed counts
+//   scan    : offsets of the events, signed counts into the all-reduce buffer, moved count
+//             into its slot, mode of this step for the kernels after it
+//   scatter : counting-sort placement of the events (delta: the list, full: every row)
+//   segsum  : signed segmented gather-sum of the rows (segsum_kernel<..., SIGNED>)
+template <int NT>
+__global__ __launch_bounds__(NT) void delta_diff_kernel(
+    const int32_t* __restrict__ labels, int32_t* __restrict__ prev, int64_t N, int K,
+    int* __restrict__ ctrl, int* __restrict__ cnt_ev, int* __restrict__ cnt_sg,
+    int* __restrict__ blk_cnt, int32_t* __restrict__ lidx, uint32_t* __restrict__ lpair,
+    int64_t per_block, uint32_t* __restrict__ zero, int64_t zero_words) {
+  extern __shared__ int s_h[];  // [K] events | [K] signed counts (delta steps)
+  __shared__ int s_cur;         // this block's moved-list cursor
+  const int tid = threadIdx.x, lane = tid & 63;
+  // the step's all-reduce buffer, cleared before anything accumulates into it (scan and
+  // segsum run after this kernel)
+  for (int64_t w = (int64_t)blockIdx.x * NT + tid; w < zero_words; w += (int64_t)gridDim.x * NT)
+    zero[w] = 0u;
+  const bool full = ctrl[TDC_DC_NEXT] != 0;
+  int* h_ev = s_h;
+  int* h_sg = s_h + K;
+  for (int k = tid; k < (full ? K : 2 * K); k += NT) s_h[k] = 0;
+  if (tid == 0) s_cur = 0;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * per_block;
+  const int64_t r1 = min(N, r0 + per_block);
+  for (int64_t c0 = r0; c0 < r1; c0 += 4 * NT) {  // block-uniform trip count (ballots below)
+    int nw[4], od[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t i = c0 + (int64_t)j * NT + tid;
+      nw[j] = od[j] = 0;
+      if (i < r1) {
+        nw[j] = labels[i];
+        od[j] = prev[i];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t i = c0 + (int64_t)j * NT + tid;
+      const bool ok = i < r1;
+      const bool mv = ok && nw[j] != od[j];
+      if (mv) prev[i] = nw[j];
+      const bool nok = (unsigned)nw[j] < (unsigned)K, ook = (unsigned)od[j] < (unsigned)K;
+      if (full) {
+        if (ok && nok) atomicAdd(h_ev + nw[j], 1);
+      } else if (mv) {
+        if (nok) { atomicAdd(h_ev + nw[j], 1); atomicAdd(h_sg + nw[j], 1); }
+        if (ook) { atomicAdd(h_ev + od[j], 1); atomicSub(h_sg + od[j], 1); }
+      }
+      // append: one LDS atomic per wave and row slot, positions by mbcnt of the ballot
+      const unsigned long long mask = __ballot(mv);
+      if (mask) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&s_cur, (int)__popcll(mask));
+        base = __shfl(base, 0, 64);
+        if (mv && !full) {
+          const int pos = base + (int)__builtin_amdgcn_mbcnt_hi(
+                                     (unsigned)(mask >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+          lidx[r0 + pos] = (int32_t)i;
+          lpair[r0 + pos] = (((uint32_t)od[j] & 0xffffu) << 16) | ((uint32_t)nw[j] & 0xffffu);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    blk_cnt[blockIdx.x] = s_cur;
+    if (s_cur) atomicAdd(ctrl + TDC_DC_MOVED, s_cur);  // one global atomic per block
+  }
+  for (int k = tid; k < K; k += NT) {
+    if (h_ev[k]) atomicAdd(cnt_ev + k, h_ev[k]);
+    if (!full && h_sg[k]) atomicAdd(cnt_sg + k, h_sg[k]);
+  }
+}
+
+// single block, 1024 threads: event offsets / cursors, the step's signed counts into the
+// all-reduce buffer (acc dtype, plus the exact hi/lo split: hi = c >> 12 is a floor for
+// negative c, so 4096 hi + lo == c still holds), the moved count into its slot
+template <typename ACC>
+__global__ __launch_bounds__(1024) void delta_scan_kernel(int* __restrict__ cnt_ev,
+                                                          int* __restrict__ cnt_sg, int K,
+                                                          int* __restrict__ offsets,
+                                                          int* __restrict__ cursor,
+                                                          int* __restrict__ ctrl,
+                                                          ACC* __restrict__ counts_acc,
+                                                          float* __restrict__ cnt_hi,
+                                                          float* __restrict__ cnt_lo,
+                                                          ACC* __restrict__ mslot) {
+  const int tid = threadIdx.x;
+  const bool full = ctrl[TDC_DC_NEXT] != 0;
+  const int per = (K + 1023) / 1024;
+  const int k0 = tid * per, k1 = min(K, k0 + per);
+  int s = 0;
+  for (int k = k0; k < k1; ++k) s += cnt_ev[k];
+  const int inc = block_inclusive_scan_1024(s);
+  int run = inc - s;
+  for (int k = k0; k < k1; ++k) {
+    const int e = cnt_ev[k];
+    const int c = full ? e : cnt_sg[k];
+    cnt_ev[k] = 0;  // both histograms are left zeroed for the next step
+    cnt_sg[k] = 0;
+    offsets[k] = run;
+    cursor[k] = run;
+    if (counts_acc) counts_acc[k] += (ACC)c;
+    if (cnt_hi && c) {
+      cnt_hi[k] += (float)(c >> 12);
+      cnt_lo[k] += (float)(c & 4095);
+    }
+    run += e;
+  }
+  if (tid == 1023) {
+    offsets[K] = inc;
+    ctrl[TDC_DC_EVENTS] = inc;
+  }
+  if (tid == 0) {
+    ctrl[TDC_DC_MODE] = full ? 1 : 0;
+    const int m = ctrl[TDC_DC_MOVED];
+    ctrl[TDC_DC_MOVED] = 0;
+    if (mslot) *mslot += (ACC)m;
+  }
+}
+
+// counting-sort placement of the step's events: a full step places every row (as
+// bscatter_kernel, with the same bin-range passes), a delta step the entries of its
+// block's moved list, each twice: row at its new cluster, row | PERM_NEG at its old one
+template <int NT>
+__global__ __launch_bounds__(NT) void delta_scatter_kernel(
+    const int32_t* __restrict__ labels, int64_t N, int K, const int* __restrict__ ctrl,
+    const int* __restrict__ blk_cnt, const int32_t* __restrict__ lidx,
+    const uint32_t* __restrict__ lpair, int* __restrict__ cursor, int32_t* __restrict__ perm,
+    int64_t per_block, int parts) {
+  extern __shared__ int s_mem[];
+  int* s_cnt = s_mem;
+  int* s_cur = s_mem + K;
+  const int tid = threadIdx.x;
+  const bool full = ctrl[TDC_DC_MODE] != 0;
+  const int64_t r0 = (int64_t)blockIdx.x * per_block;
+  const int64_t r1 = full ? min(N, r0 + per_block) : r0 + blk_cnt[blockIdx.x];
+  if (r0 >= r1) return;  // block-uniform: nothing moved in this block's rows
+  for (int k = tid; k < K; k += NT) s_cnt[k] = 0;
+  __syncthreads();
+  if (full) {
+    for (int64_t i = r0 + tid; i < r1; i += NT) {
+      const int a = labels[i];
+      if ((unsigned)a < (unsigned)K) atomicAdd(s_cnt + a, 1);
+    }
+  } else {
+    for (int64_t i = r0 + tid; i < r1; i += NT) {
+      const uint32_t pr = lpair[i];
+      const unsigned nw = pr & 0xffffu, od = pr >> 16;
+      if (nw < (unsigned)K) atomicAdd(s_cnt + nw, 1);
+      if (od < (unsigned)K) atomicAdd(s_cnt + od, 1);
+    }
+  }
+  __syncthreads();
+  for (int k = tid; k < K; k += NT) {
+    const int c = s_cnt[k];
+    s_cur[k] = c ? atomicAdd(cursor + k, c) : 0;
+  }
+  __syncthreads();
+  if (full) {
+    for (int part = 0; part < parts; ++part) {
+      const unsigned lo = (unsigned)((int64_t)K * part / parts);
+      const unsigned n = (unsigned)((int64_t)K * (part + 1) / parts) - lo;
+      for (int64_t i = r0 + tid; i < r1; i += NT) {
+        const int a = labels[i];
+        if ((unsigned)a - lo < n) perm[atomicAdd(s_cur + a, 1)] = (int32_t)i;
+      }
+    }
+  } else {
+    for (int64_t i = r0 + tid; i < r1; i += NT) {
+      const uint32_t pr = lpair[i];
+      const unsigned nw = pr & 0xffffu, od = pr >> 16;
+      const int32_t row = lidx[i];
+      if (nw < (unsigned)K) perm[atomicAdd(s_cur + nw, 1)] = row;
+      if (od < (unsigned)K) perm[atomicAdd(s_cur + od, 1)] = (int32_t)((uint32_t)row | PERM_NEG);
+    }
+  }
+}
+
 }  // namespace tdc
 
 using namespace tdc;
 
 namespace {
 
-template <typename XT, typename ACC, int VEC>
+template <typename XT, typename ACC, int VEC, bool SIGNED>
 int launch_segsum(const void* X, int64_t ldx, int D, const int32_t* perm, const int* offsets,
-                  int K, int64_t N, void* sums, int num_cus, hipStream_t s) {
+                  int K, int64_t N, void* sums, int num_cus, hipStream_t s,
+                  const int* nptr) {
   const int lanes_needed = (D + VEC - 1) / VEC;
   (void)num_cus;
   // every wave gets the same row count, so the grid is exactly the waves resident at once
   // (8 blocks per CU asked for 8 waves per SIMD where the kernel fits 5: a second, partial
-  // round of blocks)
+  // round of blocks).  With nptr (entry count on the device, at most N) the grid is sized
+  // for N and the waves re-split the actual count.
 #define TDC_SEG(TPRV)                                                                       \
   do {                                                                                      \
-    static const int64_t res = resident_blocks(segsum_kernel<XT, ACC, VEC, TPRV>, 256);     \
+    static const int64_t res = resident_blocks(segsum_kernel<XT, ACC, VEC, TPRV, SIGNED>, 256); \
     int64_t waves = res * 4;                                                                \
     int64_t rpw = (N + waves - 1) / waves;                                                  \
     if (rpw < 64) rpw = 64; /* small N (mini-batches, moved rows) */                        \
     waves = (N + rpw - 1) / rpw;                                                            \
     const dim3 grid((unsigned)((waves + 3) / 4));                                           \
-    hipLaunchKernelGGL((segsum_kernel<XT, ACC, VEC, TPRV>), grid, dim3(256), 0, s,          \
-                       (const XT*)X, ldx, D, perm, offsets, K, N, (ACC*)sums, rpw);         \
+    hipLaunchKernelGGL((segsum_kernel<XT, ACC, VEC, TPRV, SIGNED>), grid, dim3(256), 0, s,  \
+                       (const XT*)X, ldx, D, perm, offsets, K, N, (ACC*)sums, rpw, nptr);   \
   } while (0)
   if (lanes_needed <= 4) TDC_SEG(4);
   else if (lanes_needed <= 8) TDC_SEG(8);
@@ -474,25 +742,26 @@ int launch_segsum(const void* X, int64_t ldx, int D, const int32_t* perm, const 
   return 0;
 }
 
-template <typename ACC>
+template <typename ACC, bool SIGNED = false>
 int dispatch_segsum(int x_dtype, const void* X, int64_t ldx, int D, const int32_t* perm,
-                    const int* offsets, int K, int64_t N, void* sums, int num_cus, hipStream_t s) {
+                    const int* offsets, int K, int64_t N, void* sums, int num_cus, hipStream_t s,
+                    const int* nptr = nullptr) {
   const bool a16 = ((uintptr_t)X % 16) == 0;
+#define TDC_SEGD(T, V) \
+  return launch_segsum<T, ACC, V, SIGNED>(X, ldx, D, perm, offsets, K, N, sums, num_cus, s, nptr)
   if (x_dtype == TDC_BF16) {
-    if (a16 && D % 8 == 0 && ldx % 8 == 0)
-      return launch_segsum<__bf16, ACC, 8>(X, ldx, D, perm, offsets, K, N, sums, num_cus, s);
-    return launch_segsum<__bf16, ACC, 1>(X, ldx, D, perm, offsets, K, N, sums, num_cus, s);
+    if (a16 && D % 8 == 0 && ldx % 8 == 0) TDC_SEGD(__bf16, 8);
+    TDC_SEGD(__bf16, 1);
   }
   if (x_dtype == TDC_F32) {
-    if (a16 && D % 4 == 0 && ldx % 4 == 0)
-      return launch_segsum<float, ACC, 4>(X, ldx, D, perm, offsets, K, N, sums, num_cus, s);
-    return launch_segsum<float, ACC, 1>(X, ldx, D, perm, offsets, K, N, sums, num_cus, s);
+    if (a16 && D % 4 == 0 && ldx % 4 == 0) TDC_SEGD(float, 4);
+    TDC_SEGD(float, 1);
   }
   if (x_dtype == TDC_F64) {
-    if (a16 && D % 2 == 0 && ldx % 2 == 0)
-      return launch_segsum<double, ACC, 2>(X, ldx, D, perm, offsets, K, N, sums, num_cus, s);
-    return launch_segsum<double, ACC, 1>(X, ldx, D, perm, offsets, K, N, sums, num_cus, s);
+    if (a16 && D % 2 == 0 && ldx % 2 == 0) TDC_SEGD(double, 2);
+    TDC_SEGD(double, 1);
   }
+#undef TDC_SEGD
   return (int)hipErrorInvalidValue;
 }
 
@@ -567,3 +836,62 @@ int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int6
 }
 
 int64_t tdc_update_sorted_workspace(int64_t N, int K) { return 3 * (int64_t)K + 1 + N; }
+
+
+int64_t tdc_delta_workspace(int64_t N, int K) {
+  return 4 * (int64_t)K + 1 + TDC_DELTA_MAX_BLOCKS + 4 * N;
+}
+
+int tdc_delta_update(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
+                     const int32_t* labels, int32_t* prev, int K, void* sums, void* counts,
+                     int* work, int* ctrl, int num_cus, hipStream_t s, float* cnt_hi,
+                     float* cnt_lo, void* moved, void* zero_first, int64_t zero_bytes) {
+  if (zero_bytes % 4 != 0 || (zero_bytes > 0 && zero_first == nullptr))
+    return (int)hipErrorInvalidValue;
+  // events are < 2N and perm entries carry the sign in bit 31; lpair packs 16-bit labels
+  if (K <= 0 || K > TDC_DELTA_MAX_K || N >= ((int64_t)1 << 30)) return (int)hipErrorInvalidValue;
+  if (acc_dtype != TDC_F32 && acc_dtype != TDC_F64) return (int)hipErrorInvalidValue;
+  // workspace (ints): cnt_ev[K] | cnt_sg[K] | offsets[K+1] | cursor[K] | blk_cnt[MAXB] |
+  // lidx[N] | lpair[N] | perm[2N]; the histograms are zero on entry and left zero
+  int* cnt_ev = work;
+  int* cnt_sg = cnt_ev + K;
+  int* offsets = cnt_sg + K;
+  int* cursor = offsets + K + 1;
+  int* blk_cnt = cursor + K;
+  int32_t* lidx = blk_cnt + TDC_DELTA_MAX_BLOCKS;
+  uint32_t* lpair = reinterpret_cast<uint32_t*>(lidx + N);
+  int32_t* perm = reinterpret_cast<int32_t*>(lpair + N);
+  // one 1024-thread block per CU over contiguous row ranges (the diff and scatter kernels
+  // share this geometry: block b's moved list lives at [b * per, b * per + blk_cnt[b]))
+  int64_t blocks = std::max(1, std::min(num_cus, TDC_DELTA_MAX_BLOCKS));
+  int64_t per = (N + blocks - 1) / blocks;
+  if (per < 4096) per = 4096;
+  blocks = N > 0 ? (N + per - 1) / per : 0;
+  const size_t lds = 2 * sizeof(int) * (size_t)K;
+  if (blocks > 0) {
+    hipLaunchKernelGGL(delta_diff_kernel<1024>, dim3((unsigned)blocks), dim3(1024), lds, s,
+                       labels, prev, N, K, ctrl, cnt_ev, cnt_sg, blk_cnt, lidx, lpair, per,
+                       static_cast<uint32_t*>(zero_first), zero_bytes / 4);
+    TDC_CHECK_LAUNCH();
+  } else if (zero_bytes && hipMemsetAsync(zero_first, 0, (size_t)zero_bytes, s) != hipSuccess) {
+    return (int)hipErrorUnknown;
+  }
+  if (acc_dtype == TDC_F64)
+    hipLaunchKernelGGL(delta_scan_kernel<double>, dim3(1), dim3(1024), 0, s, cnt_ev, cnt_sg, K,
+                       offsets, cursor, ctrl, (double*)counts, cnt_hi, cnt_lo, (double*)moved);
+  else
+    hipLaunchKernelGGL(delta_scan_kernel<float>, dim3(1), dim3(1024), 0, s, cnt_ev, cnt_sg, K,
+                       offsets, cursor, ctrl, (float*)counts, cnt_hi, cnt_lo, (float*)moved);
+  TDC_CHECK_LAUNCH();
+  if (blocks == 0) return 0;
+  const int parts = K >= 512 && per >= 8 * (int64_t)K ? 2 : 1;
+  hipLaunchKernelGGL(delta_scatter_kernel<1024>, dim3((unsigned)blocks), dim3(1024), lds, s,
+                     labels, N, K, ctrl, blk_cnt, lidx, lpair, cursor, perm, per, parts);
+  TDC_CHECK_LAUNCH();
+  // grid sized for a full step (N events); a delta step re-splits its 2M events on device
+  if (acc_dtype == TDC_F64)
+    return dispatch_segsum<double, true>(x_dtype, X, ldx, D, perm, offsets, K, N, sums, num_cus,
+                                         s, ctrl + TDC_DC_EVENTS);
+  return dispatch_segsum<float, true>(x_dtype, X, ldx, D, perm, offsets, K, N, sums, num_cus, s,
+                                      ctrl + TDC_DC_EVENTS);
+}

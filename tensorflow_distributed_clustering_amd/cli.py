@@ -157,6 +157,9 @@ def build_parser():
                         help="replay each iteration from a captured HIP graph (1 GPU)")
     parser.add_argument("--deterministic", action="store_true",
                         help="run-to-run bitwise reproducible centroid update")
+    parser.add_argument("--update", default="auto", choices=["auto", "full", "delta"],
+                        help="K-Means centroid update: delta moves only the rows whose label "
+                             "changed between fp64 running totals (auto: where supported)")
     parser.add_argument("--spherical", action="store_true",
                         help="cosine (spherical) K-Means: unit-normalised rows and centroids")
     parser.add_argument("--dist_debug", action="store_true",
@@ -238,7 +241,8 @@ def run(args) -> int:
                             hbm_budget_gb=args.hbm_budget_gb, deterministic=args.deterministic,
                             graph=args.graph, log_every=args.log_every,
                             spherical=args.spherical, algorithm=args.algorithm,
-                            fp8_recheck=args.fp8_recheck, warmup=not args.no_warmup)
+                            fp8_recheck=args.fp8_recheck, warmup=not args.no_warmup,
+                            update=args.update)
 
         def make_model():
             if args.method_name == "distributedKMeans":

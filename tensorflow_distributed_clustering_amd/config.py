@@ -19,6 +19,7 @@ EMPTY_POLICIES = ("keep", "nan", "nan_any", "reseed", "zero")
 BACKENDS = ("auto", "hip", "torch")
 ALGORITHMS = ("lloyd", "bounded")
 COMM_MODES = ("auto", "allreduce", "rsag")
+UPDATE_MODES = ("auto", "full", "delta")
 
 
 @dataclass(frozen=True)
@@ -60,6 +61,14 @@ class ClusterConfig:
     kpp_sample_per_k greedy k-means++ runs on a uniform world-invariant sample of
                     max(kpp_sample_min, kpp_sample_per_k * K) rows when N is over 4x that
                     (0: always the full data).  The root rank logs whenever a sample is used.
+    update          Lloyd centroid update: 'full' re-sums every row each step; 'delta' keeps
+                    fp64 per-cluster totals and each step moves only the rows whose label
+                    changed (+x into the new, -x out of the old cluster; same fixed points,
+                    models/kmeans.py); 'auto' = delta where supported (resident shard, native
+                    sorted/LDS update or the torch ops, K <= 8192, keep/nan/zero policies)
+    delta_refresh   delta update: recompute the totals from every row each this many steps
+                    (0: never); a step after one that moved more than delta_theta * N rows
+                    is a full step too (the choice is made on the device)
     """
 
     n_clusters: int
@@ -95,6 +104,9 @@ class ClusterConfig:
     kpp_max_k: int = 2048       # greedy k-means++ up to this K, sampled k-means|| above
     kpp_sample_per_k: int = 256 # greedy k-means++ sample rows per centre (0: full data)
     kpp_sample_min: int = 50_000  # ... and at least this many rows
+    update: str = "auto"        # 'auto' | 'full' | 'delta' (Lloyd centroid update)
+    delta_refresh: int = 32     # delta update: full re-sum every this many steps (0: never)
+    delta_theta: float = 0.4    # ... and after a step that moved more than this share of rows
 
     def __post_init__(self):
         if self.n_clusters <= 0:
@@ -113,6 +125,10 @@ class ClusterConfig:
             raise ValueError(f"algorithm must be one of {ALGORITHMS}")
         if self.comm_mode not in COMM_MODES:
             raise ValueError(f"comm_mode must be one of {COMM_MODES}")
+        if self.update not in UPDATE_MODES:
+            raise ValueError(f"update must be one of {UPDATE_MODES}")
+        if self.delta_refresh < 0 or not (0.0 <= self.delta_theta <= 1.0):
+            raise ValueError("delta_refresh must be >= 0 and delta_theta in [0, 1]")
 
     def replace(self, **kw) -> "ClusterConfig":
         return dataclasses.replace(self, **kw)

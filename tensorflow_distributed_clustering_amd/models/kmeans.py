@@ -256,6 +256,12 @@ class LloydEngine(OomGuard):
         if acc == torch.float32 and not self.count_split:
             acc = torch.float64
         self.rsag = self._use_rsag(comm, cfg, k * self.d * torch.tensor([], dtype=acc).element_size())
+        # delta update: only the rows whose label changed move between fp64 running totals
+        self.delta = None
+        if (cfg.update != "full" and self.delta_ok and not self.streamed and not self.rsag
+                and cfg.empty_cluster in ("keep", "nan", "zero") and not cfg.deterministic):
+            self.delta = self.local.make_delta(self.n_local, k, self.d, cfg.delta_refresh,
+                                               cfg.delta_theta, cfg.empty_cluster)
         W = comm.world_size
         if self.rsag:
             align = math.lcm(max(1, self.local.row_align), W)
@@ -271,10 +277,13 @@ class LloydEngine(OomGuard):
         # buf = [sums kpad*D | counts kpad | (hi kpad | lo kpad) | (flags kpad)]: the sums
         # block is what a reduce-scatter splits by rank; the small tail is all-reduced
         nsmall = 1 + (2 if self.count_split else 0) + (1 if self.nan_any else 0)
+        # + 1 slot: rows whose label changed this step (delta update: picks the next mode;
+        #   always there, so every rank's buffer has the same layout before the ranks agree
+        #   on the update mode in init_centroids)
         # + 1 slot: "a rank ran out of memory in this step's local work" (oom_pending)
         self.oom_guard = bool(cfg.oom_recovery) and self.oom_guard_ok
-        self.buf = torch.zeros(kpad * self.d + nsmall * kpad + (1 if self.oom_guard else 0),
-                               dtype=acc, device=dev)
+        ntail = 1 + (1 if self.oom_guard else 0)
+        self.buf = torch.zeros(kpad * self.d + nsmall * kpad + ntail, dtype=acc, device=dev)
         self.sums_pad = self.buf[: kpad * self.d].view(kpad, self.d)
         self.sums = self.sums_pad[:k]
         self.small = self.buf[kpad * self.d:]
@@ -288,6 +297,8 @@ class LloydEngine(OomGuard):
             row = 3
         self.empty_flags = self.small[row * kpad: row * kpad + k] if self.nan_any else None
         self.oom_flag = self.buf[-1:] if self.oom_guard else None
+        off = kpad * self.d + nsmall * kpad
+        self.moved_slot = self.buf[off: off + 1]
         self.C_pad = torch.zeros(kpad, self.d, dtype=self.local.c_dtype, device=dev)
         self.C = self.C_pad[:k]
         if self.rsag:
@@ -310,10 +321,11 @@ class LloydEngine(OomGuard):
         # resident sorted update: the step's zero fill of buf rides in the update's first
         # kernel (one launch less per step; the small-shard step is launch-bound)
         upd = getattr(self.local, "update", None)
-        self._zero_fused = (isinstance(upd, NativeUpdate) and upd.fuses_zero()
-                            and not self.streamed and type(self) is LloydEngine)
-        if self._zero_fused:
+        self._zero_fused_full = (isinstance(upd, NativeUpdate) and upd.fuses_zero()
+                                 and not self.streamed and type(self) is LloydEngine)
+        if self._zero_fused_full:
             upd.zero_buf = self.buf
+        self._set_delta(self.delta)
         self.n_iter = 0
         self.c0 = None
         if self.oom_guard:
@@ -321,6 +333,8 @@ class LloydEngine(OomGuard):
         if not defer_init:
             self.init_centroids()
 
+    # delta centroid update allowed (subclasses with their own step: off)
+    delta_ok = True
     # exact count halves in the buffer (subclasses with their own count bookkeeping: off)
     exact_counts_ok = True
     # mid-run OOM flag in the buffer (subclasses with their own step: off)
@@ -338,6 +352,8 @@ class LloydEngine(OomGuard):
 
     def exact_counts(self) -> torch.Tensor:
         """Global cluster sizes of the last update (fp64, exact past 2^24)."""
+        if self.delta is not None:
+            return self.delta.counts.clone()
         if self.count_split:
             return join_counts(self.cnt_hi, self.cnt_lo)
         return self.counts.double()
@@ -350,10 +366,31 @@ class LloydEngine(OomGuard):
             self._c_synced = True
         return self.C
 
+    def _set_delta(self, delta):
+        self.delta = delta
+        # the native diff kernel clears buf (the full sorted update's hist kernel otherwise)
+        self._zero_fused = (bool(getattr(delta, "native", False)) if delta is not None
+                            else self._zero_fused_full)
+
+    def _agree_update_mode(self):
+        """Every rank runs the same update mode (the totals are replicated): the delta
+        update only if every rank supports it (a rank whose planner streams its shard
+        cannot).  Collective."""
+        ok = self.delta is not None
+        if self.comm.collective:
+            ok = self.comm.max_scalar(0.0 if ok else 1.0) == 0.0
+        if not ok:
+            self._set_delta(None)
+        if self.cfg.update == "delta" and self.delta is None:
+            raise ValueError("update='delta' needs a resident shard on every rank, a sorted/LDS "
+                             "native update or the torch ops, K <= 8192, empty_cluster in "
+                             "keep/nan/zero and no deterministic / rsag / bounded mode")
+
     def init_centroids(self):
         """Centroid init (collective: every rank calls it, in the same order).  Kept out
         of the constructor's local allocations so a setup OOM can be agreed on first."""
         cfg, comm, k = self.cfg, self.comm, self.k
+        self._agree_update_mode()
         if self._x0 is not None:
             c0 = init_centers(cfg.init, self._x0, self.row_offset, self.n_global, k, comm,
                               cfg.seed, given=self._init_given, kpp_max_k=cfg.kpp_max_k,
@@ -370,6 +407,8 @@ class LloydEngine(OomGuard):
         self.c0 = c0
         self.C.copy_(c0.to(self.local.c_dtype))  # never alias c0
         self.local.prepare(self.C)
+        if self.delta is not None:
+            self.delta.reset()
         self._x0 = None
         return self
 
@@ -414,7 +453,7 @@ class LloydEngine(OomGuard):
                 self.counts.masked_fill_(self.empty_flags > 0, 0)
             if self.shift is not None:
                 self.shift.zero_()
-            self.local.finalize(self.sums, self.counts, self.C, self.shift)
+            self._finalize()
         if self.cfg.spherical:  # project the means back to the sphere
             self.centers()
             self.C.div_(self.C.norm(dim=1, keepdim=True).clamp_min_(1e-30))
@@ -424,8 +463,54 @@ class LloydEngine(OomGuard):
         self.n_iter += 1
         return inertia
 
+    def _split(self):
+        return (self.cnt_hi, self.cnt_lo) if self.count_split else None
+
+    def _delta_update(self):
+        self.delta.update(self.local.x, self.labels, self.sums, self.counts, self._split(),
+                          self.moved_slot, self.buf if self._zero_fused else None)
+
+    def _finalize(self):
+        if self.delta is not None:
+            cm2, cnorm = self.local.bf16_operands()
+            self.delta.finalize(self.sums, self.counts, self._split(), self.moved_slot, self.C,
+                                self.local.policy, self.shift, cm2, cnorm, self.n_global)
+            self.local.after_finalize(self.C)
+        else:
+            self.local.finalize(self.sums, self.counts, self.C, self.shift)
+
+    def update_stats(self) -> Optional[dict]:
+        """Delta-update bookkeeping so far (host read): moved rows summed over the steps
+        that had a previous assignment, those steps, full steps, all steps; None without
+        the delta update."""
+        return self.delta.stats_host() if self.delta is not None else None
+
+    @property
+    def update_mode(self) -> str:
+        return "delta" if self.delta is not None else "full"
+
+    def phase_fns(self):
+        """(name, fn) of one resident step's phases in order (timing breakdowns): the
+        buffer fill, assign, local update, all-reduce, finalize."""
+        loc = self.local
+        if self.delta is not None:
+            assign = lambda: loc.assign(self.C, self.labels, None)
+            update = self._delta_update
+        elif isinstance(getattr(loc, "update", None), NativeUpdate):
+            assign = lambda: loc.assign(self.C, self.labels, None)
+            update = lambda: loc.update(loc.x, self.labels, self.sums, self.counts)
+        else:
+            assign = lambda: loc.step(self.C, self.labels, None, self.sums, self.counts)
+            update = lambda: None
+        return [("zero", self.buf.zero_), ("assign", assign), ("update", update),
+                ("allreduce", lambda: self.comm.allreduce_bucketed_(self.buf, self.bucket_bytes)),
+                ("finalize", self._finalize)]
+
     def _local_step(self, mind):
-        if not self.streamed:
+        if self.delta is not None:
+            self.local.assign(self.C, self.labels, mind)
+            self._delta_update()
+        elif not self.streamed:
             self.local.step(self.C, self.labels, mind, self.sums, self.counts)
         else:
             for start, chunk in self._chunks():

@@ -22,13 +22,12 @@ Variants (picked by :func:`make_lloyd_ops`):
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
 
 from .. import _native
-from ..parallel.dist import split_counts
+from ..parallel.dist import join_counts, split_counts
 from . import reference as ref
 
 POLICY_CODES = {"keep": 0, "reseed": 0, "nan": 1, "nan_any": 1, "zero": 2}
@@ -170,6 +169,134 @@ class NativeUpdate:
                                        *(self.count_split or (None, None)))
 
 
+# ----------------------------------------------------------------- delta update
+# ctrl words (csrc/kernels.h TdcDeltaCtrl)
+DC_NEXT, DC_MODE, DC_MOVED, DC_EVENTS, DC_PREVOK, DC_ITER, DC_WORDS = 0, 1, 2, 3, 4, 5, 16
+DELTA_MAX_K = 8192
+
+
+class DeltaState:
+    """Running state of the delta centroid update of plain Lloyd (ClusterConfig.update).
+
+    Invariant: ``G = [sums K*D | counts K]`` (fp64, replicated on every rank) are the
+    per-cluster totals of the assignment held in ``prev`` (the previous step's labels on
+    every rank).  A *delta* step sums only the rows whose label changed, +x into the new
+    and -x out of the old cluster, into the step's all-reduce buffer; the finalize adds
+    the all-reduced deltas to G and divides.  A *full* step sums every row and replaces G.
+    The mode of each step lives in ``ctrl`` on the device: the previous finalize picks it
+    from the all-reduced moved count (the same on every rank), so the step needs no host
+    sync and stays capturable.  Full steps: the first one after :meth:`reset`, every
+    ``refresh`` steps, and after a step that moved more than ``theta`` of all rows.
+
+    The reference re-summed every row every iteration (K Where/Gather chains + a CPU
+    bincount, `scripts/distribuitedClustering.py:237-263`); the fixed points are the same.
+    """
+
+    def __init__(self, n: int, k: int, d: int, device, refresh: int, theta: float):
+        self.n, self.k, self.d = n, k, d
+        self.refresh, self.theta = int(refresh), float(theta)
+        self.prev = torch.zeros(max(1, n), dtype=torch.int32, device=device)
+        self.G = torch.zeros(k * d + k, dtype=torch.float64, device=device)
+        self.ctrl = torch.zeros(DC_WORDS, dtype=torch.int32, device=device)
+        # [moved rows (steps with a valid prev), such steps, full steps, steps]
+        self.stats = torch.zeros(4, dtype=torch.float64, device=device)
+        self.reset()
+
+    @property
+    def sums(self) -> torch.Tensor:
+        return self.G[: self.k * self.d].view(self.k, self.d)
+
+    @property
+    def counts(self) -> torch.Tensor:
+        return self.G[self.k * self.d:]
+
+    def reset(self):
+        """The next step is a full one and ``prev`` holds no labels yet (after the centroid
+        init, or anything else that breaks the invariant)."""
+        self.ctrl.zero_()
+        self.ctrl[DC_NEXT] = 1
+
+    def stats_host(self) -> dict:
+        v = self.stats.tolist()
+        return {"moved_rows": v[0], "moved_steps": v[1], "full_steps": v[2], "steps": v[3]}
+
+
+class NativeDelta(DeltaState):
+    """HIP delta update (csrc/update_sorted.hip delta_*, centroids.hip finalize_delta)."""
+    native = True
+
+    def __init__(self, ops, n, k, d, device, refresh, theta):
+        super().__init__(n, k, d, device, refresh, theta)
+        self.ops = ops
+        self.work = torch.zeros(int(ops.delta_workspace(n, k)), dtype=torch.int32, device=device)
+
+    def update(self, x, labels, sums, counts, split, moved, zero_buf):
+        hi, lo = split or (None, None)
+        self.ops.delta_update(x, labels, self.prev, sums, counts, self.work, self.ctrl, hi, lo,
+                              moved, zero_buf)
+
+    def finalize(self, sums, counts, split, moved, C, policy, shift, cm2, cnorm, n_global):
+        hi, lo = split or (None, None)
+        self.ops.delta_finalize(sums.reshape(-1), counts, hi, lo, moved, self.G, C, policy, shift,
+                                cm2, cnorm, self.ctrl, self.stats, self.refresh,
+                                self.theta * float(n_global))
+
+
+class TorchDelta(DeltaState):
+    """The same state machine in PyTorch ops (CPU ranks over gloo, ``backend='torch'``)."""
+    native = False
+
+    def __init__(self, n, k, d, device, refresh, theta, empty_cluster="keep"):
+        super().__init__(n, k, d, device, refresh, theta)
+        self.empty_cluster = empty_cluster
+
+    def update(self, x, labels, sums, counts, split, moved, zero_buf):
+        full = bool(self.ctrl[DC_NEXT])
+        n, k, d = x.shape[0], self.k, sums.shape[1]
+        new = labels[:n].long()
+        old = self.prev[:n].long()
+        mv = new != old
+        xs = x[:, :d].to(sums.dtype)
+        if full:
+            sums.index_add_(0, new, xs)
+            c = torch.bincount(new, minlength=k)
+        else:
+            idx = torch.nonzero(mv).flatten()
+            sums.index_add_(0, new[idx], xs[idx])
+            sums.index_add_(0, old[idx], -xs[idx])
+            c = torch.bincount(new[idx], minlength=k) - torch.bincount(old[idx], minlength=k)
+        counts.add_(c.to(counts.dtype))
+        if split is not None:
+            split_counts(c, *split)
+        self.prev[:n].copy_(labels[:n])
+        if moved is not None:
+            moved.add_(mv.sum().to(moved.dtype))
+        self.ctrl[DC_MODE] = int(full)
+
+    def finalize(self, sums, counts, split, moved, C, policy, shift, cm2, cnorm, n_global):
+        full = bool(self.ctrl[DC_MODE])
+        dc = join_counts(*split) if split is not None else counts.double()
+        if full:
+            self.G.zero_()
+        self.sums.add_(sums.double())
+        self.counts.add_(dc)
+        new = ref.finalize(self.sums, self.counts, C, self.empty_cluster)
+        if shift is not None:
+            dd = new.double() - C.double()
+            shift.fill_(float((dd * dd).sum(1).max()) if dd.numel() else 0.0)
+        C.copy_(new)
+        it = int(self.ctrl[DC_ITER]) + 1
+        prev_ok = bool(self.ctrl[DC_PREVOK])
+        m = float(moved) if moved is not None else 0.0
+        nxt = (self.refresh > 0 and it % self.refresh == 0) or \
+              (prev_ok and m > self.theta * float(n_global))
+        self.ctrl[DC_ITER] = it
+        self.ctrl[DC_NEXT] = int(nxt)
+        self.ctrl[DC_PREVOK] = 1
+        self.stats += torch.tensor([m if prev_ok else 0.0, float(prev_ok), float(full), 1.0],
+                                   dtype=torch.float64, device=self.stats.device)
+
+
 def deterministic_update(x, labels, sums, counts):
     """Run-to-run bitwise reproducible partial sums (SURVEY.md §5.2 ``--deterministic``):
     PyTorch's sort-based ``index_put_(accumulate=True)`` under deterministic algorithms
@@ -256,6 +383,25 @@ class _LocalOpsBase:
             shift.fill_(max(float(shift.max()), float((d * d).sum(1).max())))
         C.copy_(new)
 
+    # ------------------------------------------------------------- delta update
+    def make_delta(self, n: int, k: int, d: int, refresh: int, theta: float,
+                   empty_cluster: str = "keep"):
+        """A :class:`DeltaState` for this shard, or None where the delta update is not
+        supported (fused assign+update kernels, the deterministic update, K > 8192)."""
+        upd = getattr(self, "update", None)
+        if not isinstance(upd, NativeUpdate) or upd.deterministic or k > DELTA_MAX_K:
+            return None
+        if n >= (1 << 30):
+            return None
+        return NativeDelta(self.ops, n, k, d, self.device, refresh, theta)
+
+    def bf16_operands(self):
+        """(Cm2, cnorm) the finalize kernel writes for the next assignment, or (None, None)."""
+        return None, None
+
+    def after_finalize(self, C: torch.Tensor):
+        """Operand prep the finalize kernel does not do itself (fp8 re-quantisation)."""
+
     # ------------------------------------------------------------- exact counts
     def supports_count_split(self) -> bool:
         return isinstance(getattr(self, "update", None), NativeUpdate)
@@ -299,6 +445,9 @@ class TorchLloyd(_LocalOpsBase):
         if mind is not None:
             mind.copy_(md)
 
+    def make_delta(self, n, k, d, refresh, theta, empty_cluster="keep"):
+        return TorchDelta(n, k, d, self.device, refresh, theta, empty_cluster)
+
 
 class HipBf16Lloyd(_LocalOpsBase):
     """bf16 shard [N, DP] (zero-padded to an MFMA-friendly width) + fp32 centroids."""
@@ -335,6 +484,9 @@ class HipBf16Lloyd(_LocalOpsBase):
 
     def finalize(self, sums, counts, C, shift):
         self.ops.finalize(sums, counts, C, self.policy, shift, self.cm2, self.cnorm)
+
+    def bf16_operands(self):
+        return self.cm2, self.cnorm
 
     # -------------------------------------------------- mini-batches by row index
     def supports_indexed(self) -> bool:
@@ -447,6 +599,9 @@ class HipWideBf16Lloyd(_GroupedAssign, _LocalOpsBase):
 
     def finalize(self, sums, counts, C, shift):
         self.ops.finalize(sums, counts, C, self.policy, shift, self.cm2, self.cnorm)
+
+    def bf16_operands(self):
+        return self.cm2, self.cnorm
 
     row_align = 32
 
@@ -567,6 +722,9 @@ class HipFp8Lloyd(_GroupedAssign, _LocalOpsBase):
         self.ops.finalize(sums, counts, C, self.policy, shift, None, None)
         self.prepare(C)
 
+    def after_finalize(self, C):
+        self.prepare(C)
+
     row_align = 32
 
     def pad_rows(self, kpad):
@@ -617,6 +775,9 @@ class HipSmallLloyd(_HipExactBase):
 
     def supports_count_split(self) -> bool:
         return False  # the fused kernel accumulates counts itself (fp64 buffers only)
+
+    def make_delta(self, *a, **kw):
+        return None  # one fused assign + accumulate pass reads X once either way
 
     def step(self, C, labels, mind, sums, counts):
         self.ops.lloyd_small(self.x, C, None if self.skip_step_labels else labels, mind, sums,

@@ -36,6 +36,22 @@ def test_bench_json_contract(gpus, scaling):
     assert d["value"] == pytest.approx(n / (d["ms_per_step"] / 1e3), rel=1e-6)
     if gpus > 1:  # per-phase times (max over ranks) ride along at world > 1
         assert set(d["phase_ms"]) == {"zero", "assign", "update", "allreduce", "finalize"}
+    # the update mode of the timed steps and the correctness witness (after the timing)
+    assert d["update"]["mode"] == "delta" and 0.0 <= d["update"]["moved_frac_mean"] <= 1.0
+    assert d["check"]["sample_rows"] == 20000 if n == 20000 else d["check"]["sample_rows"] > 0
+    assert d["check"]["agree_fp64_sample"] >= 0.99 and d["check"]["inertia"] > 0
+
+
+def test_bench_update_full_and_witness():
+    """--update full times the re-summing update; both modes report the witness, and the
+    fits agree."""
+    args = ["--steps", "4", "--warmup", "1", "--n-per-gpu", "40000", "--k", "12", "--dim", "6",
+            "--dtype", "fp32"]
+    dd = _run(args)
+    df = _run(args + ["--update", "full"])
+    assert dd["update"]["mode"] == "delta" and df["update"]["mode"] == "full"
+    assert df["check"]["agree_fp64_sample"] >= 0.99
+    assert dd["check"]["inertia"] == pytest.approx(df["check"]["inertia"], rel=1e-9)
 
 
 def test_bench_headline_is_strong_scaling_at_10m(tmp_path):

@@ -39,7 +39,8 @@ def _worker(rank, world, port, method, init, q, n, d, k, iters, seed, extra):
     eng = getattr(model, "engine_", None)
     if eng is not None:
         info = dict(rsag=getattr(eng, "rsag", False), split=getattr(eng, "count_split", False),
-                    counts=r.counts)
+                    counts=r.counts, update_mode=getattr(eng, "update_mode", None),
+                    update_stats=eng.update_stats() if hasattr(eng, "update_stats") else None)
     if rank == 0:
         q.put((r.centers, labels.numpy(), r.inertia, r.n_iter, r.init_centers, info))
     D.destroy_comm()
@@ -128,6 +129,38 @@ def test_fp32_buffer_exact_counts(world, mode):
     assert np.all(info["counts"] == np.round(info["counts"]))
     c1, *_ = run_world(1, extra={"dtype": "fp32"}, **kw)
     np.testing.assert_allclose(c, c1, rtol=2e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_delta_update_equals_full(world):
+    """update='delta' (only the rows whose label changed move between replicated fp64
+    totals; full re-sum every 4 steps) reaches the full update's fit at every world size,
+    and the ranks agree on every step's mode (the moved count rides in the all-reduce)."""
+    kw = dict(k=9, d=4, n=9001, iters=14, init="first_k")
+    cf, lf, inf_, itf, _, f = run_world(world, extra={"update": "full"}, **kw)
+    cd, ld, ind, itd, _, dlt = run_world(world, extra={"update": "delta", "delta_refresh": 4},
+                                         **kw)
+    assert f["update_mode"] == "full" and dlt["update_mode"] == "delta"
+    st = dlt["update_stats"]
+    assert st["steps"] == 14 and st["full_steps"] == 1 + 13 // 4, st
+    np.testing.assert_allclose(cd, cf, rtol=1e-10, atol=1e-10)
+    np.testing.assert_array_equal(ld, lf)
+    assert abs(ind - inf_) <= 1e-9 * abs(inf_) and itd == itf
+    np.testing.assert_array_equal(dlt["counts"], f["counts"])
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_delta_theta_fallback(world):
+    """theta = 0: any step that moved a row makes the next one a full step (decided from
+    the all-reduced moved count, so every rank switches together); same fit."""
+    kw = dict(k=6, d=3, n=6007, iters=8)
+    cf, lf, *_ = run_world(world, extra={"update": "full"}, **kw)
+    cd, ld, _, _, _, info = run_world(world, extra={"update": "delta", "delta_theta": 0.0,
+                                                    "delta_refresh": 0}, **kw)
+    st = info["update_stats"]
+    assert st["full_steps"] >= 2 and st["moved_rows"] > 0
+    np.testing.assert_allclose(cd, cf, rtol=1e-10, atol=1e-10)
+    np.testing.assert_array_equal(ld, lf)
 
 
 def _count_worker(rank, world, port, q):
@@ -293,6 +326,9 @@ def _warmup_worker(rank, world, port, q):
     c0 = eng.C.clone()
     eng.warmup(force=True)  # collective decision: rank 1 cannot, so neither warms up
     same = bool(torch.equal(eng.C, c0)) and eng.n_iter == 0
+    # the streamed rank cannot run the delta update, so no rank does (one buffer layout,
+    # one mode per step)
+    same = same and eng.update_mode == "full"
     for _ in range(2):
         eng.step()
     q.put((rank, same, eng.C.numpy().copy()))

@@ -64,6 +64,24 @@ def _worker(port, q):
             res.append((np.asarray(r.centers), labels.cpu().numpy(),
                         bool(getattr(model.engine_, "rsag", False))))
         out[name] = res
+    # the whole step captured into a hipGraph WITH its RCCL all-reduce (the multi-GPU
+    # bench's --graph path) against eager steps on the same group; delta update on
+    from tensorflow_distributed_clustering_amd.models.kmeans import LloydEngine
+    n, d, k = 200_003, 128, 256
+    x = gaussian_blobs(n, d, k, seed=7, dtype=torch.bfloat16, device=comm.device)
+    cfg = tdc.ClusterConfig(n_clusters=k, max_iter=8, dtype="bf16", init="random", seed=7,
+                            delta_refresh=3)
+    res = []
+    for graph in (False, True):
+        eng = LloydEngine(x, cfg, comm, n, 0)
+        if graph:
+            eng.capture(include_collectives=True)
+        for _ in range(8):
+            eng.step()
+        torch.cuda.synchronize()
+        res.append((eng.C.cpu().numpy(), eng.update_mode, eng._graph is not None
+                    if hasattr(eng, "_graph") else False))
+    out["graph"] = res
     comm.barrier()
     q.put(out)
     D.destroy_comm()
@@ -112,3 +130,11 @@ def test_rccl_bounded_matches_local(rccl_results):
     (c_r, l_r, _), (c_l, l_l, _) = rccl_results["bounded"]
     np.testing.assert_allclose(c_r, c_l, rtol=2e-3, atol=2e-3)
     assert (l_r == l_l).mean() > 0.999
+
+
+def test_rccl_graph_capture_with_collectives_equals_eager(rccl_results):
+    """capture(include_collectives=True) on the RCCL group: replayed steps (all-reduce
+    inside the graph) reach the eager steps' centroids."""
+    (c_e, mode_e, g_e), (c_g, mode_g, g_g) = rccl_results["graph"]
+    assert not g_e and g_g and mode_e == mode_g == "delta"
+    np.testing.assert_allclose(c_g, c_e, rtol=1e-5, atol=1e-5)
