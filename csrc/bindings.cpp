@@ -36,6 +36,7 @@ int dcode(at::ScalarType t) {
     case at::kFloat: return TDC_F32;
     case at::kDouble: return TDC_F64;
     case at::kBFloat16: return TDC_BF16;
+    case at::kLong: return TDC_I64;  // fixed-point accumulation (deterministic update)
     default: TORCH_CHECK(false, "tdc: unsupported dtype ", t);
   }
   return -1;
@@ -157,7 +158,8 @@ void update(const at::Tensor& X, const at::Tensor& labels, at::Tensor& sums, at:
   check_rows(X, "X");
   TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous(), "tdc.update: labels int32");
   TORCH_CHECK(sums.dim() == 2 && sums.is_contiguous() && counts.is_contiguous(), "tdc.update: sums");
-  TORCH_CHECK(sums.scalar_type() == counts.scalar_type(), "tdc.update: sums/counts dtype");
+  TORCH_CHECK(sums.scalar_type() == counts.scalar_type() && sums.scalar_type() != at::kLong,
+              "tdc.update: sums/counts dtype (fp32/fp64; fixed point runs the sorted update)");
   TORCH_CHECK(X.size(1) >= sums.size(1), "tdc.update: X narrower than sums");
   TORCH_CHECK(labels.numel() >= X.size(0), "tdc.update: labels shorter than X");
   TORCH_CHECK(counts.numel() >= sums.size(0), "tdc.update: counts shorter than K");
@@ -182,10 +184,16 @@ void check_split(const std::optional<at::Tensor>& hi, const std::optional<at::Te
                 "tdc.", op, ": cnt_hi/cnt_lo must be contiguous fp32 [K]");
 }
 
+void check_fixed(const at::Tensor& sums, double fixed_scale, const char* op) {
+  if (sums.scalar_type() == at::kLong)
+    TORCH_CHECK(fixed_scale > 0.0, "tdc.", op, ": int64 (fixed-point) sums need fixed_scale > 0");
+}
+
 void update_sorted(const at::Tensor& X, const at::Tensor& labels, at::Tensor& sums,
                    at::Tensor& counts, at::Tensor& work, const std::optional<at::Tensor>& cnt_hi,
                    const std::optional<at::Tensor>& cnt_lo,
-                   const std::optional<at::Tensor>& zero_first) {
+                   const std::optional<at::Tensor>& zero_first, double fixed_scale) {
+  check_fixed(sums, fixed_scale, "update_sorted");
   check_cuda(X, "X");
   check_rows(X, "X");
   TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous() && labels.numel() >= X.size(0),
@@ -211,7 +219,8 @@ void update_sorted(const at::Tensor& X, const at::Tensor& labels, at::Tensor& su
                           (int)sums.size(0), sums.data_ptr(), counts.data_ptr(),
                           work.data_ptr<int>(), num_cus(X.device().index()), cur_stream(),
                           nullptr, static_cast<float*>(opt_ptr(cnt_hi)),
-                          static_cast<float*>(opt_ptr(cnt_lo)), opt_ptr(zero_first), zbytes),
+                          static_cast<float*>(opt_ptr(cnt_lo)), opt_ptr(zero_first), zbytes,
+                          fixed_scale),
         "update_sorted");
 }
 
@@ -419,7 +428,8 @@ int64_t fcm_mfma_workspace(const at::Tensor& like, int64_t N, int64_t K, int64_t
 void finalize(const std::optional<at::Tensor>& sums, const std::optional<at::Tensor>& counts,
               at::Tensor& C, int64_t policy, const std::optional<at::Tensor>& shift,
               const std::optional<at::Tensor>& Cm2, const std::optional<at::Tensor>& cnorm,
-              const std::optional<at::Tensor>& drift, const std::optional<at::Tensor>& maxdrift) {
+              const std::optional<at::Tensor>& drift, const std::optional<at::Tensor>& maxdrift,
+              double fixed_scale) {
   check_cuda(C, "C");
   TORCH_CHECK(C.is_contiguous() && C.dim() == 2, "tdc.finalize: C");
   const int K = (int)C.size(0), D = (int)C.size(1);
@@ -427,6 +437,8 @@ void finalize(const std::optional<at::Tensor>& sums, const std::optional<at::Ten
   if (sums.has_value() && sums->defined()) {
     TORCH_CHECK(counts.has_value() && counts->defined(), "tdc.finalize: counts required");
     TORCH_CHECK(sums->is_contiguous() && sums->numel() == (int64_t)K * D, "tdc.finalize: sums");
+    TORCH_CHECK(counts->scalar_type() == sums->scalar_type(), "tdc.finalize: counts dtype");
+    check_fixed(*sums, fixed_scale, "finalize");
     acc = dcode(sums->scalar_type());
   }
   int Kp = K, DP = D;
@@ -457,7 +469,8 @@ void finalize(const std::optional<at::Tensor>& sums, const std::optional<at::Ten
   const DevGuard guard(C.device());
   check(tdc_finalize(acc, dcode(C.scalar_type()), opt_ptr(sums), opt_ptr(counts), K, D,
                      C.data_ptr(), (int)policy, sh, opt_ptr(Cm2),
-                     static_cast<float*>(opt_ptr(cnorm)), Kp, DP, cur_stream(), dr, mdr),
+                     static_cast<float*>(opt_ptr(cnorm)), Kp, DP, cur_stream(), dr, mdr,
+                     fixed_scale),
         "finalize");
 }
 
@@ -546,8 +559,10 @@ void check_ctrl(const at::Tensor& ctrl, const at::Tensor& like, const char* op) 
 void delta_update(const at::Tensor& X, const at::Tensor& labels, at::Tensor& prev, at::Tensor& sums,
                   at::Tensor& counts, at::Tensor& work, at::Tensor& ctrl,
                   const std::optional<at::Tensor>& cnt_hi, const std::optional<at::Tensor>& cnt_lo,
-                  const std::optional<at::Tensor>& moved, const std::optional<at::Tensor>& zero_first) {
+                  const std::optional<at::Tensor>& moved, const std::optional<at::Tensor>& zero_first,
+                  double fixed_scale) {
   check_cuda(X, "X");
+  check_fixed(sums, fixed_scale, "delta_update");
   check_rows(X, "X");
   const int64_t N = X.size(0);
   TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous() && labels.numel() >= N,
@@ -584,7 +599,7 @@ void delta_update(const at::Tensor& X, const at::Tensor& labels, at::Tensor& pre
                          work.data_ptr<int>(), ctrl.data_ptr<int>(), num_cus(X.device().index()),
                          cur_stream(), static_cast<float*>(opt_ptr(cnt_hi)),
                          static_cast<float*>(opt_ptr(cnt_lo)), opt_ptr(moved), opt_ptr(zero_first),
-                         zbytes),
+                         zbytes, fixed_scale),
         "delta_update");
 }
 
@@ -594,8 +609,9 @@ void delta_finalize(const at::Tensor& sums, const at::Tensor& counts,
                     int64_t policy, const std::optional<at::Tensor>& shift,
                     const std::optional<at::Tensor>& Cm2, const std::optional<at::Tensor>& cnorm,
                     at::Tensor& ctrl, const std::optional<at::Tensor>& stats, int64_t refresh,
-                    double theta_n) {
+                    double theta_n, double fixed_scale) {
   check_cuda(C, "C");
+  check_fixed(sums, fixed_scale, "delta_finalize");
   TORCH_CHECK(C.is_contiguous() && C.dim() == 2, "tdc.delta_finalize: C");
   const int K = (int)C.size(0), D = (int)C.size(1);
   TORCH_CHECK(sums.is_contiguous() && sums.numel() == (int64_t)K * D, "tdc.delta_finalize: sums");
@@ -633,7 +649,7 @@ void delta_finalize(const at::Tensor& sums, const at::Tensor& counts,
                            static_cast<const float*>(opt_ptr(cnt_lo)), opt_ptr(moved),
                            G.data_ptr<double>(), K, D, C.data_ptr(), (int)policy, sh, opt_ptr(Cm2),
                            static_cast<float*>(opt_ptr(cnorm)), Kp, DP, ctrl.data_ptr<int>(), st,
-                           (int)refresh, theta_n, cur_stream()),
+                           (int)refresh, theta_n, cur_stream(), fixed_scale),
         "delta_finalize");
 }
 
@@ -897,7 +913,7 @@ TORCH_LIBRARY(tdc, m) {
   m.def("lloyd_small(Tensor X, Tensor C, Tensor(a!)? labels, Tensor(b!)? mind, Tensor(c!) sums, Tensor(d!) counts) -> ()");
   m.def("update(Tensor X, Tensor labels, Tensor(a!) sums, Tensor(b!) counts) -> ()");
   m.def("update_sorted_workspace(int N, int K) -> int", &update_sorted_workspace);
-  m.def("update_sorted(Tensor X, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work, Tensor(d!)? cnt_hi=None, Tensor(e!)? cnt_lo=None, Tensor(f!)? zero_first=None) -> ()");
+  m.def("update_sorted(Tensor X, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work, Tensor(d!)? cnt_hi=None, Tensor(e!)? cnt_lo=None, Tensor(f!)? zero_first=None, float fixed_scale=0.0) -> ()");
   m.def("fcm_small_supported(ScalarType dtype, int K, int D) -> bool", &fcm_small_supported);
   m.def("fcm_small(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!)? labels, Tensor(b!) wx, Tensor(c!) ws) -> ()");
   m.def("fcm_tower_stats(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) rowinfo) -> ()");
@@ -912,15 +928,15 @@ TORCH_LIBRARY(tdc, m) {
   m.def("recheck_top2(Tensor X, Tensor C, Tensor(a!) labels, Tensor labels2, Tensor d1, Tensor d2, float tau) -> int");
   m.def("quant_fp8(Tensor X, int valid, int neg2, Tensor(a!) Q, Tensor(b!) S, Tensor(c!)? norm) -> ()");
   m.def("kpp_step(Tensor X, Tensor cand, Tensor(a!) closest, int mode, Tensor(b!) pots) -> ()");
-  m.def("finalize(Tensor? sums, Tensor? counts, Tensor(a!) C, int policy, Tensor(b!)? shift, Tensor(c!)? Cm2, Tensor(d!)? cnorm, Tensor(e!)? drift=None, Tensor(f!)? maxdrift=None) -> ()");
+  m.def("finalize(Tensor? sums, Tensor? counts, Tensor(a!) C, int policy, Tensor(b!)? shift, Tensor(c!)? Cm2, Tensor(d!)? cnorm, Tensor(e!)? drift=None, Tensor(f!)? maxdrift=None, float fixed_scale=0.0) -> ()");
   m.def("assign_bf16_indexed(Tensor X, Tensor rowidx, Tensor Cm2, Tensor cnorm, Tensor(a!) labels, Tensor(b!)? mind) -> ()");
   m.def("update_sorted_indexed(Tensor X, Tensor rowidx, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work, Tensor(d!)? cnt_hi=None, Tensor(e!)? cnt_lo=None) -> ()");
   m.def("assign_bf16_top2(Tensor X, Tensor? rowidx, Tensor Cm2, Tensor cnorm, Tensor(a!) labels, Tensor(b!) mind, Tensor(c!) mind2) -> ()");
   m.def("bounds_filter(Tensor labels, Tensor(a!) ub, Tensor(b!) lb, Tensor drift, Tensor maxdrift, float slack, Tensor(c!) active, Tensor(d!) count) -> ()");
   m.def("bounds_scatter(Tensor active, Tensor count, Tensor blab, Tensor d1, Tensor d2, Tensor(a!) labels, Tensor(b!) ub, Tensor(c!) lb, Tensor(d!) moved_idx, Tensor(e!) moved_old, Tensor(f!) moved_new, Tensor(g!) mcount) -> ()");
   m.def("delta_workspace(int N, int K) -> int", &delta_workspace);
-  m.def("delta_update(Tensor X, Tensor labels, Tensor(a!) prev, Tensor(b!) sums, Tensor(c!) counts, Tensor(d!) work, Tensor(e!) ctrl, Tensor(f!)? cnt_hi=None, Tensor(g!)? cnt_lo=None, Tensor(h!)? moved=None, Tensor(i!)? zero_first=None) -> ()");
-  m.def("delta_finalize(Tensor sums, Tensor counts, Tensor? cnt_hi, Tensor? cnt_lo, Tensor? moved, Tensor(a!) G, Tensor(b!) C, int policy, Tensor(c!)? shift, Tensor(d!)? Cm2, Tensor(e!)? cnorm, Tensor(f!) ctrl, Tensor(g!)? stats, int refresh, float theta_n) -> ()");
+  m.def("delta_update(Tensor X, Tensor labels, Tensor(a!) prev, Tensor(b!) sums, Tensor(c!) counts, Tensor(d!) work, Tensor(e!) ctrl, Tensor(f!)? cnt_hi=None, Tensor(g!)? cnt_lo=None, Tensor(h!)? moved=None, Tensor(i!)? zero_first=None, float fixed_scale=0.0) -> ()");
+  m.def("delta_finalize(Tensor sums, Tensor counts, Tensor? cnt_hi, Tensor? cnt_lo, Tensor? moved, Tensor(a!) G, Tensor(b!) C, int policy, Tensor(c!)? shift, Tensor(d!)? Cm2, Tensor(e!)? cnorm, Tensor(f!) ctrl, Tensor(g!)? stats, int refresh, float theta_n, float fixed_scale=0.0) -> ()");
   m.def("sculley_update(Tensor sums, Tensor counts, Tensor(a!) C, Tensor(b!) v, Tensor(c!)? shift, Tensor(d!)? Cm2, Tensor(e!)? cnorm) -> ()");
 }
 

@@ -9,6 +9,7 @@
 //   Cm2[k] = -2 * bf16(c_k)   (exact scaling), cnorm[k] = ||bf16(c_k)||^2 (fp32),
 //   pad rows k >= K: Cm2 = 0, cnorm = 3e38 (never selected).
 #include <algorithm>
+#include <type_traits>
 
 #include "tdc_common.h"
 #include "kernels.h"
@@ -111,7 +112,8 @@ __global__ __launch_bounds__(256) void finalize_kernel(const ACC* __restrict__ s
                                                        __bf16* __restrict__ Cm2,
                                                        float* __restrict__ cnorm, int Kp, int DP,
                                                        float* __restrict__ drift,
-                                                       float* __restrict__ maxdrift) {
+                                                       float* __restrict__ maxdrift,
+                                                       double inv_scale) {
   const int rows = Cm2 ? (Kp > K ? Kp : K) : K;
   unsigned shmax = 0u, dmax = 0u;
   for (int k = blockIdx.x * 4 + (threadIdx.x >> 6); k < rows; k += gridDim.x * 4) {
@@ -119,10 +121,18 @@ __global__ __launch_bounds__(256) void finalize_kernel(const ACC* __restrict__ s
       pad_row(k, Cm2, cnorm, DP);
       continue;
     }
-    const ACC cnt = sums ? counts[k] : (ACC)1;
-    finalize_row(k, D, sums != nullptr, cnt,
-                 [&](int d) { return sums[(int64_t)k * D + d]; }, C, policy, Cm2, cnorm, DP,
-                 shift != nullptr, drift, shmax, dmax);
+    if constexpr (std::is_same<ACC, long long>::value) {
+      // fixed-point sums (the deterministic update): value = sum / scale
+      const double cnt = sums ? (double)counts[k] : 1.0;
+      finalize_row(k, D, sums != nullptr, cnt,
+                   [&](int d) { return (double)sums[(int64_t)k * D + d] * inv_scale; }, C,
+                   policy, Cm2, cnorm, DP, shift != nullptr, drift, shmax, dmax);
+    } else {
+      const ACC cnt = sums ? counts[k] : (ACC)1;
+      finalize_row(k, D, sums != nullptr, cnt,
+                   [&](int d) { return sums[(int64_t)k * D + d]; }, C, policy, Cm2, cnorm, DP,
+                   shift != nullptr, drift, shmax, dmax);
+    }
   }
   if (sums && shift) block_max_shift(shmax, shift);
   if (sums && maxdrift) {
@@ -145,7 +155,7 @@ __global__ __launch_bounds__(256) void finalize_delta_kernel(
     const ACC* __restrict__ moved, double* __restrict__ G, int K, int D, CT* __restrict__ C,
     int policy, float* __restrict__ shift, __bf16* __restrict__ Cm2, float* __restrict__ cnorm,
     int Kp, int DP, int* __restrict__ ctrl, double* __restrict__ stats, int refresh,
-    double theta_n) {
+    double theta_n, double inv_scale) {
   const int lane = threadIdx.x & 63;
   const bool full = ctrl[TDC_DC_MODE] != 0;
   const int rows = Cm2 ? (Kp > K ? Kp : K) : K;
@@ -161,7 +171,7 @@ __global__ __launch_bounds__(256) void finalize_delta_kernel(
     finalize_row(k, D, true, gc,
                  [&](int d) {
                    const int64_t e = (int64_t)k * D + d;
-                   const double g = (full ? 0.0 : G[e]) + (double)dsums[e];
+                   const double g = (full ? 0.0 : G[e]) + (double)dsums[e] * inv_scale;
                    G[e] = g;
                    return g;
                  },
@@ -191,13 +201,14 @@ template <typename ACC, typename CT>
 int launch_finalize_delta(const void* dsums, const void* dcounts, const float* cnt_hi,
                           const float* cnt_lo, const void* moved, double* G, int K, int D, void* C,
                           int policy, float* shift, void* Cm2, float* cnorm, int Kp, int DP,
-                          int* ctrl, double* stats, int refresh, double theta_n, hipStream_t s) {
+                          int* ctrl, double* stats, int refresh, double theta_n, hipStream_t s,
+                          double inv_scale) {
   const int rows = Cm2 ? (Kp > K ? Kp : K) : K;
   const int blocks = std::max(1, std::min((rows + 3) / 4, MAX_BLOCKS));
   hipLaunchKernelGGL((finalize_delta_kernel<ACC, CT>), dim3((unsigned)blocks), dim3(256), 0, s,
                      (const ACC*)dsums, (const ACC*)dcounts, cnt_hi, cnt_lo, (const ACC*)moved, G,
                      K, D, (CT*)C, policy, shift, (__bf16*)Cm2, cnorm, Kp, DP, ctrl, stats,
-                     refresh, theta_n);
+                     refresh, theta_n, inv_scale);
   TDC_CHECK_LAUNCH();
   return 0;
 }
@@ -205,13 +216,13 @@ int launch_finalize_delta(const void* dsums, const void* dcounts, const float* c
 template <typename ACC, typename CT>
 int launch_finalize(const void* sums, const void* counts, int K, int D, void* C, int policy,
                     float* shift, void* Cm2, float* cnorm, int Kp, int DP, hipStream_t s,
-                    float* drift, float* maxdrift) {
+                    float* drift, float* maxdrift, double inv_scale = 1.0) {
   const int rows = Cm2 ? (Kp > K ? Kp : K) : K;
   if (rows <= 0) return 0;  // an rsag rank with no centroid rows of its own: nothing to do
   const int blocks = std::min((rows + 3) / 4, MAX_BLOCKS);
   hipLaunchKernelGGL((finalize_kernel<ACC, CT>), dim3((unsigned)blocks), dim3(256), 0,
                      s, (const ACC*)sums, (const ACC*)counts, K, D, (CT*)C, policy, shift,
-                     (__bf16*)Cm2, cnorm, Kp, DP, drift, maxdrift);
+                     (__bf16*)Cm2, cnorm, Kp, DP, drift, maxdrift, inv_scale);
   TDC_CHECK_LAUNCH();
   return 0;
 }
@@ -305,7 +316,17 @@ int tdc_sculley_update(int acc_dtype, int c_dtype, const void* sums, const void*
 
 int tdc_finalize(int acc_dtype, int c_dtype, const void* sums, const void* counts, int K, int D,
                  void* C, int policy, float* shift, void* Cm2, float* cnorm, int Kp, int DP,
-                 hipStream_t s, float* drift, float* maxdrift) {
+                 hipStream_t s, float* drift, float* maxdrift, double fixed_scale) {
+  if (acc_dtype == TDC_I64) {
+    if (!(fixed_scale > 0.0)) return (int)hipErrorInvalidValue;
+    if (c_dtype == TDC_F32)
+      return launch_finalize<long long, float>(sums, counts, K, D, C, policy, shift, Cm2, cnorm,
+                                               Kp, DP, s, drift, maxdrift, 1.0 / fixed_scale);
+    if (c_dtype == TDC_F64)
+      return launch_finalize<long long, double>(sums, counts, K, D, C, policy, shift, Cm2, cnorm,
+                                                Kp, DP, s, drift, maxdrift, 1.0 / fixed_scale);
+    return (int)hipErrorInvalidValue;
+  }
   if (acc_dtype == TDC_F64 && c_dtype == TDC_F32)
     return launch_finalize<double, float>(sums, counts, K, D, C, policy, shift, Cm2, cnorm, Kp, DP, s,
                                          drift, maxdrift);
@@ -325,10 +346,15 @@ int tdc_delta_finalize(int acc_dtype, int c_dtype, const void* dsums, const void
                        const float* cnt_hi, const float* cnt_lo, const void* moved, double* G,
                        int K, int D, void* C, int policy, float* shift, void* Cm2, float* cnorm,
                        int Kp, int DP, int* ctrl, double* stats, int refresh, double theta_n,
-                       hipStream_t s) {
+                       hipStream_t s, double fixed_scale) {
+  if (acc_dtype == TDC_I64 && !(fixed_scale > 0.0)) return (int)hipErrorInvalidValue;
+  const double inv = acc_dtype == TDC_I64 ? 1.0 / fixed_scale : 1.0;
 #define TDC_FD(A, T)                                                                        \
   return launch_finalize_delta<A, T>(dsums, dcounts, cnt_hi, cnt_lo, moved, G, K, D, C, policy, \
-                                     shift, Cm2, cnorm, Kp, DP, ctrl, stats, refresh, theta_n, s)
+                                     shift, Cm2, cnorm, Kp, DP, ctrl, stats, refresh, theta_n, s, \
+                                     inv)
+  if (acc_dtype == TDC_I64 && c_dtype == TDC_F32) TDC_FD(long long, float);
+  if (acc_dtype == TDC_I64 && c_dtype == TDC_F64) TDC_FD(long long, double);
   if (acc_dtype == TDC_F64 && c_dtype == TDC_F32) TDC_FD(double, float);
   if (acc_dtype == TDC_F32 && c_dtype == TDC_F32) TDC_FD(float, float);
   if (acc_dtype == TDC_F64 && c_dtype == TDC_F64) TDC_FD(double, double);

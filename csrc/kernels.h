@@ -6,7 +6,11 @@
 #include <stdint.h>
 
 // dtype codes shared with the bindings
-enum TdcDtype { TDC_F32 = 0, TDC_F64 = 1, TDC_BF16 = 2, TDC_FP8 = 3 };
+enum TdcDtype { TDC_F32 = 0, TDC_F64 = 1, TDC_BF16 = 2, TDC_FP8 = 3, TDC_I64 = 4 };
+// TDC_I64 as an accumulation dtype = fixed point (the deterministic update): partial sums
+// of round-toward-zero(x * fixed_scale) in int64 (fixed_scale a power of two chosen by the
+// caller so that every |sum| < 2^62); integer sums do not depend on the order of the
+// atomics, so the update (and the all-reduce of int64) is bitwise reproducible.
 
 // N1/N6  bf16 MFMA distance + argmin. X [N, ldx] bf16 (first DP columns used, DP in
 // {32,64,128,256}), Cm2 [Kp, DP] bf16 = -2*c, cnorm [Kp] fp32 (pad rows: 0 / 3e38),
@@ -70,11 +74,13 @@ int tdc_update_lds(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t
 // cnt_hi / cnt_lo (nullable, fp32 [K]): the exact count split of an fp32 all-reduce
 // buffer, hi += c >> 12, lo += c & 4095 (each term stays an integer below 2^24, so the
 // fp32 all-reduce sums them exactly; count = 4096 hi + lo up to 2^36).
+// acc_dtype TDC_I64: fixed-point sums (fixed_scale) and int64 counts.
 int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
                       const int32_t* labels, int K, void* sums, void* counts, int* work,
                       int num_cus, hipStream_t stream, const int32_t* rowidx = nullptr,
                       float* cnt_hi = nullptr, float* cnt_lo = nullptr,
-                      void* zero_first = nullptr, int64_t zero_bytes = 0);
+                      void* zero_first = nullptr, int64_t zero_bytes = 0,
+                      double fixed_scale = 0.0);
 int64_t tdc_update_sorted_workspace(int64_t N, int K);
 
 // N4/N5  fused small-K Fuzzy C-Means tower: sum_i w_ki x_i, sum_i w_ki, argmax labels.
@@ -123,9 +129,11 @@ int64_t tdc_fcm_mfma_workspace(int64_t N, int K, int Kp, int DP, int num_cus);
 // policy: 0 keep, 1 nan, 2 zero.
 // drift (nullable, [K]) = ||bf16(c_new) - bf16(c_old)|| per centroid, maxdrift (nullable,
 // zeroed by the caller) = its max: the centroid movement the bounds of bounded Lloyd need.
+// acc_dtype TDC_I64: fixed-point sums (divided by fixed_scale) and int64 counts.
 int tdc_finalize(int acc_dtype, int c_dtype, const void* sums, const void* counts, int K,
                  int D, void* C, int policy, float* shift, void* Cm2, float* cnorm, int Kp,
-                 int DP, hipStream_t stream, float* drift = nullptr, float* maxdrift = nullptr);
+                 int DP, hipStream_t stream, float* drift = nullptr, float* maxdrift = nullptr,
+                 double fixed_scale = 0.0);
 
 // Mini-batch (Sculley) update: n = counts[k] > 0 -> C[k] = (v[k] C[k] + sums[k]) / (v[k] + n),
 // v[k] += n (v fp64 [K]); shift (nullable, zeroed by the caller) = max ||dC_k||^2 over the
@@ -189,7 +197,8 @@ constexpr int TDC_DELTA_MAX_BLOCKS = 1024;  // per-block moved-list slots in the
 int tdc_delta_update(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
                      const int32_t* labels, int32_t* prev, int K, void* sums, void* counts,
                      int* work, int* ctrl, int num_cus, hipStream_t stream, float* cnt_hi,
-                     float* cnt_lo, void* moved, void* zero_first, int64_t zero_bytes);
+                     float* cnt_lo, void* moved, void* zero_first, int64_t zero_bytes,
+                     double fixed_scale = 0.0);
 int64_t tdc_delta_workspace(int64_t N, int K);
 // The step's finalize: G (fp64 [K*D + K] totals) += or = the all-reduced buffer (by
 // ctrl[MODE]), C = G means (policy as tdc_finalize), optional bf16 operand prep, shift;
@@ -200,4 +209,4 @@ int tdc_delta_finalize(int acc_dtype, int c_dtype, const void* dsums, const void
                        const float* cnt_hi, const float* cnt_lo, const void* moved, double* G,
                        int K, int D, void* C, int policy, float* shift, void* Cm2, float* cnorm,
                        int Kp, int DP, int* ctrl, double* stats, int refresh, double theta_n,
-                       hipStream_t stream);
+                       hipStream_t stream, double fixed_scale = 0.0);

@@ -44,6 +44,10 @@ template <typename T, typename A> __device__ __forceinline__ A to_acc(T v) { ret
 // global_atomic_add_f32 / _f64; agent scope is the default).
 __device__ __forceinline__ void atomic_add(float* p, float v) { atomicAdd(p, v); }
 __device__ __forceinline__ void atomic_add(double* p, double v) { atomicAdd(p, v); }
+// fixed-point partials (deterministic update): two's-complement wrap-around add
+__device__ __forceinline__ void atomic_add(long long* p, long long v) {
+  atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v);
+}
 
 // A wave-uniform pointer in SGPRs (readfirstlane of both halves): the saddr operand of
 // an inline-asm global / LDS-DMA load, when the compiler cannot prove the value uniform.

@@ -243,92 +243,75 @@ __global__ __launch_bounds__(NT) void bscatter_kernel(const int32_t* __restrict_
 #undef TDC_ROW
 }
 
-template <typename XT, int VEC> struct RowLoad;
-template <> struct RowLoad<__bf16, 8> {
-  typedef float acc_t;
-  __device__ static void add(const __bf16* p, float (&a)[8]) {
-    const uint4 t = *reinterpret_cast<const uint4*>(p);
-    a[0] += __uint_as_float(t.x << 16); a[1] += __uint_as_float(t.x & 0xffff0000u);
-    a[2] += __uint_as_float(t.y << 16); a[3] += __uint_as_float(t.y & 0xffff0000u);
-    a[4] += __uint_as_float(t.z << 16); a[5] += __uint_as_float(t.z & 0xffff0000u);
-    a[6] += __uint_as_float(t.w << 16); a[7] += __uint_as_float(t.w & 0xffff0000u);
-  }
-};
-template <> struct RowLoad<float, 4> {
-  typedef float acc_t;
-  __device__ static void add(const float* p, float (&a)[4]) {
-    const float4 t = *reinterpret_cast<const float4*>(p);
-    a[0] += t.x; a[1] += t.y; a[2] += t.z; a[3] += t.w;
-  }
-};
-template <> struct RowLoad<double, 2> {
-  typedef double acc_t;
-  __device__ static void add(const double* p, double (&a)[2]) {
-    const double2 t = *reinterpret_cast<const double2*>(p);
-    a[0] += t.x; a[1] += t.y;
-  }
-};
-// split load / accumulate (so a batch of row loads can be in flight before any add)
+// Per-element accumulator conversion: fp32 / fp64 partials, or fixed point (the
+// deterministic update): round-toward-zero of v * 2^S into int64, whose sums are exact and
+// therefore independent of the order the atomics land in.  The scale is a power of two,
+// so v * scale is exact; |sum| < 2^62 by the caller's choice of S.
+template <typename AT> __device__ __forceinline__ AT acc_cvt(float v, float scale) {
+  if constexpr (std::is_same<AT, long long>::value) return (long long)(v * scale);
+  else return (AT)v;
+}
+template <typename AT> __device__ __forceinline__ AT acc_cvt(double v, double scale) {
+  if constexpr (std::is_same<AT, long long>::value) return (long long)(v * scale);
+  else return (AT)v;
+}
+
+// Split load / accumulate (so a batch of row loads can be in flight before any add).  sg
+// is 0 or 0x80000000 (a delta update's subtracted rows), XOR-ed into every element's sign
+// bit: one VALU per element on top of the conversion, folded away when sg is 0.
 template <typename XT, int VEC> struct RowRaw;
 template <> struct RowRaw<__bf16, 8> {
   typedef uint4 raw_t;
+  typedef float sc_t;
   __device__ static raw_t load(const __bf16* p) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
     return make_uint4(v.x, v.y, v.z, v.w);
   }
-  __device__ static void add(const raw_t& t, float (&a)[8]) {
-    a[0] += __uint_as_float(t.x << 16); a[1] += __uint_as_float(t.x & 0xffff0000u);
-    a[2] += __uint_as_float(t.y << 16); a[3] += __uint_as_float(t.y & 0xffff0000u);
-    a[4] += __uint_as_float(t.z << 16); a[5] += __uint_as_float(t.z & 0xffff0000u);
-    a[6] += __uint_as_float(t.w << 16); a[7] += __uint_as_float(t.w & 0xffff0000u);
+  template <typename AT>
+  __device__ static void add(const raw_t& t, unsigned sg, AT (&a)[8], float sc) {
+    a[0] += acc_cvt<AT>(__uint_as_float((t.x << 16) ^ sg), sc);
+    a[1] += acc_cvt<AT>(__uint_as_float((t.x & 0xffff0000u) ^ sg), sc);
+    a[2] += acc_cvt<AT>(__uint_as_float((t.y << 16) ^ sg), sc);
+    a[3] += acc_cvt<AT>(__uint_as_float((t.y & 0xffff0000u) ^ sg), sc);
+    a[4] += acc_cvt<AT>(__uint_as_float((t.z << 16) ^ sg), sc);
+    a[5] += acc_cvt<AT>(__uint_as_float((t.z & 0xffff0000u) ^ sg), sc);
+    a[6] += acc_cvt<AT>(__uint_as_float((t.w << 16) ^ sg), sc);
+    a[7] += acc_cvt<AT>(__uint_as_float((t.w & 0xffff0000u) ^ sg), sc);
   }
 };
 template <> struct RowRaw<float, 4> {
   typedef float4 raw_t;
+  typedef float sc_t;
   __device__ static raw_t load(const float* p) { return *reinterpret_cast<const float4*>(p); }
-  __device__ static void add(const raw_t& t, float (&a)[4]) {
-    a[0] += t.x; a[1] += t.y; a[2] += t.z; a[3] += t.w;
+  template <typename AT>
+  __device__ static void add(const raw_t& t, unsigned sg, AT (&a)[4], float sc) {
+    a[0] += acc_cvt<AT>(__uint_as_float(__float_as_uint(t.x) ^ sg), sc);
+    a[1] += acc_cvt<AT>(__uint_as_float(__float_as_uint(t.y) ^ sg), sc);
+    a[2] += acc_cvt<AT>(__uint_as_float(__float_as_uint(t.z) ^ sg), sc);
+    a[3] += acc_cvt<AT>(__uint_as_float(__float_as_uint(t.w) ^ sg), sc);
   }
 };
 template <> struct RowRaw<double, 2> {
   typedef double2 raw_t;
+  typedef double sc_t;
   __device__ static raw_t load(const double* p) { return *reinterpret_cast<const double2*>(p); }
-  __device__ static void add(const raw_t& t, double (&a)[2]) { a[0] += t.x; a[1] += t.y; }
-};
-
-// signed accumulation (delta updates): sg is 0 or 0x80000000, XOR-ed into the sign bit of
-// every element -- one VALU per element on top of the conversion, no multiply
-template <typename XT, int VEC> struct RowRawSigned;
-template <> struct RowRawSigned<__bf16, 8> {
-  __device__ static void add(const uint4& t, unsigned sg, float (&a)[8]) {
-    a[0] += __uint_as_float((t.x << 16) ^ sg); a[1] += __uint_as_float((t.x & 0xffff0000u) ^ sg);
-    a[2] += __uint_as_float((t.y << 16) ^ sg); a[3] += __uint_as_float((t.y & 0xffff0000u) ^ sg);
-    a[4] += __uint_as_float((t.z << 16) ^ sg); a[5] += __uint_as_float((t.z & 0xffff0000u) ^ sg);
-    a[6] += __uint_as_float((t.w << 16) ^ sg); a[7] += __uint_as_float((t.w & 0xffff0000u) ^ sg);
-  }
-};
-template <> struct RowRawSigned<float, 4> {
-  __device__ static void add(const float4& t, unsigned sg, float (&a)[4]) {
-    a[0] += __uint_as_float(__float_as_uint(t.x) ^ sg);
-    a[1] += __uint_as_float(__float_as_uint(t.y) ^ sg);
-    a[2] += __uint_as_float(__float_as_uint(t.z) ^ sg);
-    a[3] += __uint_as_float(__float_as_uint(t.w) ^ sg);
-  }
-};
-template <> struct RowRawSigned<double, 2> {
-  __device__ static void add(const double2& t, unsigned sg, double (&a)[2]) {
+  template <typename AT>
+  __device__ static void add(const raw_t& t, unsigned sg, AT (&a)[2], double sc) {
     const long long s = (long long)sg << 32;
-    a[0] += __longlong_as_double(__double_as_longlong(t.x) ^ s);
-    a[1] += __longlong_as_double(__double_as_longlong(t.y) ^ s);
+    a[0] += acc_cvt<AT>(__longlong_as_double(__double_as_longlong(t.x) ^ s), sc);
+    a[1] += acc_cvt<AT>(__longlong_as_double(__double_as_longlong(t.y) ^ s), sc);
   }
 };
 
+// one element per lane (unaligned rows / odd widths)
 template <typename XT> struct RowLoad1 {
   typedef typename std::conditional<sizeof(XT) == 8, double, float>::type acc_t;
-  __device__ static void add(const XT* p, acc_t (&a)[1]) { a[0] += (acc_t)p[0]; }
-  __device__ static void add(const XT* p, unsigned sg, acc_t (&a)[1]) {
-    a[0] += sg ? -(acc_t)p[0] : (acc_t)p[0];
+  typedef acc_t sc_t;
+  template <typename AT>
+  __device__ static void add(const XT* p, unsigned sg, AT (&a)[1], sc_t sc) {
+    const acc_t v = (acc_t)p[0];
+    a[0] += acc_cvt<AT>(sg ? -v : v, sc);
   }
 };
 
@@ -340,14 +323,20 @@ constexpr unsigned PERM_NEG = 0x80000000u;
 // SIGNED (delta updates): a perm entry with PERM_NEG set subtracts its row.  nptr
 // (nullable): the entry count lives on the device (delta updates decide it there); the
 // waves then split it evenly themselves (at least 64 entries each, the rest exit).
+// ACC = long long: fixed-point partials (v * scale in int64, the deterministic update).
 template <typename XT, typename ACC, int VEC, int TPR, bool SIGNED = false>
 __global__ __launch_bounds__(256) void segsum_kernel(const XT* __restrict__ X, int64_t ldx, int D,
                                                      const int32_t* __restrict__ perm,
                                                      const int* __restrict__ offsets, int K,
                                                      int64_t N, ACC* __restrict__ sums,
                                                      int64_t rows_per_wave,
-                                                     const int* __restrict__ nptr = nullptr) {
-  typedef typename RowLoad1<XT>::acc_t AT;  // fp64 data -> fp64 partials, else fp32
+                                                     const int* __restrict__ nptr,
+                                                     double fixed_scale) {
+  // fp64 data -> fp64 partials, else fp32; fixed point -> int64
+  typedef typename std::conditional<std::is_same<ACC, long long>::value, long long,
+                                    typename RowLoad1<XT>::acc_t>::type AT;
+  typedef typename RowLoad1<XT>::sc_t SC;
+  const SC sc = (SC)fixed_scale;
   constexpr int G = 64 / TPR;
   constexpr int U = 8;  // rows per group in flight
   const int lane = threadIdx.x & 63;
@@ -434,10 +423,8 @@ __global__ __launch_bounds__(256) void segsum_kernel(const XT* __restrict__ X, i
         if (colok) {
 #pragma unroll
           for (int u = 0; u < U; ++u)
-            if (p + g + u * G < pe) {
-              if constexpr (SIGNED) RowRawSigned<XT, VEC>::add(xv[u], sg[u], acc);
-              else RowRaw<XT, VEC>::add(xv[u], acc);
-            }
+            if (p + g + u * G < pe)
+              RowRaw<XT, VEC>::template add<AT>(xv[u], SIGNED ? sg[u] : 0u, acc, sc);
         }
         if (closes) {
 #pragma unroll
@@ -476,11 +463,9 @@ __global__ __launch_bounds__(256) void segsum_kernel(const XT* __restrict__ X, i
           if (colok) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-              if constexpr (SIGNED)
-                RowLoad1<XT>::add(X + (int64_t)((unsigned)idx[u] & ~PERM_NEG) * ldx + col,
-                                  (unsigned)idx[u] & PERM_NEG, acc);
-              else
-                RowLoad1<XT>::add(X + (int64_t)idx[u] * ldx + col, acc);
+              const unsigned e = (unsigned)idx[u];
+              RowLoad1<XT>::template add<AT>(X + (int64_t)(SIGNED ? e & ~PERM_NEG : e) * ldx + col,
+                                             SIGNED ? e & PERM_NEG : 0u, acc, sc);
             }
           }
           j += U * G;
@@ -492,11 +477,9 @@ __global__ __launch_bounds__(256) void segsum_kernel(const XT* __restrict__ X, i
           }
           const int32_t idx = perm[j];
           if (colok) {
-            if constexpr (SIGNED)
-              RowLoad1<XT>::add(X + (int64_t)((unsigned)idx & ~PERM_NEG) * ldx + col,
-                                (unsigned)idx & PERM_NEG, acc);
-            else
-              RowLoad1<XT>::add(X + (int64_t)idx * ldx + col, acc);
+            const unsigned e = (unsigned)idx;
+            RowLoad1<XT>::template add<AT>(X + (int64_t)(SIGNED ? e & ~PERM_NEG : e) * ldx + col,
+                                           SIGNED ? e & PERM_NEG : 0u, acc, sc);
           }
           j += G;
         }
@@ -714,7 +697,7 @@ namespace {
 template <typename XT, typename ACC, int VEC, bool SIGNED>
 int launch_segsum(const void* X, int64_t ldx, int D, const int32_t* perm, const int* offsets,
                   int K, int64_t N, void* sums, int num_cus, hipStream_t s,
-                  const int* nptr) {
+                  const int* nptr, double fixed_scale) {
   const int lanes_needed = (D + VEC - 1) / VEC;
   (void)num_cus;
   // every wave gets the same row count, so the grid is exactly the waves resident at once
@@ -730,7 +713,8 @@ int launch_segsum(const void* X, int64_t ldx, int D, const int32_t* perm, const 
     waves = (N + rpw - 1) / rpw;                                                            \
     const dim3 grid((unsigned)((waves + 3) / 4));                                           \
     hipLaunchKernelGGL((segsum_kernel<XT, ACC, VEC, TPRV, SIGNED>), grid, dim3(256), 0, s,  \
-                       (const XT*)X, ldx, D, perm, offsets, K, N, (ACC*)sums, rpw, nptr);   \
+                       (const XT*)X, ldx, D, perm, offsets, K, N, (ACC*)sums, rpw, nptr,    \
+                       fixed_scale);                                                        \
   } while (0)
   if (lanes_needed <= 4) TDC_SEG(4);
   else if (lanes_needed <= 8) TDC_SEG(8);
@@ -745,10 +729,11 @@ int launch_segsum(const void* X, int64_t ldx, int D, const int32_t* perm, const 
 template <typename ACC, bool SIGNED = false>
 int dispatch_segsum(int x_dtype, const void* X, int64_t ldx, int D, const int32_t* perm,
                     const int* offsets, int K, int64_t N, void* sums, int num_cus, hipStream_t s,
-                    const int* nptr = nullptr) {
+                    const int* nptr = nullptr, double fixed_scale = 0.0) {
   const bool a16 = ((uintptr_t)X % 16) == 0;
-#define TDC_SEGD(T, V) \
-  return launch_segsum<T, ACC, V, SIGNED>(X, ldx, D, perm, offsets, K, N, sums, num_cus, s, nptr)
+#define TDC_SEGD(T, V)                                                                     \
+  return launch_segsum<T, ACC, V, SIGNED>(X, ldx, D, perm, offsets, K, N, sums, num_cus, s, \
+                                          nptr, fixed_scale)
   if (x_dtype == TDC_BF16) {
     if (a16 && D % 8 == 0 && ldx % 8 == 0) TDC_SEGD(__bf16, 8);
     TDC_SEGD(__bf16, 1);
@@ -770,9 +755,12 @@ int dispatch_segsum(int x_dtype, const void* X, int64_t ldx, int D, const int32_
 int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
                       const int32_t* labels, int K, void* sums, void* counts, int* work,
                       int num_cus, hipStream_t s, const int32_t* rowidx, float* cnt_hi,
-                      float* cnt_lo, void* zero_first, int64_t zero_bytes) {
+                      float* cnt_lo, void* zero_first, int64_t zero_bytes, double fixed_scale) {
   if (zero_bytes % 4 != 0 || (zero_bytes > 0 && zero_first == nullptr))
     return (int)hipErrorInvalidValue;
+  if (acc_dtype != TDC_F32 && acc_dtype != TDC_F64 && acc_dtype != TDC_I64)
+    return (int)hipErrorInvalidValue;
+  if (acc_dtype == TDC_I64 && !(fixed_scale > 0.0)) return (int)hipErrorInvalidValue;
   if (N <= 0) {
     if (zero_bytes && hipMemsetAsync(zero_first, 0, (size_t)zero_bytes, s) != hipSuccess)
       return (int)hipErrorUnknown;
@@ -800,6 +788,9 @@ int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int6
   if (acc_dtype == TDC_F64)
     hipLaunchKernelGGL(scan_kernel<double>, dim3(1), dim3(1024), 0, s, cnt, K, offsets, cursor,
                        (double*)counts, cnt_hi, cnt_lo);
+  else if (acc_dtype == TDC_I64)
+    hipLaunchKernelGGL(scan_kernel<long long>, dim3(1), dim3(1024), 0, s, cnt, K, offsets,
+                       cursor, (long long*)counts, cnt_hi, cnt_lo);
   else
     hipLaunchKernelGGL(scan_kernel<float>, dim3(1), dim3(1024), 0, s, cnt, K, offsets, cursor,
                        (float*)counts, cnt_hi, cnt_lo);
@@ -832,6 +823,9 @@ int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int6
   }
   if (acc_dtype == TDC_F64)
     return dispatch_segsum<double>(x_dtype, X, ldx, D, perm, offsets, K, N, sums, num_cus, s);
+  if (acc_dtype == TDC_I64)
+    return dispatch_segsum<long long>(x_dtype, X, ldx, D, perm, offsets, K, N, sums, num_cus, s,
+                                      nullptr, fixed_scale);
   return dispatch_segsum<float>(x_dtype, X, ldx, D, perm, offsets, K, N, sums, num_cus, s);
 }
 
@@ -845,12 +839,15 @@ int64_t tdc_delta_workspace(int64_t N, int K) {
 int tdc_delta_update(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
                      const int32_t* labels, int32_t* prev, int K, void* sums, void* counts,
                      int* work, int* ctrl, int num_cus, hipStream_t s, float* cnt_hi,
-                     float* cnt_lo, void* moved, void* zero_first, int64_t zero_bytes) {
+                     float* cnt_lo, void* moved, void* zero_first, int64_t zero_bytes,
+                     double fixed_scale) {
   if (zero_bytes % 4 != 0 || (zero_bytes > 0 && zero_first == nullptr))
     return (int)hipErrorInvalidValue;
+  if (acc_dtype == TDC_I64 && !(fixed_scale > 0.0)) return (int)hipErrorInvalidValue;
   // events are < 2N and perm entries carry the sign in bit 31; lpair packs 16-bit labels
   if (K <= 0 || K > TDC_DELTA_MAX_K || N >= ((int64_t)1 << 30)) return (int)hipErrorInvalidValue;
-  if (acc_dtype != TDC_F32 && acc_dtype != TDC_F64) return (int)hipErrorInvalidValue;
+  if (acc_dtype != TDC_F32 && acc_dtype != TDC_F64 && acc_dtype != TDC_I64)
+    return (int)hipErrorInvalidValue;
   // workspace (ints): cnt_ev[K] | cnt_sg[K] | offsets[K+1] | cursor[K] | blk_cnt[MAXB] |
   // lidx[N] | lpair[N] | perm[2N]; the histograms are zero on entry and left zero
   int* cnt_ev = work;
@@ -879,6 +876,10 @@ int tdc_delta_update(int x_dtype, int acc_dtype, const void* X, int64_t N, int64
   if (acc_dtype == TDC_F64)
     hipLaunchKernelGGL(delta_scan_kernel<double>, dim3(1), dim3(1024), 0, s, cnt_ev, cnt_sg, K,
                        offsets, cursor, ctrl, (double*)counts, cnt_hi, cnt_lo, (double*)moved);
+  else if (acc_dtype == TDC_I64)
+    hipLaunchKernelGGL(delta_scan_kernel<long long>, dim3(1), dim3(1024), 0, s, cnt_ev, cnt_sg,
+                       K, offsets, cursor, ctrl, (long long*)counts, cnt_hi, cnt_lo,
+                       (long long*)moved);
   else
     hipLaunchKernelGGL(delta_scan_kernel<float>, dim3(1), dim3(1024), 0, s, cnt_ev, cnt_sg, K,
                        offsets, cursor, ctrl, (float*)counts, cnt_hi, cnt_lo, (float*)moved);
@@ -892,6 +893,9 @@ int tdc_delta_update(int x_dtype, int acc_dtype, const void* X, int64_t N, int64
   if (acc_dtype == TDC_F64)
     return dispatch_segsum<double, true>(x_dtype, X, ldx, D, perm, offsets, K, N, sums, num_cus,
                                          s, ctrl + TDC_DC_EVENTS);
+  if (acc_dtype == TDC_I64)
+    return dispatch_segsum<long long, true>(x_dtype, X, ldx, D, perm, offsets, K, N, sums,
+                                            num_cus, s, ctrl + TDC_DC_EVENTS, fixed_scale);
   return dispatch_segsum<float, true>(x_dtype, X, ldx, D, perm, offsets, K, N, sums, num_cus, s,
                                       ctrl + TDC_DC_EVENTS);
 }

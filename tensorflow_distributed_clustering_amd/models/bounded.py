@@ -41,6 +41,7 @@ class BoundedLloydEngine(LloydEngine):
     # the totals are fp64 (gbuf) and the per-step deltas small: plain [sums | counts] buffer
     exact_counts_ok = False
     delta_ok = False  # its own moved-row bookkeeping (bounds_scatter)
+    fixed_ok = False  # float delta arithmetic on buf (deterministic: plain Lloyd steps)
     rsag_ok = False
     warmup_ok = False  # the bounds and running totals are incremental
     oom_guard_ok = False

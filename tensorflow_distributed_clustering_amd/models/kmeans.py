@@ -249,13 +249,19 @@ class LloydEngine(OomGuard):
         self._x0 = x0
         self._init_given = init_centers_
         acc = acc_dtype_for(cfg.dtype, k, self.d)
+        # deterministic native update: int64 fixed-point partials (ops.NativeUpdate), the
+        # scale agreed on by the ranks in init_centroids
+        self.fixed = bool(self.local.fixed_point()) and self.fixed_ok
+        if self.fixed:
+            acc = torch.int64
         # fp32 partial sums: the counts also travel as exact integer halves (hi, lo) in the
         # same buffer (parallel/dist.split_counts); without the kernel support: fp64 buffer
         self.count_split = (acc == torch.float32 and self.exact_counts_ok
                             and self.local.supports_count_split())
         if acc == torch.float32 and not self.count_split:
             acc = torch.float64
-        self.rsag = self._use_rsag(comm, cfg, k * self.d * torch.tensor([], dtype=acc).element_size())
+        self.rsag = (not self.fixed) and self._use_rsag(
+            comm, cfg, k * self.d * torch.tensor([], dtype=acc).element_size())
         # delta update: only the rows whose label changed move between fp64 running totals
         self.delta = None
         if (cfg.update != "full" and self.delta_ok and not self.streamed and not self.rsag
@@ -335,6 +341,9 @@ class LloydEngine(OomGuard):
 
     # delta centroid update allowed (subclasses with their own step: off)
     delta_ok = True
+    # fixed-point (int64) buffers for the deterministic update (subclasses that do float
+    # arithmetic on buf: off)
+    fixed_ok = True
     # exact count halves in the buffer (subclasses with their own count bookkeeping: off)
     exact_counts_ok = True
     # mid-run OOM flag in the buffer (subclasses with their own step: off)
@@ -386,11 +395,33 @@ class LloydEngine(OomGuard):
                              "native update or the torch ops, K <= 8192, empty_cluster in "
                              "keep/nan/zero and no deterministic / rsag / bounded mode")
 
+    def _agree_fixed_scale(self):
+        """Deterministic update: the fixed-point scale 2^S of the int64 partials, from the
+        global max |x| and N (collective; one max-reduction, plus one pass over a streamed
+        shard).  Every rank uses the same S, so the int64 all-reduce adds like terms."""
+        from ..ops import fixed_point_scale
+        if isinstance(self.source, ResidentSource):
+            xs = [self.local.x]
+        else:
+            xs = (chunk for _, chunk in self._chunks())
+        m = 0.0
+        for xc in xs:
+            if xc.numel():
+                m = max(m, float(xc[:, : self.d].abs().max()))
+        m = self.comm.max_scalar(m)
+        scale = fixed_point_scale(m, self.n_global)
+        self.local.set_fixed_scale(scale)
+        if self.delta is not None:
+            self.delta.fixed_scale = scale
+        self.fixed_scale = scale
+
     def init_centroids(self):
         """Centroid init (collective: every rank calls it, in the same order).  Kept out
         of the constructor's local allocations so a setup OOM can be agreed on first."""
         cfg, comm, k = self.cfg, self.comm, self.k
         self._agree_update_mode()
+        if self.fixed:
+            self._agree_fixed_scale()
         if self._x0 is not None:
             c0 = init_centers(cfg.init, self._x0, self.row_offset, self.n_global, k, comm,
                               cfg.seed, given=self._init_given, kpp_max_k=cfg.kpp_max_k,

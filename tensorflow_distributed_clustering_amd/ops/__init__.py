@@ -112,15 +112,28 @@ def use_native(device: torch.device, backend: str) -> bool:
 
 class NativeUpdate:
     """N2 dispatcher: LDS-privatised histogram when K x D fits one LDS slice, otherwise
-    counting sort + segmented gather-sum (workspace allocated once per shard)."""
+    counting sort + segmented gather-sum (workspace allocated once per shard).
+
+    ``deterministic`` (ClusterConfig.deterministic): the sorted path with
+    FIXED-POINT partials -- every element is rounded toward zero to an int64 multiple of
+    2^-S (``fixed_scale`` = 2^S, chosen by the engine from the global max |x| and N so no
+    sum can overflow) and summed in int64.  Integer addition is associative, so the float
+    atomics' arrival order no longer matters: the update, the int64 all-reduce and the
+    finalize are bitwise reproducible run to run and across world sizes.  Callers with
+    float buffers (mini-batches) get the fixed-point sums converted back."""
 
     LDS_BUDGET = 64 * 1024
 
-    def __init__(self, ops, n: int, k: int, d: int, x_dtype: torch.dtype, device):
+    def __init__(self, ops, n: int, k: int, d: int, x_dtype: torch.dtype, device,
+                 deterministic: bool = False):
         self.ops = ops
+        self.deterministic = bool(deterministic)
         es = 8 if x_dtype == torch.float64 else 4
         self.kind = "lds" if k * (d + 1) * es + 4 * k <= self.LDS_BUDGET else "sorted"
+        if self.deterministic:
+            self.kind = "sorted"
         self.work = None
+        self._fx = None
         if self.kind == "sorted":
             self.work = self._workspace(n, k, device)
 
@@ -130,7 +143,8 @@ class NativeUpdate:
         return torch.zeros(int(_native.require().update_sorted_workspace(n, k)),
                            dtype=torch.int32, device=device)
 
-    deterministic = False
+    # 2^S of the fixed-point partials (deterministic); set by the engine before the first step
+    fixed_scale = 0.0
     # (hi, lo) fp32 [K] views of the all-reduce buffer: exact count halves
     # (parallel/dist.split_counts), accumulated by the scan kernel of the sorted update
     count_split = None
@@ -139,22 +153,38 @@ class NativeUpdate:
     zero_buf = None
 
     def fuses_zero(self) -> bool:
-        return self.kind == "sorted" and not self.deterministic
+        return self.kind == "sorted"
 
     def __call__(self, x, labels, sums, counts):
-        if self.deterministic or self.kind == "lds":
-            if self.deterministic:
-                deterministic_update(x, labels, sums, counts)
-            else:
-                self.ops.update(x, labels, sums, counts)
+        if self.kind == "lds":
+            self.ops.update(x, labels, sums, counts)
             if self.count_split is not None:
                 split_counts(torch.bincount(labels[: x.shape[0]].long(), minlength=sums.shape[0]),
                              *self.count_split)
             return
         if self.work.numel() < int(self.ops.update_sorted_workspace(x.shape[0], sums.shape[0])):
             self.work = self._workspace(x.shape[0], sums.shape[0], x.device)
+        if self.deterministic and sums.dtype != torch.int64:
+            self._fixed_into_float(x, labels, sums, counts)
+            return
         self.ops.update_sorted(x, labels, sums, counts, self.work, *(self.count_split or (None, None)),
-                               self.zero_buf)
+                               self.zero_buf, self.fixed_scale if sums.dtype == torch.int64 else 0.0)
+
+    def _fixed_into_float(self, x, labels, sums, counts):
+        """Deterministic partials for a float buffer: fixed-point into an int64 scratch
+        (scale from this call's rows), then added to the caller's buffer."""
+        k, d = sums.shape
+        if self._fx is None or self._fx.numel() != k * d + k:
+            self._fx = torch.zeros(k * d + k, dtype=torch.int64, device=x.device)
+        self._fx.zero_()
+        n = x.shape[0]
+        scale = fixed_point_scale(float(x[:, :d].abs().max()) if n else 0.0, n)
+        fs, fc = self._fx[: k * d].view(k, d), self._fx[k * d:]
+        self.ops.update_sorted(x, labels, fs, fc, self.work, None, None, None, scale)
+        sums.add_((fs.double() / scale).to(sums.dtype))
+        counts.add_(fc.to(counts.dtype))
+        if self.count_split is not None:
+            split_counts(fc, *self.count_split)
 
 
     def supports_indexed(self) -> bool:
@@ -222,8 +252,11 @@ class DeltaState:
 
 
 class NativeDelta(DeltaState):
-    """HIP delta update (csrc/update_sorted.hip delta_*, centroids.hip finalize_delta)."""
+    """HIP delta update (csrc/update_sorted.hip delta_*, centroids.hip finalize_delta).
+    With int64 buffers (the deterministic update) the deltas are fixed point
+    (``fixed_scale``, set by the engine) and exactly reproducible."""
     native = True
+    fixed_scale = 0.0
 
     def __init__(self, ops, n, k, d, device, refresh, theta):
         super().__init__(n, k, d, device, refresh, theta)
@@ -232,14 +265,16 @@ class NativeDelta(DeltaState):
 
     def update(self, x, labels, sums, counts, split, moved, zero_buf):
         hi, lo = split or (None, None)
+        fx = self.fixed_scale if sums.dtype == torch.int64 else 0.0
         self.ops.delta_update(x, labels, self.prev, sums, counts, self.work, self.ctrl, hi, lo,
-                              moved, zero_buf)
+                              moved, zero_buf, fx)
 
     def finalize(self, sums, counts, split, moved, C, policy, shift, cm2, cnorm, n_global):
         hi, lo = split or (None, None)
+        fx = self.fixed_scale if sums.dtype == torch.int64 else 0.0
         self.ops.delta_finalize(sums.reshape(-1), counts, hi, lo, moved, self.G, C, policy, shift,
                                 cm2, cnorm, self.ctrl, self.stats, self.refresh,
-                                self.theta * float(n_global))
+                                self.theta * float(n_global), fx)
 
 
 class TorchDelta(DeltaState):
@@ -297,20 +332,14 @@ class TorchDelta(DeltaState):
                                    dtype=torch.float64, device=self.stats.device)
 
 
-def deterministic_update(x, labels, sums, counts):
-    """Run-to-run bitwise reproducible partial sums (SURVEY.md §5.2 ``--deterministic``):
-    PyTorch's sort-based ``index_put_(accumulate=True)`` under deterministic algorithms
-    instead of the float atomics of the HIP update kernels."""
-    prev = torch.are_deterministic_algorithms_enabled()
-    torch.use_deterministic_algorithms(True, warn_only=True)
-    try:
-        idx = (labels[: x.shape[0]].long(),)
-        d = sums.shape[1]
-        sums.index_put_(idx, x[:, :d].to(sums.dtype), accumulate=True)
-        counts.index_put_(idx, torch.ones(x.shape[0], dtype=counts.dtype, device=x.device),
-                          accumulate=True)
-    finally:
-        torch.use_deterministic_algorithms(prev)
+def fixed_point_scale(max_abs: float, n_rows: int) -> float:
+    """2^S for fixed-point partial sums of up to ``n_rows`` values of magnitude <=
+    ``max_abs``: the largest power of two with max_abs * n_rows * 2^S < 2^61 (int64 with a
+    bit of headroom), clamped to [2^-60, 2^60]."""
+    import math
+    bound = max(float(max_abs), 1e-30) * max(1, int(n_rows))
+    s = math.floor(61 - math.log2(bound)) - 1
+    return float(2.0 ** max(-60, min(60, s)))
 
 
 class _LocalOpsBase:
@@ -325,6 +354,19 @@ class _LocalOpsBase:
 
     # centroid dtype kept by the driver
     c_dtype = torch.float32
+    # 2^S of fixed-point (int64) partial sums -- the deterministic update; 0: float sums
+    fixed_scale = 0.0
+
+    def set_fixed_scale(self, scale: float):
+        self.fixed_scale = float(scale)
+        upd = getattr(self, "update", None)
+        if isinstance(upd, NativeUpdate):
+            upd.fixed_scale = float(scale)
+
+    def fixed_point(self) -> bool:
+        """Deterministic partials in int64 fixed point (native update, deterministic)."""
+        upd = getattr(self, "update", None)
+        return isinstance(upd, NativeUpdate) and upd.deterministic
 
     @property
     def layout(self):
@@ -389,7 +431,7 @@ class _LocalOpsBase:
         """A :class:`DeltaState` for this shard, or None where the delta update is not
         supported (fused assign+update kernels, the deterministic update, K > 8192)."""
         upd = getattr(self, "update", None)
-        if not isinstance(upd, NativeUpdate) or upd.deterministic or k > DELTA_MAX_K:
+        if not isinstance(upd, NativeUpdate) or k > DELTA_MAX_K:
             return None
         if n >= (1 << 30):
             return None
@@ -483,7 +525,8 @@ class HipBf16Lloyd(_LocalOpsBase):
         self.ops.assign_bf16(self.x, self.cm2, self.cnorm, labels, mind)
 
     def finalize(self, sums, counts, C, shift):
-        self.ops.finalize(sums, counts, C, self.policy, shift, self.cm2, self.cnorm)
+        self.ops.finalize(sums, counts, C, self.policy, shift, self.cm2, self.cnorm,
+                          fixed_scale=self.fixed_scale)
 
     def bf16_operands(self):
         return self.cm2, self.cnorm
@@ -515,7 +558,7 @@ class HipBf16Lloyd(_LocalOpsBase):
 
     def finalize_rows(self, sums, counts, C, shift, r0, kr):
         self.ops.finalize(sums, counts, C, self.policy, shift, self.cm2[r0:r0 + kr],
-                          self.cnorm[r0:r0 + kr])
+                          self.cnorm[r0:r0 + kr], fixed_scale=self.fixed_scale)
 
 
 class _GroupedAssign:
@@ -598,7 +641,8 @@ class HipWideBf16Lloyd(_GroupedAssign, _LocalOpsBase):
         self.update(self.x, labels, sums, counts)
 
     def finalize(self, sums, counts, C, shift):
-        self.ops.finalize(sums, counts, C, self.policy, shift, self.cm2, self.cnorm)
+        self.ops.finalize(sums, counts, C, self.policy, shift, self.cm2, self.cnorm,
+                          fixed_scale=self.fixed_scale)
 
     def bf16_operands(self):
         return self.cm2, self.cnorm
@@ -617,7 +661,7 @@ class HipWideBf16Lloyd(_GroupedAssign, _LocalOpsBase):
 
     def finalize_rows(self, sums, counts, C, shift, r0, kr):
         self.ops.finalize(sums, counts, C, self.policy, shift, self.cm2[r0:r0 + kr],
-                          self.cnorm[r0:r0 + kr])
+                          self.cnorm[r0:r0 + kr], fixed_scale=self.fixed_scale)
 
 
 class HipFp8Lloyd(_GroupedAssign, _LocalOpsBase):
@@ -719,7 +763,8 @@ class HipFp8Lloyd(_GroupedAssign, _LocalOpsBase):
         self.update(self.x, labels, sums, counts)
 
     def finalize(self, sums, counts, C, shift):
-        self.ops.finalize(sums, counts, C, self.policy, shift, None, None)
+        self.ops.finalize(sums, counts, C, self.policy, shift, None, None,
+                          fixed_scale=self.fixed_scale)
         self.prepare(C)
 
     def after_finalize(self, C):
@@ -744,7 +789,8 @@ class HipFp8Lloyd(_GroupedAssign, _LocalOpsBase):
         # finalises nothing but still writes its padding operands (quant of 0 rows: zeros
         # and the BIG pad norm)
         if C.shape[0]:
-            self.ops.finalize(sums, counts, C, self.policy, shift, None, None)
+            self.ops.finalize(sums, counts, C, self.policy, shift, None, None,
+                              fixed_scale=self.fixed_scale)
         self.ops.quant_fp8(C, C.shape[0], 1, self.cm2[r0:r0 + kr], self.cs[r0:r0 + kr],
                            self.cnorm[r0:r0 + kr])
 
@@ -759,11 +805,13 @@ class _HipExactBase(_LocalOpsBase):
         self.update = NativeUpdate(self.ops, self.n, k, self.d, tdt, x.device)
 
     def finalize(self, sums, counts, C, shift):
-        self.ops.finalize(sums, counts, C, self.policy, shift, None, None)
+        self.ops.finalize(sums, counts, C, self.policy, shift, None, None,
+                          fixed_scale=self.fixed_scale)
 
     def finalize_rows(self, sums, counts, C, shift, r0, kr):
         if C.shape[0]:
-            self.ops.finalize(sums, counts, C, self.policy, shift, None, None)
+            self.ops.finalize(sums, counts, C, self.policy, shift, None, None,
+                              fixed_scale=self.fixed_scale)
 
 
 class HipSmallLloyd(_HipExactBase):
@@ -830,8 +878,11 @@ def make_lloyd_ops(x: torch.Tensor, k: int, dtype: str = "bf16", backend: str = 
     ``kgroup_bytes`` / ``fp8_recheck``: ClusterConfig tunables of the wide-D / fp8 assign
     (K-group size; near-tie re-check margin), applied to the ops that have them."""
     ops = _make_lloyd_ops(x, k, dtype, backend, empty_cluster, deterministic)
-    if deterministic and isinstance(getattr(ops, "update", None), NativeUpdate):
-        ops.update.deterministic = True
+    upd = getattr(ops, "update", None)
+    if deterministic and isinstance(upd, NativeUpdate) and not upd.deterministic:
+        # fixed-point partials: always the sorted path (the LDS path sums in float atomics)
+        ops.update = NativeUpdate(upd.ops, ops.n, k, ops.d, ops.x.dtype, ops.device,
+                                  deterministic=True)
     if isinstance(ops, _GroupedAssign) and kgroup_bytes:
         ops.kgroup_bytes = int(kgroup_bytes)
         ops.kg = kgroup_tiles(ops._row_bytes, ops.kp, group_bytes=ops.kgroup_bytes)

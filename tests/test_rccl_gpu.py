@@ -35,6 +35,7 @@ CASES = [
     ("fused_fp64", "fp64", 100_001, 5, 3, 5, "kmeans", {}),
     ("fcm_fp64", "fp64", 50_000, 5, 4, 5, "fcm", {}),
     ("bounded", "bf16", 200_003, 128, 1024, 12, "kmeans", {"algorithm": "bounded"}),
+    ("deterministic", "bf16", 200_003, 128, 256, 5, "kmeans", {"deterministic": True}),
 ]
 
 
@@ -138,3 +139,11 @@ def test_rccl_graph_capture_with_collectives_equals_eager(rccl_results):
     (c_e, mode_e, g_e), (c_g, mode_g, g_g) = rccl_results["graph"]
     assert not g_e and g_g and mode_e == mode_g == "delta"
     np.testing.assert_allclose(c_g, c_e, rtol=1e-5, atol=1e-5)
+
+
+def test_rccl_deterministic_int64_allreduce_bitwise(rccl_results):
+    """Fixed-point partials through an int64 RCCL all-reduce: the RCCL fit equals the
+    no-group fit bit for bit (integer sums do not depend on any reduction order)."""
+    (c_r, l_r, _), (c_l, l_l, _) = rccl_results["deterministic"]
+    assert np.array_equal(c_r, c_l)
+    np.testing.assert_array_equal(l_r, l_l)

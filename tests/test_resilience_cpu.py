@@ -11,7 +11,7 @@ import torch
 
 import tensorflow_distributed_clustering_amd as tdc
 from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs
-from tensorflow_distributed_clustering_amd.ops import deterministic_update
+from tensorflow_distributed_clustering_amd.ops import fixed_point_scale
 from tensorflow_distributed_clustering_amd.ops import reference as ref
 from tensorflow_distributed_clustering_amd.utils import checkpoint as ck
 from tensorflow_distributed_clustering_amd.utils import faults
@@ -103,16 +103,25 @@ def test_setup_oom_gives_up_after_retries(monkeypatch):
     assert faults.is_oom(ei.value)
 
 
-def test_deterministic_update_matches_reference():
-    g = torch.Generator().manual_seed(0)
-    x = torch.randn(3000, 7, generator=g, dtype=torch.float64)
-    lab = torch.randint(0, 9, (3000,), generator=g, dtype=torch.int32)
-    sums = torch.zeros(9, 7, dtype=torch.float64)
-    counts = torch.zeros(9, dtype=torch.float64)
-    deterministic_update(x, lab, sums, counts)
-    rs, rc = ref.cluster_sums(x, lab, 9, acc_dtype=torch.float64)
-    torch.testing.assert_close(sums, rs)
-    torch.testing.assert_close(counts, rc)
+def test_fixed_point_scale_bounds_the_sums():
+    """The deterministic update's int64 fixed point: 2^S with max|x| * N * 2^S < 2^61, the
+    largest such power of two (clamped), so no per-cluster sum can overflow int64."""
+    import math
+    for m, n in [(15.0, 10_000_000), (1e-3, 100), (1e6, 10 ** 9), (0.0, 5), (7.5, 1)]:
+        s = fixed_point_scale(m, n)
+        assert s == 2.0 ** round(math.log2(s))
+        assert max(m, 1e-30) * n * s < 2.0 ** 61
+        if 2.0 ** -60 < s < 2.0 ** 60:
+            assert max(m, 1e-30) * n * s * 4 >= 2.0 ** 61  # not needlessly coarse
+    assert fixed_point_scale(15.0, 10_000_000) == 2.0 ** 32
+
+
+def test_deterministic_cpu_fit_reproducible():
+    x = gaussian_blobs(20000, 5, 6, seed=4, dtype=torch.float64)
+    cfg = tdc.ClusterConfig(n_clusters=6, max_iter=6, dtype="fp64", deterministic=True)
+    a = tdc.KMeans(cfg).fit(x).result_
+    b = tdc.KMeans(cfg).fit(x).result_
+    assert np.array_equal(a.centers, b.centers) and torch.equal(a.labels, b.labels)
 
 
 def test_cli_checkpoint_resume(tmp_path):

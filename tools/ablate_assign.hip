@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "assign_mfma_impl.h"
+#include "assign_mfma_legacy.h"  // tools/
 
 using namespace tdc;
 
