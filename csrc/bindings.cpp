@@ -331,6 +331,75 @@ void fcm_wide(int64_t pass, const at::Tensor& X, const at::Tensor& C, double m, 
         "fcm_wide");
 }
 
+// the row pass of the wide towers alone (G [M, K] of d2 -> labels, and w in place)
+void fcm_wide_rows(at::Tensor& G, int64_t K, double m, bool nan_to_zero, at::Tensor& labels,
+                   bool write_w) {
+  check_cuda(G, "G");
+  TORCH_CHECK((G.scalar_type() == at::kFloat || G.scalar_type() == at::kDouble) &&
+                  G.is_contiguous() && G.dim() == 2 && G.size(1) == K,
+              "tdc.fcm_wide_rows: G [M, K] fp32/fp64");
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous() &&
+                  labels.numel() >= G.size(0), "tdc.fcm_wide_rows: labels int32 [M]");
+  TORCH_CHECK(m > 1.0, "tdc.fcm_wide_rows: fuzzifier must be > 1");
+  const DevGuard guard(G.device());
+  check(tdc_fcm_wide(write_w ? 1 : 3, dcode(G.scalar_type()), nullptr, G.size(0), 0, 1, nullptr,
+                     (int)K, m, nan_to_zero ? 1 : 0, G.data_ptr(), labels.data_ptr<int32_t>(),
+                     nullptr, nullptr, num_cus(G.device().index()), cur_stream()),
+        "fcm_wide_rows");
+}
+
+int64_t fcm_mfma_wide_workspace(const at::Tensor& like, int64_t M, int64_t Kp, int64_t DP) {
+  return tdc_fcm_mfma_wide_workspace(M, (int)Kp, (int)DP, num_cus(like.device().index()));
+}
+
+void fcm_mfma_wide(int64_t pass, const at::Tensor& Xh, const at::Tensor& Xl, const at::Tensor& xx,
+                   const at::Tensor& Ch, const at::Tensor& Cl, const at::Tensor& cc, int64_t K,
+                   int64_t D, at::Tensor& G, const std::optional<at::Tensor>& work,
+                   const std::optional<at::Tensor>& shift, const std::optional<at::Tensor>& wx,
+                   const std::optional<at::Tensor>& ws) {
+  check_cuda(Xh, "Xh");
+  const int64_t M = Xh.size(0), DP = Xh.size(1), Kp = Ch.size(0);
+  for (const at::Tensor* t : {&Xh, &Xl, &Ch, &Cl})
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->is_contiguous() && t->dim() == 2 &&
+                    t->size(1) == DP, "tdc.fcm_mfma_wide: hi/lo operands bf16 [rows, DP]");
+  TORCH_CHECK(Xl.size(0) == M && Cl.size(0) == Kp, "tdc.fcm_mfma_wide: hi/lo row counts");
+  TORCH_CHECK(DP % 128 == 0 && DP >= 128 && DP <= 1024 && Kp % 128 == 0 && Kp >= K && D <= DP,
+              "tdc.fcm_mfma_wide: DP in 128..1024 (x128), Kp % 128 == 0");
+  TORCH_CHECK(xx.scalar_type() == at::kFloat && xx.is_contiguous() && xx.numel() >= M &&
+                  cc.scalar_type() == at::kFloat && cc.is_contiguous() && cc.numel() >= Kp,
+              "tdc.fcm_mfma_wide: norms fp32");
+  TORCH_CHECK(G.scalar_type() == at::kFloat && G.is_contiguous() && G.numel() >= M * K,
+              "tdc.fcm_mfma_wide: G fp32 [M, K]");
+  float* wk = nullptr;
+  double *pwx = nullptr, *pws = nullptr;
+  if (pass == 2) {
+    TORCH_CHECK(work.has_value() && work->defined() && work->scalar_type() == at::kFloat &&
+                    work->is_contiguous() &&
+                    work->numel() >= tdc_fcm_mfma_wide_workspace(M, (int)Kp, (int)DP,
+                                                                 num_cus(Xh.device().index())),
+                "tdc.fcm_mfma_wide: workspace fp32 too small");
+    TORCH_CHECK(wx.has_value() && ws.has_value() && wx->scalar_type() == at::kDouble &&
+                    ws->scalar_type() == at::kDouble && wx->is_contiguous() &&
+                    ws->is_contiguous() && wx->numel() == K * D && ws->numel() == K,
+                "tdc.fcm_mfma_wide: wx [K, D] / ws [K] fp64");
+    wk = work->data_ptr<float>();
+    pwx = wx->data_ptr<double>();
+    pws = ws->data_ptr<double>();
+    if (shift.has_value() && shift->defined())
+      TORCH_CHECK(shift->scalar_type() == at::kFloat && shift->numel() >= D,
+                  "tdc.fcm_mfma_wide: shift fp32 [D]");
+  } else {
+    TORCH_CHECK(pass == 0, "tdc.fcm_mfma_wide: pass 0 (distances) or 2 (W^T X)");
+  }
+  const DevGuard guard(Xh.device());
+  check(tdc_fcm_mfma_wide((int)pass, Xh.data_ptr(), Xl.data_ptr(), xx.data_ptr<float>(), M,
+                          (int)DP, (int)D, Ch.data_ptr(), Cl.data_ptr(), cc.data_ptr<float>(),
+                          (int)K, (int)Kp, G.data_ptr<float>(), wk,
+                          static_cast<const float*>(opt_ptr(shift)), pwx, pws,
+                          num_cus(Xh.device().index()), cur_stream()),
+        "fcm_mfma_wide");
+}
+
 void fcm_split_rows(const at::Tensor& src, int64_t valid, int64_t neg2, at::Tensor& hi,
                     at::Tensor& lo, const std::optional<at::Tensor>& norm,
                     const std::optional<at::Tensor>& shift) {
@@ -919,6 +988,9 @@ TORCH_LIBRARY(tdc, m) {
   m.def("fcm_tower_stats(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) rowinfo) -> ()");
   m.def("fcm_tower_accum(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor rowinfo, Tensor(a!) wx, Tensor(b!) ws) -> ()");
   m.def("fcm_wide(int stage, Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!) G, Tensor(b!)? labels=None, Tensor(c!)? wx=None, Tensor(d!)? ws=None) -> ()");
+  m.def("fcm_wide_rows(Tensor(a!) G, int K, float m, bool nan_to_zero, Tensor(b!) labels, bool write_w) -> ()");
+  m.def("fcm_mfma_wide_workspace(Tensor like, int M, int Kp, int DP) -> int");
+  m.def("fcm_mfma_wide(int stage, Tensor Xh, Tensor Xl, Tensor xx, Tensor Ch, Tensor Cl, Tensor cc, int K, int D, Tensor(a!) G, Tensor(b!)? work=None, Tensor? shift=None, Tensor(c!)? wx=None, Tensor(d!)? ws=None) -> ()");
   m.def("fcm_split_rows(Tensor src, int valid, int neg2, Tensor(a!) hi, Tensor(b!) lo, Tensor(c!)? norm, Tensor? shift=None) -> ()");
   m.def("fcm_mfma_stats(Tensor Xh, Tensor Xl, Tensor xx, Tensor Ch, Tensor Cl, Tensor cc, int K, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) rowinfo) -> ()");
   m.def("fcm_mfma_accum(Tensor Xh, Tensor Xl, Tensor xx, Tensor rowinfo, Tensor Ch, Tensor Cl, Tensor cc, int K, float m, bool nan_to_zero, Tensor(a!) wx, Tensor(b!) ws, Tensor(c!) work, Tensor? shift=None) -> ()");
@@ -955,6 +1027,9 @@ TORCH_LIBRARY_IMPL(tdc, CUDA, m) {
   m.impl("fcm_mfma_workspace", &fcm_mfma_workspace);
   m.impl("fcm_tower_accum", &fcm_tower_accum);
   m.impl("fcm_wide", &fcm_wide);
+  m.impl("fcm_wide_rows", &fcm_wide_rows);
+  m.impl("fcm_mfma_wide_workspace", &fcm_mfma_wide_workspace);
+  m.impl("fcm_mfma_wide", &fcm_mfma_wide);
   m.impl("finalize", &finalize);
   m.impl("delta_update", &delta_update);
   m.impl("delta_finalize", &delta_finalize);

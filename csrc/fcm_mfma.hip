@@ -678,6 +678,354 @@ int launch_maccum(const void* Xh, const void* Xl, const float* xx, const float* 
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------
+// Wide D (DP = 256 ... 1024, multiples of 128): the tower's operands no longer fit a wave's
+// registers (a 32-point hi/lo fragment set is DP/2 VGPRs, the [32 x DP] W^T X tile DP/2
+// accumulators), so the wide path runs over row chunks with the [rows, K] block in HBM,
+// like fcm_wide.hip, but both products on the matrix cores (the same hi/lo bf16 split):
+//   wide_dist : G[r, k] = ||x||^2 + ||c||^2 + x.(-2c)  (3 MFMAs per product), a point within
+//               2^-16 ||x||^2 of a centroid stored as exactly 0 (fcm_wide_rows' on-centroid
+//               rule), 128-point x 128-centroid tiles, 32-feature hi/lo stages by LDS-DMA
+//   (fcm_wide_rows turns d2 into w = u^m in place, csrc/fcm_wide.hip)
+//   wide_wtx  : W^T X of 128-centroid x 128-feature output tiles over a row range: the W
+//               stage (fp32 w -> hi/lo bf16) goes through registers into row-major LDS
+//               images, X hi/lo by LDS-DMA; both MFMA operands come from transposed reads
+//               (ds_read_b64_tr_b16), so neither needs a transposed copy in HBM
+// ---------------------------------------------------------------------------------------
+constexpr int WT = 128;  // tile edge (points / centroids / features)
+
+// 64-byte rows (32 bf16 features) of a stage image: chunk c of row r at 16 (c ^ ((r>>2)&3))
+// -- every ds_read_b128 lane group of the 32x32x16 operand read is conflict-free
+__device__ __forceinline__ int w64off(int r, int c) { return r * 64 + 16 * (c ^ ((r >> 2) & 3)); }
+// 256-byte rows (128 bf16): the row/transpose dual-use image (b) of the guide (T10)
+__device__ __forceinline__ int w256off(int r, int c) {
+  return r * 256 + 16 * (c ^ (((r & 3) << 2) | ((r >> 2) & 3)));
+}
+
+// G [M, K] fp32 for the M rows of the chunk (grid: M/128 x Kp/128 tiles, XCD-grouped so the
+// centroid tiles of one row tile share an L2).  4 waves, wave (wr, wc) owns points
+// wr*64 + [0, 64) x centroids wc*64 + [0, 64): 2 x 2 MFMA tiles of 32x32.
+__global__ __launch_bounds__(256, 2) void fcm_wide_dist_kernel(
+    const __bf16* __restrict__ Xh, const __bf16* __restrict__ Xl, const float* __restrict__ xx,
+    int64_t M, int DP, const __bf16* __restrict__ Ch, const __bf16* __restrict__ Cl,
+    const float* __restrict__ cc, int K, int nct, float* __restrict__ G) {
+  constexpr int IMG = WT * 64;          // one (hi or lo, X or C) 32-feature stage image
+  constexpr int STAGE = 4 * IMG;        // Xh | Xl | Ch | Cl
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  __shared__ float s_xn[WT];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int wr = w >> 1, wc = w & 1;
+  int64_t L = blockIdx.x;
+  {  // XCD-aware order: consecutive work items (the centroid tiles of a row tile) on one XCD
+    const int64_t per = (int64_t)gridDim.x / 8;
+    if (per * 8 == (int64_t)gridDim.x) L = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+  }
+  const int ct = (int)(L % nct);
+  const int64_t r0 = (L / nct) * WT;
+  const int k0 = ct * WT;
+  const int64_t ldb = (int64_t)DP * 2;  // row pitch in bytes (X and C alike)
+
+  // LDS-DMA pieces: wave w loads image w (Xh, Xl, Ch, Cl) of every stage, 8 x 1 KiB pieces
+  // of 16 rows; the swizzle is applied on the source side (w64off is an involution in c)
+  unsigned voff[8];
+  const int last = (int)min((int64_t)WT - 1, M - 1 - r0);  // X rows past the chunk: clamped
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int row = p * 16 + (lane >> 2), cs = lane & 3;
+    const int rr = (w < 2 && row > last) ? last : row;
+    voff[p] = (unsigned)(rr * ldb + 16 * (cs ^ ((row >> 2) & 3)));
+  }
+  const __bf16* src0 = w == 0 ? Xh + r0 * DP : w == 1 ? Xl + r0 * DP
+                     : w == 2 ? Ch + (int64_t)k0 * DP : Cl + (int64_t)k0 * DP;
+  const char* srcb = reinterpret_cast<const char*>(uniform_ptr(src0));
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  auto issue = [&](int st, int buf) __attribute__((always_inline)) {
+    const char* base = srcb + (int64_t)st * 64;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const unsigned dst = lds0 + buf * STAGE + wu * IMG + p * 1024;
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
+                   :: "s"(__builtin_amdgcn_readfirstlane(dst)), "v"(voff[p]), "s"(base)
+                   : "memory", "m0");
+    }
+  };
+  const int nst = DP / 32;
+  issue(0, 0);
+  if (tid < WT) s_xn[tid] = (r0 + tid < M) ? xx[r0 + tid] : 0.f;
+
+  // accumulators start at ||x||^2 + ||c||^2 (registers: points, lanes: centroids)
+  f32x16 acc[2][2];
+  __syncthreads();  // s_xn
+#pragma unroll
+  for (int tj = 0; tj < 2; ++tj) {
+    const float cn = cc[k0 + wc * 64 + tj * 32 + r];
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const f32x4 xn4 = *reinterpret_cast<const f32x4*>(&s_xn[wr * 64 + ti * 32 + 8 * g4 + 4 * h]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[ti][tj][4 * g4 + e] = xn4[e] + cn;
+      }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // fragment addresses: row R (point or centroid), k16 step s, half h -> chunk 2s + h
+  const int xr = (r >> 2) & 3;
+  unsigned ao[2][2], bo[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      ao[t][st] = lds0 + 0 * IMG + (wr * 64 + t * 32 + r) * 64 + 16 * ((2 * st + h) ^ xr);
+      bo[t][st] = lds0 + 2 * IMG + (wc * 64 + t * 32 + r) * 64 + 16 * ((2 * st + h) ^ xr);
+    }
+  for (int st = 0; st < nst; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nst) issue(st + 1, buf ^ 1);
+    const unsigned bo_ = buf * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(ah[t]) : "v"(ao[t][ks] + bo_));
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(al[t]) : "v"(ao[t][ks] + bo_), "i"(IMG));
+        asm volatile("ds_read_b128 %0, %1 offset:0" : "=v"(bh[t]) : "v"(bo[t][ks] + bo_));
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bl[t]) : "v"(bo[t][ks] + bo_), "i"(IMG));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj) {
+          acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ti], bh[tj], acc[ti][tj], 0, 0, 0);
+          acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ti], bl[tj], acc[ti][tj], 0, 0, 0);
+          acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[ti], bh[tj], acc[ti][tj], 0, 0, 0);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage st + 1 landed (this wave's part)
+    __syncthreads();
+  }
+  // epilogue: lanes = centroids (coalesced 128-B row segments), registers = points
+#pragma unroll
+  for (int tj = 0; tj < 2; ++tj) {
+    const int k = k0 + wc * 64 + tj * 32 + r;
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int pr = wr * 64 + ti * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        const int64_t row = r0 + pr;
+        if (row < M && k < K) {
+          const float d2 = acc[ti][tj][i];
+          G[row * (int64_t)K + k] = d2 <= ZERO_FLOOR * s_xn[pr] ? 0.f : d2;
+        }
+      }
+  }
+}
+
+// part[split, k, d] (+ part_ws[split, k] from the feature-tile-0 blocks) of
+// sum_{rows of the split} w[r, k] x[r, d]; reduced by fcm_reduce_kernel
+__global__ __launch_bounds__(256, 2) void fcm_wide_wtx_kernel(
+    const float* __restrict__ W, const __bf16* __restrict__ Xh, const __bf16* __restrict__ Xl,
+    int64_t M, int DP, int K, int Kp, int nkt, int ndt, int64_t rows_per_split,
+    float* __restrict__ part, float* __restrict__ part_ws) {
+  constexpr int RS = 32;                 // data rows per stage (two k16 steps)
+  constexpr int IMG = RS * 256;          // one [32 rows x 128] bf16 image
+  constexpr int STAGE = 4 * IMG;         // Wh | Wl | Xh | Xl
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 1, wc = w & 1;
+  int64_t L = blockIdx.x;
+  {
+    const int64_t per = (int64_t)gridDim.x / 8;
+    if (per * 8 == (int64_t)gridDim.x) L = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+  }
+  const int kt = (int)(L % nkt);
+  const int dt = (int)((L / nkt) % ndt);
+  const int64_t split = L / ((int64_t)nkt * ndt);
+  const int k0 = kt * WT, d0 = dt * WT;
+  const int64_t a = split * rows_per_split;
+  const int64_t b = min(M, a + rows_per_split);
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+
+  // ---- W stage through registers: thread -> data row tid/8, centroids 16 (tid%8) + [0,16)
+  const int wrow = tid >> 3, wcol = (tid & 7) * 16;
+  const bool kin = k0 + wcol < K;        // K % 16 == 0 is not required: per-element below
+  float4 wv[4];
+  float wsum[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) wsum[e] = 0.f;
+  auto wload = [&](int64_t rb) __attribute__((always_inline)) {
+    const int64_t row = rb + wrow;
+    const bool ok = row < b;
+    const float* src = W + (ok ? row : a) * (int64_t)K + k0 + wcol;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ok && kin) {
+        if ((K & 3) == 0 && k0 + wcol + 16 <= K) v = *reinterpret_cast<const float4*>(src + 4 * q);
+        else {
+          float t[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) t[e] = (k0 + wcol + 4 * q + e < K) ? src[4 * q + e] : 0.f;
+          v = make_float4(t[0], t[1], t[2], t[3]);
+        }
+      }
+      wv[q] = v;
+    }
+  };
+  auto wstore = [&](int buf) __attribute__((always_inline)) {
+    bf16x8 hv[2], lv[2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float f[4] = {wv[q].x, wv[q].y, wv[q].z, wv[q].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = 4 * q + e;
+        const __bf16 hb = (__bf16)f[e];
+        hv[j >> 3][j & 7] = hb;
+        lv[j >> 3][j & 7] = (__bf16)(f[e] - (float)hb);
+        wsum[j] += f[e];
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int off = w256off(wrow, (wcol >> 3) + c);
+      *reinterpret_cast<bf16x8*>(smem + buf * STAGE + off) = hv[c];
+      *reinterpret_cast<bf16x8*>(smem + buf * STAGE + IMG + off) = lv[c];
+    }
+  };
+  // ---- X stage by LDS-DMA: waves 0-1 load Xh pieces, 2-3 Xl; 4 pieces of 4 rows each
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const int ximg = wu >> 1;              // 0: Xh, 1: Xl
+  unsigned xoffv[4];
+  int xrow[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int row = ((w & 1) * 4 + p) * 4 + (lane >> 4), cs = lane & 15;
+    xrow[p] = row;
+    xoffv[p] = (unsigned)(16 * (cs ^ (((row & 3) << 2) | ((row >> 2) & 3))));
+  }
+  const char* xsrc = reinterpret_cast<const char*>(uniform_ptr(ximg ? Xl : Xh));
+  auto xissue = [&](int64_t rb, int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int pc = (wu & 1) * 4 + p;
+      const unsigned dst = lds0 + buf * STAGE + (2 + ximg) * IMG + pc * 1024;
+      int64_t row = rb + xrow[p];
+      if (row >= b) row = b - 1;  // rows past the range: any valid row (their w is 0)
+      const unsigned vo = (unsigned)((row - a) * (int64_t)DP * 2 + d0 * 2) + xoffv[p];
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
+                   :: "s"(__builtin_amdgcn_readfirstlane(dst)), "v"(vo),
+                      "s"(xsrc + a * (int64_t)DP * 2)
+                   : "memory", "m0");
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[ti][tj][i] = 0.f;
+
+  // transposed-read lane geometry (T10): group g, row q4, column quad p4
+  const int g = lane >> 4, gi = lane & 15, q4 = gi >> 2, p4 = gi & 3;
+  // per (operand tile t, k16 step s): byte offsets of the two 4-row blocks
+  unsigned wo[2][2][2], xo[2][2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int rA = 16 * s + 4 * (g >> 1) + q4;
+      const int cw = (wr * 64 + t * 32 + 16 * (g & 1)) >> 3;
+      const int cx = (wc * 64 + t * 32 + 16 * (g & 1)) >> 3;
+      wo[t][s][0] = lds0 + w256off(rA, cw + (p4 >> 1)) + 8 * (p4 & 1);
+      wo[t][s][1] = lds0 + w256off(rA + 8, cw + (p4 >> 1)) + 8 * (p4 & 1);
+      xo[t][s][0] = lds0 + 2 * IMG + w256off(rA, cx + (p4 >> 1)) + 8 * (p4 & 1);
+      xo[t][s][1] = lds0 + 2 * IMG + w256off(rA + 8, cx + (p4 >> 1)) + 8 * (p4 & 1);
+    }
+
+  if (a < b) {
+    wload(a);
+    xissue(a, 0);
+    wstore(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int buf = 0;
+  for (int64_t rb = a; rb < b; rb += RS) {
+    const bool more = rb + RS < b;
+    if (more) {
+      wload(rb + RS);
+      xissue(rb + RS, buf ^ 1);
+    }
+    const unsigned bo_ = buf * STAGE;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      s16x4 wh[2][2], wl[2][2], xh[2][2], xl[2][2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          wh[t][q] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(wo[t][s][q] + bo_));
+          wl[t][q] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(wo[t][s][q] + bo_ + IMG));
+          xh[t][q] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(xo[t][s][q] + bo_));
+          xl[t][q] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(xo[t][s][q] + bo_ + IMG));
+        }
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti) {
+        const bf16x8 ah = __builtin_bit_cast(bf16x8, __builtin_shufflevector(wh[ti][0], wh[ti][1], 0, 1, 2, 3, 4, 5, 6, 7));
+        const bf16x8 al = __builtin_bit_cast(bf16x8, __builtin_shufflevector(wl[ti][0], wl[ti][1], 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj) {
+          const bf16x8 bh = __builtin_bit_cast(bf16x8, __builtin_shufflevector(xh[tj][0], xh[tj][1], 0, 1, 2, 3, 4, 5, 6, 7));
+          const bf16x8 bl = __builtin_bit_cast(bf16x8, __builtin_shufflevector(xl[tj][0], xl[tj][1], 0, 1, 2, 3, 4, 5, 6, 7));
+          acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[ti][tj], 0, 0, 0);
+          acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[ti][tj], 0, 0, 0);
+          acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[ti][tj], 0, 0, 0);
+        }
+      }
+    }
+    if (more) wstore(buf ^ 1);  // its previous contents were read before the last barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    buf ^= 1;
+  }
+  // ---- output: registers = centroids (i&3)+8(i>>2)+4h, lanes = features
+  const int r = lane & 31, h = lane >> 5;
+  float* slab = part + split * (int64_t)Kp * DP;
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int k = k0 + wr * 64 + ti * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        const int d = d0 + wc * 64 + tj * 32 + r;
+        slab[(int64_t)k * DP + d] = acc[ti][tj][i];
+      }
+  if (dt == 0) {  // column sums of W: the 32 threads of one centroid group meet in LDS
+    float* red = reinterpret_cast<float*>(smem);  // idle after the last barrier
+#pragma unroll
+    for (int e = 0; e < 16; ++e) red[wrow * WT + wcol + e] = wsum[e];
+    __syncthreads();
+    if (tid < WT) {
+      float sacc = 0.f;
+      for (int q = 0; q < RS; ++q) sacc += red[q * WT + tid];
+      part_ws[split * (int64_t)Kp + k0 + tid] = sacc;
+    }
+  }
+}
+
 }  // namespace
 }  // namespace tdc
 
@@ -691,6 +1039,60 @@ int tdc_fcm_split_rows(const float* src, int64_t rows, int64_t valid, int d, int
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(split_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, rows, valid,
                      d, ld, DP, neg2, shift, (__bf16*)hi, (__bf16*)lo, norm);
+  TDC_CHECK_LAUNCH();
+  return 0;
+}
+
+// wide-D row-chunk passes (see fcm_wide_dist_kernel): geometry of the W^T X partial slabs
+static void wide_wtx_geometry(int64_t M, int Kp, int DP, int num_cus, int* nkt, int* ndt,
+                              int64_t* splits, int64_t* rps) {
+  *nkt = Kp / WT;
+  *ndt = DP / WT;
+  const int64_t tiles = (M + 31) / 32;
+  const int64_t items = (int64_t)(*nkt) * (*ndt);
+  int64_t sp = ((int64_t)num_cus * 2 + items - 1) / items;
+  if (sp > tiles) sp = tiles;
+  if (sp < 1) sp = 1;
+  *rps = ((tiles + sp - 1) / sp) * 32;
+  *splits = (M + *rps - 1) / *rps;
+}
+
+int64_t tdc_fcm_mfma_wide_workspace(int64_t M, int Kp, int DP, int num_cus) {
+  int nkt, ndt;
+  int64_t splits, rps;
+  wide_wtx_geometry(M, Kp, DP, num_cus, &nkt, &ndt, &splits, &rps);
+  return splits * (int64_t)Kp * (DP + 1);
+}
+
+int tdc_fcm_mfma_wide(int pass, const void* Xh, const void* Xl, const float* xx, int64_t M,
+                      int DP, int D, const void* Ch, const void* Cl, const float* cc, int K,
+                      int Kp, float* G, float* work, const float* shift, double* wx, double* ws,
+                      int num_cus, hipStream_t s) {
+  if (M <= 0 || K <= 0) return 0;
+  if (DP % WT != 0 || DP < WT || DP > 1024 || Kp % WT != 0 || Kp < K || D > DP)
+    return (int)hipErrorInvalidValue;
+  if (pass == 0) {
+    const int nct = Kp / WT;
+    const int64_t nb = ((M + WT - 1) / WT) * nct;
+    hipLaunchKernelGGL(fcm_wide_dist_kernel, dim3((unsigned)nb), dim3(256), 0, s,
+                       (const __bf16*)Xh, (const __bf16*)Xl, xx, M, DP, (const __bf16*)Ch,
+                       (const __bf16*)Cl, cc, K, nct, G);
+    TDC_CHECK_LAUNCH();
+    return 0;
+  }
+  if (pass != 2) return (int)hipErrorInvalidValue;
+  int nkt, ndt;
+  int64_t splits, rps;
+  wide_wtx_geometry(M, Kp, DP, num_cus, &nkt, &ndt, &splits, &rps);
+  float* part_ws = work + splits * (int64_t)Kp * DP;
+  const int64_t nb = splits * nkt * ndt;
+  hipLaunchKernelGGL(fcm_wide_wtx_kernel, dim3((unsigned)nb), dim3(256), 0, s, (const float*)G,
+                     (const __bf16*)Xh, (const __bf16*)Xl, M, DP, K, Kp, nkt, ndt, rps, work,
+                     part_ws);
+  TDC_CHECK_LAUNCH();
+  const int64_t tot = (int64_t)K * DP + K;
+  hipLaunchKernelGGL(fcm_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, work,
+                     part_ws, splits, K, Kp, DP, D, shift, wx, ws);
   TDC_CHECK_LAUNCH();
   return 0;
 }

@@ -122,6 +122,17 @@ int tdc_fcm_mfma(int pass, const void* Xh, const void* Xl, const float* xx, int6
                  int nan_to_zero, int32_t* labels, float* rowinfo, double* wx, double* ws,
                  float* work, const float* shift, int num_cus, hipStream_t stream);
 int64_t tdc_fcm_mfma_workspace(int64_t N, int K, int Kp, int DP, int num_cus);
+// Wide D (DP in 128 ... 1024, multiples of 128), over a chunk of M rows with the [M, K]
+// block G (fp32): pass 0: G = d2 (hi/lo MFMA, distances within 2^-16 ||x||^2 of a centroid
+// stored as 0, the on-centroid rule of tdc_fcm_wide pass 1, which then turns G into w);
+// pass 2: wx [K, D] / ws [K] (fp64) += W^T X / sum W through per-split slabs in work (fp32
+// [tdc_fcm_mfma_wide_workspace]); shift as tdc_fcm_mfma.  Xh/Xl/Ch/Cl/cc as tdc_fcm_mfma
+// with Kp % 128 == 0.
+int tdc_fcm_mfma_wide(int pass, const void* Xh, const void* Xl, const float* xx, int64_t M,
+                      int DP, int D, const void* Ch, const void* Cl, const float* cc, int K,
+                      int Kp, float* G, float* work, const float* shift, double* wx, double* ws,
+                      int num_cus, hipStream_t stream);
+int64_t tdc_fcm_mfma_wide_workspace(int64_t M, int Kp, int DP, int num_cus);
 
 // N3  finalize: C = sums/counts (empty policy), max shift^2 -> shift (float, atomic max),
 // optional bf16 prep of the next assignment (Cm2 [Kp, DP] = -2*bf16(c), cnorm [Kp]).

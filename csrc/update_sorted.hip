@@ -317,6 +317,8 @@ template <typename XT> struct RowLoad1 {
 
 // perm entries of a delta update carry the sign in bit 31 (row numbers are < 2^31)
 constexpr unsigned PERM_NEG = 0x80000000u;
+// segment offsets staged in LDS by the segsum kernel up to this many entries (32 KiB)
+constexpr int SEG_LDS_OFF_MAX = 8193;
 
 // each wave: rows [a, b) of the sorted permutation; TPR lanes per row, G = 64/TPR rows
 // in flight per wave-instruction, columns [c0, c0 + TPR*VEC) per pass.
@@ -349,19 +351,30 @@ __global__ __launch_bounds__(256) void segsum_kernel(const XT* __restrict__ X, i
     if (rows_per_wave < 64) rows_per_wave = 64;
   }
   const int64_t a = wave * rows_per_wave;
+  if ((int64_t)blockIdx.x * 4 * rows_per_wave >= N) return;  // block-uniform: nothing to sum
+  // The segment offsets (just written by the scan, mostly in another XCD's L2) go to LDS
+  // with one coalesced read per block: the binary search below and every segment change
+  // were chains of dependent global loads per wave (a 39 us delta step at ~50K entries).
+  extern __shared__ int s_off[];
+  const bool lds_off = K + 1 <= SEG_LDS_OFF_MAX;  // the launch sizes the dynamic LDS to match
+  if (lds_off) {
+    for (int i = threadIdx.x; i <= K; i += blockDim.x) s_off[i] = offsets[i];
+    __syncthreads();
+  }
+  const int* __restrict__ off = lds_off ? s_off : offsets;
   if (a >= N) return;
   const int64_t b = min(N, a + rows_per_wave);
   // segment containing a: largest k with offsets[k] <= a
   int lo = 0, hi = K;  // invariant offsets[lo] <= a < offsets[hi]
   while (hi - lo > 1) {
     const int mid = (lo + hi) >> 1;
-    if (offsets[mid] <= a) lo = mid; else hi = mid;
+    if (off[mid] <= a) lo = mid; else hi = mid;
   }
   for (int c0 = 0; c0 < D; c0 += TPR * VEC) {
     const int col = c0 + t * VEC;
     const bool colok = col < D;
     int k = lo;
-    int64_t kend = offsets[k + 1];
+    int64_t kend = off[k + 1];
     AT acc[VEC];
 #pragma unroll
     for (int e = 0; e < VEC; ++e) acc[e] = 0;
@@ -384,7 +397,7 @@ __global__ __launch_bounds__(256) void segsum_kernel(const XT* __restrict__ X, i
       // same-address conflict inside each atomic instruction.
       typedef typename RowRaw<XT, VEC>::raw_t raw_t;
       int64_t p = a;
-      int64_t knext = k + 1 < K ? offsets[k + 2] : N;
+      int64_t knext = k + 1 < K ? off[k + 2] : N;
       int64_t pe = min(min(b, kend), p + U * G);
       int32_t nidx[U];
 #pragma unroll
@@ -410,7 +423,7 @@ __global__ __launch_bounds__(256) void segsum_kernel(const XT* __restrict__ X, i
           do {  // next non-empty segment (the boundary after it is prefetched)
             ++kn;
             kendn = knextn;
-            knextn = kn + 1 < K ? offsets[kn + 2] : N;
+            knextn = kn + 1 < K ? off[kn + 2] : N;
           } while (kendn <= pe && kn + 1 < K);
         }
         const int64_t pn = pe;
@@ -473,7 +486,7 @@ __global__ __launch_bounds__(256) void segsum_kernel(const XT* __restrict__ X, i
           while (j >= kend) {
             TDC_FLUSH(k);
             ++k;
-            kend = offsets[k + 1];
+            kend = off[k + 1];
           }
           const int32_t idx = perm[j];
           if (colok) {
@@ -700,6 +713,7 @@ int launch_segsum(const void* X, int64_t ldx, int D, const int32_t* perm, const 
                   const int* nptr, double fixed_scale) {
   const int lanes_needed = (D + VEC - 1) / VEC;
   (void)num_cus;
+  const size_t lds = K + 1 <= SEG_LDS_OFF_MAX ? sizeof(int) * (size_t)(K + 1) : 0;
   // every wave gets the same row count, so the grid is exactly the waves resident at once
   // (8 blocks per CU asked for 8 waves per SIMD where the kernel fits 5: a second, partial
   // round of blocks).  With nptr (entry count on the device, at most N) the grid is sized
@@ -712,7 +726,7 @@ int launch_segsum(const void* X, int64_t ldx, int D, const int32_t* perm, const 
     if (rpw < 64) rpw = 64; /* small N (mini-batches, moved rows) */                        \
     waves = (N + rpw - 1) / rpw;                                                            \
     const dim3 grid((unsigned)((waves + 3) / 4));                                           \
-    hipLaunchKernelGGL((segsum_kernel<XT, ACC, VEC, TPRV, SIGNED>), grid, dim3(256), 0, s,  \
+    hipLaunchKernelGGL((segsum_kernel<XT, ACC, VEC, TPRV, SIGNED>), grid, dim3(256), lds, s, \
                        (const XT*)X, ldx, D, perm, offsets, K, N, (ACC*)sums, rpw, nptr,    \
                        fixed_scale);                                                        \
   } while (0)

@@ -265,7 +265,7 @@ class LloydEngine(OomGuard):
         # delta update: only the rows whose label changed move between fp64 running totals
         self.delta = None
         if (cfg.update != "full" and self.delta_ok and not self.streamed and not self.rsag
-                and cfg.empty_cluster in ("keep", "nan", "zero") and not cfg.deterministic):
+                and cfg.empty_cluster in ("keep", "nan", "zero")):
             self.delta = self.local.make_delta(self.n_local, k, self.d, cfg.delta_refresh,
                                                cfg.delta_theta, cfg.empty_cluster)
         W = comm.world_size
@@ -393,7 +393,7 @@ class LloydEngine(OomGuard):
         if self.cfg.update == "delta" and self.delta is None:
             raise ValueError("update='delta' needs a resident shard on every rank, a sorted/LDS "
                              "native update or the torch ops, K <= 8192, empty_cluster in "
-                             "keep/nan/zero and no deterministic / rsag / bounded mode")
+                             "keep/nan/zero and no rsag / bounded mode")
 
     def _agree_fixed_scale(self):
         """Deterministic update: the fixed-point scale 2^S of the int64 partials, from the

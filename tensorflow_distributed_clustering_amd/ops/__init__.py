@@ -1024,12 +1024,16 @@ class HipMfmaFCM(_LocalOpsBase):
     normaliser + label) and an accumulate pass (distances -> w -> W^T X, all on MFMA)."""
     name = "hip_fcm_mfma"
 
+    @staticmethod
+    def _pick_dp(d: int) -> Optional[int]:
+        return fcm_mfma_dim(d)
+
     def __init__(self, x, k, m=2.0, nan_to_zero=True):
         super().__init__(x, k, "keep")
         self.ops = _native.require()
-        self.dp = fcm_mfma_dim(self.d)
+        self.dp = self._pick_dp(self.d)
         if self.dp is None:
-            raise ValueError(f"MFMA FCM supports D <= {FCM_MFMA_DIMS[-1]}, got {self.d}")
+            raise ValueError(f"{type(self).__name__} does not support D = {self.d}")
         self.c_dtype = torch.float32
         self.m = float(m)
         self.nan_to_zero = bool(nan_to_zero)
@@ -1113,6 +1117,70 @@ class HipMfmaFCM(_LocalOpsBase):
         self.ops.finalize(sums, counts, C, 0, shift, None, None)
 
 
+FCM_MFMA_WIDE_MAX_D = 1024
+
+
+def fcm_mfma_wide_dim(d: int) -> Optional[int]:
+    """Padded width (a multiple of 128) of the wide MFMA FCM path, 128 < D <= 1024."""
+    if d <= FCM_MFMA_DIMS[-1] or d > FCM_MFMA_WIDE_MAX_D:
+        return None
+    return -(-d // 128) * 128
+
+
+class HipMfmaWideFCM(HipMfmaFCM):
+    """fp32 FCM for 128 < D <= 1024 on bf16 matrix cores (csrc/fcm_mfma.hip wide_*): the
+    tower's hi/lo operands no longer fit a wave's registers, so each row chunk runs
+    three native kernels with its [rows, K] block G in HBM, like HipWideFCM, but with both
+    products on MFMA: distances (xh ch + xh cl + xl ch) into G, memberships w = u^m in
+    place (the wide tower's row pass), then W^T X from G and the hi/lo rows (W split into
+    hi/lo bf16 on its way through LDS) into per-split slabs reduced in fp64."""
+    name = "hip_fcm_mfma"
+    chunk_elems = 1 << 27
+    max_chunk_rows = 1 << 20  # keeps every per-split X offset of the W^T X pass in 32 bits
+
+    @staticmethod
+    def _pick_dp(d: int) -> Optional[int]:
+        return fcm_mfma_wide_dim(d)
+
+    def __init__(self, x, k, m=2.0, nan_to_zero=True):
+        self.G = None
+        self._wwork = None
+        super().__init__(x, k, m, nan_to_zero)
+
+    def _block(self):
+        rows = max(1, min(self.n, self.chunk_elems // max(1, self.k), self.max_chunk_rows))
+        if self.G is None or self.G.shape[0] < rows:
+            self.G = torch.empty(rows, self.k, dtype=torch.float32, device=self.device)
+        need = int(self.ops.fcm_mfma_wide_workspace(self.cc, rows, self.kp, self.dp))
+        if self._wwork is None or self._wwork.numel() < need:
+            self._wwork = torch.empty(need, dtype=torch.float32, device=self.device)
+        return rows
+
+    def _chunks(self):
+        rows = self._block()
+        for s in range(0, self.n, rows):
+            e = min(self.n, s + rows)
+            yield s, e, self.G[: e - s]
+
+    def step(self, C, labels, wx, ws):
+        self.prepare(C)
+        k, d = self.k, self.d
+        for s, e, g in self._chunks():
+            xh, xl, xx = self.xh[s:e], self.xl[s:e], self.xx[s:e]
+            self.ops.fcm_mfma_wide(0, xh, xl, xx, self.ch, self.cl, self.cc, k, d, g)
+            self.ops.fcm_wide_rows(g, k, self.m, self.nan_to_zero, labels[s:e], True)
+            self.ops.fcm_mfma_wide(2, xh, xl, xx, self.ch, self.cl, self.cc, k, d, g,
+                                   self._wwork, self.mu, wx, ws)
+
+    def assign(self, C, labels):
+        self.prepare(C)
+        k, d = self.k, self.d
+        for s, e, g in self._chunks():
+            self.ops.fcm_mfma_wide(0, self.xh[s:e], self.xl[s:e], self.xx[s:e], self.ch, self.cl,
+                                   self.cc, k, d, g)
+            self.ops.fcm_wide_rows(g, k, self.m, self.nan_to_zero, labels[s:e], False)
+
+
 class HipWideFCM(_LocalOpsBase):
     """FCM for any D in fp32 / fp64 (csrc/fcm_wide.hip): exact difference-form distances of a
     row chunk into the [rows, K] block G (the only intermediate, up to ``chunk_elems``
@@ -1171,8 +1239,11 @@ def make_fcm_ops(x: torch.Tensor, k: int, dtype: str = "fp64", m: float = 2.0,
     tdt = torch.float64 if dtype == "fp64" else torch.float32
     if _native.require().fcm_small_supported(tdt, k, d):
         return HipSmallFCM(x, k, dtype, m, nan_to_zero)
-    if dtype == "fp32" and d > 16 and k >= FCM_MFMA_MIN_K and fcm_mfma_dim(d) is not None:
-        return HipMfmaFCM(x, k, m, nan_to_zero)
+    if dtype == "fp32" and d > 16 and k >= FCM_MFMA_MIN_K:
+        if fcm_mfma_dim(d) is not None:
+            return HipMfmaFCM(x, k, m, nan_to_zero)
+        if fcm_mfma_wide_dim(d) is not None:
+            return HipMfmaWideFCM(x, k, m, nan_to_zero)
     if d <= 256:
         return HipTowerFCM(x, k, dtype, m, nan_to_zero)
     return HipWideFCM(x, k, dtype, m, nan_to_zero)

@@ -69,7 +69,10 @@ def test_deterministic_fit_bitwise_reproducible(gpu, update):
     assert np.array_equal(a.centers, b.centers)
     assert torch.equal(a.labels, b.labels)
     f = tdc.KMeans(cfg.replace(deterministic=False), device=gpu).fit(x).result_
-    np.testing.assert_allclose(a.centers, f.centers, rtol=1e-5, atol=1e-5)
+    # the float update's sums differ in the last bits; a bf16 near tie that flips one row
+    # moves its two centroids by ~|x - c| / count, so compare per centroid
+    ok = np.isclose(a.centers, f.centers, rtol=1e-5, atol=1e-5).all(1)
+    assert ok.mean() >= 0.99, ok.mean()
     assert (a.labels == f.labels).float().mean().item() > 0.999
 
 

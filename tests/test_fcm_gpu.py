@@ -80,6 +80,29 @@ def test_fcm_mfma_matches_oracle(gpu, k, d, m, nz):
     assert torch.equal(lab, lab2)
 
 
+@pytest.mark.parametrize("k,d", [(33, 256), (257, 384), (1024, 768), (100, 1024), (64, 200)])
+@pytest.mark.parametrize("m", [2.0, 1.5, 3.0])
+@pytest.mark.parametrize("nz", [True, False])
+def test_fcm_mfma_wide_matches_oracle(gpu, k, d, m, nz):
+    """fp32, 128 < D <= 1024 on the matrix cores (distance GEMM into the row block, the
+    row pass, W^T X GEMM), over several chunks with a ragged tail, against the fp64 oracle
+    with the register MFMA tower's tolerances."""
+    from tensorflow_distributed_clustering_amd.ops import HipMfmaWideFCM
+    n = 9001
+    x, c = _data(n, k, d, 5 * k + d)
+    xg, cg = x.float().to(gpu), c.float().to(gpu)
+    ops = HipMfmaWideFCM(xg, k, m, nz)
+    ops.chunk_elems = 4000 * k
+    lab = torch.empty(n, dtype=torch.int32, device=gpu)
+    wx = torch.zeros(k, d, dtype=torch.float64, device=gpu)
+    ws = torch.zeros(k, dtype=torch.float64, device=gpu)
+    ops.step(cg, lab, wx, ws)
+    _check(wx.cpu(), ws.cpu(), lab, xg.cpu(), cg.cpu(), m, nz, 2e-3 * m, 0.998)
+    lab2 = torch.full_like(lab, -1)
+    ops.assign(cg, lab2)
+    assert torch.equal(lab, lab2)
+
+
 @pytest.mark.parametrize("k,d,m", [(32, 20, 8.0), (64, 24, 12.0), (48, 33, 10.0)])
 @pytest.mark.parametrize("nz", [True, False])
 def test_fcm_mfma_large_fuzzifier(gpu, k, d, m, nz):
@@ -125,21 +148,24 @@ def test_fcm_wide_matches_oracle(gpu, dt, k, d, nz):
     """D > 256 (past the register towers): the native wide tower -- exact difference-form
     distances of a row chunk into [rows, K], memberships in place, W^T X -- against the fp64
     oracle, over several chunks with a ragged tail (a point exactly on a centroid included)."""
-    from tensorflow_distributed_clustering_amd.ops import HipWideFCM, make_fcm_ops
+    from tensorflow_distributed_clustering_amd.ops import (HipMfmaWideFCM, HipWideFCM,
+                                                            make_fcm_ops)
     n = 6001
     m = 2.0 if d != 300 else 3.0
     x, c = _data(n, k, d, k * 3 + d)
     xg, cg = x.to(dt).to(gpu), c.to(dt).to(gpu)
     ops = make_fcm_ops(xg, k, "fp64" if dt == torch.float64 else "fp32", m, nz)
-    assert isinstance(ops, HipWideFCM)
+    # fp64: the exact SIMT wide tower; fp32 (K >= 32): the wide MFMA path
+    assert isinstance(ops, HipWideFCM if dt == torch.float64 else HipMfmaWideFCM)
     ops.chunk_elems = 2500 * k  # 3 chunks, the last ragged
     lab = torch.empty(n, dtype=torch.int32, device=gpu)
     wx = torch.zeros(k, d, dtype=torch.float64, device=gpu)
     ws = torch.zeros(k, dtype=torch.float64, device=gpu)
     ops.step(cg, lab, wx, ws)
-    rtol = 1e-9 if dt == torch.float64 else 2e-4 * m
-    _check(wx.cpu(), ws.cpu(), lab, xg.cpu(), cg.cpu(), m, nz, rtol,
-           0.99999 if dt == torch.float64 else 0.999)
+    if dt == torch.float64:
+        _check(wx.cpu(), ws.cpu(), lab, xg.cpu(), cg.cpu(), m, nz, 1e-9, 0.99999)
+    else:  # bf16x3 distances, as the register MFMA tower
+        _check(wx.cpu(), ws.cpu(), lab, xg.cpu(), cg.cpu(), m, nz, 2e-3 * m, 0.998)
     lab2 = torch.full_like(lab, -1)
     ops.assign(cg, lab2)
     assert torch.equal(lab, lab2)
@@ -158,7 +184,8 @@ def test_fcm_dispatch_native_up_to_1024(gpu):
 @pytest.mark.parametrize("dtype,d,k,backend", [("fp64", 5, 32, "hip_fcm_small"),
                                                ("fp64", 5, 40, "hip_fcm_small"),
                                                ("fp64", 384, 50, "hip_fcm_wide"),
-                                               ("fp32", 512, 64, "hip_fcm_wide"),
+                                               ("fp32", 512, 64, "hip_fcm_mfma"),
+                                               ("fp32", 768, 40, "hip_fcm_mfma"),
                                                ("fp64", 6, 40, "hip_fcm_tower"),
                                                ("fp64", 64, 100, "hip_fcm_tower"),
                                                ("fp32", 12, 64, "hip_fcm_tower"),
