@@ -192,7 +192,8 @@ void check_fixed(const at::Tensor& sums, double fixed_scale, const char* op) {
 void update_sorted(const at::Tensor& X, const at::Tensor& labels, at::Tensor& sums,
                    at::Tensor& counts, at::Tensor& work, const std::optional<at::Tensor>& cnt_hi,
                    const std::optional<at::Tensor>& cnt_lo,
-                   const std::optional<at::Tensor>& zero_first, double fixed_scale) {
+                   const std::optional<at::Tensor>& zero_first, double fixed_scale,
+                   bool work_clean) {
   check_fixed(sums, fixed_scale, "update_sorted");
   check_cuda(X, "X");
   check_rows(X, "X");
@@ -220,7 +221,7 @@ void update_sorted(const at::Tensor& X, const at::Tensor& labels, at::Tensor& su
                           work.data_ptr<int>(), num_cus(X.device().index()), cur_stream(),
                           nullptr, static_cast<float*>(opt_ptr(cnt_hi)),
                           static_cast<float*>(opt_ptr(cnt_lo)), opt_ptr(zero_first), zbytes,
-                          fixed_scale),
+                          fixed_scale, work_clean ? 1 : 0),
         "update_sorted");
 }
 
@@ -590,7 +591,7 @@ void assign_bf16_indexed(const at::Tensor& X, const at::Tensor& rowidx, const at
 void update_sorted_indexed(const at::Tensor& X, const at::Tensor& rowidx, const at::Tensor& labels,
                            at::Tensor& sums, at::Tensor& counts, at::Tensor& work,
                            const std::optional<at::Tensor>& cnt_hi,
-                           const std::optional<at::Tensor>& cnt_lo) {
+                           const std::optional<at::Tensor>& cnt_lo, bool work_clean) {
   check_cuda(X, "X");
   check_rows(X, "X");
   const int64_t B = labels.numel();
@@ -612,7 +613,8 @@ void update_sorted_indexed(const at::Tensor& X, const at::Tensor& rowidx, const 
                           (int)sums.size(0), sums.data_ptr(), counts.data_ptr(),
                           work.data_ptr<int>(), num_cus(X.device().index()), cur_stream(),
                           rowidx.data_ptr<int32_t>(), static_cast<float*>(opt_ptr(cnt_hi)),
-                          static_cast<float*>(opt_ptr(cnt_lo))),
+                          static_cast<float*>(opt_ptr(cnt_lo)), nullptr, 0, 0.0,
+                          work_clean ? 1 : 0),
         "update_sorted_indexed");
 }
 
@@ -629,7 +631,7 @@ void delta_update(const at::Tensor& X, const at::Tensor& labels, at::Tensor& pre
                   at::Tensor& counts, at::Tensor& work, at::Tensor& ctrl,
                   const std::optional<at::Tensor>& cnt_hi, const std::optional<at::Tensor>& cnt_lo,
                   const std::optional<at::Tensor>& moved, const std::optional<at::Tensor>& zero_first,
-                  double fixed_scale) {
+                  double fixed_scale, bool work_clean) {
   check_cuda(X, "X");
   check_fixed(sums, fixed_scale, "delta_update");
   check_rows(X, "X");
@@ -668,7 +670,7 @@ void delta_update(const at::Tensor& X, const at::Tensor& labels, at::Tensor& pre
                          work.data_ptr<int>(), ctrl.data_ptr<int>(), num_cus(X.device().index()),
                          cur_stream(), static_cast<float*>(opt_ptr(cnt_hi)),
                          static_cast<float*>(opt_ptr(cnt_lo)), opt_ptr(moved), opt_ptr(zero_first),
-                         zbytes, fixed_scale),
+                         zbytes, fixed_scale, work_clean ? 1 : 0),
         "delta_update");
 }
 
@@ -982,7 +984,7 @@ TORCH_LIBRARY(tdc, m) {
   m.def("lloyd_small(Tensor X, Tensor C, Tensor(a!)? labels, Tensor(b!)? mind, Tensor(c!) sums, Tensor(d!) counts) -> ()");
   m.def("update(Tensor X, Tensor labels, Tensor(a!) sums, Tensor(b!) counts) -> ()");
   m.def("update_sorted_workspace(int N, int K) -> int", &update_sorted_workspace);
-  m.def("update_sorted(Tensor X, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work, Tensor(d!)? cnt_hi=None, Tensor(e!)? cnt_lo=None, Tensor(f!)? zero_first=None, float fixed_scale=0.0) -> ()");
+  m.def("update_sorted(Tensor X, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work, Tensor(d!)? cnt_hi=None, Tensor(e!)? cnt_lo=None, Tensor(f!)? zero_first=None, float fixed_scale=0.0, bool work_clean=False) -> ()");
   m.def("fcm_small_supported(ScalarType dtype, int K, int D) -> bool", &fcm_small_supported);
   m.def("fcm_small(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!)? labels, Tensor(b!) wx, Tensor(c!) ws) -> ()");
   m.def("fcm_tower_stats(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) rowinfo) -> ()");
@@ -1002,12 +1004,12 @@ TORCH_LIBRARY(tdc, m) {
   m.def("kpp_step(Tensor X, Tensor cand, Tensor(a!) closest, int mode, Tensor(b!) pots) -> ()");
   m.def("finalize(Tensor? sums, Tensor? counts, Tensor(a!) C, int policy, Tensor(b!)? shift, Tensor(c!)? Cm2, Tensor(d!)? cnorm, Tensor(e!)? drift=None, Tensor(f!)? maxdrift=None, float fixed_scale=0.0) -> ()");
   m.def("assign_bf16_indexed(Tensor X, Tensor rowidx, Tensor Cm2, Tensor cnorm, Tensor(a!) labels, Tensor(b!)? mind) -> ()");
-  m.def("update_sorted_indexed(Tensor X, Tensor rowidx, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work, Tensor(d!)? cnt_hi=None, Tensor(e!)? cnt_lo=None) -> ()");
+  m.def("update_sorted_indexed(Tensor X, Tensor rowidx, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work, Tensor(d!)? cnt_hi=None, Tensor(e!)? cnt_lo=None, bool work_clean=False) -> ()");
   m.def("assign_bf16_top2(Tensor X, Tensor? rowidx, Tensor Cm2, Tensor cnorm, Tensor(a!) labels, Tensor(b!) mind, Tensor(c!) mind2) -> ()");
   m.def("bounds_filter(Tensor labels, Tensor(a!) ub, Tensor(b!) lb, Tensor drift, Tensor maxdrift, float slack, Tensor(c!) active, Tensor(d!) count) -> ()");
   m.def("bounds_scatter(Tensor active, Tensor count, Tensor blab, Tensor d1, Tensor d2, Tensor(a!) labels, Tensor(b!) ub, Tensor(c!) lb, Tensor(d!) moved_idx, Tensor(e!) moved_old, Tensor(f!) moved_new, Tensor(g!) mcount) -> ()");
   m.def("delta_workspace(int N, int K) -> int", &delta_workspace);
-  m.def("delta_update(Tensor X, Tensor labels, Tensor(a!) prev, Tensor(b!) sums, Tensor(c!) counts, Tensor(d!) work, Tensor(e!) ctrl, Tensor(f!)? cnt_hi=None, Tensor(g!)? cnt_lo=None, Tensor(h!)? moved=None, Tensor(i!)? zero_first=None, float fixed_scale=0.0) -> ()");
+  m.def("delta_update(Tensor X, Tensor labels, Tensor(a!) prev, Tensor(b!) sums, Tensor(c!) counts, Tensor(d!) work, Tensor(e!) ctrl, Tensor(f!)? cnt_hi=None, Tensor(g!)? cnt_lo=None, Tensor(h!)? moved=None, Tensor(i!)? zero_first=None, float fixed_scale=0.0, bool work_clean=False) -> ()");
   m.def("delta_finalize(Tensor sums, Tensor counts, Tensor? cnt_hi, Tensor? cnt_lo, Tensor? moved, Tensor(a!) G, Tensor(b!) C, int policy, Tensor(c!)? shift, Tensor(d!)? Cm2, Tensor(e!)? cnorm, Tensor(f!) ctrl, Tensor(g!)? stats, int refresh, float theta_n, float fixed_scale=0.0) -> ()");
   m.def("sculley_update(Tensor sums, Tensor counts, Tensor(a!) C, Tensor(b!) v, Tensor(c!)? shift, Tensor(d!)? Cm2, Tensor(e!)? cnorm) -> ()");
 }

@@ -65,8 +65,9 @@ int tdc_update_lds(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t
                    hipStream_t stream);
 
 // N2 (large K x D): counting sort by label + segmented row gather-sum.  work: int32
-// workspace of tdc_update_sorted_workspace(N, K) elements, ZERO-FILLED when allocated (its
-// histogram part is left zeroed by every call).  sums/counts are accumulated (caller
+// workspace of tdc_update_sorted_workspace(N, K) elements.  Its histogram part must be zero
+// on entry: work_clean != 0 says it is (a workspace zero-filled when allocated and only
+// used by these calls, which leave it zeroed); work_clean == 0 clears it first.  sums/counts are accumulated (caller
 // zeroes them once per pass); zero_first (nullable, zero_bytes a multiple of 4) is cleared
 // by the first kernel before anything accumulates -- the caller's zero fill of the
 // all-reduce buffer without a launch of its own.
@@ -80,7 +81,7 @@ int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int6
                       int num_cus, hipStream_t stream, const int32_t* rowidx = nullptr,
                       float* cnt_hi = nullptr, float* cnt_lo = nullptr,
                       void* zero_first = nullptr, int64_t zero_bytes = 0,
-                      double fixed_scale = 0.0);
+                      double fixed_scale = 0.0, int work_clean = 0);
 int64_t tdc_update_sorted_workspace(int64_t N, int K);
 
 // N4/N5  fused small-K Fuzzy C-Means tower: sum_i w_ki x_i, sum_i w_ki, argmax labels.
@@ -203,13 +204,14 @@ constexpr int TDC_DELTA_MAX_BLOCKS = 1024;  // per-block moved-list slots in the
 // assignment) vs prev (the previous one; prev = labels on return) -> sums / counts (the
 // step's all-reduce buffer views: deltas of the moved rows, or full partials), the exact
 // count split as tdc_update_sorted (signed), moved (nullable, acc dtype [1]) += rows that
-// changed label.  work: int32 [tdc_delta_workspace(N, K)], zero-filled once.  K <=
-// TDC_DELTA_MAX_K, N < 2^30.
+// changed label.  work: int32 [tdc_delta_workspace(N, K)]; work_clean as
+// tdc_update_sorted (its two histograms zero on entry, left zero).  K <= TDC_DELTA_MAX_K,
+// N < 2^30.
 int tdc_delta_update(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
                      const int32_t* labels, int32_t* prev, int K, void* sums, void* counts,
                      int* work, int* ctrl, int num_cus, hipStream_t stream, float* cnt_hi,
                      float* cnt_lo, void* moved, void* zero_first, int64_t zero_bytes,
-                     double fixed_scale = 0.0);
+                     double fixed_scale = 0.0, int work_clean = 0);
 int64_t tdc_delta_workspace(int64_t N, int K);
 // The step's finalize: G (fp64 [K*D + K] totals) += or = the all-reduced buffer (by
 // ctrl[MODE]), C = G means (policy as tdc_finalize), optional bf16 operand prep, shift;

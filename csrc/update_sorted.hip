@@ -27,6 +27,22 @@
 namespace tdc {
 
 constexpr int LDS_HIST_MAX_K = 16384;
+constexpr int64_t ZERO_WORDS_PER_BLOCK = 16384;  // 1024 threads x one 16-B store each, x4
+
+// Clear words [0, n) of z with 16-B stores when z is 16-B aligned (a torch allocation or a
+// view at its start), from thread t of T; the caller's grid covers n / ZERO_WORDS_PER_BLOCK
+// blocks at least (the fill no longer runs on the few blocks a small row range needs).
+__device__ __forceinline__ void zero_fill(uint32_t* __restrict__ z, int64_t n, int64_t t,
+                                          int64_t T) {
+  int64_t done = 0;
+  if (((uintptr_t)z & 15) == 0) {
+    uint4* z4 = reinterpret_cast<uint4*>(z);
+    const int64_t n4 = n >> 2;
+    for (int64_t w = t; w < n4; w += T) z4[w] = make_uint4(0u, 0u, 0u, 0u);
+    done = n4 << 2;
+  }
+  for (int64_t w = done + t; w < n; w += T) z[w] = 0u;
+}
 
 template <int NT>
 __global__ __launch_bounds__(NT) void hist_kernel(const int32_t* __restrict__ labels, int64_t N,
@@ -38,10 +54,10 @@ __global__ __launch_bounds__(NT) void hist_kernel(const int32_t* __restrict__ la
   // the caller's accumulation buffer (the all-reduce buffer of the step), cleared here
   // instead of by a separate fill launch: scan / segsum accumulate into it only after
   // this kernel has finished
-  for (int64_t w = (int64_t)blockIdx.x * NT + tid; w < zero_words; w += (int64_t)gridDim.x * NT)
-    zero[w] = 0u;
+  if (zero_words) zero_fill(zero, zero_words, (int64_t)blockIdx.x * NT + tid, (int64_t)gridDim.x * NT);
   const int64_t r0 = (int64_t)blockIdx.x * per_block;
   const int64_t r1 = min(N, r0 + per_block);
+  if (r0 >= N) return;  // a block of the zero fill only (block-uniform)
   const bool lds = K <= LDS_HIST_MAX_K;
   if (lds) {
     for (int k = tid; k < K; k += NT) s_h[k] = 0;
@@ -535,8 +551,8 @@ __global__ __launch_bounds__(NT) void delta_diff_kernel(
   const int tid = threadIdx.x, lane = tid & 63;
   // the step's all-reduce buffer, cleared before anything accumulates into it (scan and
   // segsum run after this kernel)
-  for (int64_t w = (int64_t)blockIdx.x * NT + tid; w < zero_words; w += (int64_t)gridDim.x * NT)
-    zero[w] = 0u;
+  if (zero_words) zero_fill(zero, zero_words, (int64_t)blockIdx.x * NT + tid, (int64_t)gridDim.x * NT);
+  if ((int64_t)blockIdx.x * per_block >= N) return;  // a block of the zero fill only
   const bool full = ctrl[TDC_DC_NEXT] != 0;
   int* h_ev = s_h;
   int* h_sg = s_h + K;
@@ -769,7 +785,8 @@ int dispatch_segsum(int x_dtype, const void* X, int64_t ldx, int D, const int32_
 int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int64_t ldx, int D,
                       const int32_t* labels, int K, void* sums, void* counts, int* work,
                       int num_cus, hipStream_t s, const int32_t* rowidx, float* cnt_hi,
-                      float* cnt_lo, void* zero_first, int64_t zero_bytes, double fixed_scale) {
+                      float* cnt_lo, void* zero_first, int64_t zero_bytes, double fixed_scale,
+                      int work_clean) {
   if (zero_bytes % 4 != 0 || (zero_bytes > 0 && zero_first == nullptr))
     return (int)hipErrorInvalidValue;
   if (acc_dtype != TDC_F32 && acc_dtype != TDC_F64 && acc_dtype != TDC_I64)
@@ -787,6 +804,8 @@ int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int6
   int* offsets = cnt + K;
   int* cursor = offsets + K + 1;
   int32_t* perm = cursor + K;
+  if (!work_clean && hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)K, s) != hipSuccess)
+    return (int)hipErrorUnknown;
   {
     // one 1024-thread block per CU: a quarter of the global flush atomics of 4 x 256-thread
     // blocks per CU (each block adds its whole LDS histogram into cnt)
@@ -794,6 +813,8 @@ int tdc_update_sorted(int x_dtype, int acc_dtype, const void* X, int64_t N, int6
     int64_t per = (N + blocks - 1) / blocks;
     if (per < 4096) per = 4096;
     blocks = (N + per - 1) / per;
+    // extra blocks for a large zero fill next to a small row range (they only clear)
+    blocks = std::max(blocks, (zero_bytes / 4 + ZERO_WORDS_PER_BLOCK - 1) / ZERO_WORDS_PER_BLOCK);
     const size_t lds = K <= LDS_HIST_MAX_K ? sizeof(int) * (size_t)K : 0;
     hipLaunchKernelGGL(hist_kernel<1024>, dim3((unsigned)blocks), dim3(1024), lds, s, labels, N, K,
                        cnt, per, static_cast<uint32_t*>(zero_first), zero_bytes / 4);
@@ -854,7 +875,7 @@ int tdc_delta_update(int x_dtype, int acc_dtype, const void* X, int64_t N, int64
                      const int32_t* labels, int32_t* prev, int K, void* sums, void* counts,
                      int* work, int* ctrl, int num_cus, hipStream_t s, float* cnt_hi,
                      float* cnt_lo, void* moved, void* zero_first, int64_t zero_bytes,
-                     double fixed_scale) {
+                     double fixed_scale, int work_clean) {
   if (zero_bytes % 4 != 0 || (zero_bytes > 0 && zero_first == nullptr))
     return (int)hipErrorInvalidValue;
   if (acc_dtype == TDC_I64 && !(fixed_scale > 0.0)) return (int)hipErrorInvalidValue;
@@ -872,6 +893,8 @@ int tdc_delta_update(int x_dtype, int acc_dtype, const void* X, int64_t N, int64
   int32_t* lidx = blk_cnt + TDC_DELTA_MAX_BLOCKS;
   uint32_t* lpair = reinterpret_cast<uint32_t*>(lidx + N);
   int32_t* perm = reinterpret_cast<int32_t*>(lpair + N);
+  if (!work_clean && hipMemsetAsync(cnt_ev, 0, 2 * sizeof(int) * (size_t)K, s) != hipSuccess)
+    return (int)hipErrorUnknown;
   // one 1024-thread block per CU over contiguous row ranges (the diff and scatter kernels
   // share this geometry: block b's moved list lives at [b * per, b * per + blk_cnt[b]))
   int64_t blocks = std::max(1, std::min(num_cus, TDC_DELTA_MAX_BLOCKS));
@@ -880,7 +903,9 @@ int tdc_delta_update(int x_dtype, int acc_dtype, const void* X, int64_t N, int64
   blocks = N > 0 ? (N + per - 1) / per : 0;
   const size_t lds = 2 * sizeof(int) * (size_t)K;
   if (blocks > 0) {
-    hipLaunchKernelGGL(delta_diff_kernel<1024>, dim3((unsigned)blocks), dim3(1024), lds, s,
+    const int64_t gblocks =
+        std::max(blocks, (zero_bytes / 4 + ZERO_WORDS_PER_BLOCK - 1) / ZERO_WORDS_PER_BLOCK);
+    hipLaunchKernelGGL(delta_diff_kernel<1024>, dim3((unsigned)gblocks), dim3(1024), lds, s,
                        labels, prev, N, K, ctrl, cnt_ev, cnt_sg, blk_cnt, lidx, lpair, per,
                        static_cast<uint32_t*>(zero_first), zero_bytes / 4);
     TDC_CHECK_LAUNCH();

@@ -60,7 +60,9 @@ class ClusterConfig:
                     greedy k-means++ (K dependent sweeps would take hours at K=65536)
     kpp_sample_per_k greedy k-means++ runs on a uniform world-invariant sample of
                     max(kpp_sample_min, kpp_sample_per_k * K) rows when N is over 4x that
-                    (0: always the full data).  The root rank logs whenever a sample is used.
+                    (0: always the full data -- for a streamed / generated source that
+                    gathers every row onto each device).  The root rank logs whenever a
+                    sample is used.
     update          Lloyd centroid update: 'full' re-sums every row each step; 'delta' keeps
                     fp64 per-cluster totals and each step moves only the rows whose label
                     changed (+x into the new, -x out of the old cluster; same fixed points,

@@ -194,7 +194,7 @@ class PlainHostSource(HostSource):
 
 def plan_chunk_rows(n_rows: int, row_bytes: int, k: int, d: int, device,
                     budget_gb: float = 0.0, reserve_frac: float = 0.15,
-                    per_row_extra: int = 16) -> int:
+                    per_row_extra: int = 16, extra_fixed: int = 0) -> int:
     """Rows of one resident chunk that fit the HBM budget (0 = the whole shard fits).
 
     per_row_extra covers labels (4 B), the counting-sort permutation (4 B) and the
@@ -210,7 +210,7 @@ def plan_chunk_rows(n_rows: int, row_bytes: int, k: int, d: int, device,
     else:
         return 0
     budget *= (1.0 - reserve_frac)
-    fixed = k * d * 16 + (64 << 20)
+    fixed = k * d * 16 + (64 << 20) + int(extra_fixed)
     per_row = row_bytes + per_row_extra
     if n_rows * per_row + fixed <= budget:
         return 0
@@ -220,7 +220,7 @@ def plan_chunk_rows(n_rows: int, row_bytes: int, k: int, d: int, device,
 
 def plan_resident_rows(n_rows: int, row_bytes: int, chunk_rows: int, k: int, d: int, device,
                        budget_gb: float = 0.0, reserve_frac: float = 0.15,
-                       per_row_extra: int = 16) -> int:
+                       per_row_extra: int = 16, extra_fixed: int = 0) -> int:
     """Rows of a streamed shard that can stay resident in HBM next to the streaming
     buffers (2 device slots of chunk_rows) and the per-row work buffers of all rows."""
     device = torch.device(device)
@@ -231,5 +231,6 @@ def plan_resident_rows(n_rows: int, row_bytes: int, chunk_rows: int, k: int, d: 
     else:
         budget, _ = torch.cuda.mem_get_info(device)
     budget *= (1.0 - reserve_frac)
-    fixed = k * d * 16 + (64 << 20) + 2 * chunk_rows * row_bytes + n_rows * per_row_extra
+    fixed = (k * d * 16 + (64 << 20) + 2 * chunk_rows * row_bytes + n_rows * per_row_extra
+             + int(extra_fixed))
     return int(max(0, min(n_rows, (budget - fixed) // row_bytes)))

@@ -216,11 +216,15 @@ class FuzzyCMeans:
             es = 8 if tdt == torch.float64 else 4
             # MFMA tower keeps hi/lo bf16 rows + norms + row info next to the chunk
             row_bytes = d * es + 4 * d + 16
+            # the wide towers (D > 128) hold a [rows, K] block of up to 2^27 elements
+            from ..ops import HipWideFCM
+            g_bytes = HipWideFCM.chunk_elems * es if d > 128 else 0
             chunk = want or plan_chunk_rows(n, row_bytes, cfg.n_clusters, d, dev,
-                                            cfg.hbm_budget_gb)
+                                            cfg.hbm_budget_gb, extra_fixed=g_bytes)
             if chunk:
                 resident = 0 if want else plan_resident_rows(n, row_bytes, chunk, cfg.n_clusters,
-                                                             d, dev, cfg.hbm_budget_gb)
+                                                             d, dev, cfg.hbm_budget_gb,
+                                                             extra_fixed=g_bytes)
                 return HostSource(xn, layout, dev, row_offset, resident_rows=resident), chunk
         elif want:
             return HostSource(xn, layout, dev, row_offset), want

@@ -404,8 +404,9 @@ def init_centers_from_source(method: str, source, row_offset: int, n_global: int
     """Init for streamed / generated shards (rows are gathered from the source).
 
     k-means++ on a source that is not device-resident runs on a uniform random sample of
-    max(50 K, 256 k) rows (replicated), the standard sample-based seeding for data that
-    cannot be swept K times.
+    max(kpp_sample_min, kpp_sample_per_k * k) rows (replicated), the standard sample-based
+    seeding for data that cannot be swept K times.  kpp_sample_per_k = 0 ("always the full
+    data", ClusterConfig) gathers EVERY row onto each device: only for shards that fit.
     """
     if rows is not None:
         return gather_rows_from_source(source, row_offset, rows, comm, d)
@@ -421,7 +422,8 @@ def init_centers_from_source(method: str, source, row_offset: int, n_global: int
     if method == "first_k":
         return gather_rows_from_source(source, row_offset, range(k), comm, d)
     if method in ("kmeans++", "kmeans||"):
-        m = min(n_global, max(kpp_sample_min, (kpp_sample_per_k or KPP_SAMPLE_PER_K) * k))
+        m = n_global if kpp_sample_per_k <= 0 else \
+            min(n_global, max(kpp_sample_min, kpp_sample_per_k * k))
         if m < n_global:
             _note(comm, f"{method} on a streamed shard seeds on a uniform sample of {m} of "
                         f"{n_global} rows")

@@ -167,8 +167,11 @@ class NativeUpdate:
         if self.deterministic and sums.dtype != torch.int64:
             self._fixed_into_float(x, labels, sums, counts)
             return
+        # work_clean: the workspace was zero-filled when allocated and every call leaves
+        # its histogram zeroed (no memset launch per step)
         self.ops.update_sorted(x, labels, sums, counts, self.work, *(self.count_split or (None, None)),
-                               self.zero_buf, self.fixed_scale if sums.dtype == torch.int64 else 0.0)
+                               self.zero_buf, self.fixed_scale if sums.dtype == torch.int64 else 0.0,
+                               True)
 
     def _fixed_into_float(self, x, labels, sums, counts):
         """Deterministic partials for a float buffer: fixed-point into an int64 scratch
@@ -180,7 +183,7 @@ class NativeUpdate:
         n = x.shape[0]
         scale = fixed_point_scale(float(x[:, :d].abs().max()) if n else 0.0, n)
         fs, fc = self._fx[: k * d].view(k, d), self._fx[k * d:]
-        self.ops.update_sorted(x, labels, fs, fc, self.work, None, None, None, scale)
+        self.ops.update_sorted(x, labels, fs, fc, self.work, None, None, None, scale, True)
         sums.add_((fs.double() / scale).to(sums.dtype))
         counts.add_(fc.to(counts.dtype))
         if self.count_split is not None:
@@ -196,7 +199,7 @@ class NativeUpdate:
         if self.work is None or self.work.numel() < need:
             self.work = self._workspace(rowidx.shape[0], sums.shape[0], x.device)
         self.ops.update_sorted_indexed(x, rowidx, labels, sums, counts, self.work,
-                                       *(self.count_split or (None, None)))
+                                       *(self.count_split or (None, None)), True)
 
 
 # ----------------------------------------------------------------- delta update
@@ -267,7 +270,7 @@ class NativeDelta(DeltaState):
         hi, lo = split or (None, None)
         fx = self.fixed_scale if sums.dtype == torch.int64 else 0.0
         self.ops.delta_update(x, labels, self.prev, sums, counts, self.work, self.ctrl, hi, lo,
-                              moved, zero_buf, fx)
+                              moved, zero_buf, fx, True)
 
     def finalize(self, sums, counts, split, moved, C, policy, shift, cm2, cnorm, n_global):
         hi, lo = split or (None, None)
