@@ -130,3 +130,18 @@ def test_num_batches_averages_fits_from_shared_init(data, tmp_path):
     avg = ck.load(path)
     assert avg.method == "batched-average" and avg.meta["num_batches"] == 3
     np.testing.assert_allclose(avg.centers, got, rtol=1e-12)
+
+
+def test_update_mode_flag_same_fit(data, tmp_path):
+    """--update full / delta (the moved-rows update between fp64 totals) and --deterministic
+    reach the same centroids through the CLI."""
+    outs = []
+    for extra in (["--update", "full"], ["--update", "delta"], ["--deterministic"]):
+        cen = str(tmp_path / f"c{len(outs)}.csv")
+        r = run_cli(*base_args(data, str(tmp_path / "log.csv"),
+                               extra=["--device", "cpu", "--dtype", "fp64", "--init", "random",
+                                      "--centroids_out", cen, *extra]))
+        assert r.returncode == 0, r.stderr
+        outs.append(np.loadtxt(cen, delimiter=","))
+    np.testing.assert_allclose(outs[1], outs[0], rtol=1e-10, atol=1e-10)
+    np.testing.assert_allclose(outs[2], outs[0], rtol=1e-10, atol=1e-10)

@@ -166,6 +166,28 @@ def test_update_sorted_zero_first_and_clean_workspace(gpu, n, k):
     torch.testing.assert_close(sums.double(), s_ref, rtol=1e-3, atol=1e-2)
 
 
+def test_update_sorted_large_zero_fill_small_rows_and_dirty_workspace(gpu):
+    """A few rows next to a large all-reduce buffer (the fill gets blocks of its own, 16-B
+    stores, ragged tail), and a workspace with a dirty histogram: work_clean=False (the
+    default) clears it first, so the counts are still right."""
+    from tensorflow_distributed_clustering_amd import _native
+    ops = _native.require()
+    n, k, d = 700, 4096, 256
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(n, d, generator=g).to(torch.bfloat16).to(gpu)
+    lab = torch.randint(0, k, (n,), generator=g, dtype=torch.int32).to(gpu)
+    work = torch.randint(1, 9, (int(ops.update_sorted_workspace(n, k)),), generator=g,
+                         dtype=torch.int32).to(gpu)  # garbage histogram
+    buf = torch.full((k * d + k + 4096 * 1024 + 3,), 5.0, dtype=torch.float32, device=gpu)
+    sums, counts = buf[: k * d].view(k, d), buf[k * d: k * d + k]
+    ops.update_sorted(x, lab, sums, counts, work, None, None, buf)
+    torch.cuda.synchronize()
+    s_ref, c_ref = ref.cluster_sums(x.double(), lab, k, acc_dtype=torch.float64)
+    assert torch.equal(counts.double(), c_ref)
+    assert float(buf[k * d + k:].abs().max()) == 0.0
+    torch.testing.assert_close(sums.double(), s_ref, rtol=1e-3, atol=1e-2)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.float64])
 @pytest.mark.parametrize("k,d", [(3, 5), (6, 5), (9, 5), (12, 5), (15, 5), (16, 5), (8, 2),
                                  (16, 8), (4, 16), (32, 3)])
