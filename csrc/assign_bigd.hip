@@ -30,6 +30,8 @@
 // refill, so the only vmcnt wait per stage is the counted one on the ring.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "kernels.h"
 #include "tdc_common.h"
 
@@ -38,6 +40,7 @@ namespace bigd {
 
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
 constexpr float BIGN = 3.0e38f;
 
 struct OpBf16 {
@@ -228,13 +231,16 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
   float best = INFINITY, best2 = INFINITY;
   int bt = 0, bt2 = 0;
   // one ring stage: the tile, its norms and its scales all arrived by LDS-DMA NST-1
-  // stages ago, so the only vmcnt wait per stage is the counted one on the ring
-  auto stage = [&](int i) __attribute__((always_inline)) {
+  // stages ago, so the only vmcnt wait per stage is the counted one on the ring.  The ring
+  // slot is a compile-time constant (the stage loop below is unrolled by NST): the LDS
+  // addresses of the slot and of the refill destinations fold into immediates instead of a
+  // runtime i % NST and its address arithmetic every stage (~2.7 SALU per MFMA before).
+  auto stage = [&](int i, auto slot_c) __attribute__((always_inline)) {
+    constexpr int slot = decltype(slot_c)::value;
     const int t = t0 + i;
-    const int slot = i % NST;
     if constexpr (!(ABL & 1)) {
       const int in = i + NST - 1;
-      issue(t0 + (in < nt ? in : nt - 1), in % NST);
+      issue(t0 + (in < nt ? in : nt - 1), (slot + NST - 1) % NST);
     }
 #pragma unroll 1
     for (int qh = 0; qh < QH; ++qh) {
@@ -257,10 +263,18 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
     }
     int sa_row[NSW];
     if constexpr (OP::SCALED) {
+      // the row's E8M0 scales as 8-byte reads (rows are SB = D/32 bytes apart: 8-B aligned).
+      // At D=768 the 24-B row pitch made every ds_read_b32 2-way bank-conflicted (lanes r and
+      // r+16); ds_read_b64 over 64 banks is conflict-free there, and half the instructions.
+      static_assert(NSW % 2 == 0, "scale dwords in pairs");
       const unsigned sbase = xbase + NRM_B + (qh * 32 + r) * SB;
 #pragma unroll
-      for (int j = 0; j < NSW; ++j)
-        asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(sa_row[j]) : "v"(sbase), "i"(4 * j));
+      for (int j = 0; j < NSW / 2; ++j) {
+        i32x2 v;
+        asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(sbase), "i"(8 * j));
+        sa_row[2 * j] = v[0];
+        sa_row[2 * j + 1] = v[1];
+      }
     }
     const unsigned qbase = lds_base + slot * STAGE_B + qh * 32 * RB;
     // A fragments via inline-asm ds_read_b128: the compiler cannot prove they do not
@@ -352,7 +366,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * VPS) : "memory");
   __builtin_amdgcn_s_barrier();
 
-  for (int i = 0; i < nt; ++i) stage(i);
+  for (int i = 0; i < nt; i += NST) {
+    stage(i, std::integral_constant<int, 0>{});
+    if constexpr (NST > 1) if (i + 1 < nt) stage(i + 1, std::integral_constant<int, 1 % NST>{});
+    if constexpr (NST > 2) if (i + 2 < nt) stage(i + 2, std::integral_constant<int, 2 % NST>{});
+    if constexpr (NST > 3) if (i + 3 < nt) stage(i + 3, std::integral_constant<int, 3 % NST>{});
+  }
+  static_assert(NST <= 4, "stage loop unrolled up to 4 slots");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   const float ob = __shfl_xor(best, 32, 64);
