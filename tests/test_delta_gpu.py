@@ -22,16 +22,19 @@ def _ops():
 @pytest.mark.parametrize("xdt,acc,split", [(torch.bfloat16, torch.float32, True),
                                            (torch.float32, torch.float64, False),
                                            (torch.float64, torch.float64, False)])
-@pytest.mark.parametrize("n,d,k", [(50_003, 128, 1024), (9000, 37, 100), (70_000, 64, 8192)])
-def test_delta_update_op_vs_torch(gpu, xdt, acc, split, n, d, k):
+@pytest.mark.parametrize("n,d,k,off", [(50_003, 128, 1024, 0), (9000, 37, 100, 0),
+                                       (70_000, 64, 8192, 0), (30_001, 128, 512, 1)])
+def test_delta_update_op_vs_torch(gpu, xdt, acc, split, n, d, k, off):
+    """off = 1: labels / prev are views one element into their buffers (not 16-B aligned:
+    the diff kernel's scalar-load form)."""
     ops = _ops()
     g = torch.Generator().manual_seed(n + k)
     x = torch.randn(n, d, generator=g, dtype=torch.float64).to(xdt).to(gpu)
-    prev = torch.randint(0, k, (n,), generator=g, dtype=torch.int32)
+    prev = torch.randint(0, k, (n + off,), generator=g, dtype=torch.int32)
     labels = prev.clone()
-    mv = torch.rand(n, generator=g) < 0.07
+    mv = torch.rand(n + off, generator=g) < 0.07
     labels[mv] = torch.randint(0, k, (int(mv.sum()),), generator=g, dtype=torch.int32)
-    prev, labels = prev.to(gpu), labels.to(gpu)
+    prev, labels = prev.to(gpu)[off:], labels.to(gpu)[off:]
     work = torch.zeros(int(ops.delta_workspace(n, k)), dtype=torch.int32, device=gpu)
     ctrl = torch.zeros(DC_WORDS, dtype=torch.int32, device=gpu)
     buf = torch.full((k * d + 3 * k + 1,), 7.0, dtype=acc, device=gpu)  # garbage: zeroed first
