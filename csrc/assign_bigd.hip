@@ -130,6 +130,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
   static_assert(PIECES % WAVES == 0, "stage must split evenly over the waves");
   static_assert(!OP::SCALED || NK % 2 == 0, "fp8: D must be a multiple of 128");
   constexpr unsigned EMB = 15u;
+  // deferred epilogue (below) where its extra accumulator registers fit: one wave per SIMD
+  // (512 VGPR+AGPR) below D = 1024 bf16 (where hipcc then re-loads the point fragments
+  // instead), or two with at most 96 point-fragment VGPRs (fp8 up to D = 768)
+  constexpr bool DEFER = (WAVES <= 4 && HALFB / 4 <= 224) || (OP::SCALED && HALFB / 4 <= 96);
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   // ---- XCD-major work item: (centroid group g, point block pb) ----
@@ -230,6 +234,36 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
   };
   float best = INFINITY, best2 = INFINITY;
   int bt = 0, bt2 = 0;
+  // Deferred epilogue (DEFER): the min-reduction of tile i runs between the MFMAs of tile
+  // i+1 (accp, independent of the chain in flight), so the VALU issues under the matrix
+  // pipe instead of after every chain, where both waves of a SIMD sat in it at the same
+  // time (fp8 D=768: 72.0 -> 69.8 ms per 2M x 65536 pass, profiles/fp8_defer_epi_ab_r04f.txt).
+  f32x16 accp;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) accp[j] = INFINITY;  // no pending tile: min stays +inf
+  int ttp = 0;
+  float pm = INFINITY, pm2 = INFINITY;
+  auto epi_elem = [&](int j) __attribute__((always_inline)) {
+    const float v = __uint_as_float((__float_as_uint(accp[j]) & ~EMB) | (unsigned)j);
+    if constexpr (TOP2) pm2 = __builtin_amdgcn_fmed3f(pm, pm2, v);  // pm <= pm2 kept
+    pm = __builtin_fminf(pm, v);
+  };
+  auto epi_fold = [&]() __attribute__((always_inline)) {
+    const bool up = pm < best;
+    if constexpr (TOP2) {  // runner-up of {best, best2} U {pm, pm2}, with its tile
+      const float c = up ? best : pm;
+      const int ct = up ? bt : ttp;
+      const bool s2 = pm2 < c;
+      const float cand = s2 ? pm2 : c;
+      const int candt = s2 ? ttp : ct;
+      const bool up2 = cand < best2;
+      best2 = up2 ? cand : best2;
+      bt2 = up2 ? candt : bt2;
+    }
+    best = up ? pm : best;
+    bt = up ? ttp : bt;
+    pm = pm2 = INFINITY;
+  };
   // one ring stage: the tile, its norms and its scales all arrived by LDS-DMA NST-1
   // stages ago, so the only vmcnt wait per stage is the counted one on the ring.  The ring
   // slot is a compile-time constant (the stage loop below is unrolled by NST): the LDS
@@ -242,7 +276,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
       const int in = i + NST - 1;
       issue(t0 + (in < nt ? in : nt - 1), (slot + NST - 1) % NST);
     }
-#pragma unroll 1
+#pragma unroll
     for (int qh = 0; qh < QH; ++qh) {
     // LDS byte address of this lane's row in the slot
     const unsigned rbase = lds_base + slot * STAGE_B + (qh * 32 + r) * RB;
@@ -321,6 +355,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
       } else {
         acc = mma<OP>(a0, bq[kk], acc, 0, 0);
       }
+      // the previous tile's epilogue, spread over the chain (folds to constants unrolled)
+      if constexpr (DEFER && !(ABL & 4)) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (j * NK / 16 == kk) epi_elem(j);
+      }
       __builtin_amdgcn_sched_barrier(0);
       a0 = a1;
       a1 = a2;
@@ -328,28 +368,16 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
     if constexpr (ABL & 4) {
 #pragma unroll
       for (int j = 0; j < 16; ++j) asm volatile("" ::"v"(acc[j]));
+    } else if constexpr (DEFER) {
+      epi_fold();
+      accp = acc;
+      ttp = t * QH + qh;  // 32-row tile index
     } else {
-      float m = INFINITY, m2 = INFINITY;
+      accp = acc;
+      ttp = t * QH + qh;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const float v = __uint_as_float((__float_as_uint(acc[j]) & ~EMB) | (unsigned)j);
-        if constexpr (TOP2) m2 = __builtin_amdgcn_fmed3f(m, m2, v);  // m <= m2 kept
-        m = __builtin_fminf(m, v);
-      }
-      const int tt = t * QH + qh;  // 32-row tile index
-      const bool up = m < best;
-      if constexpr (TOP2) {  // runner-up of {best, best2} U {m, m2}, with its tile
-        const float c = up ? best : m;
-        const int ct = up ? bt : tt;
-        const bool s2 = m2 < c;
-        const float cand = s2 ? m2 : c;
-        const int candt = s2 ? tt : ct;
-        const bool up2 = cand < best2;
-        best2 = up2 ? cand : best2;
-        bt2 = up2 ? candt : bt2;
-      }
-      best = up ? m : best;
-      bt = up ? tt : bt;
+      for (int j = 0; j < 16; ++j) epi_elem(j);
+      epi_fold();
     }
     }  // qh
     if constexpr (ABL & 1) {
@@ -374,6 +402,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
   }
   static_assert(NST <= 4, "stage loop unrolled up to 4 slots");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (DEFER && !(ABL & 4)) {  // the last tile's epilogue
+#pragma unroll
+    for (int j = 0; j < 16; ++j) epi_elem(j);
+    epi_fold();
+  }
 
   const float ob = __shfl_xor(best, 32, 64);
   const int obt = __shfl_xor(bt, 32, 64);
@@ -591,9 +624,9 @@ int tdc_assign_bigd(int dtype, const void* X, const void* Xs, int64_t N, int64_t
     const int64_t ldb = ldx * 2;
     switch (DP) {
       case 384: return launch_bigd<OpBf16, 384, 8, 4>(X, nullptr, N, ldb, Cm2, nullptr, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
-      case 512: return launch_bigd<OpBf16, 512, 8, 4>(X, nullptr, N, ldb, Cm2, nullptr, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
-      // D > 512: the point fragments (D/4 VGPRs) need one wave per SIMD (4-wave groups,
-      // accumulators in AGPRs); 48 KiB stages, 3 deep
+      // D >= 512: the point fragments (D/4 VGPRs) need one wave per SIMD (4-wave groups,
+      // accumulators in AGPRs; 8 waves spilled 45 VGPRs at D=512); 32-48 KiB stages, 3 deep
+      case 512: return launch_bigd<OpBf16, 512, 4, 3>(X, nullptr, N, ldb, Cm2, nullptr, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
       case 640: return launch_bigd<OpBf16, 640, 4, 3>(X, nullptr, N, ldb, Cm2, nullptr, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
       case 768: return launch_bigd<OpBf16, 768, 4, 3>(X, nullptr, N, ldb, Cm2, nullptr, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);
       case 896: return launch_bigd<OpBf16, 896, 4, 2>(X, nullptr, N, ldb, Cm2, nullptr, cnorm, Kp, kg_tiles, xnorm, labels, mind, keys, stream);

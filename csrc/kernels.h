@@ -198,7 +198,7 @@ enum TdcDeltaCtrl {
   TDC_DC_ITER = 5,    // steps since the last reset
   TDC_DC_WORDS = 16
 };
-constexpr int TDC_DELTA_MAX_K = 8192;       // two K-int LDS histograms per block (64 KiB)
+constexpr int TDC_DELTA_MAX_K = 65536;      // labels packed in 16 bits in the moved list
 constexpr int TDC_DELTA_MAX_BLOCKS = 1024;  // per-block moved-list slots in the workspace
 // One local update of a Lloyd step in the mode ctrl[NEXT] says: labels (this step's
 // assignment) vs prev (the previous one; prev = labels on return) -> sums / counts (the

@@ -335,6 +335,9 @@ template <typename XT> struct RowLoad1 {
 constexpr unsigned PERM_NEG = 0x80000000u;
 // segment offsets staged in LDS by the segsum kernel up to this many entries (32 KiB)
 constexpr int SEG_LDS_OFF_MAX = 8193;
+// delta update: K up to which the diff / scatter kernels keep their two K-int tables in
+// LDS (64 KiB); above it they use the global histograms / cursors directly
+constexpr int DELTA_LDS_K = 8192;
 
 // each wave: rows [a, b) of the sorted permutation; TPR lanes per row, G = 64/TPR rows
 // in flight per wave-instruction, columns [c0, c0 + TPR*VEC) per pass.
@@ -552,7 +555,7 @@ __global__ __launch_bounds__(NT) void delta_diff_kernel(
     int* __restrict__ ctrl, int* __restrict__ cnt_ev, int* __restrict__ cnt_sg,
     int* __restrict__ blk_cnt, int32_t* __restrict__ lidx, uint32_t* __restrict__ lpair,
     int64_t per_block, uint32_t* __restrict__ zero, int64_t zero_words) {
-  extern __shared__ int s_h[];  // [K] events | [K] signed counts (delta steps)
+  extern __shared__ int s_h[];  // [K] events | [K] signed counts (delta steps), K <= DELTA_LDS_K
   __shared__ int s_cur;         // this block's moved-list cursor
   const int tid = threadIdx.x, lane = tid & 63;
   // the step's all-reduce buffer, cleared before anything accumulates into it (scan and
@@ -560,9 +563,12 @@ __global__ __launch_bounds__(NT) void delta_diff_kernel(
   if (zero_words) zero_fill(zero, zero_words, (int64_t)blockIdx.x * NT + tid, (int64_t)gridDim.x * NT);
   if ((int64_t)blockIdx.x * per_block >= N) return;  // a block of the zero fill only
   const bool full = ctrl[TDC_DC_NEXT] != 0;
-  int* h_ev = s_h;
-  int* h_sg = s_h + K;
-  for (int k = tid; k < (full ? K : 2 * K); k += NT) s_h[k] = 0;
+  // large K: the histograms are the global ones (a delta step touches few bins)
+  const bool lds = K <= DELTA_LDS_K;
+  int* h_ev = lds ? s_h : cnt_ev;
+  int* h_sg = lds ? s_h + K : cnt_sg;
+  if (lds)
+    for (int k = tid; k < (full ? K : 2 * K); k += NT) s_h[k] = 0;
   if (tid == 0) s_cur = 0;
   __syncthreads();
   const int64_t r0 = (int64_t)blockIdx.x * per_block;
@@ -637,10 +643,11 @@ __global__ __launch_bounds__(NT) void delta_diff_kernel(
     blk_cnt[blockIdx.x] = s_cur;
     if (s_cur) atomicAdd(ctrl + TDC_DC_MOVED, s_cur);  // one global atomic per block
   }
-  for (int k = tid; k < K; k += NT) {
-    if (h_ev[k]) atomicAdd(cnt_ev + k, h_ev[k]);
-    if (!full && h_sg[k]) atomicAdd(cnt_sg + k, h_sg[k]);
-  }
+  if (lds)
+    for (int k = tid; k < K; k += NT) {
+      if (h_ev[k]) atomicAdd(cnt_ev + k, h_ev[k]);
+      if (!full && h_sg[k]) atomicAdd(cnt_sg + k, h_sg[k]);
+    }
 }
 
 // single block, 1024 threads: event offsets / cursors, the step's signed counts into the
@@ -707,6 +714,24 @@ __global__ __launch_bounds__(NT) void delta_scatter_kernel(
   const int64_t r0 = (int64_t)blockIdx.x * per_block;
   const int64_t r1 = full ? min(N, r0 + per_block) : r0 + blk_cnt[blockIdx.x];
   if (r0 >= r1) return;  // block-uniform: nothing moved in this block's rows
+  if (K > DELTA_LDS_K) {
+    // large K: one returning global cursor atomic per event (no block aggregation)
+    if (full) {
+      for (int64_t i = r0 + tid; i < r1; i += NT) {
+        const int a = labels[i];
+        if ((unsigned)a < (unsigned)K) perm[atomicAdd(cursor + a, 1)] = (int32_t)i;
+      }
+    } else {
+      for (int64_t i = r0 + tid; i < r1; i += NT) {
+        const uint32_t pr = lpair[i];
+        const unsigned nw = pr & 0xffffu, od = pr >> 16;
+        const int32_t row = lidx[i];
+        if (nw < (unsigned)K) perm[atomicAdd(cursor + nw, 1)] = row;
+        if (od < (unsigned)K) perm[atomicAdd(cursor + od, 1)] = (int32_t)((uint32_t)row | PERM_NEG);
+      }
+    }
+    return;
+  }
   for (int k = tid; k < K; k += NT) s_cnt[k] = 0;
   __syncthreads();
   if (full) {
@@ -934,7 +959,7 @@ int tdc_delta_update(int x_dtype, int acc_dtype, const void* X, int64_t N, int64
   per = (per + 7) / 8 * 8;  // block ranges start 32-B aligned (the V4 diff kernel)
   blocks = N > 0 ? (N + per - 1) / per : 0;
   const bool v4 = (((uintptr_t)labels | (uintptr_t)prev) & 15) == 0;
-  const size_t lds = 2 * sizeof(int) * (size_t)K;
+  const size_t lds = K <= DELTA_LDS_K ? 2 * sizeof(int) * (size_t)K : 0;
   if (blocks > 0) {
     const int64_t gblocks =
         std::max(blocks, (zero_bytes / 4 + ZERO_WORDS_PER_BLOCK - 1) / ZERO_WORDS_PER_BLOCK);

@@ -67,7 +67,7 @@ class ClusterConfig:
                     fp64 per-cluster totals and each step moves only the rows whose label
                     changed (+x into the new, -x out of the old cluster; same fixed points,
                     models/kmeans.py); 'auto' = delta where supported (resident shard, native
-                    sorted/LDS update or the torch ops, K <= 8192, keep/nan/zero policies)
+                    sorted/LDS update or the torch ops, K <= 65536, keep/nan/zero policies)
     delta_refresh   delta update: recompute the totals from every row each this many steps
                     (0: never); a step after one that moved more than delta_theta * N rows
                     is a full step too (the choice is made on the device)

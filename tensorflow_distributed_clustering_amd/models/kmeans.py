@@ -392,7 +392,7 @@ class LloydEngine(OomGuard):
             self._set_delta(None)
         if self.cfg.update == "delta" and self.delta is None:
             raise ValueError("update='delta' needs a resident shard on every rank, a sorted/LDS "
-                             "native update or the torch ops, K <= 8192, empty_cluster in "
+                             "native update or the torch ops, K <= 65536, empty_cluster in "
                              "keep/nan/zero and no rsag / bounded mode")
 
     def _agree_fixed_scale(self):

@@ -205,7 +205,7 @@ class NativeUpdate:
 # ----------------------------------------------------------------- delta update
 # ctrl words (csrc/kernels.h TdcDeltaCtrl)
 DC_NEXT, DC_MODE, DC_MOVED, DC_EVENTS, DC_PREVOK, DC_ITER, DC_WORDS = 0, 1, 2, 3, 4, 5, 16
-DELTA_MAX_K = 8192
+DELTA_MAX_K = 65536
 
 
 class DeltaState:
@@ -432,7 +432,7 @@ class _LocalOpsBase:
     def make_delta(self, n: int, k: int, d: int, refresh: int, theta: float,
                    empty_cluster: str = "keep"):
         """A :class:`DeltaState` for this shard, or None where the delta update is not
-        supported (fused assign+update kernels, the deterministic update, K > 8192)."""
+        supported (fused assign+update kernels, K > 65536, shards of 2^30 rows or more)."""
         upd = getattr(self, "update", None)
         if not isinstance(upd, NativeUpdate) or k > DELTA_MAX_K:
             return None

@@ -23,7 +23,8 @@ def _ops():
                                            (torch.float32, torch.float64, False),
                                            (torch.float64, torch.float64, False)])
 @pytest.mark.parametrize("n,d,k,off", [(50_003, 128, 1024, 0), (9000, 37, 100, 0),
-                                       (70_000, 64, 8192, 0), (30_001, 128, 512, 1)])
+                                       (70_000, 64, 8192, 0), (30_001, 128, 512, 1),
+                                       (90_000, 48, 20_000, 0), (40_000, 32, 65_536, 1)])
 def test_delta_update_op_vs_torch(gpu, xdt, acc, split, n, d, k, off):
     """off = 1: labels / prev are views one element into their buffers (not 16-B aligned:
     the diff kernel's scalar-load form)."""
@@ -160,6 +161,7 @@ def test_delta_matches_full_50_iterations(gpu):
     ("fp8", 40_000, 256, 300),      # fp8 assign, update from the bf16 shard, re-quantise
     ("fp32", 50_000, 100, 128),     # exact tiled assign
     ("fp64", 50_000, 20, 50),       # SIMT assign, fp64 rows
+    ("fp8", 150_000, 256, 12_000),  # K > 8192: global histograms / cursors
 ])
 def test_delta_matches_full_other_paths(gpu, dtype, n, d, k):
     tdt = {"bf16": torch.bfloat16, "fp8": torch.bfloat16, "fp32": torch.float32,
