@@ -10,9 +10,11 @@
 //                                          rounded w, so each centroid is an exact convex
 //                                          combination of its weights)
 // Two kernels, like fcm_tower.hip:
-//   fcm_mfma_stats: 4 waves x 2 tiles of 32 points; the hi/lo point fragments stay in VGPRs,
-//     64-centroid hi/lo stages stream through LDS; per point sum_k t, the zero-distance
-//     count and argmin d2 -> rowinfo (see fcm_tower.hip) and the label.
+//   fcm_mfma_stats: 8 waves x 32 points; the hi/lo point fragments stay in VGPRs,
+//     64-centroid stages stream through LDS; per point sum_k t, the on-centroid rule and
+//     argmin d2 -> rowinfo (see fcm_tower.hip) and the label.  From DP = 64 the stats pass
+//     (fcm_mfma_stats1) runs ONE product (xh.ch) and corrects the two nearest centroids'
+//     terms with the cross terms afterwards (see there).
 //   fcm_mfma_accum: block = 128 centroids (32 per wave, hi/lo fragments in VGPRs) x a row
 //     range.  64-point hi/lo X tiles are staged in LDS once and read twice: by rows (the
 //     distance A operand) and transposed with ds_read_b64_tr_b16 (the W^T X B operand).
@@ -26,6 +28,8 @@
 // 2^-17 ||x||^2): a point on a centroid keeps the reference's NaN -> 0 semantics.  Rows
 // and centroids are shifted by a fixed vector (the shard mean) before the split, so the
 // expansion's cancellation is relative to the data spread, not to its offset.
+#include <type_traits>
+
 #include "tdc_common.h"
 #include "kernels.h"
 #include "fcm_math.h"
@@ -256,6 +260,268 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats_kernel(
     const bool on = (other ? v1 : v0) <= __uint_as_float(__float_as_uint(zf) & ~15u);
     labels[row0] = (on && prm.nz) ? 0 : (other ? l1 : l0);
     rowinfo[row0] = on ? (prm.nz ? 0.f : -1.f) : __builtin_amdgcn_rcpf(S);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// pass 1, one product (DP >= 64): the row statistics need fp32-faithful distances only where
+// they dominate.  sum_k t_k is ruled by the nearest centroids, whose d2 is small against
+// ||x||^2 + ||c||^2 (the expansion's cancellation), while the far terms carry the bf16
+// product's ~2^-9 / sqrt(D) relative error harmlessly.  So the MFMAs compute xh.ch only
+// (a third of the bf16x3 work, hi centroid images only), the epilogue keeps each row's
+// two nearest centroids (tag-in-mantissa min + v_med3 runner-up), and at the end the two
+// get the cross terms xh.cl + xl.ch on the VALU (the lo point fragments stay in registers,
+// the centroid rows come from L2): their d2 then equals the accumulate pass's bf16x3 value
+// up to fp32 rounding, and sum_k t_k swaps their one-product terms for the corrected ones.
+// The label (nearest of the two) and the on-centroid rule use the corrected d2.
+// ---------------------------------------------------------------------------------------
+template <int DP, int MODE, int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats1_kernel(
+    const __bf16* __restrict__ Xh, const __bf16* __restrict__ Xl, const float* __restrict__ xx,
+    int64_t N, const __bf16* __restrict__ Ch, const __bf16* __restrict__ Cl,
+    const float* __restrict__ cc, int K, int nstages, MParam prm, int32_t* __restrict__ labels,
+    float* __restrict__ rowinfo) {
+  constexpr int BN = 64;
+  constexpr int CPR = DP / 8;
+  constexpr int KS = DP / 16;
+  constexpr int HALF = DP / 2;
+  constexpr int IMGB = BN * DP * 2;           // bytes of one hi stage image
+  __shared__ __attribute__((aligned(16))) char s_c[2][IMGB];
+  __shared__ __attribute__((aligned(16))) float s_n[2][BN];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t row0 = (int64_t)blockIdx.x * (WAVES * 32) + (int64_t)w * 32 + r;
+  const int64_t row = row0 < N ? row0 : N - 1;
+
+  bf16x8 bh[KS], bl[KS];
+  {
+    const bf16x8* sh = reinterpret_cast<const bf16x8*>(Xh + row * DP + h * HALF);
+    const bf16x8* sl = reinterpret_cast<const bf16x8*>(Xl + row * DP + h * HALF);
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      bh[kk] = sh[kk];
+      bl[kk] = sl[kk];
+    }
+  }
+  const float xn = xx[row];
+  const float zf = ZERO_FLOOR * xn;
+
+  // hi stage images by LDS-DMA, as the bf16x3 kernel (source-side swizzle, saddr form)
+  constexpr int PPI = IMGB / 1024;
+  constexpr int PPW = PPI / WAVES;
+  static_assert(IMGB % 1024 == 0 && PPI % WAVES == 0 && PPW >= 1, "stage pieces");
+  constexpr int G = CPR < 16 ? CPR : 16;
+  constexpr int RPB = 16 / G;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  unsigned voff[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int q = (w * PPW + i) * 64 + lane;
+    const int rr = q / CPR, cs = q % CPR;
+    voff[i] = (unsigned)(rr * DP * 2 + 16 * (cs ^ ((rr / RPB) & (G - 1))));
+  }
+  const unsigned lds_c = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)&s_c[0][0];
+  const unsigned lds_n = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)&s_n[0][0];
+  auto stage_load = [&](int T, int B) __attribute__((always_inline)) {
+    const __bf16* base = Ch + (int64_t)T * BN * DP;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const unsigned dst = lds_c + B * IMGB + (wu * PPW + i) * 1024;
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
+                   :: "s"(__builtin_amdgcn_readfirstlane(dst)), "v"(voff[i]),
+                      "s"(uniform_ptr(base))
+                   : "memory", "m0");
+    }
+    if (wu == 0 && lane < BN / 4) {
+      const float* nb = cc + (int64_t)T * BN;
+      const unsigned nd = lds_n + B * BN * 4;
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
+                   :: "s"(__builtin_amdgcn_readfirstlane(nd)), "v"((unsigned)(lane * 16)),
+                      "s"(uniform_ptr(nb)) : "memory", "m0");
+    }
+  };
+  stage_load(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // keys: the tagged d2 bits compared as int32 (no canonicalising v_max per v_min_f32; all
+  // negative keys order below the positive ones, reversed among themselves -- a negative
+  // one-product d2 lies within the product error of 0 and the fix-up re-sorts the two)
+  constexpr int KINF = 0x7f800000;
+  float S = 0.f;
+  int best = KINF, best2 = KINF;
+  int bt = 0, bt2 = 0;
+  // top-2 fold of one tile's (m, m2) into (best, bt), (best2, bt2)
+  auto fold = [&](int m, int m2, int tt) __attribute__((always_inline)) {
+    const bool up = m < best;
+    const int c = up ? best : m;
+    const int ct = up ? bt : tt;
+    const bool s2 = m2 < c;
+    const int cand = s2 ? m2 : c;
+    const int candt = s2 ? tt : ct;
+    const bool up2 = cand < best2;
+    best2 = up2 ? cand : best2;
+    bt2 = up2 ? candt : bt2;
+    best = up ? m : best;
+    bt = up ? tt : bt;
+  };
+  // register i = centroid (i&3)+8(i>>2)+4h of the half; the key is the UNclamped one-product
+  // d2 with the register index in its low mantissa bits, and t is taken of the key itself
+  // (2^-19 relative off d2), so the fix-up can take out exactly the term it added
+  auto elem = [&](float a, int i, int& m, int& m2, float& sp) __attribute__((always_inline)) {
+    const int pk = (int)((__float_as_uint(a + xn) & ~15u) | (unsigned)i);
+    sp += mt<MODE>(fmaxf(__int_as_float(pk), zf), prm.expo);
+    m2 = max(m, min(m2, pk));  // median of (m, m2, pk), m <= m2 kept
+    m = min(m, pk);
+  };
+  // the MFMAs of half Q into acc; with EPI, the previous tile's epilogue (accp: all 32
+  // centroids real) issues between them, 16/KS elements per MFMA: at one product the
+  // epilogue VALU is as long as the MFMA chain, and in program order after it the wave
+  // would leave the matrix pipe idle for its whole length
+  auto phase = [&](f32x16& acc, int Q, const char* cb, const float* ns, const f32x16& accp,
+                   int ttp, auto epi_c) __attribute__((always_inline)) {
+    constexpr bool EPI = decltype(epi_c)::value;
+    const int crow = Q * 32 + r;
+    f32x16 init;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const f32x4 n4 = *reinterpret_cast<const f32x4*>(&ns[Q * 32 + 8 * g4 + 4 * h]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) init[4 * g4 + e] = n4[e];
+    }
+    bf16x8 ah[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk)
+      ah[kk] = as_bf16x8(*reinterpret_cast<const uint4*>(cb + coff<DP>(crow, h * (CPR / 2) + kk)));
+    __builtin_amdgcn_sched_barrier(0);
+    int m = KINF, m2 = KINF;
+    float sp = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[kk], bh[kk], kk == 0 ? init : acc, 0, 0, 0);
+      if constexpr (EPI) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (i * KS / 16 == kk) elem(accp[i], i, m, m2, sp);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if constexpr (EPI) {
+      S += sp;
+      fold(m, m2, ttp);
+    }
+  };
+  // stand-alone epilogue with the pad-centroid mask (the last stage)
+  auto epi = [&](const f32x16& acc, int Q, int T) __attribute__((always_inline)) {
+    const int kvalid = K - (T * BN + Q * 32 + 4 * h);
+    int m = KINF, m2 = KINF;
+    float sp = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const bool v = (i & 3) + 8 * (i >> 2) < kvalid;
+      int m_ = m, m2_ = m2;
+      float sp_ = sp;
+      elem(acc[i], i, m_, m2_, sp_);
+      m = v ? m_ : m;
+      m2 = v ? m2_ : m2;
+      sp = v ? sp_ : sp;
+    }
+    S += sp;
+    fold(m, m2, 2 * T + Q);
+  };
+  using WITH = std::integral_constant<bool, true>;
+  using WITHOUT = std::integral_constant<bool, false>;
+
+  f32x16 acc0, acc1;
+  for (int t = 0; t < nstages; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nstages) stage_load(t + 1, buf ^ 1);
+    const char* cb = s_c[buf];
+    const float* ns = s_n[buf];
+    // wave-uniform: are all 32 centroids of half (t-1, 1) / (t, 0) real?
+    if (t > 0 && K - ((t - 1) * BN + 32) >= 32) {
+      phase(acc0, 0, cb, ns, acc1, 2 * t - 1, WITH{});
+    } else {
+      phase(acc0, 0, cb, ns, acc1, 0, WITHOUT{});
+      if (t > 0) epi(acc1, 1, t - 1);
+    }
+    if (K - t * BN >= 32) {
+      phase(acc1, 1, cb, ns, acc0, 2 * t, WITH{});
+    } else {
+      phase(acc1, 1, cb, ns, acc0, 0, WITHOUT{});
+      epi(acc0, 0, t);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  epi(acc1, 1, nstages - 1);
+
+  // ---- the row's two nearest over both lane halves, by (d2, label): same in both lanes ----
+  S += __shfl_xor(S, 32, 64);
+  auto lab_of = [&](float v, int t) {
+    const unsigned e = __float_as_uint(v) & 15u;
+    return t * 32 + (int)(e & 3) + 8 * (int)(e >> 2) + 4 * h;
+  };
+  auto lt = [](float a, int la, float b, int lb) { return a < b || (a == b && la < lb); };
+  // the keys as floats (tag bits kept: the t the loop added was taken of exactly these)
+  const float v0 = __int_as_float(best), w0 = __int_as_float(best2);
+  const int l0 = lab_of(v0, bt), k0 = lab_of(w0, bt2);
+  const float v1 = __shfl_xor(v0, 32, 64), w1 = __shfl_xor(w0, 32, 64);
+  const int l1 = __shfl_xor(l0, 32, 64), k1 = __shfl_xor(k0, 32, 64);
+  float va = v0, vb = v1;
+  int la = l0, lb = l1;
+  if (lt(v1, l1, v0, l0)) { va = v1; la = l1; vb = v0; lb = l0; }
+  if (lt(w0, k0, vb, lb)) { vb = w0; lb = k0; }
+  if (lt(w1, k1, vb, lb)) { vb = w1; lb = k1; }
+  const bool has_b = vb < INFINITY && lb < K;
+  // m = 2: the runner-up's correction matters only while its term is within 1/32 of the
+  // nearest's (the one-product error of d2 relative to d2 falls as 1/d2, so the term
+  // error falls as 1/d2^2); flatter t = d2^(-1/(m-1)) of other m: always
+  const bool fix_b = has_b && (MODE != 2 || fmaxf(vb, zf) < 32.f * fmaxf(va, zf));
+
+  // ---- cross terms xh.cl + xl.ch of the two over this lane's half, summed over halves ----
+  // (both rows at once, two 16-B chunk pairs per scheduling region: the loads of a region
+  // are in flight together without every chunk of both rows held in registers at once)
+  auto cross = [&](int k) __attribute__((always_inline)) {
+    const bf16x8* ph = reinterpret_cast<const bf16x8*>(Ch + (int64_t)k * DP + h * HALF);
+    const bf16x8* pl = reinterpret_cast<const bf16x8*>(Cl + (int64_t)k * DP + h * HALF);
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int k4 = 0; k4 < KS; k4 += 4) {
+      bf16x8 chv[4], clv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        chv[u] = ph[k4 + u];
+        clv[u] = pl[k4 + u];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s0 = fmaf((float)bh[k4 + u][j], (float)clv[u][j], s0);
+          s1 = fmaf((float)bl[k4 + u][j], (float)chv[u][j], s1);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    return s0 + s1;
+  };
+  // (lanes r and r+32 hold the same row's two halves and take the same branches)
+  float xa = cross(la), xb = 0.f;
+  if (fix_b) xb = cross(lb);
+  xa += __shfl_xor(xa, 32, 64);
+  xb += __shfl_xor(xb, 32, 64);
+  const float da = fmaxf(va + xa, zf);
+  const float db = has_b ? fmaxf(vb + xb, zf) : INFINITY;
+  float Sf = S - mt<MODE>(fmaxf(va, zf), prm.expo) + mt<MODE>(da, prm.expo);
+  if (fix_b) Sf += mt<MODE>(db, prm.expo) - mt<MODE>(fmaxf(vb, zf), prm.expo);
+  const bool bwin = lt(db, lb, da, la);
+  const float dmin = bwin ? db : da;
+  const int lab = bwin ? lb : la;
+  if (h == 0 && row0 < N) {
+    const bool on = dmin <= zf;
+    labels[row0] = (on && prm.nz) ? 0 : lab;
+    rowinfo[row0] = on ? (prm.nz ? 0.f : -1.f) : __builtin_amdgcn_rcpf(Sf);
   }
 }
 
@@ -628,8 +894,19 @@ int launch_mstats(const void* Xh, const void* Xl, const float* xx, int64_t N, co
   hipLaunchKernelGGL((fcm_mfma_stats_kernel<DP, MODE, WAVES>), dim3((unsigned)blocks), dim3(WAVES * 64), 0, s, \
                      (const __bf16*)Xh, (const __bf16*)Xl, xx, N, (const __bf16*)Ch,          \
                      (const __bf16*)Cl, cc, K, Kp / 64, p, labels, rowinfo)
-  if (m == 2.0) TDC_LS(2); else TDC_LS(0);
+#define TDC_LS1(MODE)                                                                         \
+  hipLaunchKernelGGL((fcm_mfma_stats1_kernel<DP, MODE, WAVES>), dim3((unsigned)blocks), dim3(WAVES * 64), 0, s, \
+                     (const __bf16*)Xh, (const __bf16*)Xl, xx, N, (const __bf16*)Ch,          \
+                     (const __bf16*)Cl, cc, K, Kp / 64, p, labels, rowinfo)
+  // one product + fix-up from DP = 64 (fcm10m 19.05 -> 18.60 ms, profiles/fcm_stats1_ab_r04m.txt);
+  // at DP = 32 the bf16x3 kernel's 6 MFMAs per tile are not what bounds it
+  if constexpr (DP >= 64) {
+    if (m == 2.0) TDC_LS1(2); else TDC_LS1(0);
+  } else {
+    if (m == 2.0) TDC_LS(2); else TDC_LS(0);
+  }
 #undef TDC_LS
+#undef TDC_LS1
   TDC_CHECK_LAUNCH();
   return 0;
 }
