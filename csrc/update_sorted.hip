@@ -263,12 +263,14 @@ __global__ __launch_bounds__(NT) void bscatter_kernel(const int32_t* __restrict_
 // deterministic update): round-toward-zero of v * 2^S into int64, whose sums are exact and
 // therefore independent of the order the atomics land in.  The scale is a power of two,
 // so v * scale is exact; |sum| < 2^62 by the caller's choice of S.
+// fixed point: |v * scale| <= 2^30 by the scale's contract (ops.fixed_point_scale), so the
+// truncation is one v_cvt_i32 (+ sign extension) instead of an emulated float -> int64
 template <typename AT> __device__ __forceinline__ AT acc_cvt(float v, float scale) {
-  if constexpr (std::is_same<AT, long long>::value) return (long long)(v * scale);
+  if constexpr (std::is_same<AT, long long>::value) return (long long)(int)(v * scale);
   else return (AT)v;
 }
 template <typename AT> __device__ __forceinline__ AT acc_cvt(double v, double scale) {
-  if constexpr (std::is_same<AT, long long>::value) return (long long)(v * scale);
+  if constexpr (std::is_same<AT, long long>::value) return (long long)(int)(v * scale);
   else return (AT)v;
 }
 

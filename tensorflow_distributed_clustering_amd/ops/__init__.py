@@ -337,12 +337,16 @@ class TorchDelta(DeltaState):
 
 def fixed_point_scale(max_abs: float, n_rows: int) -> float:
     """2^S for fixed-point partial sums of up to ``n_rows`` values of magnitude <=
-    ``max_abs``: the largest power of two with max_abs * n_rows * 2^S < 2^61 (int64 with a
-    bit of headroom), clamped to [2^-60, 2^60]."""
+    ``max_abs``: the largest power of two with max_abs * 2^S <= 2^30 (every element's fixed
+    point fits an int32: the kernels convert it with one v_cvt_i32_f32 instead of the
+    emulated float -> int64 conversion) and max_abs * n_rows * 2^S < 2^61 (no int64 sum
+    can overflow), clamped to [2^-60, 2^60].  The step 2^-S is max_abs * 2^-30 or finer:
+    below the fp32 ulp of the largest element."""
     import math
-    bound = max(float(max_abs), 1e-30) * max(1, int(n_rows))
-    s = math.floor(61 - math.log2(bound)) - 1
-    return float(2.0 ** max(-60, min(60, s)))
+    m = max(float(max_abs), 1e-30)
+    s_sum = math.floor(61 - math.log2(m * max(1, int(n_rows)))) - 1
+    s_elem = math.floor(30 - math.log2(m))
+    return float(2.0 ** max(-60, min(60, s_sum, s_elem)))
 
 
 class _LocalOpsBase:

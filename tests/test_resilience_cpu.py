@@ -104,16 +104,20 @@ def test_setup_oom_gives_up_after_retries(monkeypatch):
 
 
 def test_fixed_point_scale_bounds_the_sums():
-    """The deterministic update's int64 fixed point: 2^S with max|x| * N * 2^S < 2^61, the
-    largest such power of two (clamped), so no per-cluster sum can overflow int64."""
+    """The deterministic update's int64 fixed point: 2^S with max|x| * N * 2^S < 2^61 (no
+    per-cluster sum can overflow int64) and max|x| * 2^S <= 2^30 (every element's fixed
+    point fits an int32), the largest such power of two (clamped)."""
     import math
-    for m, n in [(15.0, 10_000_000), (1e-3, 100), (1e6, 10 ** 9), (0.0, 5), (7.5, 1)]:
+    for m, n in [(15.0, 10_000_000), (1e-3, 100), (1e6, 10 ** 9), (0.0, 5), (7.5, 1),
+                 (2.0, 2 ** 40)]:
         s = fixed_point_scale(m, n)
+        mm = max(m, 1e-30)
         assert s == 2.0 ** round(math.log2(s))
-        assert max(m, 1e-30) * n * s < 2.0 ** 61
-        if 2.0 ** -60 < s < 2.0 ** 60:
-            assert max(m, 1e-30) * n * s * 4 >= 2.0 ** 61  # not needlessly coarse
-    assert fixed_point_scale(15.0, 10_000_000) == 2.0 ** 32
+        assert mm * n * s < 2.0 ** 61 and mm * s <= 2.0 ** 30
+        if 2.0 ** -60 < s < 2.0 ** 60:  # not needlessly coarse: one of the bounds is tight
+            assert mm * n * s * 4 >= 2.0 ** 61 or mm * s * 2 > 2.0 ** 30
+    assert fixed_point_scale(15.0, 10_000_000) == 2.0 ** 26
+    assert fixed_point_scale(2.0, 2 ** 40) == 2.0 ** 19  # the sum bound binds
 
 
 def test_deterministic_cpu_fit_reproducible():
