@@ -184,6 +184,9 @@ void check_split(const std::optional<at::Tensor>& hi, const std::optional<at::Te
                 "tdc.", op, ": cnt_hi/cnt_lo must be contiguous fp32 [K]");
 }
 
+// int64 sums = fixed point: each element is truncated to (int32)(x * fixed_scale), so the
+// caller's scale must keep max|x| * fixed_scale <= 2^30 (ops.fixed_point_scale does; the
+// hardware conversion saturates beyond it) and max|x| * N * fixed_scale < 2^63.
 void check_fixed(const at::Tensor& sums, double fixed_scale, const char* op) {
   if (sums.scalar_type() == at::kLong)
     TORCH_CHECK(fixed_scale > 0.0, "tdc.", op, ": int64 (fixed-point) sums need fixed_scale > 0");
