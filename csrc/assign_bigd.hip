@@ -130,6 +130,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
   static_assert(PIECES % WAVES == 0, "stage must split evenly over the waves");
   static_assert(!OP::SCALED || NK % 2 == 0, "fp8: D must be a multiple of 128");
   constexpr unsigned EMB = 15u;
+  // MFMAs of a stage issued after its barrier (their fragments already in registers):
+  // fp8 D=768 69.4 -> 67.7 ms, D=512 26.5 -> 24.7 ms per pass (profiles/early_release_ab_r04s.txt)
+  constexpr int ER = 2;
+  static_assert(ER >= 1 && ER <= 2 && NK >= 2, "early release after the last fragment reads");
   // deferred epilogue (below) where its extra accumulator registers fit: one wave per SIMD
   // (512 VGPR+AGPR) below D = 1024 bf16 (where hipcc then re-loads the point fragments
   // instead), or two with at most 96 point-fragment VGPRs (fp8 up to D = 768)
@@ -338,9 +342,25 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
       if (kk + 2 < NK) a2 = lds_frag(kk + 2);
       // reads still allowed in flight when a0 is consumed: those of a1 and a2
       constexpr int PER = UPF;  // ds_read instructions per fragment
-      if (kk + 2 < NK) asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(2 * PER) : "memory");
-      else if (kk + 1 < NK) asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(PER) : "memory");
-      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (qh == QH - 1 && kk == NK - ER) {
+        // early slot release: the stage's last ER fragments are in registers, so the
+        // stage-end wait and barrier go here and those ER MFMAs run after it, under the
+        // next stage's refill issue and first LDS reads (instead of the matrix pipe idling
+        // through the barrier and the next stage's read latency)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (ABL & 1) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * VPS) : "memory");  // stage i+1 landed
+        }
+        if constexpr (!(ABL & 2)) __builtin_amdgcn_s_barrier();  // ... for every wave's pieces
+      } else if (kk + 2 < NK) {
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(2 * PER) : "memory");
+      } else if (kk + 1 < NK) {
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(PER) : "memory");
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (OP::SCALED) {
         // the scale row was read before the fragments, so it has landed by the first wait
@@ -380,13 +400,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
       epi_fold();
     }
     }  // qh
-    if constexpr (ABL & 1) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * VPS) : "memory");  // stage i+1 landed
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if constexpr (!(ABL & 2)) __builtin_amdgcn_s_barrier();  // ... for every wave's pieces
   };
 
 #pragma unroll

@@ -404,6 +404,13 @@ void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int6
         if (kk + 2 < KS) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
         else if (kk + 1 < KS) asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
         else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (q == QT - 1 && kk == KS - 1) {
+          // early slot release: the stage's last fragment is in registers, so the stage-end
+          // wait and barrier go before its P MFMAs, which then run under the next stage's
+          // refill issue and first LDS reads
+          asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * VPS) : "memory");  // stage t+1 landed
+          __builtin_amdgcn_s_barrier();  // ... for every wave's pieces
+        }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int p = 0; p < P; ++p)
@@ -431,8 +438,6 @@ void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int6
       best[p] = up ? m[p] : best[p];
       bt[p] = up ? t : bt[p];
     }
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * VPS) : "memory");  // stage t+1 landed
-    __builtin_amdgcn_s_barrier();  // ... for every wave's pieces
   };
 
   for (int t0 = 0; t0 < ntiles; t0 += NST) {

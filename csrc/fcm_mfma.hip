@@ -712,21 +712,22 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
   }
   // W^T X of half SUB (weights WH/WL): A = W (row = centroid, k = points), B = X^T via
   // transposed reads (T10), prefetched one (s, dt) step ahead; INTERLEAVE runs between
-#define TDC_WTX(SUB, WH, WL, INTERLEAVE)                                                  \
+#define TDC_WTX(SUB, WH, WL, INTERLEAVE, LAST)                                            \
   {                                                                                       \
     s16x4 h0, h1, l0, l1;                                                                 \
     TDC_TRLD(SUB, 0, h0, h1, l0, l1)                                                      \
     _Pragma("unroll") for (int t = 0; t < 2 * NDT; ++t) {                                 \
       s16x4 nh0, nh1, nl0, nl1;                                                           \
-      TDC_TRLD(SUB, (t + 1 < 2 * NDT ? t + 1 : t), nh0, nh1, nl0, nl1)                    \
+      if (t + 1 < 2 * NDT) TDC_TRLD(SUB, t + 1, nh0, nh1, nl0, nl1)                       \
       const int s = t / NDT, dt = t % NDT;                                                \
       const bf16x8 xbh = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7)); \
       const bf16x8 xbl = __builtin_bit_cast(bf16x8, __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7)); \
+      if (t + 1 == 2 * NDT) { LAST }                                                      \
       out[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(WH[s], xbh, out[dt], 0, 0, 0);    \
       out[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(WH[s], xbl, out[dt], 0, 0, 0);    \
       out[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(WL[s], xbh, out[dt], 0, 0, 0);    \
       INTERLEAVE(t * EPW, EPW)                                                            \
-      h0 = nh0; h1 = nh1; l0 = nl0; l1 = nl1;                                             \
+      if (t + 1 < 2 * NDT) { h0 = nh0; h1 = nh1; l0 = nl0; l1 = nl1; }                   \
     }                                                                                     \
   }
 #define TDC_NONE(I0, CNT)
@@ -737,8 +738,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
       TDC_LOADQ(0)
       TDC_DIST(acc1, 1, TDC_MEMB0)
       TDC_LOADQ(1)
-      TDC_WTX(0, wh0, wl0, TDC_MEMB1)
-      TDC_WTX(1, wh1, wl1, TDC_NONE)
+      TDC_WTX(0, wh0, wl0, TDC_MEMB1, )
+      TDC_WTX(1, wh1, wl1, TDC_NONE, )
     } else {
       // 8 waves: row statistics read from LDS per group of 4 elements (no xq/iq arrays
       // live across the distance MFMAs: the 2-wave register budget is 256)
@@ -763,7 +764,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
           wl0[i >> 3][i & 7] = (__bf16)(wv - (float)bhv);
         }
       }
-      TDC_WTX(sub, wh0, wl0, TDC_NONE)
+      // early tile release: the tile's last transposed X reads are in registers, so the
+      // next tile's row statistics and the barrier go before the last three W^T X MFMAs,
+      // which then run under the next tile's first LDS reads (fcm10m -0.5 %)
+      TDC_WTX(sub, wh0, wl0, TDC_NONE, { if (more) TDC_TILE_STORE(buf ^ 1) __syncthreads(); })
     }
 #undef TDC_NONE
 #undef TDC_MEMB0
@@ -773,8 +777,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
 #undef TDC_LOADQ
 #undef TDC_WTX
 #undef TDC_TRLD
-    if (more) TDC_TILE_STORE(buf ^ 1)
-    __syncthreads();
+    if (WAVES == 4) {
+      if (more) TDC_TILE_STORE(buf ^ 1)
+      __syncthreads();
+    }
     buf ^= 1;
   }
 #undef TDC_TILE_LOAD
