@@ -656,7 +656,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     constexpr int EPK = 16 / KS;          // membership elements per distance k-step
     constexpr int EPW = 16 / (2 * NDT);   // membership elements per W^T X (s, dt) step
     f32x16 acc0, acc1;
-    bf16x8 wh0[2], wl0[2], wh1[2], wl1[2];
+    bf16x8 wh0[2], wh1[2];
     f32x4 xq[4], iq[4];
 #define TDC_DIST(ACC, SUB, INTERLEAVE)                                                    \
   {                                                                                       \
@@ -676,8 +676,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
       al = aln;                                                                           \
     }                                                                                     \
   }
-  // memberships of elements [I0, I0 + CNT) of half SUB (distances in ACC) -> WH/WL
-#define TDC_MEMB(ACC, WH, WL, I0, CNT)                                                    \
+  // memberships of elements [I0, I0 + CNT) of half SUB (distances in ACC) -> WH
+#define TDC_MEMB(ACC, WH, I0, CNT)                                                    \
   _Pragma("unroll") for (int q = 0; q < (CNT); ++q) {                                     \
     const int i = (I0) + q, g4 = i >> 2, e = i & 3;                                       \
     const float zf = ZERO_FLOOR * xq[g4][e];                                              \
@@ -685,10 +685,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     float u = mt<MODE>(d2, prm.expo) * iq[g4][e];                                         \
     if constexpr (!NZ) u = iq[g4][e] < 0.f ? (d2 <= zf ? 1.f : 0.f) : u;                  \
     const float wv = mw<MODE>(u, prm.m);                                                  \
-    wsum += wv;                                                                           \
     const __bf16 bhv = (__bf16)wv;                                                        \
     WH[i >> 3][i & 7] = bhv;                                                              \
-    WL[i >> 3][i & 7] = (__bf16)(wv - (float)bhv);                                        \
+    wsum += (float)bhv;  /* the rounded weight: each centroid an exact convex combination */ \
   }
 #define TDC_LOADQ(SUB)                                                                    \
   _Pragma("unroll") for (int g4 = 0; g4 < 4; ++g4) {                                      \
@@ -696,7 +695,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     xq[g4] = *reinterpret_cast<const f32x4*>(&s_xx[buf][pt]);                             \
     iq[g4] = *reinterpret_cast<const f32x4*>(&s_in[buf][pt]);                             \
   }
-  // W^T X of half SUB (weights WH/WL): A = W (row = centroid, k = points), B = X^T via
+  // W^T X of half SUB (weights WH): A = W (row = centroid, k = points), B = X^T via
   // transposed reads (T10); INTERLEAVE runs between the (s, dt) steps
 #define TDC_TRLD(SUB, T_, H0, H1, L0, L1)                                                \
   {                                                                                       \
@@ -710,9 +709,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     L0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xl + oA));                  \
     L1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xl + oB));                  \
   }
-  // W^T X of half SUB (weights WH/WL): A = W (row = centroid, k = points), B = X^T via
-  // transposed reads (T10), prefetched one (s, dt) step ahead; INTERLEAVE runs between
-#define TDC_WTX(SUB, WH, WL, INTERLEAVE, LAST)                                            \
+  // W^T X of half SUB (weights WH, bf16): A = W (row = centroid, k = points), B = X^T hi and
+  // lo via transposed reads (T10), prefetched one (s, dt) step ahead; INTERLEAVE runs between
+#define TDC_WTX(SUB, WH, INTERLEAVE, LAST)                                            \
   {                                                                                       \
     s16x4 h0, h1, l0, l1;                                                                 \
     TDC_TRLD(SUB, 0, h0, h1, l0, l1)                                                      \
@@ -725,21 +724,20 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
       if (t + 1 == 2 * NDT) { LAST }                                                      \
       out[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(WH[s], xbh, out[dt], 0, 0, 0);    \
       out[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(WH[s], xbl, out[dt], 0, 0, 0);    \
-      out[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(WL[s], xbh, out[dt], 0, 0, 0);    \
       INTERLEAVE(t * EPW, EPW)                                                            \
       if (t + 1 < 2 * NDT) { h0 = nh0; h1 = nh1; l0 = nl0; l1 = nl1; }                   \
     }                                                                                     \
   }
 #define TDC_NONE(I0, CNT)
-#define TDC_MEMB0(I0, CNT) TDC_MEMB(acc0, wh0, wl0, I0, CNT)
-#define TDC_MEMB1(I0, CNT) TDC_MEMB(acc1, wh1, wl1, I0, CNT)
+#define TDC_MEMB0(I0, CNT) TDC_MEMB(acc0, wh0, I0, CNT)
+#define TDC_MEMB1(I0, CNT) TDC_MEMB(acc1, wh1, I0, CNT)
     if constexpr (WAVES == 4) {
       TDC_DIST(acc0, 0, TDC_NONE)
       TDC_LOADQ(0)
       TDC_DIST(acc1, 1, TDC_MEMB0)
       TDC_LOADQ(1)
-      TDC_WTX(0, wh0, wl0, TDC_MEMB1, )
-      TDC_WTX(1, wh1, wl1, TDC_NONE, )
+      TDC_WTX(0, wh0, TDC_MEMB1, )
+      TDC_WTX(1, wh1, TDC_NONE, )
     } else {
       // 8 waves: row statistics read from LDS per group of 4 elements (no xq/iq arrays
       // live across the distance MFMAs: the 2-wave register budget is 256)
@@ -758,16 +756,15 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
           float u = mt<MODE>(d2, prm.expo) * iq[0][e];
           if constexpr (!NZ) u = iq[0][e] < 0.f ? (d2 <= zf ? 1.f : 0.f) : u;
           const float wv = mw<MODE>(u, prm.m);
-          wsum += wv;
           const __bf16 bhv = (__bf16)wv;
           wh0[i >> 3][i & 7] = bhv;
-          wl0[i >> 3][i & 7] = (__bf16)(wv - (float)bhv);
+          wsum += (float)bhv;
         }
       }
       // early tile release: the tile's last transposed X reads are in registers, so the
       // next tile's row statistics and the barrier go before the last three W^T X MFMAs,
       // which then run under the next tile's first LDS reads (fcm10m -0.5 %)
-      TDC_WTX(sub, wh0, wl0, TDC_NONE, { if (more) TDC_TILE_STORE(buf ^ 1) __syncthreads(); })
+      TDC_WTX(sub, wh0, TDC_NONE, { if (more) TDC_TILE_STORE(buf ^ 1) __syncthreads(); })
     }
 #undef TDC_NONE
 #undef TDC_MEMB0
