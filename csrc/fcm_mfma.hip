@@ -968,7 +968,7 @@ int launch_maccum(const void* Xh, const void* Xl, const float* xx, const float* 
 //               rule), 128-point x 128-centroid tiles, 32-feature hi/lo stages by LDS-DMA
 //   (fcm_wide_rows turns d2 into w = u^m in place, csrc/fcm_wide.hip)
 //   wide_wtx  : W^T X of 128-centroid x 128-feature output tiles over a row range: the W
-//               stage (fp32 w -> hi/lo bf16) goes through registers into row-major LDS
+//               stage (fp32 w -> bf16, column sums of the rounded w) goes through registers into row-major LDS
 //               images, X hi/lo by LDS-DMA; both MFMA operands come from transposed reads
 //               (ds_read_b64_tr_b16), so neither needs a transposed copy in HBM
 // ---------------------------------------------------------------------------------------
@@ -1118,7 +1118,7 @@ __global__ __launch_bounds__(256, 2) void fcm_wide_wtx_kernel(
     float* __restrict__ part, float* __restrict__ part_ws) {
   constexpr int RS = 32;                 // data rows per stage (two k16 steps)
   constexpr int IMG = RS * 256;          // one [32 rows x 128] bf16 image
-  constexpr int STAGE = 4 * IMG;         // Wh | Wl | Xh | Xl
+  constexpr int STAGE = 3 * IMG;         // W (bf16) | Xh | Xl
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = w >> 1, wc = w & 1;
@@ -1161,8 +1161,10 @@ __global__ __launch_bounds__(256, 2) void fcm_wide_wtx_kernel(
       wv[q] = v;
     }
   };
+  // W rounded to bf16 (RNE), the column sums taken of the same rounded weights: each
+  // centroid is an exact convex combination (as the register tower, fcm_mfma_accum_kernel)
   auto wstore = [&](int buf) __attribute__((always_inline)) {
-    bf16x8 hv[2], lv[2];
+    bf16x8 hv[2];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const float f[4] = {wv[q].x, wv[q].y, wv[q].z, wv[q].w};
@@ -1171,15 +1173,13 @@ __global__ __launch_bounds__(256, 2) void fcm_wide_wtx_kernel(
         const int j = 4 * q + e;
         const __bf16 hb = (__bf16)f[e];
         hv[j >> 3][j & 7] = hb;
-        lv[j >> 3][j & 7] = (__bf16)(f[e] - (float)hb);
-        wsum[j] += f[e];
+        wsum[j] += (float)hb;
       }
     }
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const int off = w256off(wrow, (wcol >> 3) + c);
       *reinterpret_cast<bf16x8*>(smem + buf * STAGE + off) = hv[c];
-      *reinterpret_cast<bf16x8*>(smem + buf * STAGE + IMG + off) = lv[c];
     }
   };
   // ---- X stage by LDS-DMA: waves 0-1 load Xh pieces, 2-3 Xl; 4 pieces of 4 rows each
@@ -1198,7 +1198,7 @@ __global__ __launch_bounds__(256, 2) void fcm_wide_wtx_kernel(
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int pc = (wu & 1) * 4 + p;
-      const unsigned dst = lds0 + buf * STAGE + (2 + ximg) * IMG + pc * 1024;
+      const unsigned dst = lds0 + buf * STAGE + (1 + ximg) * IMG + pc * 1024;
       int64_t row = rb + xrow[p];
       if (row >= b) row = b - 1;  // rows past the range: any valid row (their w is 0)
       const unsigned vo = (unsigned)((row - a) * (int64_t)DP * 2 + d0 * 2) + xoffv[p];
@@ -1230,8 +1230,8 @@ __global__ __launch_bounds__(256, 2) void fcm_wide_wtx_kernel(
       const int cx = (wc * 64 + t * 32 + 16 * (g & 1)) >> 3;
       wo[t][s][0] = lds0 + w256off(rA, cw + (p4 >> 1)) + 8 * (p4 & 1);
       wo[t][s][1] = lds0 + w256off(rA + 8, cw + (p4 >> 1)) + 8 * (p4 & 1);
-      xo[t][s][0] = lds0 + 2 * IMG + w256off(rA, cx + (p4 >> 1)) + 8 * (p4 & 1);
-      xo[t][s][1] = lds0 + 2 * IMG + w256off(rA + 8, cx + (p4 >> 1)) + 8 * (p4 & 1);
+      xo[t][s][0] = lds0 + IMG + w256off(rA, cx + (p4 >> 1)) + 8 * (p4 & 1);
+      xo[t][s][1] = lds0 + IMG + w256off(rA + 8, cx + (p4 >> 1)) + 8 * (p4 & 1);
     }
 
   if (a < b) {
@@ -1251,27 +1251,24 @@ __global__ __launch_bounds__(256, 2) void fcm_wide_wtx_kernel(
     const unsigned bo_ = buf * STAGE;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      s16x4 wh[2][2], wl[2][2], xh[2][2], xl[2][2];
+      s16x4 wh[2][2], xh[2][2], xl[2][2];
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           wh[t][q] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(wo[t][s][q] + bo_));
-          wl[t][q] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(wo[t][s][q] + bo_ + IMG));
           xh[t][q] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(xo[t][s][q] + bo_));
           xl[t][q] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(uintptr_t)(xo[t][s][q] + bo_ + IMG));
         }
 #pragma unroll
       for (int ti = 0; ti < 2; ++ti) {
         const bf16x8 ah = __builtin_bit_cast(bf16x8, __builtin_shufflevector(wh[ti][0], wh[ti][1], 0, 1, 2, 3, 4, 5, 6, 7));
-        const bf16x8 al = __builtin_bit_cast(bf16x8, __builtin_shufflevector(wl[ti][0], wl[ti][1], 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
         for (int tj = 0; tj < 2; ++tj) {
           const bf16x8 bh = __builtin_bit_cast(bf16x8, __builtin_shufflevector(xh[tj][0], xh[tj][1], 0, 1, 2, 3, 4, 5, 6, 7));
           const bf16x8 bl = __builtin_bit_cast(bf16x8, __builtin_shufflevector(xl[tj][0], xl[tj][1], 0, 1, 2, 3, 4, 5, 6, 7));
           acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[ti][tj], 0, 0, 0);
           acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[ti][tj], 0, 0, 0);
-          acc[ti][tj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[ti][tj], 0, 0, 0);
         }
       }
     }
