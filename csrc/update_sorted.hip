@@ -368,11 +368,13 @@ __global__ __launch_bounds__(256) void segsum_kernel(const XT* __restrict__ X, i
   if (nptr) {
     // a delta step's events: few, spread over many short segments (a wave pays one HBM
     // round trip per segment it walks), so they go to as many waves as the grid has, at
-    // least 8 each -- not 64: at 150 events a 64-event wave walked ~30 segments (31 us)
+    // least 4 each -- not 64: at 150 events a 64-event wave walked ~30 segments (31 us);
+    // 4 / 8 / 16: 12.4 / 14.2 / 17.8 us at the 1.25M-row shard, 29.2 / 28.5 / 28.1 us at
+    // 10M rows (profiles/segsum_minrows_ab_r04za.txt)
     N = *nptr;
     const int64_t waves = (int64_t)gridDim.x * 4;
     rows_per_wave = (N + waves - 1) / waves;
-    if (rows_per_wave < 8) rows_per_wave = 8;
+    if (rows_per_wave < 4) rows_per_wave = 4;
   }
   const int64_t a = wave * rows_per_wave;
   if ((int64_t)blockIdx.x * 4 * rows_per_wave >= N) return;  // block-uniform: nothing to sum
