@@ -192,9 +192,11 @@ def main(argv=None):
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         init_s = comm.max_scalar(time.perf_counter() - t_i)
+    graph = False
     if a.mode == "lloyd" and a.method == "kmeans" and a.algorithm == "lloyd" and a.graph \
             and dev.type == "cuda":
         eng.capture(include_collectives=comm.collective)
+        graph = True
 
     for _ in range(a.warmup):
         eng.step()
@@ -267,6 +269,7 @@ def main(argv=None):
         }
         if update_info is not None:
             out["update"] = update_info
+        out["graph_replay"] = graph
         if check is not None:
             out["check"] = check
         if breakdown:
