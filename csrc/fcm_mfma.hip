@@ -294,15 +294,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats1_kernel(
   const int64_t row0 = (int64_t)blockIdx.x * (WAVES * 32) + (int64_t)w * 32 + r;
   const int64_t row = row0 < N ? row0 : N - 1;
 
+  // hi point fragments for the MFMAs; the lo ones are loaded for the fix-up at the end (the
+  // same bytes, 32 VGPRs fewer through the loop: they hold the next half's A fragments)
   bf16x8 bh[KS], bl[KS];
   {
     const bf16x8* sh = reinterpret_cast<const bf16x8*>(Xh + row * DP + h * HALF);
-    const bf16x8* sl = reinterpret_cast<const bf16x8*>(Xl + row * DP + h * HALF);
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk) {
-      bh[kk] = sh[kk];
-      bl[kk] = sl[kk];
-    }
+    for (int kk = 0; kk < KS; ++kk) bh[kk] = sh[kk];
   }
   const float xn = xx[row];
   const float zf = ZERO_FLOOR * xn;
@@ -379,10 +377,17 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats1_kernel(
   // centroids real) issues between them, 16/KS elements per MFMA: at one product the
   // epilogue VALU is as long as the MFMA chain, and in program order after it the wave
   // would leave the matrix pipe idle for its whole length
-  auto phase = [&](f32x16& acc, int Q, const char* cb, const float* ns, const f32x16& accp,
-                   int ttp, auto epi_c) __attribute__((always_inline)) {
-    constexpr bool EPI = decltype(epi_c)::value;
+  // A fragments of half Q of a stage (both halves are read at the stage start, so the
+  // second half's reads are in flight under the first half's MFMAs)
+  auto frags = [&](bf16x8 (&ah)[KS], int Q, const char* cb) __attribute__((always_inline)) {
     const int crow = Q * 32 + r;
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk)
+      ah[kk] = as_bf16x8(*reinterpret_cast<const uint4*>(cb + coff<DP>(crow, h * (CPR / 2) + kk)));
+  };
+  auto phase = [&](f32x16& acc, int Q, const bf16x8 (&ah)[KS], const float* ns,
+                   const f32x16& accp, int ttp, auto epi_c) __attribute__((always_inline)) {
+    constexpr bool EPI = decltype(epi_c)::value;
     f32x16 init;
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
@@ -390,11 +395,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats1_kernel(
 #pragma unroll
       for (int e = 0; e < 4; ++e) init[4 * g4 + e] = n4[e];
     }
-    bf16x8 ah[KS];
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk)
-      ah[kk] = as_bf16x8(*reinterpret_cast<const uint4*>(cb + coff<DP>(crow, h * (CPR / 2) + kk)));
-    __builtin_amdgcn_sched_barrier(0);
     int m = KINF, m2 = KINF;
     float sp = 0.f;
 #pragma unroll
@@ -439,21 +439,29 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats1_kernel(
     if (t + 1 < nstages) stage_load(t + 1, buf ^ 1);
     const char* cb = s_c[buf];
     const float* ns = s_n[buf];
+    bf16x8 ah0[KS], ah1[KS];
+    frags(ah0, 0, cb);
+    frags(ah1, 1, cb);
     // wave-uniform: are all 32 centroids of half (t-1, 1) / (t, 0) real?
     if (t > 0 && K - ((t - 1) * BN + 32) >= 32) {
-      phase(acc0, 0, cb, ns, acc1, 2 * t - 1, WITH{});
+      phase(acc0, 0, ah0, ns, acc1, 2 * t - 1, WITH{});
     } else {
-      phase(acc0, 0, cb, ns, acc1, 0, WITHOUT{});
+      phase(acc0, 0, ah0, ns, acc1, 0, WITHOUT{});
       if (t > 0) epi(acc1, 1, t - 1);
     }
     if (K - t * BN >= 32) {
-      phase(acc1, 1, cb, ns, acc0, 2 * t, WITH{});
+      phase(acc1, 1, ah1, ns, acc0, 2 * t, WITH{});
     } else {
-      phase(acc1, 1, cb, ns, acc0, 0, WITHOUT{});
+      phase(acc1, 1, ah1, ns, acc0, 0, WITHOUT{});
       epi(acc0, 0, t);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  }
+  {
+    const bf16x8* sl = reinterpret_cast<const bf16x8*>(Xl + row * DP + h * HALF);
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) bl[kk] = sl[kk];
   }
   epi(acc1, 1, nstages - 1);
 
