@@ -393,7 +393,8 @@ void fcm_mfma_wide(int64_t pass, const at::Tensor& Xh, const at::Tensor& Xl, con
       TORCH_CHECK(shift->scalar_type() == at::kFloat && shift->numel() >= D,
                   "tdc.fcm_mfma_wide: shift fp32 [D]");
   } else {
-    TORCH_CHECK(pass == 0, "tdc.fcm_mfma_wide: pass 0 (distances) or 2 (W^T X)");
+    TORCH_CHECK(pass == 0 || pass == 1,
+                "tdc.fcm_mfma_wide: pass 0 (distances, on-centroid floor), 1 (raw distances) or 2 (W^T X)");
   }
   const DevGuard guard(Xh.device());
   check(tdc_fcm_mfma_wide((int)pass, Xh.data_ptr(), Xl.data_ptr(), xx.data_ptr<float>(), M,
@@ -619,6 +620,141 @@ void update_sorted_indexed(const at::Tensor& X, const at::Tensor& rowidx, const 
                           static_cast<float*>(opt_ptr(cnt_lo)), nullptr, 0, 0.0,
                           work_clean ? 1 : 0),
         "update_sorted_indexed");
+}
+
+// ---- fp32 / fp64 assignment on the matrix cores (kernels.h tdc_x3_*) ----
+double x3_tau(int64_t DP) { return (double)tdc_x3_tau((int)DP); }
+
+void x3_split(const at::Tensor& src, int64_t valid, int64_t neg2, at::Tensor& hi, at::Tensor& lo,
+              const std::optional<at::Tensor>& norm) {
+  check_cuda(src, "src");
+  check_rows(src, "src");
+  TORCH_CHECK(src.scalar_type() == at::kFloat || src.scalar_type() == at::kDouble,
+              "tdc.x3_split: src fp32/fp64");
+  TORCH_CHECK(hi.scalar_type() == at::kBFloat16 && lo.scalar_type() == at::kBFloat16 &&
+                  hi.is_contiguous() && lo.is_contiguous() && hi.sizes() == lo.sizes() && hi.dim() == 2,
+              "tdc.x3_split: hi/lo bf16 [rows, DP]");
+  const int64_t rows = hi.size(0);
+  const int DP = (int)hi.size(1);
+  TORCH_CHECK(src.size(1) <= DP && valid <= rows && valid <= src.size(0), "tdc.x3_split: shapes");
+  if (norm.has_value() && norm->defined())
+    TORCH_CHECK(norm->scalar_type() == at::kFloat && norm->is_contiguous() && norm->numel() >= rows,
+                "tdc.x3_split: norm fp32 [rows]");
+  const DevGuard guard(src.device());
+  check(tdc_x3_split(dcode(src.scalar_type()), src.data_ptr(), rows, valid, (int)src.size(1),
+                     src.stride(0), DP, (int)neg2, hi.data_ptr(), lo.data_ptr(),
+                     static_cast<float*>(opt_ptr(norm)), cur_stream()),
+        "x3_split");
+}
+
+void check_x3_state(const at::Tensor& cmax2, const at::Tensor& amb, const at::Tensor& amb_count,
+                    int64_t rows, const char* op) {
+  TORCH_CHECK(cmax2.scalar_type() == at::kFloat && cmax2.numel() >= 1, "tdc.", op, ": cmax2 fp32 [1]");
+  TORCH_CHECK(amb_count.scalar_type() == at::kInt && amb_count.numel() >= 1, "tdc.", op,
+              ": amb_count int32 [1]");
+  TORCH_CHECK(amb.scalar_type() == at::kInt && amb.is_contiguous() && amb.numel() >= 2 * rows,
+              "tdc.", op, ": amb int32 [2 * rows]");
+}
+
+void x3_prep(const at::Tensor& cnorm, int64_t K, at::Tensor& cmax2, at::Tensor& amb_count) {
+  check_cuda(cnorm, "cnorm");
+  TORCH_CHECK(cnorm.scalar_type() == at::kFloat && cnorm.is_contiguous() && cnorm.numel() >= K,
+              "tdc.x3_prep: cnorm fp32 [>= K]");
+  TORCH_CHECK(cmax2.scalar_type() == at::kFloat && amb_count.scalar_type() == at::kInt,
+              "tdc.x3_prep: cmax2 fp32, amb_count int32");
+  const DevGuard guard(cnorm.device());
+  check(tdc_x3_prep(cnorm.data_ptr<float>(), (int)K, cmax2.data_ptr<float>(),
+                    amb_count.data_ptr<int>(), cur_stream()),
+        "x3_prep");
+}
+
+void x3_recheck(const at::Tensor& X, const at::Tensor& C, at::Tensor& labels, const at::Tensor& amb,
+                const at::Tensor& amb_count) {
+  check_cuda(X, "X");
+  check_rows(X, "X");
+  TORCH_CHECK(X.scalar_type() == at::kFloat || X.scalar_type() == at::kDouble, "tdc.x3_recheck: X");
+  TORCH_CHECK(C.scalar_type() == X.scalar_type() && C.is_contiguous() && C.dim() == 2 &&
+                  C.size(1) <= X.size(1) && C.size(1) <= 1024,
+              "tdc.x3_recheck: C [K, D <= 1024] in the X dtype");
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous() && labels.numel() >= X.size(0),
+              "tdc.x3_recheck: labels int32 [N]");
+  TORCH_CHECK(amb.scalar_type() == at::kInt && amb.is_contiguous() && amb.numel() >= 2 * X.size(0) &&
+                  amb_count.scalar_type() == at::kInt,
+              "tdc.x3_recheck: amb int32 [2N], amb_count int32 [1]");
+  const DevGuard guard(X.device());
+  check(tdc_x3_recheck(dcode(X.scalar_type()), X.data_ptr(), X.stride(0), (int)C.size(1), C.data_ptr(),
+                       (int)C.size(0), labels.data_ptr<int32_t>(),
+                       reinterpret_cast<const int2*>(amb.data_ptr<int>()), amb_count.data_ptr<int>(),
+                       num_cus(X.device().index()), cur_stream()),
+        "x3_recheck");
+}
+
+// prep (cmax, list reset) + bf16x3 assignment + exact re-check of the listed rows
+void x3_assign(const at::Tensor& X, const at::Tensor& Xh, const at::Tensor& Xl, const at::Tensor& Ch,
+               const at::Tensor& Cl, const at::Tensor& cnorm, const at::Tensor& C, at::Tensor& labels,
+               const std::optional<at::Tensor>& mind, at::Tensor& amb, at::Tensor& cmax2,
+               at::Tensor& amb_count, bool recheck) {
+  check_cuda(Xh, "Xh");
+  TORCH_CHECK(Xh.scalar_type() == at::kBFloat16 && Xl.scalar_type() == at::kBFloat16 &&
+                  Ch.scalar_type() == at::kBFloat16 && Cl.scalar_type() == at::kBFloat16,
+              "tdc.x3_assign: hi/lo operands bf16");
+  TORCH_CHECK(Xh.is_contiguous() && Xl.is_contiguous() && Ch.is_contiguous() && Cl.is_contiguous() &&
+                  Xh.sizes() == Xl.sizes() && Ch.sizes() == Cl.sizes() && Xh.dim() == 2 && Ch.dim() == 2,
+              "tdc.x3_assign: Xh/Xl [N, DP], Ch/Cl [Kp, DP] contiguous");
+  const int64_t N = Xh.size(0);
+  const int DP = (int)Xh.size(1);
+  const int Kp = (int)Ch.size(0);
+  TORCH_CHECK(Ch.size(1) == DP, "tdc.x3_assign: DP mismatch");
+  TORCH_CHECK(DP == 32 || DP == 64 || DP == 128 || DP == 256, "tdc.x3_assign: DP 32/64/128/256");
+  TORCH_CHECK(Kp % (DP == 256 ? 32 : 64) == 0 && cnorm.scalar_type() == at::kFloat &&
+                  cnorm.is_contiguous() && cnorm.numel() >= Kp,
+              "tdc.x3_assign: Kp % 64 (% 32 at DP 256), cnorm fp32 [Kp]");
+  const int K = (int)C.size(0);
+  TORCH_CHECK(K <= Kp && C.size(1) <= DP, "tdc.x3_assign: C [K <= Kp, D <= DP]");
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous() && labels.numel() >= N,
+              "tdc.x3_assign: labels int32 [N]");
+  check_x3_state(cmax2, amb, amb_count, N, "x3_assign");
+  float* md = nullptr;
+  if (mind.has_value() && mind->defined()) {
+    TORCH_CHECK(mind->scalar_type() == at::kFloat && mind->numel() >= N && mind->is_contiguous(),
+                "tdc.x3_assign: mind fp32 [N]");
+    md = mind->data_ptr<float>();
+  }
+  if (recheck) {
+    check_rows(X, "X");
+    TORCH_CHECK(X.size(0) >= N && (X.scalar_type() == at::kFloat || X.scalar_type() == at::kDouble) &&
+                    C.scalar_type() == X.scalar_type() && C.is_contiguous(),
+                "tdc.x3_assign: X / C fp32 or fp64 (same dtype)");
+  }
+  const DevGuard guard(Xh.device());
+  hipStream_t s = cur_stream();
+  int2* list = reinterpret_cast<int2*>(amb.data_ptr<int>());
+  check(tdc_x3_prep(cnorm.data_ptr<float>(), K, cmax2.data_ptr<float>(), amb_count.data_ptr<int>(), s),
+        "x3_prep");
+  check(tdc_assign_x3(Xh.data_ptr(), Xl.data_ptr(), N, DP, Ch.data_ptr(), Cl.data_ptr(),
+                      cnorm.data_ptr<float>(), Kp, cmax2.data_ptr<float>(), tdc_x3_tau(DP),
+                      labels.data_ptr<int32_t>(), md, list, amb_count.data_ptr<int>(), s),
+        "assign_x3");
+  if (recheck)
+    check(tdc_x3_recheck(dcode(X.scalar_type()), X.data_ptr(), X.stride(0), (int)C.size(1), C.data_ptr(),
+                         K, labels.data_ptr<int32_t>(), list, amb_count.data_ptr<int>(),
+                         num_cus(X.device().index()), s),
+          "x3_recheck");
+}
+
+void x3_rows(const at::Tensor& G, int64_t row0, const at::Tensor& xx, const at::Tensor& cmax2,
+             double tau, at::Tensor& labels, at::Tensor& amb, at::Tensor& amb_count) {
+  check_cuda(G, "G");
+  TORCH_CHECK(G.scalar_type() == at::kFloat && G.is_contiguous() && G.dim() == 2, "tdc.x3_rows: G fp32 [M, K]");
+  const int64_t M = G.size(0);
+  TORCH_CHECK(xx.scalar_type() == at::kFloat && xx.numel() >= M, "tdc.x3_rows: xx fp32 [M]");
+  TORCH_CHECK(labels.scalar_type() == at::kInt && labels.numel() >= row0 + M, "tdc.x3_rows: labels");
+  check_x3_state(cmax2, amb, amb_count, row0 + M, "x3_rows");
+  const DevGuard guard(G.device());
+  check(tdc_x3_rows(G.data_ptr<float>(), M, (int)G.size(1), row0, xx.data_ptr<float>(),
+                    cmax2.data_ptr<float>(), (float)tau, labels.data_ptr<int32_t>(),
+                    reinterpret_cast<int2*>(amb.data_ptr<int>()), amb_count.data_ptr<int>(), cur_stream()),
+        "x3_rows");
 }
 
 // ---- delta update of plain Lloyd (kernels.h tdc_delta_*) ----
@@ -1015,6 +1151,12 @@ TORCH_LIBRARY(tdc, m) {
   m.def("delta_update(Tensor X, Tensor labels, Tensor(a!) prev, Tensor(b!) sums, Tensor(c!) counts, Tensor(d!) work, Tensor(e!) ctrl, Tensor(f!)? cnt_hi=None, Tensor(g!)? cnt_lo=None, Tensor(h!)? moved=None, Tensor(i!)? zero_first=None, float fixed_scale=0.0, bool work_clean=False) -> ()");
   m.def("delta_finalize(Tensor sums, Tensor counts, Tensor? cnt_hi, Tensor? cnt_lo, Tensor? moved, Tensor(a!) G, Tensor(b!) C, int policy, Tensor(c!)? shift, Tensor(d!)? Cm2, Tensor(e!)? cnorm, Tensor(f!) ctrl, Tensor(g!)? stats, int refresh, float theta_n, float fixed_scale=0.0) -> ()");
   m.def("sculley_update(Tensor sums, Tensor counts, Tensor(a!) C, Tensor(b!) v, Tensor(c!)? shift, Tensor(d!)? Cm2, Tensor(e!)? cnorm) -> ()");
+  m.def("x3_tau(int DP) -> float", &x3_tau);
+  m.def("x3_split(Tensor src, int valid, int neg2, Tensor(a!) hi, Tensor(b!) lo, Tensor(c!)? norm) -> ()");
+  m.def("x3_prep(Tensor cnorm, int K, Tensor(a!) cmax2, Tensor(b!) amb_count) -> ()");
+  m.def("x3_assign(Tensor X, Tensor Xh, Tensor Xl, Tensor Ch, Tensor Cl, Tensor cnorm, Tensor C, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!) amb, Tensor(d!) cmax2, Tensor(e!) amb_count, bool recheck=True) -> ()");
+  m.def("x3_rows(Tensor G, int row0, Tensor xx, Tensor cmax2, float tau, Tensor(a!) labels, Tensor(b!) amb, Tensor(c!) amb_count) -> ()");
+  m.def("x3_recheck(Tensor X, Tensor C, Tensor(a!) labels, Tensor amb, Tensor amb_count) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(tdc, CUDA, m) {
@@ -1048,4 +1190,9 @@ TORCH_LIBRARY_IMPL(tdc, CUDA, m) {
   m.impl("assign_bf16_top2", &assign_bf16_top2);
   m.impl("bounds_filter", &bounds_filter);
   m.impl("bounds_scatter", &bounds_scatter);
+  m.impl("x3_split", &x3_split);
+  m.impl("x3_prep", &x3_prep);
+  m.impl("x3_assign", &x3_assign);
+  m.impl("x3_rows", &x3_rows);
+  m.impl("x3_recheck", &x3_recheck);
 }

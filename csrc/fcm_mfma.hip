@@ -996,7 +996,7 @@ __device__ __forceinline__ int w256off(int r, int c) {
 __global__ __launch_bounds__(256, 2) void fcm_wide_dist_kernel(
     const __bf16* __restrict__ Xh, const __bf16* __restrict__ Xl, const float* __restrict__ xx,
     int64_t M, int DP, const __bf16* __restrict__ Ch, const __bf16* __restrict__ Cl,
-    const float* __restrict__ cc, int K, int nct, float* __restrict__ G) {
+    const float* __restrict__ cc, int K, int nct, float* __restrict__ G, int zfloor) {
   constexpr int IMG = WT * 64;          // one (hi or lo, X or C) 32-feature stage image
   constexpr int STAGE = 4 * IMG;        // Xh | Xl | Ch | Cl
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
@@ -1112,7 +1112,7 @@ __global__ __launch_bounds__(256, 2) void fcm_wide_dist_kernel(
         const int64_t row = r0 + pr;
         if (row < M && k < K) {
           const float d2 = acc[ti][tj][i];
-          G[row * (int64_t)K + k] = d2 <= ZERO_FLOOR * s_xn[pr] ? 0.f : d2;
+          G[row * (int64_t)K + k] = (zfloor && d2 <= ZERO_FLOOR * s_xn[pr]) ? 0.f : d2;
         }
       }
   }
@@ -1356,12 +1356,13 @@ int tdc_fcm_mfma_wide(int pass, const void* Xh, const void* Xl, const float* xx,
   if (M <= 0 || K <= 0) return 0;
   if (DP % WT != 0 || DP < WT || DP > 1024 || Kp % WT != 0 || Kp < K || D > DP)
     return (int)hipErrorInvalidValue;
-  if (pass == 0) {
+  if (pass == 0 || pass == 1) {
+    // pass 1: raw d2 (no on-centroid floor) for the K-Means wide path (assign_x3.hip)
     const int nct = Kp / WT;
     const int64_t nb = ((M + WT - 1) / WT) * nct;
     hipLaunchKernelGGL(fcm_wide_dist_kernel, dim3((unsigned)nb), dim3(256), 0, s,
                        (const __bf16*)Xh, (const __bf16*)Xl, xx, M, DP, (const __bf16*)Ch,
-                       (const __bf16*)Cl, cc, K, nct, G);
+                       (const __bf16*)Cl, cc, K, nct, G, pass == 0 ? 1 : 0);
     TDC_CHECK_LAUNCH();
     return 0;
   }

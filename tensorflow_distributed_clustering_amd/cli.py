@@ -182,10 +182,19 @@ def build_parser():
     return parser
 
 
-def resolve_dtype(dtype: str, k: int, d: int) -> str:
+def resolve_dtype(dtype: str, k: int, d: int, method: str = "distributedKMeans") -> str:
+    """``--dtype auto``: the reference's data is fp64 and its distances are fp64
+    (`scripts/distribuitedClustering.py:221-234`).  K-Means keeps fp64 up to D = 1024: the
+    fp64 path assigns on the matrix cores (bf16x3 scores) and re-checks every row the error
+    bound cannot certify in fp64, so its labels are the fp64 argmin (ops.HipX3Lloyd); past
+    D = 1024 it runs fp32 exact tiles.  FCM keeps fp64 up to D = 16 and runs the exact fp32
+    towers above.  Nothing is silently dropped to bf16: the resolved dtype is printed and
+    written to --extended_log."""
     if dtype != "auto":
         return dtype
-    return "fp64" if d <= 16 else "bf16"
+    if method == "distributedFuzzyCMeans":
+        return "fp64" if d <= 16 else "fp32"
+    return "fp64" if d <= 1024 else "fp32"
 
 
 def format_row(vals) -> str:
@@ -229,7 +238,10 @@ def run(args) -> int:
         if (args.n_obs, args.n_dim) != (n_global, d) and comm.is_root:
             print(f"note: --n_obs/--n_dim are logged only; data file is {n_global}x{d}",
                   file=sys.stderr)
-        dtype = resolve_dtype(args.dtype, args.K, d)
+        dtype = resolve_dtype(args.dtype, args.K, d, args.method_name)
+        if comm.is_root and args.dtype != dtype:
+            print(f"note: --dtype {args.dtype} resolved to {dtype} (D={d}, {args.method_name})",
+                  file=sys.stderr)
         init = "first_k" if args.compat else args.init
         empty = "nan_any" if args.compat else args.empty_cluster
         cfg = ClusterConfig(n_clusters=args.K, max_iter=args.n_max_iters, tol=args.tol,
@@ -313,6 +325,7 @@ def run(args) -> int:
                         "method_name": args.method_name, "num_GPUs": comm.world_size,
                         "K": args.K, "n_obs": result.n_global, "n_dim": int(result.centers.shape[1]),
                         "n_iter": n_iter, "computation_time": comp, "backend": result.backend,
+                        "dtype": dtype,
                         "points_per_sec": result.n_global * n_iter / comp if comp > 0 else None,
                         "iters_per_sec": n_iter / comp if comp > 0 else None,
                         "warmup_step": not args.no_warmup,

@@ -20,6 +20,7 @@ BACKENDS = ("auto", "hip", "torch")
 ALGORITHMS = ("lloyd", "bounded")
 COMM_MODES = ("auto", "allreduce", "rsag")
 UPDATE_MODES = ("auto", "full", "delta")
+EXACT_ASSIGN = ("auto", "mfma", "simt")
 
 
 @dataclass(frozen=True)
@@ -30,8 +31,12 @@ class ClusterConfig:
     max_iter        fixed iteration budget (reference: ``--n_max_iters``)
     tol             stop when max centroid shift^2 <= tol (0 = run all iters,
                     the reference behaviour, `distribuitedClustering.py:163`)
-    dtype           compute dtype of the distance kernel. bf16/fp8 use MFMA;
-                    fp32/fp64 use exact-difference SIMT kernels.
+    dtype           compute dtype of the distance kernel. bf16/fp8 use MFMA; fp32/fp64
+                    K-Means (16 < D <= 1024) runs bf16x3 MFMA scores with an exact
+                    re-check of every row the error bound cannot certify, so its labels
+                    are the exact argmin of that dtype (``exact_assign='simt'``: the
+                    difference-form SIMT tiles instead); FCM fp32/fp64 use exact
+                    difference-form towers.
     init            centroid init (reference script: k-means++; CSV era: first-K)
     fuzzifier       FCM m. ``None`` = compat value D (`:121,129`).
     fcm_nan_to_zero compat: membership NaN (point on a centroid) -> 0 (`:125-126`);
@@ -109,6 +114,7 @@ class ClusterConfig:
     update: str = "auto"        # 'auto' | 'full' | 'delta' (Lloyd centroid update)
     delta_refresh: int = 32     # delta update: full re-sum every this many steps (0: never)
     delta_theta: float = 0.4    # ... and after a step that moved more than this share of rows
+    exact_assign: str = "auto"  # fp32/fp64 K-Means assign: 'auto'/'mfma' bf16x3 + exact re-check, 'simt'
 
     def __post_init__(self):
         if self.n_clusters <= 0:
@@ -129,6 +135,8 @@ class ClusterConfig:
             raise ValueError(f"comm_mode must be one of {COMM_MODES}")
         if self.update not in UPDATE_MODES:
             raise ValueError(f"update must be one of {UPDATE_MODES}")
+        if self.exact_assign not in EXACT_ASSIGN:
+            raise ValueError(f"exact_assign must be one of {EXACT_ASSIGN}")
         if self.delta_refresh < 0 or not (0.0 <= self.delta_theta <= 1.0):
             raise ValueError("delta_refresh must be >= 0 and delta_theta in [0, 1]")
 

@@ -72,6 +72,11 @@ class BoundedLloydEngine(LloydEngine):
         self.maxdrift = torch.zeros(1, dtype=torch.float32, device=dev)
         self._fresh = True       # next step is a full assignment (first step / refresh)
 
+    def rewind(self, snap: dict):
+        super().rewind(snap)
+        if self.enabled:
+            self._fresh = True  # bounds and totals are rebuilt by a full top-2 pass
+
     def graphable(self) -> bool:
         # data-dependent launch sizes (the host reads the active / moved counts)
         return False if self.enabled else super().graphable()

@@ -165,6 +165,15 @@ class FcmEngine(OomGuard):
 
     rsag = False  # (OomGuard) the FCM partials always go through one all-reduce
 
+    def snapshot(self) -> dict:
+        """Restart state (bench.py: timed iterations 1..K from the init); see LloydEngine."""
+        return {"C": self.C.clone(), "n_iter": self.n_iter}
+
+    def rewind(self, snap: dict):
+        self.C.copy_(snap["C"])
+        self.local.prepare(self.C)
+        self.n_iter = snap["n_iter"]
+
     def centers(self) -> torch.Tensor:
         return self.C
 

@@ -224,7 +224,8 @@ class LloydEngine(OomGuard):
                 source = (source.float() / n).to(source.dtype)
             x0 = source
             self.local = make_lloyd_ops(source, k, cfg.dtype, cfg.backend, cfg.empty_cluster,
-                                        cfg.deterministic, cfg.kgroup_bytes, cfg.fp8_recheck)
+                                        cfg.deterministic, cfg.kgroup_bytes, cfg.fp8_recheck,
+                                        cfg.exact_assign)
             self.source = ResidentSource(self.local.x, self.local.layout, row_offset)
             self.local.x = self.source.x
             self.device = source.device
@@ -239,7 +240,8 @@ class LloydEngine(OomGuard):
             self.n_local = int(source.n_rows)
             probe = torch.zeros(1, self.d, dtype=torch.float32, device=self.device)
             self.local = make_lloyd_ops(probe, k, cfg.dtype, cfg.backend, cfg.empty_cluster,
-                                        cfg.deterministic, cfg.kgroup_bytes, cfg.fp8_recheck)
+                                        cfg.deterministic, cfg.kgroup_bytes, cfg.fp8_recheck,
+                                        cfg.exact_assign)
             if tuple(self.local.layout) != tuple(source.layout):
                 raise ValueError(f"source layout {source.layout} != kernel layout {self.local.layout}")
             x0 = None
@@ -262,12 +264,6 @@ class LloydEngine(OomGuard):
             acc = torch.float64
         self.rsag = (not self.fixed) and self._use_rsag(
             comm, cfg, k * self.d * torch.tensor([], dtype=acc).element_size())
-        # delta update: only the rows whose label changed move between fp64 running totals
-        self.delta = None
-        if (cfg.update != "full" and self.delta_ok and not self.streamed and not self.rsag
-                and cfg.empty_cluster in ("keep", "nan", "zero")):
-            self.delta = self.local.make_delta(self.n_local, k, self.d, cfg.delta_refresh,
-                                               cfg.delta_theta, cfg.empty_cluster)
         W = comm.world_size
         if self.rsag:
             align = math.lcm(max(1, self.local.row_align), W)
@@ -276,6 +272,19 @@ class LloydEngine(OomGuard):
         else:
             kpad = k
         self.kpad = kpad
+        # delta update: only the rows whose label changed move between fp64 running totals.
+        # Under rsag each rank keeps the totals of its own slice of centroid rows (the
+        # reduce-scatter hands it exactly those deltas); the moved count and the signed
+        # count deltas ride in the all-reduced tail, so every rank picks the same mode
+        self.delta = None
+        if (cfg.update != "full" and self.delta_ok and not self.streamed
+                and cfg.empty_cluster in ("keep", "nan", "zero")):
+            g_rows = None
+            if self.rsag:
+                r0 = comm.rank * (kpad // W)
+                g_rows = max(0, min(k, r0 + kpad // W) - r0)
+            self.delta = self.local.make_delta(self.n_local, k, self.d, cfg.delta_refresh,
+                                               cfg.delta_theta, cfg.empty_cluster, g_rows)
         # 'nan_any' (script compat): K extra "empty on this rank" flags ride in the same
         # all-reduce; a cluster empty on ANY rank becomes NaN everywhere, like the
         # reference's per-GPU reduce_mean of an empty gather (`distribuitedClustering.py:240,248`)
@@ -361,6 +370,13 @@ class LloydEngine(OomGuard):
 
     def exact_counts(self) -> torch.Tensor:
         """Global cluster sizes of the last update (fp64, exact past 2^24)."""
+        if self.delta is not None and self.rsag:
+            # each rank holds the totals of its slice: gather them (collective)
+            part = torch.zeros(self._kr, dtype=torch.float64, device=self.device)
+            part[: self.delta.gk] = self.delta.counts
+            full = torch.zeros(self.kpad, dtype=torch.float64, device=self.device)
+            self.comm.all_gather_(full, part)
+            return full[: self.k].clone()
         if self.delta is not None:
             return self.delta.counts.clone()
         if self.count_split:
@@ -382,9 +398,9 @@ class LloydEngine(OomGuard):
                             else self._zero_fused_full)
 
     def _agree_update_mode(self):
-        """Every rank runs the same update mode (the totals are replicated): the delta
-        update only if every rank supports it (a rank whose planner streams its shard
-        cannot).  Collective."""
+        """Every rank runs the same update mode (the totals are replicated, or sliced by
+        rank under rsag): the delta update only if every rank supports it (a rank whose
+        planner streams its shard cannot).  Collective."""
         ok = self.delta is not None
         if self.comm.collective:
             ok = self.comm.max_scalar(0.0 if ok else 1.0) == 0.0
@@ -393,7 +409,7 @@ class LloydEngine(OomGuard):
         if self.cfg.update == "delta" and self.delta is None:
             raise ValueError("update='delta' needs a resident shard on every rank, a sorted/LDS "
                              "native update or the torch ops, K <= 65536, empty_cluster in "
-                             "keep/nan/zero and no rsag / bounded mode")
+                             "keep/nan/zero and no bounded mode")
 
     def _agree_fixed_scale(self):
         """Deterministic update: the fixed-point scale 2^S of the int64 partials, from the
@@ -510,6 +526,24 @@ class LloydEngine(OomGuard):
         else:
             self.local.finalize(self.sums, self.counts, self.C, self.shift)
 
+    # ------------------------------------------------------------ restart from a state
+    def snapshot(self) -> dict:
+        """The state the iterations can be restarted from (bench.py: the timed steps are
+        iterations 1..K from the centroid init, as the reference's computation_time,
+        `scripts/distribuitedClustering.py:277-280`, after untimed warm-up steps)."""
+        return {"C": self.C_pad.clone(), "n_iter": self.n_iter}
+
+    def rewind(self, snap: dict):
+        """Back to :meth:`snapshot`: centroids (every row, replicated), operands, iteration
+        count; the delta update starts over with a full step (its running totals describe
+        the warm-up's assignment, not one of these centroids)."""
+        self.C_pad.copy_(snap["C"])
+        self._c_synced = True
+        self.local.prepare(self.C)
+        if self.delta is not None:
+            self.delta.reset()
+        self.n_iter = snap["n_iter"]
+
     def update_stats(self) -> Optional[dict]:
         """Delta-update bookkeeping so far (host read): moved rows summed over the steps
         that had a previous assignment, those steps, full steps, all steps; None without
@@ -566,12 +600,27 @@ class LloydEngine(OomGuard):
             self.shift.zero_()
         r1 = min(k, r0 + kr)
         nv = max(0, r1 - r0)
-        self.local.finalize_rows(self._rs_out[:nv], self.counts[r0:r0 + nv],
-                                 self.C_pad[r0:r0 + nv], self.shift, r0, kr)
+        if self.delta is not None:
+            # the slice's deltas (or, on a full step, its sums) into the slice's fp64 totals;
+            # ctrl's next mode comes from the all-reduced moved count, the same on every rank
+            cm2, cnorm = self.local.bf16_operands()
+            split = ((self.cnt_hi[r0:r0 + nv], self.cnt_lo[r0:r0 + nv]) if self.count_split
+                     else None)
+            self.delta.finalize(self._rs_out[:nv], self.counts[r0:r0 + nv], split,
+                                self.moved_slot, self.C_pad[r0:r0 + nv], self.local.policy,
+                                self.shift, None if cm2 is None else cm2[r0:r0 + kr],
+                                None if cnorm is None else cnorm[r0:r0 + kr], self.n_global)
+            if cm2 is None:
+                self.local.prep_rows(self.C_pad[r0:r0 + nv], r0, kr)
+        else:
+            self.local.finalize_rows(self._rs_out[:nv], self.counts[r0:r0 + nv],
+                                     self.C_pad[r0:r0 + nv], self.shift, r0, kr)
         for t in self._gathered:
             part = t[r0:r0 + kr].contiguous()
             comm.all_gather_(t, part)
         self._c_synced = self._gathered[0] is self.C_pad
+        if self._c_synced:
+            self.local.after_gather(self.C)
         if self.shift is not None:
             comm.allreduce_(self.shift, "max")
 

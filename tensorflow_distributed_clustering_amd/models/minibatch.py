@@ -82,6 +82,16 @@ class MiniBatchStepper:
         self._shift_buf = None
         self.n_iter = 0
 
+    def snapshot(self) -> dict:
+        """Restart state (bench.py: timed steps from the init): centres and per-centre counts."""
+        return {"C": self.C.clone(), "v": self.v.clone(), "n_iter": self.n_iter}
+
+    def rewind(self, snap: dict):
+        self.C.copy_(snap["C"])
+        self.v.copy_(snap["v"])
+        self.local.prepare(self.C)
+        self.n_iter = snap["n_iter"]
+
     @property
     def resident(self) -> bool:
         return isinstance(self.source, ResidentSource)

@@ -16,7 +16,10 @@ Variants (picked by :func:`make_lloyd_ops`):
                           update from the full-precision shard
 ``HipSmallLloyd``         fused fp32/fp64 assign+accumulate (reference configs)
 ``HipSimtLloyd``          fp32/fp64 exact SIMT assign + LDS update
-``HipExactLloyd``         fp32/fp64 large-D (and bf16 D > 1024): tiled exact assign
+``HipX3Lloyd``            fp32/fp64, 16 < D <= 1024: bf16x3 MFMA scores + top-3, exact
+                          re-check of the rows the error bound cannot certify
+``HipExactLloyd``         fp32/fp64 D > 1024 (and bf16 D > 1024), or exact_assign='simt':
+                          tiled exact difference-form assign
 ``TorchLloyd``            plain PyTorch (CPU ranks, oracle)
 ========================  =====================================================
 """
@@ -225,11 +228,15 @@ class DeltaState:
     bincount, `scripts/distribuitedClustering.py:237-263`); the fixed points are the same.
     """
 
-    def __init__(self, n: int, k: int, d: int, device, refresh: int, theta: float):
+    def __init__(self, n: int, k: int, d: int, device, refresh: int, theta: float,
+                 g_rows: Optional[int] = None):
         self.n, self.k, self.d = n, k, d
+        # rows of the replicated totals this rank keeps: all K, or (reduce-scatter mode) the
+        # rank's own slice of centroid rows
+        self.gk = k if g_rows is None else int(g_rows)
         self.refresh, self.theta = int(refresh), float(theta)
         self.prev = torch.zeros(max(1, n), dtype=torch.int32, device=device)
-        self.G = torch.zeros(k * d + k, dtype=torch.float64, device=device)
+        self.G = torch.zeros(self.gk * d + self.gk, dtype=torch.float64, device=device)
         self.ctrl = torch.zeros(DC_WORDS, dtype=torch.int32, device=device)
         # [moved rows (steps with a valid prev), such steps, full steps, steps]
         self.stats = torch.zeros(4, dtype=torch.float64, device=device)
@@ -237,11 +244,11 @@ class DeltaState:
 
     @property
     def sums(self) -> torch.Tensor:
-        return self.G[: self.k * self.d].view(self.k, self.d)
+        return self.G[: self.gk * self.d].view(self.gk, self.d)
 
     @property
     def counts(self) -> torch.Tensor:
-        return self.G[self.k * self.d:]
+        return self.G[self.gk * self.d:]
 
     def reset(self):
         """The next step is a full one and ``prev`` holds no labels yet (after the centroid
@@ -261,8 +268,8 @@ class NativeDelta(DeltaState):
     native = True
     fixed_scale = 0.0
 
-    def __init__(self, ops, n, k, d, device, refresh, theta):
-        super().__init__(n, k, d, device, refresh, theta)
+    def __init__(self, ops, n, k, d, device, refresh, theta, g_rows=None):
+        super().__init__(n, k, d, device, refresh, theta, g_rows)
         self.ops = ops
         self.work = torch.zeros(int(ops.delta_workspace(n, k)), dtype=torch.int32, device=device)
 
@@ -284,8 +291,8 @@ class TorchDelta(DeltaState):
     """The same state machine in PyTorch ops (CPU ranks over gloo, ``backend='torch'``)."""
     native = False
 
-    def __init__(self, n, k, d, device, refresh, theta, empty_cluster="keep"):
-        super().__init__(n, k, d, device, refresh, theta)
+    def __init__(self, n, k, d, device, refresh, theta, empty_cluster="keep", g_rows=None):
+        super().__init__(n, k, d, device, refresh, theta, g_rows)
         self.empty_cluster = empty_cluster
 
     def update(self, x, labels, sums, counts, split, moved, zero_buf):
@@ -434,15 +441,20 @@ class _LocalOpsBase:
 
     # ------------------------------------------------------------- delta update
     def make_delta(self, n: int, k: int, d: int, refresh: int, theta: float,
-                   empty_cluster: str = "keep"):
+                   empty_cluster: str = "keep", g_rows: Optional[int] = None):
         """A :class:`DeltaState` for this shard, or None where the delta update is not
-        supported (fused assign+update kernels, K > 65536, shards of 2^30 rows or more)."""
+        supported (fused assign+update kernels, K > 65536, shards of 2^30 rows or more).
+        ``g_rows``: rows of the totals this rank keeps (reduce-scatter mode: its slice)."""
         upd = getattr(self, "update", None)
         if not isinstance(upd, NativeUpdate) or k > DELTA_MAX_K:
             return None
         if n >= (1 << 30):
             return None
-        return NativeDelta(self.ops, n, k, d, self.device, refresh, theta)
+        return NativeDelta(self.ops, n, k, d, self.device, refresh, theta, g_rows)
+
+    def prep_rows(self, C: torch.Tensor, r0: int, kr: int):
+        """rsag: the assign-operand rows [r0, r0 + kr) from the finalised centroid slice C
+        (rows past K become padding); no-op where the ranks gather the centroids."""
 
     def bf16_operands(self):
         """(Cm2, cnorm) the finalize kernel writes for the next assignment, or (None, None)."""
@@ -450,6 +462,10 @@ class _LocalOpsBase:
 
     def after_finalize(self, C: torch.Tensor):
         """Operand prep the finalize kernel does not do itself (fp8 re-quantisation)."""
+
+    def after_gather(self, C: torch.Tensor):
+        """rsag: operand prep after the all-gather, when :meth:`gather_operands` is None
+        (the ranks gathered the centroids themselves)."""
 
     # ------------------------------------------------------------- exact counts
     def supports_count_split(self) -> bool:
@@ -494,8 +510,8 @@ class TorchLloyd(_LocalOpsBase):
         if mind is not None:
             mind.copy_(md)
 
-    def make_delta(self, n, k, d, refresh, theta, empty_cluster="keep"):
-        return TorchDelta(n, k, d, self.device, refresh, theta, empty_cluster)
+    def make_delta(self, n, k, d, refresh, theta, empty_cluster="keep", g_rows=None):
+        return TorchDelta(n, k, d, self.device, refresh, theta, empty_cluster, g_rows)
 
 
 class HipBf16Lloyd(_LocalOpsBase):
@@ -566,6 +582,9 @@ class HipBf16Lloyd(_LocalOpsBase):
     def finalize_rows(self, sums, counts, C, shift, r0, kr):
         self.ops.finalize(sums, counts, C, self.policy, shift, self.cm2[r0:r0 + kr],
                           self.cnorm[r0:r0 + kr], fixed_scale=self.fixed_scale)
+
+    def prep_rows(self, C, r0, kr):
+        self.ops.finalize(None, None, C, 0, None, self.cm2[r0:r0 + kr], self.cnorm[r0:r0 + kr])
 
 
 class _GroupedAssign:
@@ -669,6 +688,9 @@ class HipWideBf16Lloyd(_GroupedAssign, _LocalOpsBase):
     def finalize_rows(self, sums, counts, C, shift, r0, kr):
         self.ops.finalize(sums, counts, C, self.policy, shift, self.cm2[r0:r0 + kr],
                           self.cnorm[r0:r0 + kr], fixed_scale=self.fixed_scale)
+
+    def prep_rows(self, C, r0, kr):
+        self.ops.finalize(None, None, C, 0, None, self.cm2[r0:r0 + kr], self.cnorm[r0:r0 + kr])
 
 
 class HipFp8Lloyd(_GroupedAssign, _LocalOpsBase):
@@ -798,6 +820,9 @@ class HipFp8Lloyd(_GroupedAssign, _LocalOpsBase):
         if C.shape[0]:
             self.ops.finalize(sums, counts, C, self.policy, shift, None, None,
                               fixed_scale=self.fixed_scale)
+        self.prep_rows(C, r0, kr)
+
+    def prep_rows(self, C, r0, kr):
         self.ops.quant_fp8(C, C.shape[0], 1, self.cm2[r0:r0 + kr], self.cs[r0:r0 + kr],
                            self.cnorm[r0:r0 + kr])
 
@@ -866,6 +891,156 @@ class HipExactLloyd(_HipExactBase):
         self.ops.assign_exact(self.x, C, labels, mind)
 
 
+X3_DIMS = (32, 64, 128, 256)
+X3_WIDE_MAX_D = 1024
+X3_MIN_D = 16  # D <= 16: the SIMT / fused kernels (a 32-wide k-step would be mostly padding)
+
+
+def x3_dim(d: int) -> Optional[int]:
+    """Padded width of the fp32/fp64 MFMA assignment: 32/64/128/256 (register-resident
+    point fragments), multiples of 128 up to 1024 (the row-chunk GEMM path), else None."""
+    for p in X3_DIMS:
+        if d <= p:
+            return p
+    if d <= X3_WIDE_MAX_D:
+        return -(-d // 128) * 128
+    return None
+
+
+def _exact_mind(x: torch.Tensor, C: torch.Tensor, labels: torch.Tensor, mind: torch.Tensor, d: int):
+    """mind[i] = ||x_i - C[labels_i]||^2 in the data's precision (inertia only: the MFMA
+    scores pick the winner, the difference form gives the distance)."""
+    n = x.shape[0]
+    Cx = C.to(x.dtype)
+    step = max(1, (1 << 28) // max(1, 8 * d))
+    for s in range(0, n, step):
+        e = min(n, s + step)
+        diff = x[s:e, :d] - Cx.index_select(0, labels[s:e].long())
+        mind[s:e] = diff.pow_(2).sum(1).to(mind.dtype)
+
+
+class HipX3Lloyd(_LocalOpsBase):
+    """fp32 / fp64 Lloyd with the assignment on the bf16 matrix cores (csrc/assign_x3.hip):
+    rows and centroids split into bf16 hi/lo terms, scores from three MFMAs per product
+    (fp32-faithful), the three smallest kept per row, and every row whose winner the
+    error bound cannot certify re-checked exactly in the data's own dtype (the two
+    candidates, or all K when a third is within the bound).  So the labels are those of
+    the exact difference-form argmin (the reference's fp64 distances,
+    `scripts/distribuitedClustering.py:221-234`), at ~1/3 of the bf16 MFMA rate instead of
+    the vector rate.  D <= 256 keeps the point fragments in registers (the ring3
+    pipeline); 256 < D <= 1024 runs the bf16x3 distance GEMM into a row-chunk block and a
+    top-3 row pass.  The update, the all-reduce and the finalize use the fp32 / fp64 rows
+    (NativeUpdate), as on the exact path."""
+    name = "hip_x3_mfma"
+    chunk_elems = 1 << 27           # wide path: [rows, K] fp32 block per chunk
+    max_chunk_rows = 1 << 20
+
+    def __init__(self, x, k, dtype="fp32", empty_cluster="keep"):
+        super().__init__(x, k, empty_cluster)
+        self.ops = _native.require()
+        self.c_dtype = TORCH_DTYPES[dtype]
+        self.dp = x3_dim(self.d)
+        if self.dp is None or dtype not in ("fp32", "fp64"):
+            raise ValueError(f"x3 path: fp32/fp64 with D <= {X3_WIDE_MAX_D}, got {dtype} D={self.d}")
+        self.wide = self.dp > X3_DIMS[-1]
+        self.kp = -(-k // (128 if self.wide else 64)) * (128 if self.wide else 64)
+        dev = x.device
+        self.ch = torch.zeros(self.kp, self.dp, dtype=torch.bfloat16, device=dev)
+        self.cl = torch.zeros_like(self.ch)
+        self.cnorm = torch.zeros(self.kp, dtype=torch.float32, device=dev)
+        self.cmax2 = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.amb_count = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.tau = float(self.ops.x3_tau(self.dp))
+        self.xh = self.xl = self.xx = self.amb = self.G = None
+        self.x = None
+        self._set_x(x)
+        self.update = NativeUpdate(self.ops, self.n, k, self.d, self.c_dtype, dev)
+
+    def _set_x(self, x):
+        if x.dtype != self.c_dtype or x.stride(-1) != 1:
+            x = x.to(self.c_dtype).contiguous()
+        n = int(x.shape[0])
+        if self.xh is None or self.xh.shape[0] < n:
+            dev = self.device
+            self.xh = torch.empty(max(n, 1), self.dp, dtype=torch.bfloat16, device=dev)
+            self.xl = torch.empty_like(self.xh)
+            self.xx = torch.empty(max(n, 1), dtype=torch.float32, device=dev) if self.wide else None
+            self.amb = torch.empty(2 * max(n, 1), dtype=torch.int32, device=dev)
+        self.x = x
+        self.n = n
+        if n:
+            self.ops.x3_split(x[:, : self.d], n, 0, self.xh[:n], self.xl[:n],
+                              self.xx[:n] if self.wide else None)
+
+    @property
+    def layout(self):
+        return (self.c_dtype, self.d)
+
+    def bind(self, x):
+        # always re-split: a streaming slot is refilled in place
+        if x.shape[1] != self.d:
+            raise ValueError(f"chunk layout {(x.dtype, x.shape[1])} != {self.layout}")
+        self._set_x(x)
+        return self
+
+    def prepare(self, C):
+        self.ops.x3_split(C.to(self.c_dtype).contiguous(), self.k, 1, self.ch, self.cl, self.cnorm)
+
+    def _chunk_rows(self):
+        rows = max(1, min(self.n, self.chunk_elems // max(1, self.k), self.max_chunk_rows))
+        if self.G is None or self.G.shape[0] < rows:
+            self.G = torch.empty(rows, self.k, dtype=torch.float32, device=self.device)
+        return rows
+
+    def assign(self, C, labels, mind):
+        n = self.n
+        if n == 0:
+            return
+        Cx = C if (C.dtype == self.c_dtype and C.is_contiguous()) else C.to(self.c_dtype).contiguous()
+        if not self.wide:
+            self.ops.x3_assign(self.x, self.xh[:n], self.xl[:n], self.ch, self.cl, self.cnorm, Cx,
+                               labels, None, self.amb, self.cmax2, self.amb_count, True)
+        else:
+            self.ops.x3_prep(self.cnorm, self.k, self.cmax2, self.amb_count)
+            rows = self._chunk_rows()
+            for s in range(0, n, rows):
+                e = min(n, s + rows)
+                g = self.G[: e - s]
+                self.ops.fcm_mfma_wide(1, self.xh[s:e], self.xl[s:e], self.xx[s:e], self.ch,
+                                       self.cl, self.cnorm, self.k, self.d, g)
+                self.ops.x3_rows(g, s, self.xx[s:e], self.cmax2, self.tau, labels, self.amb,
+                                 self.amb_count)
+            self.ops.x3_recheck(self.x, Cx, labels, self.amb, self.amb_count)
+        if mind is not None:
+            _exact_mind(self.x, C, labels, mind, self.d)
+
+    def ambiguous_rows(self) -> int:
+        """Rows the last assignment re-checked exactly (host read; diagnostics)."""
+        return int(self.amb_count.item())
+
+    def step(self, C, labels, mind, sums, counts):
+        self.assign(C, labels, mind)
+        self.update(self.x, labels, sums, counts)
+
+    def finalize(self, sums, counts, C, shift):
+        self.ops.finalize(sums, counts, C, self.policy, shift, None, None,
+                          fixed_scale=self.fixed_scale)
+        self.prepare(C)
+
+    def after_finalize(self, C):
+        self.prepare(C)
+
+    def after_gather(self, C):
+        self.prepare(C)
+
+    def finalize_rows(self, sums, counts, C, shift, r0, kr):
+        # rsag: the exact centroid rows are what the ranks all-gather (the re-check reads
+        # them; as many bytes as the hi/lo images), the operands are prepped after it
+        if C.shape[0]:
+            self.ops.finalize(sums, counts, C, self.policy, shift, None, None,
+                              fixed_scale=self.fixed_scale)
+
+
 def lloyd_layout(dtype: str, d: int):
     """(torch dtype, width) of the rows the GPU Lloyd ops for ``dtype`` consume (the
     layout a streamed source must produce; mirrors :func:`_make_lloyd_ops`)."""
@@ -879,12 +1054,15 @@ def lloyd_layout(dtype: str, d: int):
 
 def make_lloyd_ops(x: torch.Tensor, k: int, dtype: str = "bf16", backend: str = "auto",
                    empty_cluster: str = "keep", deterministic: bool = False,
-                   kgroup_bytes: int = 0, fp8_recheck: float = 0.0):
+                   kgroup_bytes: int = 0, fp8_recheck: float = 0.0, exact_assign: str = "auto"):
     """Pick the fastest local implementation for (device, dtype, K, D).
 
     ``kgroup_bytes`` / ``fp8_recheck``: ClusterConfig tunables of the wide-D / fp8 assign
-    (K-group size; near-tie re-check margin), applied to the ops that have them."""
-    ops = _make_lloyd_ops(x, k, dtype, backend, empty_cluster, deterministic)
+    (K-group size; near-tie re-check margin), applied to the ops that have them.
+    ``exact_assign`` (fp32 / fp64): 'auto' / 'mfma' = the bf16x3 MFMA assignment with the
+    exact re-check (HipX3Lloyd) for 16 < D <= 1024; 'simt' = the difference-form SIMT
+    tiles (the same labels up to the dtype's rounding, at the vector rate)."""
+    ops = _make_lloyd_ops(x, k, dtype, backend, empty_cluster, deterministic, exact_assign)
     upd = getattr(ops, "update", None)
     if deterministic and isinstance(upd, NativeUpdate) and not upd.deterministic:
         # fixed-point partials: always the sorted path (the LDS path sums in float atomics)
@@ -898,7 +1076,7 @@ def make_lloyd_ops(x: torch.Tensor, k: int, dtype: str = "bf16", backend: str = 
     return ops
 
 
-def _make_lloyd_ops(x, k, dtype, backend, empty_cluster, deterministic):
+def _make_lloyd_ops(x, k, dtype, backend, empty_cluster, deterministic, exact_assign="auto"):
     d = x.shape[1]
     if not use_native(x.device, backend):
         return TorchLloyd(x, k, dtype if dtype in ("fp64", "fp32") else "fp32", empty_cluster)
@@ -916,6 +1094,8 @@ def _make_lloyd_ops(x, k, dtype, backend, empty_cluster, deterministic):
     ops = _native.require()
     if ops.lloyd_small_supported(tdt, k, d) and not deterministic:
         return HipSmallLloyd(x, k, dtype, empty_cluster)
+    if exact_assign != "simt" and d > X3_MIN_D and x3_dim(d) is not None:
+        return HipX3Lloyd(x, k, dtype, empty_cluster)
     if d <= (64 if dtype == "fp32" else 32):
         return HipSimtLloyd(x, k, dtype, empty_cluster)
     return HipExactLloyd(x, k, dtype, empty_cluster)

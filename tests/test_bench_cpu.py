@@ -38,6 +38,10 @@ def test_bench_json_contract(gpus, scaling):
         assert set(d["phase_ms"]) == {"zero", "assign", "update", "allreduce", "finalize"}
     # the update mode of the timed steps and the correctness witness (after the timing)
     assert d["update"]["mode"] == "delta" and 0.0 <= d["update"]["moved_frac_mean"] <= 1.0
+    # the timed steps are iterations 1..K from the init (the reference's computation_time):
+    # the delta update's first full step is inside the window; the steady state rides along
+    assert d["timed_from"] == "init" and d["update"]["full_steps_timed"] >= 1
+    assert d["ms_per_step_steady"] > 0 and "moved_frac_mean" in d["update"]["steady"]
     assert d["check"]["sample_rows"] == 20000 if n == 20000 else d["check"]["sample_rows"] > 0
     assert d["check"]["agree_fp64_sample"] >= 0.99 and d["check"]["inertia"] > 0
 
@@ -90,3 +94,18 @@ def test_bench_host_source():
     d = _run(["--preset", "minibatch1b", "--n-per-gpu", "30000", "--k", "16", "--batch-size", "4096",
               "--steps", "3", "--warmup", "1", "--dtype", "fp32", "--source", "host"])
     assert d["config"]["model"] == "kmeans-minibatch" and d["source"]["chunk_rows"] == 4096
+
+
+def test_bench_from_init_equals_fit():
+    """Rewinding to the init after the warm-up: the centroids after K timed steps equal a
+    fit of K iterations from the same init (warm-up count does not matter)."""
+    import tempfile
+    outs = []
+    with tempfile.TemporaryDirectory() as td:
+        for w in (0, 3):
+            out = os.path.join(td, f"c{w}.npy")
+            d = _run(["--steps", "4", "--warmup", str(w), "--n-per-gpu", "30000", "--k", "12",
+                      "--dim", "6", "--dtype", "fp32", "--no-steady", "--centers-out", out])
+            assert d["timed_from"] == "init" and d["ms_per_step_steady"] is None
+            outs.append(np.load(out))
+    np.testing.assert_allclose(outs[0], outs[1], rtol=1e-12, atol=1e-12)

@@ -163,6 +163,34 @@ def test_delta_theta_fallback(world):
     np.testing.assert_array_equal(ld, lf)
 
 
+@pytest.mark.parametrize("world,k,extra", [
+    (2, 9, {"delta_refresh": 3}),
+    (3, 7, {"delta_refresh": 3}),
+    (3, 2, {"delta_refresh": 3}),  # the last rank's slice is all padding rows
+    (2, 6, {"delta_refresh": 0, "delta_theta": 0.0}),
+])
+def test_delta_under_rsag_equals_full(world, k, extra):
+    """Reduce-scatter mode keeps the delta update: each rank holds the fp64 totals of its
+    own slice of centroid rows, the moved count and the signed count deltas ride in the
+    all-reduced tail (every rank switches between delta and full steps together), and
+    the fit equals the full update's under rsag and the single-rank fit."""
+    kw = dict(k=k, d=4, n=9001, iters=10, init="first_k")
+    cf, lf, inf_, itf, _, f = run_world(world, extra={"update": "full", "comm_mode": "rsag"}, **kw)
+    cd, ld, ind, itd, _, dlt = run_world(world, extra=dict(update="delta", comm_mode="rsag",
+                                                           **extra), **kw)
+    assert dlt["rsag"] and dlt["update_mode"] == "delta" and f["update_mode"] == "full"
+    st = dlt["update_stats"]
+    if extra["delta_refresh"] == 3:
+        assert st["steps"] == 10 and st["full_steps"] == 1 + 9 // 3, st
+    else:
+        assert st["full_steps"] >= 2 and st["moved_rows"] > 0, st
+    np.testing.assert_allclose(cd, cf, rtol=1e-10, atol=1e-10)
+    np.testing.assert_array_equal(ld, lf)
+    np.testing.assert_array_equal(dlt["counts"], f["counts"])
+    c1, l1, *_ = run_world(1, extra={"update": "full"}, **kw)
+    np.testing.assert_allclose(cd, c1, rtol=1e-10, atol=1e-10)
+
+
 def _count_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
                       RANK=str(rank), LOCAL_RANK=str(rank))

@@ -22,7 +22,7 @@ def _free_port():
 
 
 def _worker(rank, world, port, q, dtype, n, d, k, iters, method, algorithm="lloyd",
-            comm_mode="auto"):
+            comm_mode="auto", extra=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
                       RANK=str(rank), LOCAL_RANK=str(rank), TDC_DIST_BACKEND="gloo")
     import tensorflow_distributed_clustering_amd as tdc
@@ -35,27 +35,28 @@ def _worker(rank, world, port, q, dtype, n, d, k, iters, method, algorithm="lloy
            "fp64": torch.float64}[dtype]
     x = gaussian_blobs(e - s, d, k, seed=3, row_offset=s, dtype=tdt, device=comm.device)
     cfg = tdc.ClusterConfig(n_clusters=k, max_iter=iters, dtype=dtype, init="random", seed=3,
-                            algorithm=algorithm, comm_mode=comm_mode)
+                            algorithm=algorithm, comm_mode=comm_mode, **(extra or {}))
     model = (tdc.KMeans if method == "kmeans" else tdc.FuzzyCMeans)(cfg, comm)
     model.fit(x, n_global=n, row_offset=s)
     r = model.result_
     labels = comm.gather_rows_to_root(torch.as_tensor(r.labels, device=comm.device))
     eng = model.engine_
     info = dict(rsag=getattr(eng, "rsag", False), split=getattr(eng, "count_split", False),
-                counts=r.counts)
+                counts=r.counts, update_mode=getattr(eng, "update_mode", None),
+                update_stats=eng.update_stats() if hasattr(eng, "update_stats") else None)
     if rank == 0:
         q.put((np.asarray(r.centers), labels.cpu().numpy(), r.backend, info))
     D.destroy_comm()
 
 
 def _run(world, dtype, n, d, k, iters=4, method="kmeans", algorithm="lloyd", comm_mode="auto",
-         full=False):
+         full=False, extra=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker,
                          args=(r, world, port, q, dtype, n, d, k, iters, method, algorithm,
-                               comm_mode))
+                               comm_mode, extra))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -124,3 +125,38 @@ def test_bounded_two_ranks_match_lloyd(gpu):
     assert b2 == "hip_bf16_mfma"
     np.testing.assert_allclose(c2, c1, rtol=2e-3, atol=2e-3)
     assert (l1 == l2).mean() > 0.999
+
+
+@pytest.mark.parametrize("world,dtype,d,k,comm_mode", [
+    (2, "bf16", 128, 1000, "allreduce"), (3, "bf16", 128, 1000, "allreduce"),
+    (2, "bf16", 128, 1000, "rsag"), (2, "fp8", 256, 500, "rsag"),
+    (3, "fp8", 256, 40, "rsag"),  # rank 2's slice: padding rows only
+    (2, "fp32", 96, 700, "rsag")])
+@pytest.mark.parametrize("mode", ["refresh2", "theta0"])
+def test_native_delta_multi_rank(gpu, world, dtype, d, k, comm_mode, mode):
+    """The native delta update across ranks (HIP diff / scan / scatter / segsum kernels,
+    device-side full/delta choice from the all-reduced moved count): with a refresh every
+    2 steps, or theta = 0 (any moved row makes the next step full), the ranks switch
+    modes together (the run completes and the stats count full steps) and the fit matches
+    update='full' at the same world size -- also under reduce-scatter mode, where each rank
+    keeps only its slice of the fp64 totals."""
+    n, iters = 120_001, 7
+    extra = ({"delta_refresh": 2} if mode == "refresh2" else
+             {"delta_refresh": 0, "delta_theta": 0.0})
+    cf, lf, bf, fi = _run(world, dtype, n, d, k, iters, comm_mode=comm_mode, full=True,
+                          extra={"update": "full"})
+    cd, ld, bd, di = _run(world, dtype, n, d, k, iters, comm_mode=comm_mode, full=True,
+                          extra=dict(update="delta", **extra))
+    assert bf == bd and di["update_mode"] == "delta" and fi["update_mode"] == "full"
+    assert di["rsag"] == (comm_mode == "rsag")
+    st = di["update_stats"]
+    assert st["full_steps"] >= 2 and st["full_steps"] < st["steps"], st
+    if mode == "theta0":
+        assert st["moved_rows"] > 0
+    assert di["counts"].sum() == n
+    if dtype == "fp32":
+        np.testing.assert_allclose(cd, cf, rtol=1e-4, atol=1e-4)
+    else:
+        ok = np.isclose(cd, cf, rtol=2e-3, atol=2e-3).all(1)
+        assert ok.mean() > 0.99, ok.mean()
+    assert (lf == ld).mean() > 0.99
