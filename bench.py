@@ -56,10 +56,11 @@ PRESETS = {
                        dtype="fp64", method="fcm"),
     "embed50m_fp8": dict(n_per_gpu=50_000_000, dim=768, k=65536, scaling="strong", mode="lloyd",
                          dtype="fp8"),
-    # FCM at the headline shape (fp32 memberships, m = 2; the reference's m = D = 128 would
-    # underflow every u^m)
+    # FCM at the headline shape on the MFMA tower: bf16x3 distances, fp32 memberships, bf16
+    # weights in W^T X (ops.FCM_PRECISION; --dtype fp32 runs the exact fp32 tower), m = 2
+    # (the reference's m = D = 128 would underflow every u^m)
     "fcm10m": dict(n_per_gpu=10_000_000, dim=128, k=1024, scaling="weak", mode="lloyd",
-                   dtype="fp32", method="fcm", fuzzifier=2.0),
+                   dtype="bf16", method="fcm", fuzzifier=2.0),
 }
 
 
@@ -257,7 +258,10 @@ def main(argv=None):
             update_info["steady"] = upd_steady
     check = None
     if not a.no_check and src_info is None:
-        check = witness(eng, x, n_global, s, e, comm, torch, a)
+        if a.method == "fcm":
+            check = fcm_witness(eng, x, n_global, s, e, comm, torch, a)
+        else:
+            check = witness(eng, x, n_global, s, e, comm, torch, a)
     breakdown = None
     if ((a.profile_steps or world > 1) and a.mode == "lloyd" and a.method == "kmeans"
             and a.algorithm == "lloyd" and not getattr(eng, "streamed", False)):
@@ -284,6 +288,7 @@ def main(argv=None):
             "vs_reference_best": pps / (BASELINE_FCM_POINTS_PER_SEC if a.method == "fcm"
                                         else BASELINE_POINTS_PER_SEC),
             "dtype": a.dtype,
+            "precision": precision_of(eng, a),
             "data": "synthetic gaussian blobs (on-device, counter-based), random-row init",
             "preset": a.preset,
             "init": {"method": a.init, "seconds": init_s},
@@ -348,6 +353,23 @@ def host_shard(a, n_rows, row_offset, dev, torch):
                  "hbm_budget_gb": a.hbm_budget_gb}
 
 
+def precision_of(eng, a):
+    """What the timed step computes, in words (the dtype key alone undersells fp32 on the
+    matrix cores and oversells the MFMA FCM tower)."""
+    name = getattr(getattr(eng, "local", None), "name", "")
+    if a.method == "fcm":
+        from tensorflow_distributed_clustering_amd.ops import FCM_PRECISION
+        return FCM_PRECISION.get(getattr(eng, "dtype_name", a.dtype), a.dtype)
+    if name == "hip_x3_mfma":
+        return (f"{a.dtype} exact-argmin labels: bf16x3 MFMA scores + exact {a.dtype} re-check "
+                f"of the rows the error bound cannot certify; {a.dtype} rows in the update")
+    if a.dtype == "fp8":
+        return "fp8 e4m3 block-scaled MFMA distances; sums from the bf16 rows"
+    if a.dtype == "bf16":
+        return "bf16 MFMA distances (fp32 accumulate); sums of the bf16 rows in fp32/fp64"
+    return f"{a.dtype} difference-form distances"
+
+
 def vs_baseline(a, world, pps):
     """value / the reference's number for the SAME config and GPU count, else None."""
     same = (a.n_per_gpu == 25_000_000 and a.scaling == "strong" and a.dim == 5 and a.k == 3
@@ -398,6 +420,52 @@ def phase_breakdown(eng, torch, dev, reps: int = 5):
 
 
 WITNESS_ROWS = 65536
+
+
+def fcm_witness(eng, x, n_global, s, e, comm, torch, a):
+    """FCM correctness witness, after the timed region: ONE FCM step from the final
+    centroids on a fixed sample of WITNESS_ROWS global rows (evenly spaced, world-size
+    invariant), computed by the same native tower the engine runs and by the fp64 oracle
+    (plain PyTorch difference-form distances, `scripts/distribuitedClustering.py:112-137`);
+    reported: the centroid error max|c - c_ref| / max|c_ref| and the worst relative error
+    of sum_i w_ik over the clusters holding >= 1e-6 of the total weight."""
+    from tensorflow_distributed_clustering_amd.ops import FCM_PRECISION, make_fcm_ops
+    from tensorflow_distributed_clustering_amd.ops import reference as ref
+    dev = comm.device
+    C = eng.centers().double()
+    k, d = C.shape
+    g = torch.arange(WITNESS_ROWS, dtype=torch.float64) * (n_global / WITNESS_ROWS)
+    g = torch.unique(g.floor().long())
+    loc = (g[(g >= s) & (g < e)] - s).to(dev)
+    xs = x.index_select(0, loc)[:, :d] if loc.numel() else x[:0, :d]
+    nz = eng.cfg.fcm_nan_to_zero
+    wx = torch.zeros(k, d, dtype=torch.float64, device=dev)
+    ws = torch.zeros(k, dtype=torch.float64, device=dev)
+    wr = torch.zeros(k, d, dtype=torch.float64, device=dev)
+    wsr = torch.zeros(k, dtype=torch.float64, device=dev)
+    if xs.shape[0]:
+        ops = make_fcm_ops(xs.float() if eng.dtype_name != "fp64" else xs.double(), k,
+                           eng.dtype_name, eng.m, nz, eng.cfg.backend)
+        lab = torch.empty(xs.shape[0], dtype=torch.int32, device=dev)
+        ops.step(C.to(ops.c_dtype).contiguous(), lab, wx, ws)
+        step = max(1, (1 << 25) // max(1, k))
+        for r0 in range(0, xs.shape[0], step):
+            pa, pb, _ = ref.fcm_partial(xs[r0:r0 + step].double(), C, eng.m, nz,
+                                        acc_dtype=torch.float64)
+            wr += pa
+            wsr += pb
+    for t in (wx, ws, wr, wsr):
+        comm.allreduce_(t)
+    c_k = wx / ws.clamp_min(1e-300)[:, None]
+    c_r = wr / wsr.clamp_min(1e-300)[:, None]
+    ok = wsr > 1e-6 * float(wsr.sum())
+    cerr = float((c_k - c_r)[ok].abs().max()) / max(1e-300, float(c_r[ok].abs().max())) \
+        if bool(ok.any()) else 0.0
+    werr = float(((ws - wsr).abs() / wsr.clamp_min(1e-300))[ok].max()) if bool(ok.any()) else 0.0
+    return {"fcm_centroid_rel_err": cerr, "fcm_weight_sum_rel_err": werr,
+            "sample_rows": int(comm.sum_scalar(float(loc.numel()))),
+            "precision": FCM_PRECISION.get(eng.dtype_name, eng.dtype_name),
+            "backend": ops.name if xs.shape[0] else None}
 
 
 def witness(eng, x, n_global, s, e, comm, torch, a):
@@ -453,6 +521,7 @@ def witness(eng, x, n_global, s, e, comm, torch, a):
     if amb is not None:
         # fp32/fp64 MFMA path: rows of the last label pass re-checked exactly
         out["recheck_rows_frac"] = comm.sum_scalar(float(amb())) / max(1, n_global)
+        out["rescan_rows_frac"] = comm.sum_scalar(float(eng.local.rescanned_rows())) / max(1, n_global)
     if a.dtype != "fp8":
         # fp64 argmin over the kernel's own operands (bf16 rows, bf16-rounded centroids)
         out["agree_fp64_kernel_operands"] = comm.sum_scalar(agree_op) / max(1.0, tot)

@@ -12,28 +12,28 @@
 // runs as three bf16 MFMAs per product on the ring3 pipeline of assign_mfma_impl.h
 // (centroid hi/lo images stream through LDS by LDS-DMA, point hi/lo fragments stay in
 // registers).  The epilogue keeps each row's three smallest scores (tagged, as ring3) and
-// the indices of the two smallest.  For every (row, centroid) pair
-//
-//     |s_computed - s_exact| <= eps = tau(D) * (max_k ||c_k||^2 + 2 ||x|| max_k ||c_k||)
-//
-// tau(D) = (4 D + 64) 2^-23 + 2^-16 bounds, for ANY order of the fp32 additions inside and
-// between the MFMAs (n terms: |error| <= (n - 1) 2^-23 sum |terms|, u taken as 2^-23 so a
-// truncating adder is covered too): the dropped split terms (3 2^-18 sum |x_i c_i| per
-// product, x2 for the -2c scaling), the 3 D + 1 accumulations, the fp32 ||c||^2 and the
+// the indices of the two smallest.  For every (row, centroid) pair |s_computed - s_exact|
+// <= eps(row) (x3_eps): the split terms the three products leave out, bounded by the row's
+// own ||xh||, ||xl|| and the centroid table's max ||th||, ||tl|| (Cauchy-Schwarz; RNE to
+// bf16 has unit roundoff 2^-8, so each residual is <= 2^-8 |lo|); the MFMA accumulation --
+// measured at <= 3.5 ulp(|C| + sum |a b|) per v_mfma_f32_16x16x32_bf16 on MI355X, neither a
+// single rounding nor an fma chain (tools/probe_mfma_acc.hip, profiles/probe_mfma_acc_r05.txt)
+// and taken as 8 x 2^-23 (|C| + sum |a b|) -- with the large hi.hi terms in their own chain
+// (KS MFMAs from ||c||^2) and the cross terms in a second one from 0; the fp32 ||c||^2; the
 // 4-bit index tag.  So
 //   * gap = s2 - s1 > 2 eps: the winner is certain (the exact argmin);
 //   * else, if s3 - s1 > 2 eps: the exact winner is one of the two smallest -- recomputed
 //     in the data's own precision (fp32 or fp64 difference form), ties to the lower index;
 //   * else (a third centroid within the bound): the row is re-assigned over all K exactly.
-// The ambiguous rows go to a compacted list (one ballot + one atomic per wave and point
-// tile); on Gaussian-blob data at the headline shape about 1 % need the two-candidate check
-// and ~1e-4 the full scan.  Labels therefore equal the exact argmin of the input dtype
+// The ambiguous rows go to two compacted lists (one ballot + one atomic per wave and point
+// tile each): two-candidate checks, and full re-scans (lloyd_simt.hip's tiled exact kernel
+// over the listed rows).  Labels therefore equal the exact argmin of the input dtype
 // (fp32, or fp64 for fp64 data) up to that dtype's own rounding of the distances.
 //
 // Wide D (256 < D <= 1024): the point fragments no longer fit the registers, so a row chunk
 // runs fcm_mfma.hip's bf16x3 distance GEMM into an [M, K] block (raw d2, no zero floor) and
-// x3_rows_kernel does the top-3 / list pass over it (bound tau * (||x|| + max ||c||)^2, the
-// block includes ||x||^2).
+// x3_rows_kernel does the top-3 / list pass over it (x3_eps_wide: one accumulator from
+// ||x||^2 + ||c||^2 through all 3 DP / 16 MFMAs, worst-case split term).
 #include <math.h>
 
 #include "assign_mfma_impl.h"
@@ -46,48 +46,108 @@ namespace {
 // operand prep: rows of T [rows, ld] (d valid columns) -> bf16 hi/lo [rows, DP] (of -2v when
 // neg2) + norm [rows] = ||v||^2 (pad centroid rows: BIG, so they never win)
 // ------------------------------------------------------------------------------------
+// nhl (nullable, float2 [rows]): ||hi||^2, ||lo||^2 of the row (the centroid side of the
+// per-row error bound).  Norms are summed in fp64 (one rounding to fp32 at the end).
 template <typename T>
 __global__ __launch_bounds__(256) void x3_split_kernel(const T* __restrict__ src, int64_t rows,
                                                        int64_t valid, int d, int64_t ld, int DP,
                                                        int neg2, __bf16* __restrict__ hi,
                                                        __bf16* __restrict__ lo,
-                                                       float* __restrict__ norm) {
+                                                       float* __restrict__ norm,
+                                                       float2* __restrict__ nhl) {
   const int lane = threadIdx.x & 63;
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows;
        row += (int64_t)gridDim.x * 4) {
-    T s = 0;
+    double s = 0.0, sh = 0.0, sl = 0.0;
     for (int c = lane; c < DP; c += 64) {
       const T v = (row < valid && c < d) ? src[row * ld + c] : (T)0;
-      s += v * v;
+      s += (double)v * (double)v;
       const T t = neg2 ? (T)-2 * v : v;
       const __bf16 th = (__bf16)(float)t;
+      const __bf16 tl = (__bf16)(float)(t - (T)(float)th);
       hi[row * DP + c] = th;
-      lo[row * DP + c] = (__bf16)(float)(t - (T)(float)th);
+      lo[row * DP + c] = tl;
+      sh += (double)(float)th * (double)(float)th;
+      sl += (double)(float)tl * (double)(float)tl;
     }
     s = wave_sum(s);
-    if (lane == 0 && norm) norm[row] = (neg2 && row >= valid) ? BIG : (float)s;
+    if (nhl) {
+      sh = wave_sum(sh);
+      sl = wave_sum(sl);
+    }
+    if (lane == 0) {
+      if (norm) norm[row] = (neg2 && row >= valid) ? BIG : (float)s;
+      if (nhl) nhl[row] = row < valid ? make_float2((float)sh, (float)sl) : make_float2(0.f, 0.f);
+    }
   }
 }
 
-// cmax2[0] = max_k cnorm[k] over the K valid rows; amb_count[0] = 0 (the list of the next
+// cstat = {max_k ||c_k||^2, max_k ||th_k||^2, max_k ||tl_k||^2} over the K valid rows (t =
+// -2c split into hi + lo; nhl nullable: zeros), amb_count[0..1] = 0 (the lists of the next
 // assignment).  One block.
-__global__ __launch_bounds__(1024) void x3_prep_kernel(const float* __restrict__ cnorm, int K,
-                                                       float* __restrict__ cmax2,
+__global__ __launch_bounds__(1024) void x3_prep_kernel(const float* __restrict__ cnorm,
+                                                       const float2* __restrict__ nhl, int K,
+                                                       float* __restrict__ cstat,
                                                        int* __restrict__ amb_count) {
-  __shared__ float red[16];
-  float m = 0.f;
-  for (int k = threadIdx.x; k < K; k += 1024) m = fmaxf(m, cnorm[k]);
-  m = wave_max(m);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    float v = threadIdx.x < 16 ? red[threadIdx.x] : 0.f;
-    v = wave_max(v);
-    if (threadIdx.x == 0) {
-      cmax2[0] = v;
-      amb_count[0] = 0;
+  __shared__ float red[3][16];
+  float m = 0.f, mh = 0.f, ml = 0.f;
+  for (int k = threadIdx.x; k < K; k += 1024) {
+    m = fmaxf(m, cnorm[k]);
+    if (nhl) {
+      const float2 v = nhl[k];
+      mh = fmaxf(mh, v.x);
+      ml = fmaxf(ml, v.y);
     }
   }
+  m = wave_max(m);
+  mh = wave_max(mh);
+  ml = wave_max(ml);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = m;
+    red[1][threadIdx.x >> 6] = mh;
+    red[2][threadIdx.x >> 6] = ml;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const bool in = threadIdx.x < 16;
+    const float v0 = wave_max(in ? red[0][threadIdx.x] : 0.f);
+    const float v1 = wave_max(in ? red[1][threadIdx.x] : 0.f);
+    const float v2 = wave_max(in ? red[2][threadIdx.x] : 0.f);
+    if (threadIdx.x == 0) {
+      cstat[0] = v0;
+      cstat[1] = v1;
+      cstat[2] = v2;
+      amb_count[0] = 0;
+      amb_count[1] = 0;
+    }
+  }
+}
+
+// Per-row bound on |score_computed - score_exact| over every centroid (see the file header).
+// hx, lx: ||xh||, ||xl|| of the row; cstat: the centroid-side maxima; KS k-steps of 32.
+//   split   : the products the three MFMAs leave out (xh tr, xl tl, xl tr, xr th, xr tl,
+//             xr tr), by Cauchy-Schwarz on the actual hi / lo norms, |r| <= 2^-8/(1-2^-8) |lo|
+//             (RNE to bf16: unit roundoff 2^-8);
+//   MFMAs   : measured per instruction <= 3.5 ulp(|C| + sum |a b|) (tools/probe_mfma_acc.hip,
+//             profiles/probe_mfma_acc_r05.txt), taken as 8 x 2^-23 (|C| + sum |a b|): the
+//             main chain (KS MFMAs from ||c||^2), the cross chain (2 KS MFMAs from 0) and the
+//             final add of the two;
+//   ||c||^2 : summed in fp64, one rounding to fp32;
+//   tag     : 4 index bits in the low mantissa of the score, <= 2^-19 |score|.
+__device__ __forceinline__ float x3_eps(float hx, float lx, const float* cstat, int KS) {
+  const float cn = cstat[0];
+  const float Hc = sqrtf(cstat[1]) * 1.0001f, Lc = sqrtf(cstat[2]) * 1.0001f;
+  constexpr float R8 = 0.00392157f;  // 2^-8 / (1 - 2^-8)
+  const float Rc = R8 * Lc, Rx = R8 * lx;
+  const float e_split = hx * Rc + lx * Lc + lx * Rc + Rx * Hc + Rx * Lc + Rx * Rc;
+  const float s_main = hx * Hc, s_cross = hx * Lc + lx * Hc;
+  constexpr float U8 = 8.f * 1.1920929e-7f;  // 8 x 2^-23
+  const float e_acc = U8 * ((float)KS * cn + (float)(KS + 1) * s_main) +
+                      U8 * (float)(2 * KS + 1) * s_cross +
+                      5.9604645e-8f * (cn + s_main + s_cross);  // final add, 2^-24
+  const float e_cn = 1.1920929e-7f * cn;
+  const float e_tag = 1.9073486e-6f * (cn + s_main + s_cross);  // 2^-19
+  return (e_split + e_acc + e_cn + e_tag) * 1.001f + 1e-30f;
 }
 
 // merge (v1, l1, v2, l2, v3) of two candidate sets (each v1 <= v2 <= v3, distinct centroids):
@@ -109,20 +169,28 @@ __device__ __forceinline__ void top3_merge(float& v1, int& l1, float& v2, int& l
   v3 = n3;
 }
 
-// one list entry per ambiguous row among the lanes with `amb` set: {row, runner-up (two-
-// candidate check) or -1 (full scan)}; one ballot + at most one atomic per wave
+// the lanes with `amb` set append their row: {row, runner-up} to list2 (two-candidate check,
+// count[0]) or row to listF (full exact re-scan, count[1]); per wave one ballot each and
+// at most one atomic each
 __device__ __forceinline__ void x3_append(bool amb, bool two, int64_t row, int l2,
-                                          int2* __restrict__ list, int* __restrict__ count) {
-  const unsigned long long mask = __ballot(amb);
-  if (mask == 0ull) return;
+                                          int2* __restrict__ list2, int* __restrict__ listF,
+                                          int* __restrict__ count) {
+  const unsigned long long m2 = __ballot(amb && two), mf = __ballot(amb && !two);
   const int lane = threadIdx.x & 63;
-  const int leader = __builtin_ctzll(mask);
-  int base = 0;
-  if (lane == leader) base = atomicAdd(count, __popcll(mask));
-  base = __shfl(base, leader, 64);
-  if (amb) {
-    const int idx = base + __popcll(mask & ((1ull << lane) - 1ull));
-    list[idx] = make_int2((int)row, two ? l2 : -1);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  if (m2) {
+    const int leader = __builtin_ctzll(m2);
+    int base = 0;
+    if (lane == leader) base = atomicAdd(count, __popcll(m2));
+    base = __shfl(base, leader, 64);
+    if (amb && two) list2[base + __popcll(m2 & below)] = make_int2((int)row, l2);
+  }
+  if (mf) {
+    const int leader = __builtin_ctzll(mf);
+    int base = 0;
+    if (lane == leader) base = atomicAdd(count + 1, __popcll(mf));
+    base = __shfl(base, leader, 64);
+    if (amb && !two) listF[base + __popcll(mf & below)] = (int)row;
   }
 }
 
@@ -137,8 +205,9 @@ template <int DP, int P, int NST, int QT>
 __global__ __launch_bounds__(256, 2) void assign_x3_ring_kernel(
     const __bf16* __restrict__ Xh, const __bf16* __restrict__ Xl, int64_t N,
     const __bf16* __restrict__ Ch, const __bf16* __restrict__ Cl, const float* __restrict__ cnorm,
-    int ntiles, const float* __restrict__ cmax2p, float tau, int32_t* __restrict__ labels,
-    float* __restrict__ mind, int2* __restrict__ amb, int* __restrict__ amb_count) {
+    int ntiles, const float* __restrict__ cstat, int32_t* __restrict__ labels,
+    float* __restrict__ mind, int2* __restrict__ amb, int* __restrict__ ambF,
+    int* __restrict__ amb_count) {
   constexpr int WAVES = 4;
   constexpr int BNL = 16 * QT;                 // centroids per stage
   constexpr int CPR = DP / 8;
@@ -218,22 +287,6 @@ __global__ __launch_bounds__(256, 2) void assign_x3_ring_kernel(
 #pragma unroll
   for (int t = 0; t < NST - 1; ++t) issue(t < ntiles ? t : ntiles - 1, t);
 
-  // ||x||^2 of the split row (the bound's ||x||; +||x||^2 turns a score into a distance)
-  float xs[P];
-#pragma unroll
-  for (int p = 0; p < P; ++p) {
-    float s = 0.f;
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float f = (float)bh[p][kk][j] + (float)bl[p][kk][j];
-        s = fmaf(f, f, s);
-      }
-    s += __shfl_xor(s, 16, 64);
-    xs[p] = s + __shfl_xor(s, 32, 64);
-  }
-
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * VPS) : "memory");
   __builtin_amdgcn_s_barrier();
 
@@ -279,7 +332,10 @@ __global__ __launch_bounds__(256, 2) void assign_x3_ring_kernel(
         ah1 = afrag(KS > 1 ? 1 : 0, H{});
         al1 = afrag(KS > 1 ? 1 : 0, L{});
       }
-      f32x4 acc[P];
+      // two chains: xh.th from ||c||^2 (the large terms, KS MFMAs) and the cross terms from
+      // 0 (2 KS MFMAs of ~2^-8 relative size), summed once: the large accumulator sees KS
+      // roundings instead of 3 KS (the bound x3_eps)
+      f32x4 acc[P], acx[P];
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) {
         bf16x8 ah2 = ah1, al2 = al1;
@@ -296,15 +352,16 @@ __global__ __launch_bounds__(256, 2) void assign_x3_ring_kernel(
           __builtin_amdgcn_s_barrier();
         }
         __builtin_amdgcn_sched_barrier(0);
+        const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int p = 0; p < P; ++p)
           acc[p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah0, bh[p][kk], kk == 0 ? n4 : acc[p], 0, 0, 0);
 #pragma unroll
         for (int p = 0; p < P; ++p)
-          acc[p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah0, bl[p][kk], acc[p], 0, 0, 0);
+          acx[p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah0, bl[p][kk], kk == 0 ? z4 : acx[p], 0, 0, 0);
 #pragma unroll
         for (int p = 0; p < P; ++p)
-          acc[p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al0, bh[p][kk], acc[p], 0, 0, 0);
+          acx[p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al0, bh[p][kk], acx[p], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
         ah0 = ah1;
         al0 = al1;
@@ -316,7 +373,8 @@ __global__ __launch_bounds__(256, 2) void assign_x3_ring_kernel(
       for (int p = 0; p < P; ++p) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float v = __uint_as_float((__float_as_uint(acc[p][i]) & ~EMB) | (unsigned)(q * 4 + i));
+          const float v = __uint_as_float((__float_as_uint(acc[p][i] + acx[p][i]) & ~EMB) |
+                                          (unsigned)(q * 4 + i));
           m3[p] = __builtin_amdgcn_fmed3f(m2[p], m3[p], v);
           m2[p] = __builtin_amdgcn_fmed3f(m1[p], m2[p], v);
           m1[p] = __builtin_fminf(m1[p], v);
@@ -349,10 +407,23 @@ __global__ __launch_bounds__(256, 2) void assign_x3_ring_kernel(
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  const float cmax2 = cmax2p[0] * (1.f + 1.f / 4096.f);
-  const float cmax = sqrtf(cmax2);
 #pragma unroll
   for (int p = 0; p < P; ++p) {
+    // ||xh||^2 and ||xl||^2 of the row (the per-row error bound), from the fragments still in
+    // registers (computed here, not before the K loop: no registers held through it)
+    float sh = 0.f, sl = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float fh = (float)bh[p][kk][j], fl = (float)bl[p][kk][j];
+        sh = fmaf(fh, fh, sh);
+        sl = fmaf(fl, fl, sl);
+      }
+    sh += __shfl_xor(sh, 16, 64);
+    sl += __shfl_xor(sl, 16, 64);
+    sh += __shfl_xor(sh, 32, 64);
+    sl += __shfl_xor(sl, 32, 64);
     const unsigned e1 = __float_as_uint(B1[p]) & EMB, e2 = __float_as_uint(B2[p]) & EMB;
     int l1 = T1[p] * BNL + (int)(e1 >> 2) * 16 + 4 * g + (int)(e1 & 3);
     int l2 = T2[p] * BNL + (int)(e2 >> 2) * 16 + 4 * g + (int)(e2 & 3);
@@ -365,27 +436,53 @@ __global__ __launch_bounds__(256, 2) void assign_x3_ring_kernel(
                  __shfl_xor(v2, o, 64), __shfl_xor(l2, o, 64), __shfl_xor(v3, o, 64));
     const int64_t row = pbase + p * 16 + r;
     const bool valid = g == 0 && row < N;
-    const float xb = sqrtf(xs[p]) * (1.f + 1.f / 1024.f);
-    const float eps2 = 2.f * tau * (cmax2 + 2.f * xb * cmax) + 1e-30f;
-    if (valid) {
-      labels[row] = l1;
-      if (mind) mind[row] = fmaxf(v1 + xs[p], 0.f);
+    const float eps2 = 2.f * x3_eps(sqrtf(sh) * 1.0001f, sqrtf(sl) * 1.0001f, cstat, KS);
+    if (mind) {  // + ||xh + xl||^2 turns the score into a distance (uniform branch)
+      float sx = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = (float)bh[p][kk][j] + (float)bl[p][kk][j];
+          sx = fmaf(f, f, sx);
+        }
+      sx += __shfl_xor(sx, 16, 64);
+      sx += __shfl_xor(sx, 32, 64);
+      if (valid) mind[row] = fmaxf(v1 + sx, 0.f);
     }
-    x3_append(valid && !(v2 - v1 > eps2), v3 - v1 > eps2, row, l2, amb, amb_count);
+    if (valid) labels[row] = l1;
+    x3_append(valid && !(v2 - v1 > eps2), v3 - v1 > eps2, row, l2, amb, ambF, amb_count);
   }
 }
 
 // ------------------------------------------------------------------------------------
 // wide D: top-3 / list pass over a chunk's raw d2 block G [M, K] (one wave per row)
 // ------------------------------------------------------------------------------------
+// The block comes from fcm_wide_dist_kernel: ONE accumulator per element from ||x||^2 +
+// ||c||^2 through all 3 DP / 16 MFMAs (32x32x16), no tag.  The row's hi/lo norms are not at
+// hand here, so the split term takes the worst case (||xh|| <= ||x||, ||xl|| <= 2^-8 ||x||).
+__device__ __forceinline__ float x3_eps_wide(float xb, float xn, const float* cstat, int nmf) {
+  const float cn = cstat[0];
+  const float Hc = sqrtf(cstat[1]) * 1.0001f, Lc = sqrtf(cstat[2]) * 1.0001f;
+  constexpr float R8 = 0.00392157f;
+  const float hx = xb * 1.004f, lx = R8 * xb;
+  const float Rc = R8 * Lc, Rx = R8 * lx;
+  const float e_split = hx * Rc + lx * Lc + lx * Rc + Rx * Hc + Rx * Lc + Rx * Rc;
+  const float s_all = hx * Hc + hx * Lc + lx * Hc;
+  constexpr float U8 = 8.f * 1.1920929e-7f;
+  const float e_acc = U8 * ((float)nmf * (xn + cn) + (float)(nmf + 1) * s_all);
+  const float e_norm = 1.1920929e-7f * (xn + cn) * 2.f;
+  return (e_split + e_acc + e_norm) * 1.001f + 1e-30f;
+}
+
 __global__ __launch_bounds__(256) void x3_rows_kernel(const float* __restrict__ G, int64_t M, int K,
                                                       int64_t row0, const float* __restrict__ xx,
-                                                      const float* __restrict__ cmax2p, float tau,
+                                                      const float* __restrict__ cstat, int nmf,
                                                       int32_t* __restrict__ labels,
                                                       int2* __restrict__ amb,
+                                                      int* __restrict__ ambF,
                                                       int* __restrict__ amb_count) {
   const int lane = threadIdx.x & 63;
-  const float cmax = sqrtf(cmax2p[0] * (1.f + 1.f / 4096.f));
   const int64_t nw = (int64_t)gridDim.x * 4;
   for (int64_t i0 = (int64_t)blockIdx.x * 4; i0 < M; i0 += nw) {
     const int64_t i = i0 + (threadIdx.x >> 6);
@@ -411,91 +508,59 @@ __global__ __launch_bounds__(256) void x3_rows_kernel(const float* __restrict__ 
     const bool valid = live && lane == 0;
     float eps2 = 0.f;
     if (live) {
-      const float xb = sqrtf(xx[i]) * (1.f + 1.f / 1024.f);
-      eps2 = 2.f * tau * (xb + cmax) * (xb + cmax) + 1e-30f;
+      const float xn = xx[i];
+      eps2 = 2.f * x3_eps_wide(sqrtf(xn) * 1.0001f, xn, cstat, nmf);
     }
     if (valid) labels[row0 + i] = l1 < K ? l1 : 0;
-    x3_append(valid && !(v2 - v1 > eps2), v3 - v1 > eps2, row0 + i, l2, amb, amb_count);
+    x3_append(valid && !(v2 - v1 > eps2), v3 - v1 > eps2, row0 + i, l2, amb, ambF, amb_count);
   }
 }
 
 // ------------------------------------------------------------------------------------
-// exact re-check of the listed rows (one wave per entry, grid-stride over the device count)
+// exact re-check of the two-candidate rows (one wave per entry, grid-stride over the device
+// count); the full re-scans run lloyd_simt.hip's tiled exact kernel over listF
 // ------------------------------------------------------------------------------------
 constexpr int X3_MAXD = 1024;
 
 template <typename T>
 __global__ __launch_bounds__(256) void x3_recheck_kernel(const T* __restrict__ X, int64_t ldx, int D,
-                                                         const T* __restrict__ C, int K,
+                                                         const T* __restrict__ C,
                                                          int32_t* __restrict__ labels,
                                                          const int2* __restrict__ amb,
                                                          const int* __restrict__ amb_count) {
-  __shared__ T s_x[4][X3_MAXD];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int n = amb_count[0];
   for (int64_t e = (int64_t)blockIdx.x * 4 + w; e < n; e += (int64_t)gridDim.x * 4) {
     const int2 a = amb[e];
     const int64_t row = a.x;
     const T* x = X + row * ldx;
-    const int l1 = labels[row];
-    if (a.y >= 0) {  // the exact winner is one of the two smallest scores
-      const int l2 = a.y;
-      const T* c1 = C + (int64_t)l1 * D;
-      const T* c2 = C + (int64_t)l2 * D;
-      T s1 = 0, s2 = 0;
-      for (int d = lane; d < D; d += 64) {
-        const T xv = x[d];
-        const T e1 = xv - c1[d], e2 = xv - c2[d];
-        s1 = fma(e1, e1, s1);
-        s2 = fma(e2, e2, s2);
-      }
-      s1 = wave_sum(s1);
-      s2 = wave_sum(s2);
-      if (lane == 0 && (s2 < s1 || (s2 == s1 && l2 < l1))) labels[row] = l2;
-      continue;
+    const int l1 = labels[row], l2 = a.y;
+    const T* c1 = C + (int64_t)l1 * D;
+    const T* c2 = C + (int64_t)l2 * D;
+    T s1 = 0, s2 = 0;
+    for (int d = lane; d < D; d += 64) {
+      const T xv = x[d];
+      const T e1 = xv - c1[d], e2 = xv - c2[d];
+      s1 = fma(e1, e1, s1);
+      s2 = fma(e2, e2, s2);
     }
-    // full scan: row in LDS (wave-private), lanes over centroids
-    for (int d = lane; d < D; d += 64) s_x[w][d] = x[d];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    T best = (T)INFINITY;
-    int bk = K;
-    for (int k = lane; k < K; k += 64) {
-      const T* c = C + (int64_t)k * D;
-      T s = 0;
-      for (int d = 0; d < D; ++d) {
-        const T ev = s_x[w][d] - c[d];
-        s = fma(ev, ev, s);
-      }
-      if (s < best) {
-        best = s;
-        bk = k;
-      }
-    }
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const T ob = __shfl_xor(best, o, 64);
-      const int ok = __shfl_xor(bk, o, 64);
-      const bool take = ob < best || (ob == best && ok < bk);
-      best = take ? ob : best;
-      bk = take ? ok : bk;
-    }
-    if (lane == 0 && bk < K) labels[row] = bk;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();  // s_x reads done before the next entry overwrites it
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (lane == 0 && (s2 < s1 || (s2 == s1 && l2 < l1))) labels[row] = l2;
   }
 }
 
 template <int DP, int P, int NST, int QT>
 int launch_x3(const void* Xh, const void* Xl, int64_t N, const void* Ch, const void* Cl,
-              const float* cnorm, int Kp, const float* cmax2, float tau, int32_t* labels,
-              float* mind, int2* amb, int* amb_count, hipStream_t s) {
+              const float* cnorm, int Kp, const float* cstat, int32_t* labels,
+              float* mind, int2* amb, int* ambF, int* amb_count, hipStream_t s) {
   constexpr int BNL = 16 * QT;
   if (Kp % BNL != 0) return (int)hipErrorInvalidValue;
   const int64_t per = 4 * P * 16;
   hipLaunchKernelGGL((assign_x3_ring_kernel<DP, P, NST, QT>), dim3((unsigned)((N + per - 1) / per)),
                      dim3(256), 0, s, (const __bf16*)Xh, (const __bf16*)Xl, N, (const __bf16*)Ch,
-                     (const __bf16*)Cl, cnorm, Kp / BNL, cmax2, tau, labels, mind, amb, amb_count);
+                     (const __bf16*)Cl, cnorm, Kp / BNL, cstat, labels, mind, amb, ambF,
+                     amb_count);
   TDC_CHECK_LAUNCH();
   return 0;
 }
@@ -505,74 +570,82 @@ int launch_x3(const void* Xh, const void* Xl, int64_t N, const void* Ch, const v
 
 using namespace tdc;
 
-float tdc_x3_tau(int DP) {
-  return (float)((4.0 * DP + 64.0) * ldexp(1.0, -23) + ldexp(1.0, -16));
-}
-
 int tdc_x3_split(int src_dtype, const void* src, int64_t rows, int64_t valid, int d, int64_t ld,
-                 int DP, int neg2, void* hi, void* lo, float* norm, hipStream_t s) {
+                 int DP, int neg2, void* hi, void* lo, float* norm, float* nhl, hipStream_t s) {
   if (rows <= 0) return 0;
   if (d > DP || DP % 32 != 0) return (int)hipErrorInvalidValue;
   int64_t blocks = (rows + 3) / 4;
   if (blocks > 16384) blocks = 16384;
   if (src_dtype == TDC_F32)
     hipLaunchKernelGGL(x3_split_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s,
-                       (const float*)src, rows, valid, d, ld, DP, neg2, (__bf16*)hi, (__bf16*)lo, norm);
+                       (const float*)src, rows, valid, d, ld, DP, neg2, (__bf16*)hi, (__bf16*)lo, norm,
+                       (float2*)nhl);
   else if (src_dtype == TDC_F64)
     hipLaunchKernelGGL(x3_split_kernel<double>, dim3((unsigned)blocks), dim3(256), 0, s,
-                       (const double*)src, rows, valid, d, ld, DP, neg2, (__bf16*)hi, (__bf16*)lo, norm);
+                       (const double*)src, rows, valid, d, ld, DP, neg2, (__bf16*)hi, (__bf16*)lo, norm,
+                       (float2*)nhl);
   else
     return (int)hipErrorInvalidValue;
   TDC_CHECK_LAUNCH();
   return 0;
 }
 
-int tdc_x3_prep(const float* cnorm, int K, float* cmax2, int* amb_count, hipStream_t s) {
-  hipLaunchKernelGGL(x3_prep_kernel, dim3(1), dim3(1024), 0, s, cnorm, K, cmax2, amb_count);
+int tdc_x3_prep(const float* cnorm, const float* nhl, int K, float* cstat, int* amb_count,
+                hipStream_t s) {
+  hipLaunchKernelGGL(x3_prep_kernel, dim3(1), dim3(1024), 0, s, cnorm, (const float2*)nhl, K,
+                     cstat, amb_count);
   TDC_CHECK_LAUNCH();
   return 0;
 }
 
+// amb: int32 [3 cap] = list2 (int2 [cap]) | listF (int32 [cap]); amb_count int32 [2]
 int tdc_assign_x3(const void* Xh, const void* Xl, int64_t N, int DP, const void* Ch, const void* Cl,
-                  const float* cnorm, int Kp, const float* cmax2, float tau, int32_t* labels,
-                  float* mind, int2* amb, int* amb_count, hipStream_t s) {
+                  const float* cnorm, int Kp, const float* cstat, int32_t* labels,
+                  float* mind, int32_t* amb, int64_t cap, int* amb_count, hipStream_t s) {
   if (N <= 0) return 0;
-  if (N >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  if (N >= ((int64_t)1 << 31) || cap < N) return (int)hipErrorInvalidValue;
+  int2* l2 = reinterpret_cast<int2*>(amb);
+  int* lf = amb + 2 * cap;
   switch (DP) {
     // LDS per stage: 2 images x 64 centroids x DP x 2 B; two workgroups (8 waves) per CU
-    case 32: return launch_x3<32, 8, 3, 4>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cmax2, tau, labels, mind, amb, amb_count, s);
-    case 64: return launch_x3<64, 6, 3, 4>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cmax2, tau, labels, mind, amb, amb_count, s);
-    case 128: return launch_x3<128, 4, 2, 4>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cmax2, tau, labels, mind, amb, amb_count, s);
-    case 256: return launch_x3<256, 2, 2, 2>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cmax2, tau, labels, mind, amb, amb_count, s);
+    case 32: return launch_x3<32, 6, 3, 4>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cstat, labels, mind, l2, lf, amb_count, s);
+    case 64: return launch_x3<64, 6, 3, 4>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cstat, labels, mind, l2, lf, amb_count, s);
+    case 128: return launch_x3<128, 4, 2, 4>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cstat, labels, mind, l2, lf, amb_count, s);
+    case 256: return launch_x3<256, 2, 2, 2>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cstat, labels, mind, l2, lf, amb_count, s);
   }
   return (int)hipErrorInvalidValue;
 }
 
-int tdc_x3_rows(const float* G, int64_t M, int K, int64_t row0, const float* xx, const float* cmax2,
-                float tau, int32_t* labels, int2* amb, int* amb_count, hipStream_t s) {
+int tdc_x3_rows(const float* G, int64_t M, int K, int64_t row0, const float* xx, const float* cstat,
+                int DP, int32_t* labels, int32_t* amb, int64_t cap, int* amb_count, hipStream_t s) {
   if (M <= 0) return 0;
-  if (row0 + M >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  if (row0 + M >= ((int64_t)1 << 31) || cap < row0 + M) return (int)hipErrorInvalidValue;
   int64_t blocks = (M + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(x3_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, s, G, M, K, row0, xx,
-                     cmax2, tau, labels, amb, amb_count);
+                     cstat, 3 * DP / 16, labels, reinterpret_cast<int2*>(amb), amb + 2 * cap,
+                     amb_count);
   TDC_CHECK_LAUNCH();
   return 0;
 }
 
 int tdc_x3_recheck(int dtype, const void* X, int64_t ldx, int D, const void* C, int K,
-                   int32_t* labels, const int2* amb, const int* amb_count, int num_cus,
-                   hipStream_t s) {
+                   int32_t* labels, const int32_t* amb, int64_t cap, const int* amb_count,
+                   int num_cus, hipStream_t s) {
   if (D > X3_MAXD || D <= 0) return (int)hipErrorInvalidValue;
   const dim3 grid((unsigned)(num_cus * 4));
+  const int2* l2 = reinterpret_cast<const int2*>(amb);
   if (dtype == TDC_F32)
     hipLaunchKernelGGL(x3_recheck_kernel<float>, grid, dim3(256), 0, s, (const float*)X, ldx, D,
-                       (const float*)C, K, labels, amb, amb_count);
+                       (const float*)C, labels, l2, amb_count);
   else if (dtype == TDC_F64)
     hipLaunchKernelGGL(x3_recheck_kernel<double>, grid, dim3(256), 0, s, (const double*)X, ldx, D,
-                       (const double*)C, K, labels, amb, amb_count);
+                       (const double*)C, labels, l2, amb_count);
   else
     return (int)hipErrorInvalidValue;
   TDC_CHECK_LAUNCH();
-  return 0;
+  // the rows with a third candidate inside the bound: exact re-scan over all K (tiled SIMT
+  // difference form over the listed rows, their count read on the device)
+  return tdc_assign_exact(dtype, X, cap, ldx, D, C, K, labels, nullptr, num_cus, s, amb + 2 * cap,
+                          amb_count + 1);
 }

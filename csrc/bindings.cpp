@@ -623,10 +623,8 @@ void update_sorted_indexed(const at::Tensor& X, const at::Tensor& rowidx, const 
 }
 
 // ---- fp32 / fp64 assignment on the matrix cores (kernels.h tdc_x3_*) ----
-double x3_tau(int64_t DP) { return (double)tdc_x3_tau((int)DP); }
-
 void x3_split(const at::Tensor& src, int64_t valid, int64_t neg2, at::Tensor& hi, at::Tensor& lo,
-              const std::optional<at::Tensor>& norm) {
+              const std::optional<at::Tensor>& norm, const std::optional<at::Tensor>& nhl) {
   check_cuda(src, "src");
   check_rows(src, "src");
   TORCH_CHECK(src.scalar_type() == at::kFloat || src.scalar_type() == at::kDouble,
@@ -640,31 +638,42 @@ void x3_split(const at::Tensor& src, int64_t valid, int64_t neg2, at::Tensor& hi
   if (norm.has_value() && norm->defined())
     TORCH_CHECK(norm->scalar_type() == at::kFloat && norm->is_contiguous() && norm->numel() >= rows,
                 "tdc.x3_split: norm fp32 [rows]");
+  if (nhl.has_value() && nhl->defined())
+    TORCH_CHECK(nhl->scalar_type() == at::kFloat && nhl->is_contiguous() && nhl->numel() >= 2 * rows,
+                "tdc.x3_split: nhl fp32 [rows, 2]");
   const DevGuard guard(src.device());
   check(tdc_x3_split(dcode(src.scalar_type()), src.data_ptr(), rows, valid, (int)src.size(1),
                      src.stride(0), DP, (int)neg2, hi.data_ptr(), lo.data_ptr(),
-                     static_cast<float*>(opt_ptr(norm)), cur_stream()),
+                     static_cast<float*>(opt_ptr(norm)), static_cast<float*>(opt_ptr(nhl)),
+                     cur_stream()),
         "x3_split");
 }
 
-void check_x3_state(const at::Tensor& cmax2, const at::Tensor& amb, const at::Tensor& amb_count,
-                    int64_t rows, const char* op) {
-  TORCH_CHECK(cmax2.scalar_type() == at::kFloat && cmax2.numel() >= 1, "tdc.", op, ": cmax2 fp32 [1]");
-  TORCH_CHECK(amb_count.scalar_type() == at::kInt && amb_count.numel() >= 1, "tdc.", op,
-              ": amb_count int32 [1]");
-  TORCH_CHECK(amb.scalar_type() == at::kInt && amb.is_contiguous() && amb.numel() >= 2 * rows,
-              "tdc.", op, ": amb int32 [2 * rows]");
+// amb: int32 [3 cap] (two-candidate int2 entries | full re-scan rows), amb_count int32 [2]
+int64_t check_x3_state(const at::Tensor& cstat, const at::Tensor& amb, const at::Tensor& amb_count,
+                       int64_t rows, const char* op) {
+  TORCH_CHECK(cstat.scalar_type() == at::kFloat && cstat.numel() >= 3, "tdc.", op, ": cstat fp32 [3]");
+  TORCH_CHECK(amb_count.scalar_type() == at::kInt && amb_count.numel() >= 2, "tdc.", op,
+              ": amb_count int32 [2]");
+  TORCH_CHECK(amb.scalar_type() == at::kInt && amb.is_contiguous() && amb.numel() % 3 == 0 &&
+                  amb.numel() >= 3 * rows,
+              "tdc.", op, ": amb int32 [3 * capacity >= 3 * rows]");
+  return amb.numel() / 3;
 }
 
-void x3_prep(const at::Tensor& cnorm, int64_t K, at::Tensor& cmax2, at::Tensor& amb_count) {
+void x3_prep(const at::Tensor& cnorm, const std::optional<at::Tensor>& nhl, int64_t K,
+             at::Tensor& cstat, at::Tensor& amb_count) {
   check_cuda(cnorm, "cnorm");
   TORCH_CHECK(cnorm.scalar_type() == at::kFloat && cnorm.is_contiguous() && cnorm.numel() >= K,
               "tdc.x3_prep: cnorm fp32 [>= K]");
-  TORCH_CHECK(cmax2.scalar_type() == at::kFloat && amb_count.scalar_type() == at::kInt,
-              "tdc.x3_prep: cmax2 fp32, amb_count int32");
+  if (nhl.has_value() && nhl->defined())
+    TORCH_CHECK(nhl->scalar_type() == at::kFloat && nhl->numel() >= 2 * K, "tdc.x3_prep: nhl");
+  TORCH_CHECK(cstat.scalar_type() == at::kFloat && cstat.numel() >= 3 &&
+                  amb_count.scalar_type() == at::kInt && amb_count.numel() >= 2,
+              "tdc.x3_prep: cstat fp32 [3], amb_count int32 [2]");
   const DevGuard guard(cnorm.device());
-  check(tdc_x3_prep(cnorm.data_ptr<float>(), (int)K, cmax2.data_ptr<float>(),
-                    amb_count.data_ptr<int>(), cur_stream()),
+  check(tdc_x3_prep(cnorm.data_ptr<float>(), static_cast<const float*>(opt_ptr(nhl)), (int)K,
+                    cstat.data_ptr<float>(), amb_count.data_ptr<int>(), cur_stream()),
         "x3_prep");
 }
 
@@ -678,22 +687,22 @@ void x3_recheck(const at::Tensor& X, const at::Tensor& C, at::Tensor& labels, co
               "tdc.x3_recheck: C [K, D <= 1024] in the X dtype");
   TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous() && labels.numel() >= X.size(0),
               "tdc.x3_recheck: labels int32 [N]");
-  TORCH_CHECK(amb.scalar_type() == at::kInt && amb.is_contiguous() && amb.numel() >= 2 * X.size(0) &&
-                  amb_count.scalar_type() == at::kInt,
-              "tdc.x3_recheck: amb int32 [2N], amb_count int32 [1]");
+  TORCH_CHECK(amb.scalar_type() == at::kInt && amb.is_contiguous() && amb.numel() % 3 == 0 &&
+                  amb_count.scalar_type() == at::kInt && amb_count.numel() >= 2,
+              "tdc.x3_recheck: amb int32 [3 cap], amb_count int32 [2]");
   const DevGuard guard(X.device());
   check(tdc_x3_recheck(dcode(X.scalar_type()), X.data_ptr(), X.stride(0), (int)C.size(1), C.data_ptr(),
-                       (int)C.size(0), labels.data_ptr<int32_t>(),
-                       reinterpret_cast<const int2*>(amb.data_ptr<int>()), amb_count.data_ptr<int>(),
-                       num_cus(X.device().index()), cur_stream()),
+                       (int)C.size(0), labels.data_ptr<int32_t>(), amb.data_ptr<int>(),
+                       amb.numel() / 3, amb_count.data_ptr<int>(), num_cus(X.device().index()),
+                       cur_stream()),
         "x3_recheck");
 }
 
 // prep (cmax, list reset) + bf16x3 assignment + exact re-check of the listed rows
 void x3_assign(const at::Tensor& X, const at::Tensor& Xh, const at::Tensor& Xl, const at::Tensor& Ch,
-               const at::Tensor& Cl, const at::Tensor& cnorm, const at::Tensor& C, at::Tensor& labels,
-               const std::optional<at::Tensor>& mind, at::Tensor& amb, at::Tensor& cmax2,
-               at::Tensor& amb_count, bool recheck) {
+               const at::Tensor& Cl, const at::Tensor& cnorm, const at::Tensor& cnhl,
+               const at::Tensor& C, at::Tensor& labels, const std::optional<at::Tensor>& mind,
+               at::Tensor& amb, at::Tensor& cstat, at::Tensor& amb_count, bool recheck) {
   check_cuda(Xh, "Xh");
   TORCH_CHECK(Xh.scalar_type() == at::kBFloat16 && Xl.scalar_type() == at::kBFloat16 &&
                   Ch.scalar_type() == at::kBFloat16 && Cl.scalar_type() == at::kBFloat16,
@@ -713,7 +722,9 @@ void x3_assign(const at::Tensor& X, const at::Tensor& Xh, const at::Tensor& Xl, 
   TORCH_CHECK(K <= Kp && C.size(1) <= DP, "tdc.x3_assign: C [K <= Kp, D <= DP]");
   TORCH_CHECK(labels.scalar_type() == at::kInt && labels.is_contiguous() && labels.numel() >= N,
               "tdc.x3_assign: labels int32 [N]");
-  check_x3_state(cmax2, amb, amb_count, N, "x3_assign");
+  const int64_t cap = check_x3_state(cstat, amb, amb_count, N, "x3_assign");
+  TORCH_CHECK(cnhl.scalar_type() == at::kFloat && cnhl.is_contiguous() && cnhl.numel() >= 2 * K,
+              "tdc.x3_assign: cnhl fp32 [K, 2] (centroid hi/lo norms)");
   float* md = nullptr;
   if (mind.has_value() && mind->defined()) {
     TORCH_CHECK(mind->scalar_type() == at::kFloat && mind->numel() >= N && mind->is_contiguous(),
@@ -728,32 +739,33 @@ void x3_assign(const at::Tensor& X, const at::Tensor& Xh, const at::Tensor& Xl, 
   }
   const DevGuard guard(Xh.device());
   hipStream_t s = cur_stream();
-  int2* list = reinterpret_cast<int2*>(amb.data_ptr<int>());
-  check(tdc_x3_prep(cnorm.data_ptr<float>(), K, cmax2.data_ptr<float>(), amb_count.data_ptr<int>(), s),
+  int32_t* list = amb.data_ptr<int>();
+  check(tdc_x3_prep(cnorm.data_ptr<float>(), cnhl.data_ptr<float>(), K, cstat.data_ptr<float>(),
+                    amb_count.data_ptr<int>(), s),
         "x3_prep");
   check(tdc_assign_x3(Xh.data_ptr(), Xl.data_ptr(), N, DP, Ch.data_ptr(), Cl.data_ptr(),
-                      cnorm.data_ptr<float>(), Kp, cmax2.data_ptr<float>(), tdc_x3_tau(DP),
-                      labels.data_ptr<int32_t>(), md, list, amb_count.data_ptr<int>(), s),
+                      cnorm.data_ptr<float>(), Kp, cstat.data_ptr<float>(),
+                      labels.data_ptr<int32_t>(), md, list, cap, amb_count.data_ptr<int>(), s),
         "assign_x3");
   if (recheck)
     check(tdc_x3_recheck(dcode(X.scalar_type()), X.data_ptr(), X.stride(0), (int)C.size(1), C.data_ptr(),
-                         K, labels.data_ptr<int32_t>(), list, amb_count.data_ptr<int>(),
+                         K, labels.data_ptr<int32_t>(), list, cap, amb_count.data_ptr<int>(),
                          num_cus(X.device().index()), s),
           "x3_recheck");
 }
 
-void x3_rows(const at::Tensor& G, int64_t row0, const at::Tensor& xx, const at::Tensor& cmax2,
-             double tau, at::Tensor& labels, at::Tensor& amb, at::Tensor& amb_count) {
+void x3_rows(const at::Tensor& G, int64_t row0, const at::Tensor& xx, const at::Tensor& cstat,
+             int64_t DP, at::Tensor& labels, at::Tensor& amb, at::Tensor& amb_count) {
   check_cuda(G, "G");
   TORCH_CHECK(G.scalar_type() == at::kFloat && G.is_contiguous() && G.dim() == 2, "tdc.x3_rows: G fp32 [M, K]");
   const int64_t M = G.size(0);
   TORCH_CHECK(xx.scalar_type() == at::kFloat && xx.numel() >= M, "tdc.x3_rows: xx fp32 [M]");
   TORCH_CHECK(labels.scalar_type() == at::kInt && labels.numel() >= row0 + M, "tdc.x3_rows: labels");
-  check_x3_state(cmax2, amb, amb_count, row0 + M, "x3_rows");
+  const int64_t cap = check_x3_state(cstat, amb, amb_count, row0 + M, "x3_rows");
   const DevGuard guard(G.device());
   check(tdc_x3_rows(G.data_ptr<float>(), M, (int)G.size(1), row0, xx.data_ptr<float>(),
-                    cmax2.data_ptr<float>(), (float)tau, labels.data_ptr<int32_t>(),
-                    reinterpret_cast<int2*>(amb.data_ptr<int>()), amb_count.data_ptr<int>(), cur_stream()),
+                    cstat.data_ptr<float>(), (int)DP, labels.data_ptr<int32_t>(),
+                    amb.data_ptr<int>(), cap, amb_count.data_ptr<int>(), cur_stream()),
         "x3_rows");
 }
 
@@ -1151,11 +1163,10 @@ TORCH_LIBRARY(tdc, m) {
   m.def("delta_update(Tensor X, Tensor labels, Tensor(a!) prev, Tensor(b!) sums, Tensor(c!) counts, Tensor(d!) work, Tensor(e!) ctrl, Tensor(f!)? cnt_hi=None, Tensor(g!)? cnt_lo=None, Tensor(h!)? moved=None, Tensor(i!)? zero_first=None, float fixed_scale=0.0, bool work_clean=False) -> ()");
   m.def("delta_finalize(Tensor sums, Tensor counts, Tensor? cnt_hi, Tensor? cnt_lo, Tensor? moved, Tensor(a!) G, Tensor(b!) C, int policy, Tensor(c!)? shift, Tensor(d!)? Cm2, Tensor(e!)? cnorm, Tensor(f!) ctrl, Tensor(g!)? stats, int refresh, float theta_n, float fixed_scale=0.0) -> ()");
   m.def("sculley_update(Tensor sums, Tensor counts, Tensor(a!) C, Tensor(b!) v, Tensor(c!)? shift, Tensor(d!)? Cm2, Tensor(e!)? cnorm) -> ()");
-  m.def("x3_tau(int DP) -> float", &x3_tau);
-  m.def("x3_split(Tensor src, int valid, int neg2, Tensor(a!) hi, Tensor(b!) lo, Tensor(c!)? norm) -> ()");
-  m.def("x3_prep(Tensor cnorm, int K, Tensor(a!) cmax2, Tensor(b!) amb_count) -> ()");
-  m.def("x3_assign(Tensor X, Tensor Xh, Tensor Xl, Tensor Ch, Tensor Cl, Tensor cnorm, Tensor C, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!) amb, Tensor(d!) cmax2, Tensor(e!) amb_count, bool recheck=True) -> ()");
-  m.def("x3_rows(Tensor G, int row0, Tensor xx, Tensor cmax2, float tau, Tensor(a!) labels, Tensor(b!) amb, Tensor(c!) amb_count) -> ()");
+  m.def("x3_split(Tensor src, int valid, int neg2, Tensor(a!) hi, Tensor(b!) lo, Tensor(c!)? norm, Tensor(d!)? nhl=None) -> ()");
+  m.def("x3_prep(Tensor cnorm, Tensor? nhl, int K, Tensor(a!) cstat, Tensor(b!) amb_count) -> ()");
+  m.def("x3_assign(Tensor X, Tensor Xh, Tensor Xl, Tensor Ch, Tensor Cl, Tensor cnorm, Tensor cnhl, Tensor C, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!) amb, Tensor(d!) cstat, Tensor(e!) amb_count, bool recheck=True) -> ()");
+  m.def("x3_rows(Tensor G, int row0, Tensor xx, Tensor cstat, int DP, Tensor(a!) labels, Tensor(b!) amb, Tensor(c!) amb_count) -> ()");
   m.def("x3_recheck(Tensor X, Tensor C, Tensor(a!) labels, Tensor amb, Tensor amb_count) -> ()");
 }
 

@@ -17,6 +17,9 @@
 //   fcm_wide_wtx  W^T X and sum W: 64-centroid x 64-feature output tiles over a row range,
 //                 32-row W / X slabs through LDS, 4 x 4 fp64 micro-tiles, one atomic per
 //                 output per block
+// fp64 runs the two GEMM-shaped passes on the f64 matrix cores instead
+// (fcm_wide_d2_f64m_kernel: the expansion ||x||^2 + ||c||^2 - 2 x.c with a rigorous zero
+// floor; fcm_wide_wtx_f64m_kernel), see below.
 //
 // The chunk is sized by the caller (ops.HipWideFCM: 2^27 elements of [rows, K]).
 #include "tdc_common.h"
@@ -240,10 +243,269 @@ __global__ __launch_bounds__(256) void fcm_wide_wtx_kernel(const T* __restrict__
   if (dt == 0 && tid < TK && k0 + tid < K && wsum != 0.0) atomicAdd(&ws[k0 + tid], wsum);
 }
 
+// ---------------------------------------------------------------------------------------
+// fp64 on the matrix cores (v_mfma_f64_16x16x4_f64): the reference's per-GPU DGEMM
+// (`MatMul(MU, X)`, scripts/distribuitedClustering.py:133) and its distances as GEMMs.
+// On MI355X the f64 MFMA runs at the f64 vector FMA rate, so what it buys is the
+// instruction count: one MFMA is 1024 multiply-adds (a wave-wide v_fma_f64 is 64), the
+// distance becomes the GEMM expansion ||x||^2 + ||c||^2 - 2 x.c (one product per element
+// and feature instead of a subtract + FMA), and the W^T X partials stay in 16 accumulator
+// tiles per wave (no per-output LDS traffic).  128 x 128 output tiles, 4 waves (2 x 2) of
+// 4 x 4 16x16 MFMA tiles each, 16-deep stages double-buffered through LDS.
+// f64 16x16x4 lane maps (cdna_hip_programming.md §3): A[i = l&15][k = l>>4],
+// B[k = l>>4][j = l&15], C/D: col = l&15, row = (l>>4) + 4 reg.
+// ---------------------------------------------------------------------------------------
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+constexpr int F64T = 128;  // output tile edge
+constexpr int F64S = 16;   // reduction depth per LDS stage
+
+// G[r, k] = d2 for rows [0, M) x centroids (grid: XCD-grouped (row tile, centroid tile)).
+// The norms are summed from the staged tiles (the kernel sees every feature of its rows
+// and centroids).  The expansion's rounding is at most (3D + 4) 2^-53 (||x|| + ||c||)^2 for
+// any summation order; a d2 below that bound is indistinguishable from 0 and stored as 0,
+// so a point on a centroid keeps the difference form's exact zero (the on-centroid rule
+// of fcm_wide_rows: NaN -> 0 or one-hot).
+__global__ __launch_bounds__(256, 1) void fcm_wide_d2_f64m_kernel(
+    const double* __restrict__ X, int64_t M, int64_t ldx, int D, const double* __restrict__ C,
+    int K, int nct, double* __restrict__ G) {
+  constexpr int PX = F64S + 2;  // 144-B rows: each 32-lane half of a b64 fragment read covers 64 banks once
+  __shared__ double s_x[2][F64T * PX];
+  __shared__ double s_c[2][F64T * PX];
+  __shared__ double s_xn[F64T], s_cn[F64T];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 1, wc = w & 1;
+  int64_t L = blockIdx.x;
+  {
+    const int64_t per = (int64_t)gridDim.x / 8;
+    if (per * 8 == (int64_t)gridDim.x) L = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+  }
+  const int ct = (int)(L % nct);
+  const int64_t r0 = (L / nct) * F64T;
+  const int k0 = ct * F64T;
+  // staging: thread t loads 4 features (chunk t & 3) of rows (t >> 2) and (t >> 2) + 64
+  const int srow = tid >> 2, sch = (tid & 3) * 4;
+  const double* xr[2];
+  const double* cr[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int64_t rr = min(r0 + srow + 64 * j, M - 1);
+    const int kk = min(k0 + srow + 64 * j, K - 1);
+    xr[j] = X + rr * ldx;
+    cr[j] = C + (int64_t)kk * D;
+  }
+  double vx[2][4], vc[2][4];
+  double nx[2] = {0.0, 0.0}, nc[2] = {0.0, 0.0};
+  auto load = [&](int st) __attribute__((always_inline)) {
+    const int d0 = st * F64S + sch;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool ok = d0 + e < D;
+        vx[j][e] = ok ? xr[j][d0 + e] : 0.0;
+        vc[j][e] = ok ? cr[j][d0 + e] : 0.0;
+      }
+  };
+  auto store = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s_x[buf][(srow + 64 * j) * PX + sch + e] = vx[j][e];
+        s_c[buf][(srow + 64 * j) * PX + sch + e] = vc[j][e];
+        nx[j] = fma(vx[j][e], vx[j][e], nx[j]);
+        nc[j] = fma(vc[j][e], vc[j][e], nc[j]);
+      }
+  };
+  f64x4 acc[4][4];
+#pragma unroll
+  for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 4; ++tj) acc[ti][tj] = f64x4{0.0, 0.0, 0.0, 0.0};
+  const int nst = (D + F64S - 1) / F64S;
+  load(0);
+  store(0);
+  __syncthreads();
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int st = 0; st < nst; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nst) load(st + 1);
+    const double* sx = s_x[buf] + (wr * 64 + fr) * PX + fk;
+    const double* sc = s_c[buf] + (wc * 64 + fr) * PX + fk;
+#pragma unroll
+    for (int kk = 0; kk < F64S / 4; ++kk) {
+      double a[4], b[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        a[t] = sx[t * 16 * PX + kk * 4];
+        b[t] = sc[t * 16 * PX + kk * 4];
+      }
+#pragma unroll
+      for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 4; ++tj)
+          acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti], b[tj], acc[ti][tj], 0, 0, 0);
+    }
+    if (st + 1 < nst) store(buf ^ 1);  // its previous contents were read before the last barrier
+    __syncthreads();
+  }
+  // norms: the four chunk threads of a row are lanes t, t^1, t^2, t^3 of one wave
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    nx[j] += __shfl_xor(nx[j], 1, 64);
+    nx[j] += __shfl_xor(nx[j], 2, 64);
+    nc[j] += __shfl_xor(nc[j], 1, 64);
+    nc[j] += __shfl_xor(nc[j], 2, 64);
+    if ((tid & 3) == 0) {
+      s_xn[srow + 64 * j] = nx[j];
+      s_cn[srow + 64 * j] = nc[j];
+    }
+  }
+  __syncthreads();
+  const double eb = (double)(3 * D + 4) * 0x1p-53;
+#pragma unroll
+  for (int tj = 0; tj < 4; ++tj) {
+    const int kl = wc * 64 + tj * 16 + fr;
+    const int k = k0 + kl;
+    const double cn = s_cn[kl];
+#pragma unroll
+    for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rl = wr * 64 + ti * 16 + fk + 4 * q;
+        const int64_t row = r0 + rl;
+        if (row < M && k < K) {
+          const double xn = s_xn[rl];
+          const double d2 = xn + cn - 2.0 * acc[ti][tj][q];
+          const double s = sqrt(xn) + sqrt(cn);
+          G[row * (int64_t)K + k] = d2 <= eb * s * s ? 0.0 : d2;
+        }
+      }
+  }
+}
+
+// wx[k, d] += sum_r W[r, k] x[r, d] over one split's rows (128 x 128 output tile per block);
+// ws[k] += sum_r W[r, k] (feature-tile-0 blocks); one fp64 atomic per output per block
+__global__ __launch_bounds__(256, 1) void fcm_wide_wtx_f64m_kernel(
+    const double* __restrict__ W, const double* __restrict__ X, int64_t M, int64_t ldx, int D,
+    int K, int nkt, int ndt, int64_t rows_per_split, double* __restrict__ wx,
+    double* __restrict__ ws) {
+  constexpr int PW = F64T + 16;  // 1152-B rows (= 128 mod 256): the two 16-lane groups of a
+                                 // b64 fragment read fall on disjoint bank halves
+  __shared__ double s_w[2][F64S * PW];
+  __shared__ double s_x[2][F64S * PW];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 1, wc = w & 1;
+  const int kt = (int)(blockIdx.x % nkt);
+  const int dt = (int)((blockIdx.x / nkt) % ndt);
+  const int64_t split = blockIdx.x / ((int64_t)nkt * ndt);
+  const int k0 = kt * F64T, d0 = dt * F64T;
+  const int64_t a = split * rows_per_split;
+  const int64_t b = min(M, a + rows_per_split);
+  // staging: thread t loads 8 consecutive columns (t & 15) * 8 of stage row t >> 4
+  const int srow = tid >> 4, scol = (tid & 15) * 8;
+  double vw[8], vx[8];
+  auto load = [&](int64_t rs) __attribute__((always_inline)) {
+    const int64_t r = rs + srow;
+    const bool rok = r < b;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = k0 + scol + e, d = d0 + scol + e;
+      vw[e] = (rok && k < K) ? W[r * (int64_t)K + k] : 0.0;
+      vx[e] = (rok && d < D) ? X[r * ldx + d] : 0.0;
+    }
+  };
+  auto store = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s_w[buf][srow * PW + scol + e] = vw[e];
+      s_x[buf][srow * PW + scol + e] = vx[e];
+    }
+  };
+  f64x4 acc[4][4];
+#pragma unroll
+  for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 4; ++tj) acc[ti][tj] = f64x4{0.0, 0.0, 0.0, 0.0};
+  double wsum = 0.0;
+  if (a < b) {
+    load(a);
+    store(0);
+  }
+  __syncthreads();
+  const int fr = lane & 15, fk = lane >> 4;
+  int buf = 0;
+  for (int64_t rs = a; rs < b; rs += F64S) {
+    const bool more = rs + F64S < b;
+    if (more) load(rs + F64S);
+    const double* sw = s_w[buf] + fk * PW + wr * 64 + fr;
+    const double* sx = s_x[buf] + fk * PW + wc * 64 + fr;
+#pragma unroll
+    for (int kk = 0; kk < F64S / 4; ++kk) {
+      double av[4], bv[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        av[t] = sw[kk * 4 * PW + t * 16];
+        bv[t] = sx[kk * 4 * PW + t * 16];
+      }
+#pragma unroll
+      for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 4; ++tj)
+          acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ti], bv[tj], acc[ti][tj], 0, 0, 0);
+    }
+    if (dt == 0 && tid < F64T) {
+#pragma unroll
+      for (int r = 0; r < F64S; ++r) wsum += s_w[buf][r * PW + tid];
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+#pragma unroll
+  for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 4; ++tj) {
+      const int d = d0 + wc * 64 + tj * 16 + fr;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k = k0 + wr * 64 + ti * 16 + fk + 4 * q;
+        const double v = acc[ti][tj][q];
+        if (k < K && d < D && v != 0.0) atomicAdd(&wx[(int64_t)k * D + d], v);
+      }
+    }
+  if (dt == 0 && tid < F64T && k0 + tid < K && wsum != 0.0) atomicAdd(&ws[k0 + tid], wsum);
+}
+
 template <typename T>
 int launch_wide(int pass, const void* X, int64_t M, int64_t ldx, int D, const void* C, int K,
                 double m, int nz, void* G, int32_t* labels, double* wx, double* ws, int num_cus,
                 hipStream_t s) {
+  if constexpr (sizeof(T) == 8) {
+    // fp64: both GEMM-shaped passes on the f64 matrix cores
+    if (pass == 0) {
+      const int nct = (K + F64T - 1) / F64T;
+      const int64_t nb = ((M + F64T - 1) / F64T) * nct;
+      hipLaunchKernelGGL(fcm_wide_d2_f64m_kernel, dim3((unsigned)nb), dim3(256), 0, s,
+                         (const double*)X, M, ldx, D, (const double*)C, K, nct, (double*)G);
+      TDC_CHECK_LAUNCH();
+      return 0;
+    }
+    if (pass == 2) {
+      const int nkt = (K + F64T - 1) / F64T, ndt = (D + F64T - 1) / F64T;
+      const int64_t stages = (M + F64S - 1) / F64S;
+      int64_t splits = ((int64_t)num_cus * 2 + (int64_t)nkt * ndt - 1) / ((int64_t)nkt * ndt);
+      if (splits > stages) splits = stages;
+      if (splits < 1) splits = 1;
+      const int64_t rps = ((stages + splits - 1) / splits) * F64S;
+      splits = (M + rps - 1) / rps;
+      hipLaunchKernelGGL(fcm_wide_wtx_f64m_kernel, dim3((unsigned)(splits * nkt * ndt)), dim3(256),
+                         0, s, (const double*)G, (const double*)X, M, ldx, D, K, nkt, ndt, rps,
+                         wx, ws);
+      TDC_CHECK_LAUNCH();
+      return 0;
+    }
+  }
   if (pass == 0) {
     constexpr int R = 16 * WideCfg<T>::MR;
     const dim3 grid((unsigned)((M + R - 1) / R), (unsigned)((K + 127) / 128));

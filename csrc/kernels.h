@@ -44,35 +44,42 @@ int tdc_bounds_scatter(const int32_t* active, const int* count, int64_t cap,
                        int32_t* moved_new, int* mcount, hipStream_t stream);
 
 // N1 for fp32 / fp64 data on the matrix cores (assign_x3.hip): bf16x3 scores + top-3 argmin;
-// rows whose winner the error bound tau(DP) cannot certify go to amb (int2 {row, runner-up
-// or -1}, count in amb_count) for tdc_x3_recheck.
+// rows whose winner the error bound tau(DP) cannot certify are listed in amb (int32 [3 cap]:
+// int2 {row, runner-up} two-candidate entries | int32 rows for a full re-scan; counts in
+// amb_count [2]) for tdc_x3_recheck.
 //   split: rows of src (f32/f64 [rows, ld], d valid columns) -> hi/lo bf16 [rows, DP] of v
-//          (of -2v when neg2; rows >= valid are zero, norm BIG) + norm [rows] = ||v||^2;
-//   prep : cmax2 [1] = max cnorm[0..K), amb_count [1] = 0 (before every assignment);
+//          (of -2v when neg2; rows >= valid are zero, norm BIG) + norm [rows] = ||v||^2 and
+//          nhl (nullable, float2 [rows]) = (||hi||^2, ||lo||^2);
+//   prep : cstat [3] = max over the K rows of (cnorm, ||hi||^2, ||lo||^2), amb_count [2] = 0
+//          (before every assignment);
 //   assign (DP in 32/64/128/256, Kp % 64 == 0 -- % 32 at DP 256): labels, optional mind;
 //   rows  (wide D): top-3 over a chunk's raw d2 block G [M, K] (tdc_fcm_mfma_wide pass 1),
 //          xx [M] = ||x||^2, list rows offset by row0;
 //   recheck: exact difference form in the data's dtype (X/C both f32 or f64, D <= 1024).
-float tdc_x3_tau(int DP);
 int tdc_x3_split(int src_dtype, const void* src, int64_t rows, int64_t valid, int d, int64_t ld,
-                 int DP, int neg2, void* hi, void* lo, float* norm, hipStream_t stream);
-int tdc_x3_prep(const float* cnorm, int K, float* cmax2, int* amb_count, hipStream_t stream);
+                 int DP, int neg2, void* hi, void* lo, float* norm, float* nhl, hipStream_t stream);
+int tdc_x3_prep(const float* cnorm, const float* nhl, int K, float* cstat, int* amb_count,
+                hipStream_t stream);
 int tdc_assign_x3(const void* Xh, const void* Xl, int64_t N, int DP, const void* Ch, const void* Cl,
-                  const float* cnorm, int Kp, const float* cmax2, float tau, int32_t* labels,
-                  float* mind, int2* amb, int* amb_count, hipStream_t stream);
-int tdc_x3_rows(const float* G, int64_t M, int K, int64_t row0, const float* xx, const float* cmax2,
-                float tau, int32_t* labels, int2* amb, int* amb_count, hipStream_t stream);
+                  const float* cnorm, int Kp, const float* cstat, int32_t* labels,
+                  float* mind, int32_t* amb, int64_t cap, int* amb_count, hipStream_t stream);
+int tdc_x3_rows(const float* G, int64_t M, int K, int64_t row0, const float* xx, const float* cstat,
+                int DP, int32_t* labels, int32_t* amb, int64_t cap, int* amb_count,
+                hipStream_t stream);
 int tdc_x3_recheck(int dtype, const void* X, int64_t ldx, int D, const void* C, int K,
-                   int32_t* labels, const int2* amb, const int* amb_count, int num_cus,
-                   hipStream_t stream);
+                   int32_t* labels, const int32_t* amb, int64_t cap, const int* amb_count,
+                   int num_cus, hipStream_t stream);
 
 // N1 (exact)  SIMT difference-form assignment for fp32/fp64, any K, D <= 64.
 int tdc_assign_simt(int dtype, const void* X, int64_t N, int64_t ldx, int D, const void* C,
                     int K, int32_t* labels, void* mind, hipStream_t stream);
 
 // N1 (exact, any D)  difference-form tiled assignment (fp32 / fp64), LDS use independent of D.
+// rowidx (nullable): launch row i is row rowidx[i] (labels / mind too); nptr (nullable): the
+// row count read from the device (N is then the capacity sizing the grid).
 int tdc_assign_exact(int dtype, const void* X, int64_t N, int64_t ldx, int D, const void* C, int K,
-                     int32_t* labels, void* mind, int num_cus, hipStream_t stream);
+                     int32_t* labels, void* mind, int num_cus, hipStream_t stream,
+                     const int32_t* rowidx = nullptr, const int* nptr = nullptr);
 
 // Fused small-K Lloyd step (assign + per-cluster sums/counts in registers), fp32/fp64.
 // Returns hipErrorInvalidValue if (K, D) exceeds the compiled register tiles.

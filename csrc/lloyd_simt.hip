@@ -405,12 +405,17 @@ __device__ __forceinline__ f32x2 pk_sub_hi(f32x2 xp, f32x2 c) {
 template <typename T> struct ExactCfg { static constexpr int MR = 8; };
 template <> struct ExactCfg<double> { static constexpr int MR = 4; };
 
+// rowidx (nullable): row i of the launch is row rowidx[i] of X (and of labels / mind), with
+// the row count read from the device (nptr) -- the full re-scan of the rows the fp32/fp64
+// MFMA assignment could not certify (assign_x3.hip), sized on the device
 template <typename T>
 __global__ __launch_bounds__(256) void assign_exact_kernel(const T* __restrict__ X, int64_t N,
                                                            int64_t ldx, int D,
                                                            const T* __restrict__ C, int K,
                                                            int32_t* __restrict__ labels,
-                                                           T* __restrict__ mind) {
+                                                           T* __restrict__ mind,
+                                                           const int32_t* __restrict__ rowidx,
+                                                           const int* __restrict__ nptr) {
   constexpr int MR = ExactCfg<T>::MR;
   constexpr int R = 16 * MR, KT = 128, DC = 32;
   constexpr int PX = R + 4, PC = KT + 4;  // row pitch (16-B aligned, spreads the store banks)
@@ -418,6 +423,7 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(const T* __restrict__
   __shared__ __attribute__((aligned(16))) T s_c[DC][PC];
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
   constexpr bool F32 = sizeof(T) == 4;
+  if (nptr) N = *nptr;
   for (int64_t r0 = (int64_t)blockIdx.x * R; r0 < N; r0 += (int64_t)gridDim.x * R) {
     T best[MR];
     int bk[MR];
@@ -441,7 +447,8 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(const T* __restrict__
         // coalesced along the features, stored feature-major (transposed)
         for (int e = tid; e < R * DC; e += 256) {
           const int r = e / DC, d = e % DC;
-          s_x[d][r] = (r0 + r < N && dc + d < D) ? X[(r0 + r) * ldx + dc + d] : (T)0;
+          const int64_t xr = rowidx ? (int64_t)rowidx[r0 + r < N ? r0 + r : N - 1] : r0 + r;
+          s_x[d][r] = (r0 + r < N && dc + d < D) ? X[xr * ldx + dc + d] : (T)0;
         }
         for (int e = tid; e < KT * DC; e += 256) {
           const int r = e / DC, d = e % DC;
@@ -513,15 +520,17 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(const T* __restrict__
       }
       const int64_t row = r0 + ty * MR + i;
       if (tx == 0 && row < N) {
-        labels[row] = bk[i];
-        if (mind) mind[row] = best[i];
+        const int64_t orow = rowidx ? (int64_t)rowidx[row] : row;
+        labels[orow] = bk[i];
+        if (mind) mind[orow] = best[i];
       }
     }
   }
 }
 
 int tdc_assign_exact(int dtype, const void* X, int64_t N, int64_t ldx, int D, const void* C, int K,
-                     int32_t* labels, void* mind, int num_cus, hipStream_t s) {
+                     int32_t* labels, void* mind, int num_cus, hipStream_t s,
+                     const int32_t* rowidx, const int* nptr) {
   if (N <= 0) return 0;
   (void)num_cus;
   const int64_t rows_per_tile = 16 * (dtype == TDC_F64 ? ExactCfg<double>::MR : ExactCfg<float>::MR);
@@ -533,10 +542,12 @@ int tdc_assign_exact(int dtype, const void* X, int64_t N, int64_t ldx, int D, co
   if (blocks > resident) blocks = resident;
   if (dtype == TDC_F32)
     hipLaunchKernelGGL(assign_exact_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s,
-                       (const float*)X, N, ldx, D, (const float*)C, K, labels, (float*)mind);
+                       (const float*)X, N, ldx, D, (const float*)C, K, labels, (float*)mind,
+                       rowidx, nptr);
   else if (dtype == TDC_F64)
     hipLaunchKernelGGL(assign_exact_kernel<double>, dim3((unsigned)blocks), dim3(256), 0, s,
-                       (const double*)X, N, ldx, D, (const double*)C, K, labels, (double*)mind);
+                       (const double*)X, N, ldx, D, (const double*)C, K, labels, (double*)mind,
+                       rowidx, nptr);
   else
     return (int)hipErrorInvalidValue;
   TDC_CHECK_LAUNCH();

@@ -260,17 +260,21 @@ __global__ __launch_bounds__(NT) void bscatter_kernel(const int32_t* __restrict_
 }
 
 // Per-element accumulator conversion: fp32 / fp64 partials, or fixed point (the
-// deterministic update): round-toward-zero of v * 2^S into int64, whose sums are exact and
-// therefore independent of the order the atomics land in.  The scale is a power of two,
-// so v * scale is exact; |sum| < 2^62 by the caller's choice of S.
-// fixed point: |v * scale| <= 2^30 by the scale's contract (ops.fixed_point_scale), so the
-// truncation is one v_cvt_i32 (+ sign extension) instead of an emulated float -> int64
+// deterministic update): v * 2^S rounded to the NEAREST integer (ties to even: unbiased, so
+// the rounding of the many small elements of a feature far below max|x| averages out
+// instead of drifting toward zero) in int64, whose sums are exact and therefore independent
+// of the order the atomics land in.  The scale is a power of two, so v * scale is exact;
+// |sum| < 2^62 by the caller's choice of S (ops.fixed_point_scale).
+//   bf16 / fp32 rows: |v * scale| <= 2^30 by the scale's contract, so the conversion is a
+//     v_rndne + v_cvt_i32 (+ sign extension) instead of an emulated float -> int64;
+//   fp64 rows: the scale only bounds the sums (a step ~2^30 x finer, near the fp64 ulp of
+//     the data), converted by the int64 round-to-nearest.
 template <typename AT> __device__ __forceinline__ AT acc_cvt(float v, float scale) {
-  if constexpr (std::is_same<AT, long long>::value) return (long long)(int)(v * scale);
+  if constexpr (std::is_same<AT, long long>::value) return (long long)__float2int_rn(v * scale);
   else return (AT)v;
 }
 template <typename AT> __device__ __forceinline__ AT acc_cvt(double v, double scale) {
-  if constexpr (std::is_same<AT, long long>::value) return (long long)(int)(v * scale);
+  if constexpr (std::is_same<AT, long long>::value) return __double2ll_rn(v * scale);
   else return (AT)v;
 }
 
@@ -335,6 +339,8 @@ template <typename XT> struct RowLoad1 {
 
 // perm entries of a delta update carry the sign in bit 31 (row numbers are < 2^31)
 constexpr unsigned PERM_NEG = 0x80000000u;
+// moved-list row words (delta shards have < 2^30 rows): out-of-range label flags
+constexpr unsigned LIDX_NO_NEW = 0x80000000u, LIDX_NO_OLD = 0x40000000u, LIDX_ROW = 0x3fffffffu;
 // segment offsets staged in LDS by the segsum kernel up to this many entries (32 KiB)
 constexpr int SEG_LDS_OFF_MAX = 8193;
 // delta update: K up to which the diff / scatter kernels keep their two K-int tables in
@@ -636,7 +642,10 @@ __global__ __launch_bounds__(NT) void delta_diff_kernel(
           const int pos = base + (int)__builtin_amdgcn_mbcnt_hi(
                                      (unsigned)(mask >> 32),
                                      __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
-          lidx[r0 + pos] = (int32_t)i;
+          // labels travel in 16 bits (K <= 65536, where every 16-bit value is a label), so
+          // an out-of-range label (none counted by the histograms above) is flagged in the
+          // row word instead: bit 31 = no event at the new cluster, bit 30 = none at the old
+          lidx[r0 + pos] = (int32_t)((uint32_t)i | (nok ? 0u : LIDX_NO_NEW) | (ook ? 0u : LIDX_NO_OLD));
           lpair[r0 + pos] = (((uint32_t)od[j] & 0xffffu) << 16) | ((uint32_t)nw[j] & 0xffffu);
         }
       }
@@ -729,9 +738,11 @@ __global__ __launch_bounds__(NT) void delta_scatter_kernel(
       for (int64_t i = r0 + tid; i < r1; i += NT) {
         const uint32_t pr = lpair[i];
         const unsigned nw = pr & 0xffffu, od = pr >> 16;
-        const int32_t row = lidx[i];
-        if (nw < (unsigned)K) perm[atomicAdd(cursor + nw, 1)] = row;
-        if (od < (unsigned)K) perm[atomicAdd(cursor + od, 1)] = (int32_t)((uint32_t)row | PERM_NEG);
+        const uint32_t li = (uint32_t)lidx[i];
+        const int32_t row = (int32_t)(li & LIDX_ROW);
+        if (!(li & LIDX_NO_NEW) && nw < (unsigned)K) perm[atomicAdd(cursor + nw, 1)] = row;
+        if (!(li & LIDX_NO_OLD) && od < (unsigned)K)
+          perm[atomicAdd(cursor + od, 1)] = (int32_t)((uint32_t)row | PERM_NEG);
       }
     }
     return;
@@ -747,8 +758,9 @@ __global__ __launch_bounds__(NT) void delta_scatter_kernel(
     for (int64_t i = r0 + tid; i < r1; i += NT) {
       const uint32_t pr = lpair[i];
       const unsigned nw = pr & 0xffffu, od = pr >> 16;
-      if (nw < (unsigned)K) atomicAdd(s_cnt + nw, 1);
-      if (od < (unsigned)K) atomicAdd(s_cnt + od, 1);
+      const uint32_t li = (uint32_t)lidx[i];
+      if (!(li & LIDX_NO_NEW) && nw < (unsigned)K) atomicAdd(s_cnt + nw, 1);
+      if (!(li & LIDX_NO_OLD) && od < (unsigned)K) atomicAdd(s_cnt + od, 1);
     }
   }
   __syncthreads();
@@ -770,9 +782,11 @@ __global__ __launch_bounds__(NT) void delta_scatter_kernel(
     for (int64_t i = r0 + tid; i < r1; i += NT) {
       const uint32_t pr = lpair[i];
       const unsigned nw = pr & 0xffffu, od = pr >> 16;
-      const int32_t row = lidx[i];
-      if (nw < (unsigned)K) perm[atomicAdd(s_cur + nw, 1)] = row;
-      if (od < (unsigned)K) perm[atomicAdd(s_cur + od, 1)] = (int32_t)((uint32_t)row | PERM_NEG);
+      const uint32_t li = (uint32_t)lidx[i];
+      const int32_t row = (int32_t)(li & LIDX_ROW);
+      if (!(li & LIDX_NO_NEW) && nw < (unsigned)K) perm[atomicAdd(s_cur + nw, 1)] = row;
+      if (!(li & LIDX_NO_OLD) && od < (unsigned)K)
+        perm[atomicAdd(s_cur + od, 1)] = (int32_t)((uint32_t)row | PERM_NEG);
     }
   }
 }

@@ -42,7 +42,8 @@ FCM_FP32_MIN_LOG2_W = -100.0
 
 
 def fcm_dtype(cfg: ClusterConfig, m: Optional[float] = None) -> torch.dtype:
-    """Memberships need exact-difference-grade distances: bf16/fp8 configs run fp32.
+    """Row / membership dtype: fp32 for fp32 and bf16/fp8 configs (bf16 selects the MFMA
+    towers, whose distances are bf16x3 -- fp32-faithful -- and whose W^T X weights are bf16).
 
     With the reference's fuzzifier m = D (`distribuitedClustering.py:121,129`) the weights
     u^m of a point's typical memberships u ~ 1/K fall to K^-m: 2^-144 at K=64, D=24, below
@@ -80,7 +81,11 @@ class FcmEngine(OomGuard):
         self.m = float(m) if m is not None else (float(cfg.fuzzifier) if cfg.fuzzifier is not None
                                                  else float(d))
         tdt = fcm_dtype(cfg, self.m)
-        dt_name = "fp64" if tdt == torch.float64 else "fp32"
+        # bf16 / fp8: the MFMA towers (fp32 memberships, bf16x3 distances, bf16 weights);
+        # fp32: the exact difference-form towers
+        dt_name = ("fp64" if tdt == torch.float64 else
+                   "bf16" if cfg.dtype in ("bf16", "fp8") else "fp32")
+        self.dtype_name = dt_name
         if tdt == torch.float64 and cfg.dtype != "fp64" and comm.is_root:
             print(f"[fcm] fuzzifier m={self.m:g} with K={k}: weights u^m ~ K^-m underflow fp32; "
                   f"computing in fp64", flush=True)

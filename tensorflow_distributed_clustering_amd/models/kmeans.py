@@ -35,7 +35,8 @@ import torch
 
 from ..config import ClusterConfig
 from ..data.stream import HostSource, ResidentSource, plan_chunk_rows, plan_resident_rows
-from ..ops import NativeUpdate, acc_dtype_for, lloyd_layout, make_lloyd_ops
+from ..ops import (NativeUpdate, acc_dtype_for, lloyd_fixed_extra, lloyd_layout, lloyd_row_extra,
+                   make_lloyd_ops)
 from ..parallel.dist import Comm, join_counts, local_comm
 from ..utils import faults
 from ..utils.checkpoint import RunCheckpointer
@@ -421,11 +422,15 @@ class LloydEngine(OomGuard):
         else:
             xs = (chunk for _, chunk in self._chunks())
         m = 0.0
+        wide = False
         for xc in xs:
+            wide = wide or xc.dtype == torch.float64
             if xc.numel():
-                m = max(m, float(xc[:, : self.d].abs().max()))
+                # a NaN / inf row propagates as inf: fixed_point_scale names it
+                v = xc[:, : self.d].abs().max()
+                m = max(m, float(v) if bool(torch.isfinite(v)) else math.inf)
         m = self.comm.max_scalar(m)
-        scale = fixed_point_scale(m, self.n_global)
+        scale = fixed_point_scale(m, self.n_global, elem32=not wide)
         self.local.set_fixed_scale(scale)
         if self.delta is not None:
             self.delta.fixed_scale = scale
@@ -789,13 +794,20 @@ class KMeans:
             layout = lloyd_layout(cfg.dtype, d)
             es = torch.tensor([], dtype=layout[0]).element_size()
             row_bytes = layout[1] * es
+            # per-row / fixed work buffers the resident engine will add (delta update, the
+            # fp32 MFMA path's hi/lo rows): a shard that fits only without them streams
+            delta = cfg.update != "full"
+            extra = lloyd_row_extra(cfg.dtype, d, delta)
+            fixed = lloyd_fixed_extra(cfg.n_clusters, d, delta)
             chunk = want or plan_chunk_rows(xn.shape[0], row_bytes, cfg.n_clusters, d, dev,
-                                            cfg.hbm_budget_gb)
+                                            cfg.hbm_budget_gb, per_row_extra=extra,
+                                            extra_fixed=fixed)
             if chunk:
                 resident = 0
                 if not want:  # planner-driven streaming: keep what fits in HBM resident
                     resident = plan_resident_rows(xn.shape[0], row_bytes, chunk, cfg.n_clusters,
-                                                  d, dev, cfg.hbm_budget_gb)
+                                                  d, dev, cfg.hbm_budget_gb,
+                                                  per_row_extra=lloyd_row_extra(cfg.dtype, d, False))
                 return HostSource(xn, layout, dev, row_offset, resident_rows=resident), chunk
         return torch.as_tensor(xn).to(dev), want
 

@@ -184,7 +184,8 @@ class NativeUpdate:
             self._fx = torch.zeros(k * d + k, dtype=torch.int64, device=x.device)
         self._fx.zero_()
         n = x.shape[0]
-        scale = fixed_point_scale(float(x[:, :d].abs().max()) if n else 0.0, n)
+        scale = fixed_point_scale(float(x[:, :d].abs().max()) if n else 0.0, n,
+                                  elem32=x.dtype != torch.float64)
         fs, fc = self._fx[: k * d].view(k, d), self._fx[k * d:]
         self.ops.update_sorted(x, labels, fs, fc, self.work, None, None, None, scale, True)
         sums.add_((fs.double() / scale).to(sums.dtype))
@@ -342,17 +343,23 @@ class TorchDelta(DeltaState):
                                    dtype=torch.float64, device=self.stats.device)
 
 
-def fixed_point_scale(max_abs: float, n_rows: int) -> float:
+def fixed_point_scale(max_abs: float, n_rows: int, elem32: bool = True) -> float:
     """2^S for fixed-point partial sums of up to ``n_rows`` values of magnitude <=
-    ``max_abs``: the largest power of two with max_abs * 2^S <= 2^30 (every element's fixed
-    point fits an int32: the kernels convert it with one v_cvt_i32_f32 instead of the
-    emulated float -> int64 conversion) and max_abs * n_rows * 2^S < 2^61 (no int64 sum
-    can overflow), clamped to [2^-60, 2^60].  The step 2^-S is max_abs * 2^-30 or finer:
-    below the fp32 ulp of the largest element."""
+    ``max_abs``: the largest power of two with max_abs * n_rows * 2^S < 2^61 (no int64 sum
+    can overflow) and, with ``elem32`` (bf16 / fp32 rows), max_abs * 2^S <= 2^30 (every
+    element's fixed point fits an int32: the kernels round it with one v_rndne + v_cvt_i32
+    instead of the emulated float -> int64 conversion), clamped to [2^-60, 2^60].  The
+    step 2^-S is then max_abs * 2^-30 or finer -- below the fp32 ulp of the largest
+    element; fp64 rows (``elem32=False``) get the finer step the sum bound allows.  The
+    kernels round to nearest (unbiased)."""
     import math
-    m = max(float(max_abs), 1e-30)
+    m = float(max_abs)
+    if not math.isfinite(m):
+        raise ValueError("deterministic update: the data holds a NaN or an infinity "
+                         "(no fixed-point scale exists for non-finite values)")
+    m = max(m, 1e-30)
     s_sum = math.floor(61 - math.log2(m * max(1, int(n_rows)))) - 1
-    s_elem = math.floor(30 - math.log2(m))
+    s_elem = math.floor(30 - math.log2(m)) if elem32 else s_sum
     return float(2.0 ** max(-60, min(60, s_sum, s_elem)))
 
 
@@ -948,9 +955,9 @@ class HipX3Lloyd(_LocalOpsBase):
         self.ch = torch.zeros(self.kp, self.dp, dtype=torch.bfloat16, device=dev)
         self.cl = torch.zeros_like(self.ch)
         self.cnorm = torch.zeros(self.kp, dtype=torch.float32, device=dev)
-        self.cmax2 = torch.zeros(1, dtype=torch.float32, device=dev)
-        self.amb_count = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.tau = float(self.ops.x3_tau(self.dp))
+        self.cnhl = torch.zeros(self.kp, 2, dtype=torch.float32, device=dev)  # ||th||^2, ||tl||^2
+        self.cstat = torch.zeros(3, dtype=torch.float32, device=dev)  # maxima of cnorm / cnhl
+        self.amb_count = torch.zeros(2, dtype=torch.int32, device=dev)
         self.xh = self.xl = self.xx = self.amb = self.G = None
         self.x = None
         self._set_x(x)
@@ -965,7 +972,8 @@ class HipX3Lloyd(_LocalOpsBase):
             self.xh = torch.empty(max(n, 1), self.dp, dtype=torch.bfloat16, device=dev)
             self.xl = torch.empty_like(self.xh)
             self.xx = torch.empty(max(n, 1), dtype=torch.float32, device=dev) if self.wide else None
-            self.amb = torch.empty(2 * max(n, 1), dtype=torch.int32, device=dev)
+            # re-check lists: int2 {row, runner-up} entries | full re-scan rows
+            self.amb = torch.empty(3 * max(n, 1), dtype=torch.int32, device=dev)
         self.x = x
         self.n = n
         if n:
@@ -984,7 +992,8 @@ class HipX3Lloyd(_LocalOpsBase):
         return self
 
     def prepare(self, C):
-        self.ops.x3_split(C.to(self.c_dtype).contiguous(), self.k, 1, self.ch, self.cl, self.cnorm)
+        self.ops.x3_split(C.to(self.c_dtype).contiguous(), self.k, 1, self.ch, self.cl, self.cnorm,
+                          self.cnhl)
 
     def _chunk_rows(self):
         rows = max(1, min(self.n, self.chunk_elems // max(1, self.k), self.max_chunk_rows))
@@ -997,26 +1006,31 @@ class HipX3Lloyd(_LocalOpsBase):
         if n == 0:
             return
         Cx = C if (C.dtype == self.c_dtype and C.is_contiguous()) else C.to(self.c_dtype).contiguous()
+        amb = self.amb[: 3 * n]  # the lists' layout follows their capacity: n rows
         if not self.wide:
-            self.ops.x3_assign(self.x, self.xh[:n], self.xl[:n], self.ch, self.cl, self.cnorm, Cx,
-                               labels, None, self.amb, self.cmax2, self.amb_count, True)
+            self.ops.x3_assign(self.x, self.xh[:n], self.xl[:n], self.ch, self.cl, self.cnorm,
+                               self.cnhl, Cx, labels, None, amb, self.cstat, self.amb_count, True)
         else:
-            self.ops.x3_prep(self.cnorm, self.k, self.cmax2, self.amb_count)
+            self.ops.x3_prep(self.cnorm, self.cnhl, self.k, self.cstat, self.amb_count)
             rows = self._chunk_rows()
             for s in range(0, n, rows):
                 e = min(n, s + rows)
                 g = self.G[: e - s]
                 self.ops.fcm_mfma_wide(1, self.xh[s:e], self.xl[s:e], self.xx[s:e], self.ch,
                                        self.cl, self.cnorm, self.k, self.d, g)
-                self.ops.x3_rows(g, s, self.xx[s:e], self.cmax2, self.tau, labels, self.amb,
+                self.ops.x3_rows(g, s, self.xx[s:e], self.cstat, self.dp, labels, amb,
                                  self.amb_count)
-            self.ops.x3_recheck(self.x, Cx, labels, self.amb, self.amb_count)
+            self.ops.x3_recheck(self.x, Cx, labels, amb, self.amb_count)
         if mind is not None:
             _exact_mind(self.x, C, labels, mind, self.d)
 
     def ambiguous_rows(self) -> int:
         """Rows the last assignment re-checked exactly (host read; diagnostics)."""
-        return int(self.amb_count.item())
+        return int(self.amb_count.sum().item())
+
+    def rescanned_rows(self) -> int:
+        """... of which re-scanned over all K (a third candidate within the bound)."""
+        return int(self.amb_count[1].item())
 
     def step(self, C, labels, mind, sums, counts):
         self.assign(C, labels, mind)
@@ -1039,6 +1053,23 @@ class HipX3Lloyd(_LocalOpsBase):
         if C.shape[0]:
             self.ops.finalize(sums, counts, C, self.policy, shift, None, None,
                               fixed_scale=self.fixed_scale)
+
+
+def lloyd_row_extra(dtype: str, d: int, delta: bool = True) -> int:
+    """Device bytes per row a Lloyd shard holds besides its layout row (the HBM planner's
+    per_row_extra): labels + min distances + the sorted update's permutation (16), the delta
+    update's prev / moved-list / event permutation (20), and on the fp32 / fp64 MFMA path
+    the bf16 hi/lo rows (4 x padded D) + the re-check list entry (8)."""
+    extra = 16 + (20 if delta else 0)
+    if dtype in ("fp32", "fp64") and d > X3_MIN_D and x3_dim(d) is not None:
+        extra += 4 * x3_dim(d) + 8
+    return extra
+
+
+def lloyd_fixed_extra(k: int, d: int, delta: bool = True) -> int:
+    """Device bytes a Lloyd shard holds independent of its rows beyond the planner's
+    default: the delta update's fp64 running totals."""
+    return (k * d + k) * 8 if delta else 0
 
 
 def lloyd_layout(dtype: str, d: int):
@@ -1416,17 +1447,35 @@ class HipWideFCM(_LocalOpsBase):
         self.ops.finalize(sums, counts, C, 0, shift, None, None)
 
 
+# what each FCM dtype computes (bench.py / --extended_log report it)
+FCM_PRECISION = {
+    "fp64": "fp64 distances (difference form; D > 256: the GEMM expansion on the fp64 matrix "
+            "cores), fp64 memberships and sums",
+    "fp32": "fp32 difference-form distances and memberships, fp64 sums",
+    "bf16": "bf16x3 MFMA distances (fp32-faithful), fp32 memberships, bf16 weights in the "
+            "W^T X MFMAs, fp64 sums",
+}
+
+
 def make_fcm_ops(x: torch.Tensor, k: int, dtype: str = "fp64", m: float = 2.0,
                  nan_to_zero: bool = True, backend: str = "auto"):
+    """FCM tower for (dtype, K, D).  fp64 / fp32: the exact difference-form towers (fused
+    small-K*D kernel, SIMT tower up to D = 256, wide tower above) -- the reference's
+    memberships come from exact differences (`scripts/distribuitedClustering.py:112-129`).
+    bf16 (and fp8): the MFMA towers (fp32 rows split into bf16 hi/lo, bf16x3 distances,
+    memberships in fp32, W = u^m rounded to bf16 for the W^T X MFMAs; centroid error
+    ~1e-3 of max|c| against the fp64 oracle, FCM_PRECISION) for 16 < D <= 1024, K >= 32;
+    other shapes fall back to the exact fp32 towers."""
     d = x.shape[1]
-    if dtype in ("bf16", "fp8"):
-        dtype = "fp32"  # memberships need exact-difference distances; see docs
+    mfma = dtype in ("bf16", "fp8")
+    if mfma:
+        dtype = "fp32"  # memberships and rows in fp32; the distances on the matrix cores
     if not use_native(x.device, backend):
         return TorchFCM(x, k, dtype, m, nan_to_zero)
     tdt = torch.float64 if dtype == "fp64" else torch.float32
     if _native.require().fcm_small_supported(tdt, k, d):
         return HipSmallFCM(x, k, dtype, m, nan_to_zero)
-    if dtype == "fp32" and d > 16 and k >= FCM_MFMA_MIN_K:
+    if mfma and d > 16 and k >= FCM_MFMA_MIN_K:
         if fcm_mfma_dim(d) is not None:
             return HipMfmaFCM(x, k, m, nan_to_zero)
         if fcm_mfma_wide_dim(d) is not None:

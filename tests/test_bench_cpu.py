@@ -78,6 +78,9 @@ def test_bench_headline_is_strong_scaling_at_10m(tmp_path):
 def test_bench_fcm_and_minibatch_presets():
     d = _run(["--preset", "ref25m_fcm", "--n-per-gpu", "30000", "--steps", "2", "--warmup", "1"])
     assert d["config"]["model"] == "fuzzy-cmeans" and d["dtype"] == "fp64"
+    # FCM witness: one step of the engine's tower vs the fp64 oracle on the sample rows
+    assert d["check"]["fcm_centroid_rel_err"] < 1e-9 and d["check"]["fcm_weight_sum_rel_err"] < 1e-9
+    assert d["check"]["sample_rows"] == 30000 and "fp64" in d["precision"]
     d = _run(["--preset", "minibatch1b", "--n-per-gpu", "50000", "--k", "32", "--batch-size", "4096",
               "--steps", "2", "--warmup", "1", "--dtype", "fp32"])
     assert d["config"]["model"] == "kmeans-minibatch" and d["config"]["global_batch"] == 4096

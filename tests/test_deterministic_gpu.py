@@ -22,17 +22,17 @@ def _ops():
 @pytest.mark.parametrize("xdt", [torch.bfloat16, torch.float32, torch.float64])
 @pytest.mark.parametrize("n,d,k", [(60_001, 128, 1024), (7000, 33, 50)])
 def test_fixed_point_update_exact(gpu, xdt, n, d, k):
-    """int64 sums equal sum_i trunc(x_i * 2^S) exactly (any order of the atomics)."""
+    """int64 sums equal sum_i rint(x_i * 2^S) exactly (any order of the atomics)."""
     ops = _ops()
     g = torch.Generator().manual_seed(d + k)
     x = (torch.randn(n, d, generator=g, dtype=torch.float64) * 4).to(xdt).to(gpu)
     lab = torch.randint(0, k, (n,), generator=g, dtype=torch.int32).to(gpu)
-    scale = fixed_point_scale(float(x.abs().max()), n)
+    scale = fixed_point_scale(float(x.abs().max()), n, elem32=xdt != torch.float64)
     sums = torch.zeros(k, d, dtype=torch.int64, device=gpu)
     counts = torch.zeros(k, dtype=torch.int64, device=gpu)
     work = torch.zeros(int(ops.update_sorted_workspace(n, k)), dtype=torch.int32, device=gpu)
     ops.update_sorted(x, lab, sums, counts, work, None, None, None, scale)
-    fx = (x.double() * scale).trunc().long()
+    fx = (x.double() * scale).round().long()  # round half to even, as v_rndne / int64 rn
     rs = torch.zeros(k, d, dtype=torch.int64, device=gpu).index_add_(0, lab.long(), fx)
     assert torch.equal(sums, rs)
     assert torch.equal(counts, torch.bincount(lab.long(), minlength=k))
@@ -87,3 +87,36 @@ def test_deterministic_other_dtypes(gpu, dtype, d, k):
     f = tdc.KMeans(cfg.replace(deterministic=False), device=gpu).fit(x).result_
     tol = 1e-9 if dtype == "fp64" else 1e-5
     np.testing.assert_allclose(a.centers, f.centers, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("xdt", [torch.float32, torch.float64])
+def test_deterministic_mixed_scale_unbiased(gpu, xdt):
+    """One feature ~1e4, the others ~3e-2: the fixed-point step follows the global max |x|,
+    so the small features are many steps of rounding each; rounded to nearest the errors
+    average out (round-toward-zero biased every small positive element by half a step:
+    ~1e-3 relative on their means).  fp64 rows use the finer sum-bound step."""
+    ops = _ops()
+    n, d, k = 200_000, 8, 4
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(n, d, generator=g, dtype=torch.float64) * 1e-2 + 0.03
+    x[:, 0] = torch.randn(n, generator=g, dtype=torch.float64) * 1e4
+    x = x.to(xdt).to(gpu)
+    lab = torch.randint(0, k, (n,), generator=g, dtype=torch.int32).to(gpu)
+    scale = fixed_point_scale(float(x.abs().max()), n, elem32=xdt != torch.float64)
+    sums = torch.zeros(k, d, dtype=torch.int64, device=gpu)
+    counts = torch.zeros(k, dtype=torch.int64, device=gpu)
+    work = torch.zeros(int(ops.update_sorted_workspace(n, k)), dtype=torch.int32, device=gpu)
+    ops.update_sorted(x, lab, sums, counts, work, None, None, None, scale)
+    means = (sums.double() / scale) / counts.double()[:, None]
+    rs = torch.zeros(k, d, dtype=torch.float64, device=gpu).index_add_(0, lab.long(), x.double())
+    ref = rs / torch.bincount(lab.long(), minlength=k).double()[:, None]
+    rel = ((means - ref).abs() / ref.abs())[:, 1:].max().item()
+    assert rel < (2e-5 if xdt == torch.float32 else 2e-8), rel
+
+
+def test_fixed_point_scale_rejects_non_finite():
+    import math
+    with pytest.raises(ValueError, match="NaN or an infinity"):
+        fixed_point_scale(math.inf, 10)
+    with pytest.raises(ValueError):
+        fixed_point_scale(float("nan"), 10)

@@ -118,6 +118,11 @@ def test_fixed_point_scale_bounds_the_sums():
             assert mm * n * s * 4 >= 2.0 ** 61 or mm * s * 2 > 2.0 ** 30
     assert fixed_point_scale(15.0, 10_000_000) == 2.0 ** 26
     assert fixed_point_scale(2.0, 2 ** 40) == 2.0 ** 19  # the sum bound binds
+    # fp64 rows: only the sum bound (int64 conversion), a much finer step
+    assert fixed_point_scale(15.0, 10_000_000, elem32=False) == 2.0 ** 32
+    for m, n in [(15.0, 10_000_000), (1e6, 10 ** 9)]:
+        s = fixed_point_scale(m, n, elem32=False)
+        assert m * n * s < 2.0 ** 61 and m * n * s * 4 >= 2.0 ** 61
 
 
 def test_deterministic_cpu_fit_reproducible():

@@ -77,7 +77,7 @@ def test_fcm_predict_gemm_path(gpu):
     import tensorflow_distributed_clustering_amd as tdc
     from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs
     x = gaussian_blobs(50000, 64, 32, seed=4, dtype=torch.float32, device=gpu)
-    fcm = tdc.FuzzyCMeans(tdc.ClusterConfig(n_clusters=32, max_iter=3, dtype="fp32", seed=1,
+    fcm = tdc.FuzzyCMeans(tdc.ClusterConfig(n_clusters=32, max_iter=3, dtype="bf16", seed=1,
                                             fuzzifier=2.0)).fit(x)
     assert fcm.result_.backend == "hip_fcm_mfma"
     lab = fcm.predict(x)

@@ -173,7 +173,7 @@ def test_bounded_lloyd_policies_and_spherical(gpu):
             np.testing.assert_allclose(a.centers, b.centers, rtol=0, atol=5e-2)
 
 
-@pytest.mark.parametrize("dtype,backend", [("fp32", "hip_fcm_mfma"), ("fp64", "hip_fcm_tower")])
+@pytest.mark.parametrize("dtype,backend", [("bf16", "hip_fcm_mfma"), ("fp32", "hip_fcm_tower"), ("fp64", "hip_fcm_tower")])
 def test_fcm_hbm_budget_streams_and_matches_resident(gpu, dtype, backend):
     """FCM with --hbm_budget_gb below the shard: host-resident rows stream through HBM in
     chunks (fp32: native RowStreamer + hybrid residency; fp64: plain pinned slices) and
