@@ -359,6 +359,9 @@ def precision_of(eng, a):
     name = getattr(getattr(eng, "local", None), "name", "")
     if a.method == "fcm":
         from tensorflow_distributed_clustering_amd.ops import FCM_PRECISION
+        own = getattr(getattr(eng, "local", None), "precision", None)
+        if isinstance(own, str):
+            return own
         return FCM_PRECISION.get(getattr(eng, "dtype_name", a.dtype), a.dtype)
     if name == "hip_x3_mfma":
         return (f"{a.dtype} exact-argmin labels: bf16x3 MFMA scores + exact {a.dtype} re-check "
@@ -464,7 +467,8 @@ def fcm_witness(eng, x, n_global, s, e, comm, torch, a):
     werr = float(((ws - wsr).abs() / wsr.clamp_min(1e-300))[ok].max()) if bool(ok.any()) else 0.0
     return {"fcm_centroid_rel_err": cerr, "fcm_weight_sum_rel_err": werr,
             "sample_rows": int(comm.sum_scalar(float(loc.numel()))),
-            "precision": FCM_PRECISION.get(eng.dtype_name, eng.dtype_name),
+            "precision": (getattr(ops, "precision", None) if xs.shape[0] else None)
+            or FCM_PRECISION.get(eng.dtype_name, eng.dtype_name),
             "backend": ops.name if xs.shape[0] else None}
 
 

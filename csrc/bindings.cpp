@@ -464,7 +464,8 @@ void fcm_mfma_stats(const at::Tensor& Xh, const at::Tensor& Xl, const at::Tensor
   check(tdc_fcm_mfma(0, Xh.data_ptr(), Xl.data_ptr(), xx.data_ptr<float>(), N, (int)Xh.size(1), 0,
                      Ch.data_ptr(), Cl.data_ptr(), cc.data_ptr<float>(), (int)K, (int)Ch.size(0),
                      m, nan_to_zero ? 1 : 0, labels.data_ptr<int32_t>(), rowinfo.data_ptr<float>(),
-                     nullptr, nullptr, nullptr, nullptr, num_cus(Xh.device().index()), cur_stream()),
+                     rowinfo.numel(), nullptr, nullptr, nullptr, nullptr,
+                     num_cus(Xh.device().index()), cur_stream()),
         "fcm_mfma_stats");
 }
 
@@ -489,7 +490,7 @@ void fcm_mfma_accum(const at::Tensor& Xh, const at::Tensor& Xl, const at::Tensor
   check(tdc_fcm_mfma(1, Xh.data_ptr(), Xl.data_ptr(), xx.data_ptr<float>(), N, (int)Xh.size(1),
                      (int)wx.size(1), Ch.data_ptr(), Cl.data_ptr(), cc.data_ptr<float>(), (int)K,
                      (int)Ch.size(0), m, nan_to_zero ? 1 : 0, nullptr,
-                     const_cast<float*>(rowinfo.data_ptr<float>()), wx.data_ptr<double>(),
+                     const_cast<float*>(rowinfo.data_ptr<float>()), rowinfo.numel(), wx.data_ptr<double>(),
                      ws.data_ptr<double>(), work.data_ptr<float>(),
                      static_cast<const float*>(opt_ptr(shift)), nc, cur_stream()),
         "fcm_mfma_accum");
@@ -497,6 +498,11 @@ void fcm_mfma_accum(const at::Tensor& Xh, const at::Tensor& Xl, const at::Tensor
 
 int64_t fcm_mfma_workspace(const at::Tensor& like, int64_t N, int64_t K, int64_t Kp, int64_t DP) {
   return tdc_fcm_mfma_workspace(N, (int)K, (int)Kp, (int)DP, num_cus(like.device().index()));
+}
+
+int64_t fcm_mfma_rowinfo_len(const at::Tensor& like, int64_t N, int64_t DP) {
+  (void)like;
+  return tdc_fcm_mfma_rowinfo_len(N, (int)DP);
 }
 
 void finalize(const std::optional<at::Tensor>& sums, const std::optional<at::Tensor>& counts,
@@ -1148,6 +1154,7 @@ TORCH_LIBRARY(tdc, m) {
   m.def("fcm_mfma_stats(Tensor Xh, Tensor Xl, Tensor xx, Tensor Ch, Tensor Cl, Tensor cc, int K, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) rowinfo) -> ()");
   m.def("fcm_mfma_accum(Tensor Xh, Tensor Xl, Tensor xx, Tensor rowinfo, Tensor Ch, Tensor Cl, Tensor cc, int K, float m, bool nan_to_zero, Tensor(a!) wx, Tensor(b!) ws, Tensor(c!) work, Tensor? shift=None) -> ()");
   m.def("fcm_mfma_workspace(Tensor like, int N, int K, int Kp, int DP) -> int");
+  m.def("fcm_mfma_rowinfo_len(Tensor like, int N, int DP) -> int");
   m.def("assign_bigd_supported(ScalarType dtype, int DP) -> bool", &assign_bigd_supported);
   m.def("assign_bigd(Tensor X, Tensor? Xs, Tensor xnorm, Tensor Cm2, Tensor? Cs, Tensor cnorm, int kg_tiles, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!)? keys, Tensor(d!)? labels2=None, Tensor(e!)? mind2=None) -> ()");
   m.def("recheck_top2(Tensor X, Tensor C, Tensor(a!) labels, Tensor labels2, Tensor d1, Tensor d2, float tau) -> int");
@@ -1183,6 +1190,7 @@ TORCH_LIBRARY_IMPL(tdc, CUDA, m) {
   m.impl("fcm_mfma_stats", &fcm_mfma_stats);
   m.impl("fcm_mfma_accum", &fcm_mfma_accum);
   m.impl("fcm_mfma_workspace", &fcm_mfma_workspace);
+  m.impl("fcm_mfma_rowinfo_len", &fcm_mfma_rowinfo_len);
   m.impl("fcm_tower_accum", &fcm_tower_accum);
   m.impl("fcm_wide", &fcm_wide);
   m.impl("fcm_wide_rows", &fcm_wide_rows);

@@ -28,6 +28,7 @@
 // 2^-17 ||x||^2): a point on a centroid keeps the reference's NaN -> 0 semantics.  Rows
 // and centroids are shifted by a fixed vector (the shard mean) before the split, so the
 // expansion's cancellation is relative to the data spread, not to its offset.
+#include <cstdlib>
 #include <type_traits>
 
 #include "tdc_common.h"
@@ -39,6 +40,7 @@ namespace {
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr float ZERO_FLOOR = 1.52587890625e-05f;  // 2^-16 (an exact hit computes ~2^-17 |x|^2)
@@ -280,7 +282,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats1_kernel(
     const __bf16* __restrict__ Xh, const __bf16* __restrict__ Xl, const float* __restrict__ xx,
     int64_t N, const __bf16* __restrict__ Ch, const __bf16* __restrict__ Cl,
     const float* __restrict__ cc, int K, int nstages, MParam prm, int32_t* __restrict__ labels,
-    float* __restrict__ rowinfo) {
+    float* __restrict__ rowinfo, float4* __restrict__ fix) {
   constexpr int BN = 64;
   constexpr int CPR = DP / 8;
   constexpr int KS = DP / 16;
@@ -530,6 +532,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats1_kernel(
     const bool on = dmin <= zf;
     labels[row0] = (on && prm.nz) ? 0 : lab;
     rowinfo[row0] = on ? (prm.nz ? 0.f : -1.f) : __builtin_amdgcn_rcpf(Sf);
+    // the two corrected d2 the sum used, for the one-product accumulate pass
+    if (fix)
+      fix[row0] = make_float4(da, fix_b ? db : 0.f, __int_as_float(la),
+                              __int_as_float(fix_b ? lb : -1));
   }
 }
 
@@ -542,10 +548,28 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats1_kernel(
 // WAVES = 8: two waves per SIMD, wave w owns centroid group w & 3 and point half w >> 2
 // (no intra-wave pipeline: the other wave on the SIMD issues its MFMAs under this wave's
 // membership VALU); the two halves' W^T X partials meet in LDS at the end.
-template <int DP, int MODE, bool NZ, int WAVES>
+//
+// STAG (8 waves): the two waves of a SIMD (w and w + 4, same centroid group, point halves 0
+// and 1) run the same program and with one barrier per tile they ran in lockstep -- both
+// in their distance MFMAs, then both in their membership VALU, then both in W^T X, so the
+// VALU segment stood beside an idle matrix pipe.  Staggered, waves 4-7 defer each tile's
+// memberships and W^T X by one tile (distances carried across the barrier in registers,
+// MI355X_MICROARCH.md item 9): in one barrier interval wave w runs dist(t) | memb(t) |
+// W^T X(t) while wave w + 4 runs memb(t-1) | W^T X(t-1) | dist(t), so each one's
+// membership VALU issues beside the other's MFMAs.  Tile t is then read in two intervals:
+// three LDS tile buffers.
+//
+// ONE (DP >= 64, with the stats pass's fix-up rows): the distances are ONE product, xh.ch,
+// like the stats pass's (fcm_mfma_stats1), and each row's two nearest centroids take the
+// stats pass's corrected d2 (fix = {d2a, d2b, la, lb} per row; lb = -1 when the stats pass
+// kept the runner-up's one-product term).  The memberships then use the same d2 as the
+// denominator sum_k t_k of the stats pass (up to the fp32 rounding of the two MFMA orders),
+// and the distance MFMAs drop from 3 x DP/16 to DP/16 per 32 x 32 tile.
+template <int DP, int MODE, bool NZ, int WAVES, bool STAG, bool ONE>
 __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     const __bf16* __restrict__ Xh, const __bf16* __restrict__ Xl, const float* __restrict__ xx,
-    const float* __restrict__ rowinfo, int64_t N, const __bf16* __restrict__ Ch,
+    const float* __restrict__ rowinfo, const float* __restrict__ fix, int64_t N,
+    const __bf16* __restrict__ Ch,
     const __bf16* __restrict__ Cl, const float* __restrict__ cc, int K, int nkt,
     int64_t rows_per_split, int xcd_map, MParam prm, float* __restrict__ part,
     float* __restrict__ part_ws, int KP) {
@@ -557,9 +581,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
   constexpr int IMG = TP * DP * 2;        // bytes of one hi (or lo) image
   constexpr int NT = WAVES * 64;
   static_assert(WAVES == 4 || WAVES == 8, "4 or 8 waves");
-  __shared__ __attribute__((aligned(16))) char s_x[2][2 * IMG];
-  __shared__ __attribute__((aligned(16))) float s_xx[2][TP];
-  __shared__ __attribute__((aligned(16))) float s_in[2][TP];
+  static_assert(!STAG || WAVES == 8, "the stagger pairs the two waves of a SIMD");
+  static_assert(!ONE || WAVES == 8, "one-product form: 8 waves");
+  constexpr int NBUF = STAG ? 3 : 2;
+  constexpr int NRS = ONE ? 6 : 2;        // row statistics: xx, 1/S (+ d2a, d2b, la, lb)
+  __shared__ __attribute__((aligned(16))) char s_x[NBUF][2 * IMG];
+  __shared__ __attribute__((aligned(16))) float s_rs[NBUF][NRS][TP];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
@@ -585,7 +612,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) {
       ch[kk] = sh[kk];
-      cl[kk] = sl[kk];
+      if constexpr (!ONE) cl[kk] = sl[kk];
     }
     ccl = cc[kc];
   }
@@ -630,17 +657,19 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
                       "v"((unsigned)(rr_ * DP * 2) + pcol[i]), "s"(uniform_ptr(base_))    \
                    : "memory", "m0");                                                     \
     }                                                                                     \
-    if (tid < 2 * TP) {                                                                   \
-      const int64_t gr = (R0_) + (tid & (TP - 1));                                        \
-      /* padded rows: a huge norm keeps t finite (rcp(0) * info 0 would be NaN) */       \
-      pv = gr < b ? (tid < TP ? xx[gr] : rowinfo[gr]) : (tid < TP ? 1.0e30f : 0.f);       \
+    if (tid < NRS * TP) {                                                                 \
+      /* wave w loads statistic w of the tile's rows; padded rows: a huge norm keeps t   \
+         finite (rcp(0) * info 0 would be NaN), no fix-up centroid */                    \
+      const int64_t gr = (R0_) + lane;                                                    \
+      if (w == 0) pv = gr < b ? xx[gr] : 1.0e30f;                                         \
+      else if (w == 1) pv = gr < b ? rowinfo[gr] : 0.f;                                   \
+      else pv = gr < b ? fix[gr * 4 + (w - 2)] : (w >= 4 ? __int_as_float(-1) : 0.f);     \
     }                                                                                     \
   }
 #define TDC_TILE_STORE(B_)                                                                \
   {                                                                                       \
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                      \
-    if (tid < TP) s_xx[B_][tid] = pv;                                                     \
-    else if (tid < 2 * TP) s_in[B_][tid - TP] = pv;                                       \
+    if (tid < NRS * TP) s_rs[B_][w][lane] = pv;                                          \
   }
   if (a < b) {
     TDC_TILE_LOAD(a, 0)
@@ -650,38 +679,28 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
 
   // transposed-read lane geometry (T10): group g, row q4, column quad p4
   const int g = lane >> 4, gi = lane & 15, q4 = gi >> 2, p4 = gi & 3;
-  int buf = 0;
-  for (int64_t r0 = a; r0 < b; r0 += TP) {
-    const bool more = r0 + TP < b;
-    // buffer buf ^ 1 was last read in the previous tile, before its barrier
-    if (more) TDC_TILE_LOAD(r0 + TP, buf ^ 1)
-    const char* xh = s_x[buf];
-    const char* xl = s_x[buf] + IMG;
-    // Software pipeline over the two 32-point halves, written out explicitly so that the
-    // membership VALU of one half issues between the MFMAs of the other (one wave per
-    // SIMD: nothing else hides it):
-    //   dist(0) | dist(1) + memberships(0) | W^T X(0) + memberships(1) | W^T X(1)
-    constexpr int EPK = 16 / KS;          // membership elements per distance k-step
-    constexpr int EPW = 16 / (2 * NDT);   // membership elements per W^T X (s, dt) step
-    f32x16 acc0, acc1;
-    bf16x8 wh0[2], wh1[2];
-    f32x4 xq[4], iq[4];
+  constexpr int EPK = 16 / KS;          // membership elements per distance k-step
+  constexpr int EPW = 16 / (2 * NDT);   // membership elements per W^T X (s, dt) step
 #define TDC_DIST(ACC, SUB, INTERLEAVE)                                                    \
   {                                                                                       \
     _Pragma("unroll") for (int i = 0; i < 16; ++i) ACC[i] = ccl;                         \
     const int prow = (SUB) * 32 + r;                                                      \
     bf16x8 ah = as_bf16x8(*reinterpret_cast<const uint4*>(xh + xoff<DP>(prow, h * (CPR / 2)))); \
-    bf16x8 al = as_bf16x8(*reinterpret_cast<const uint4*>(xl + xoff<DP>(prow, h * (CPR / 2)))); \
+    bf16x8 al;                                                                            \
+    if constexpr (!ONE) al = as_bf16x8(*reinterpret_cast<const uint4*>(xl + xoff<DP>(prow, h * (CPR / 2)))); \
     _Pragma("unroll") for (int kk = 0; kk < KS; ++kk) {                                   \
       const int kn = kk + 1 < KS ? kk + 1 : kk;                                           \
       const bf16x8 ahn = as_bf16x8(*reinterpret_cast<const uint4*>(xh + xoff<DP>(prow, h * (CPR / 2) + kn))); \
-      const bf16x8 aln = as_bf16x8(*reinterpret_cast<const uint4*>(xl + xoff<DP>(prow, h * (CPR / 2) + kn))); \
+      bf16x8 aln;                                                                         \
+      if constexpr (!ONE) aln = as_bf16x8(*reinterpret_cast<const uint4*>(xl + xoff<DP>(prow, h * (CPR / 2) + kn))); \
       ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, ch[kk], ACC, 0, 0, 0);            \
-      ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, cl[kk], ACC, 0, 0, 0);            \
-      ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, ch[kk], ACC, 0, 0, 0);            \
+      if constexpr (!ONE) {                                                               \
+        ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, cl[kk], ACC, 0, 0, 0);          \
+        ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, ch[kk], ACC, 0, 0, 0);          \
+      }                                                                                   \
       INTERLEAVE(kk * EPK, EPK)                                                           \
       ah = ahn;                                                                           \
-      al = aln;                                                                           \
+      if constexpr (!ONE) al = aln;                                                       \
     }                                                                                     \
   }
   // memberships of elements [I0, I0 + CNT) of half SUB (distances in ACC) -> WH
@@ -700,8 +719,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
 #define TDC_LOADQ(SUB)                                                                    \
   _Pragma("unroll") for (int g4 = 0; g4 < 4; ++g4) {                                      \
     const int pt = (SUB) * 32 + 8 * g4 + 4 * h;                                           \
-    xq[g4] = *reinterpret_cast<const f32x4*>(&s_xx[buf][pt]);                             \
-    iq[g4] = *reinterpret_cast<const f32x4*>(&s_in[buf][pt]);                             \
+    xq[g4] = *reinterpret_cast<const f32x4*>(&s_rs[buf][0][pt]);                          \
+    iq[g4] = *reinterpret_cast<const f32x4*>(&s_rs[buf][1][pt]);                          \
   }
   // W^T X of half SUB (weights WH): A = W (row = centroid, k = points), B = X^T via
   // transposed reads (T10); INTERLEAVE runs between the (s, dt) steps
@@ -739,6 +758,91 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
 #define TDC_NONE(I0, CNT)
 #define TDC_MEMB0(I0, CNT) TDC_MEMB(acc0, wh0, I0, CNT)
 #define TDC_MEMB1(I0, CNT) TDC_MEMB(acc1, wh1, I0, CNT)
+  // the 8-wave membership step of half SUB: row statistics read from LDS buffer B_ per group
+  // of 4 elements (no xq/iq arrays live across the distance MFMAs: the 2-wave register
+  // budget is 256)
+#define TDC_MEMB8(ACC, WH, SUB, B_)                                                       \
+  _Pragma("unroll") for (int g4 = 0; g4 < 4; ++g4) {                                      \
+    const int pt = (SUB) * 32 + 8 * g4 + 4 * h;                                           \
+    const f32x4 xq4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][0][pt]);                  \
+    const f32x4 iq4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][1][pt]);                  \
+    f32x4 da4, db4;                                                                       \
+    i32x4 la4, lb4;                                                                       \
+    if constexpr (ONE) {                                                                  \
+      da4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][2][pt]);                            \
+      db4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][3][pt]);                            \
+      la4 = *reinterpret_cast<const i32x4*>(&s_rs[B_][4][pt]);                            \
+      lb4 = *reinterpret_cast<const i32x4*>(&s_rs[B_][5][pt]);                            \
+    }                                                                                     \
+    _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                       \
+      const int i = 4 * g4 + e;                                                           \
+      const float zf = ZERO_FLOOR * xq4[e];                                               \
+      float d2 = fmaxf(ACC[i] + xq4[e], zf);                                              \
+      if constexpr (ONE) {                                                                \
+        d2 = kc == la4[e] ? da4[e] : d2;                                                  \
+        d2 = kc == lb4[e] ? db4[e] : d2;                                                  \
+      }                                                                                   \
+      float u = mt<MODE>(d2, prm.expo) * iq4[e];                                          \
+      if constexpr (!NZ) u = iq4[e] < 0.f ? (d2 <= zf ? 1.f : 0.f) : u;                   \
+      const float wv = mw<MODE>(u, prm.m);                                                \
+      const __bf16 bhv = (__bf16)wv;                                                      \
+      WH[i >> 3][i & 7] = bhv;                                                            \
+      wsum += (float)bhv;                                                                 \
+    }                                                                                     \
+  }
+  if constexpr (STAG) {
+    // interval it: tile it is in buffer it % 3 (loaded during interval it - 1), tile it + 1
+    // loads into the next buffer, tile it - 1 (the lagging waves' memberships and W^T X)
+    // stays in the previous one
+    const int sub = w >> 2;
+    const int64_t ntile = (b - a + TP - 1) / TP;
+    f32x16 acc0;
+    bf16x8 wh0[2];
+    int bc = 0;
+    for (int64_t it = 0; it <= ntile; ++it) {
+      const bool cur = it < ntile, more = it + 1 < ntile;
+      const int bn = bc == 2 ? 0 : bc + 1, bp = bc == 0 ? 2 : bc - 1;
+      if (more) TDC_TILE_LOAD(a + (it + 1) * TP, bn)
+      if (sub == 0) {
+        if (cur) {
+          const char* xh = s_x[bc];
+          const char* xl = s_x[bc] + IMG;
+          TDC_DIST(acc0, 0, TDC_NONE)
+          TDC_MEMB8(acc0, wh0, 0, bc)
+          TDC_WTX(0, wh0, TDC_NONE, )
+        }
+      } else {
+        if (it > 0) {
+          const char* xh = s_x[bp];
+          const char* xl = s_x[bp] + IMG;
+          TDC_MEMB8(acc0, wh0, 1, bp)
+          TDC_WTX(1, wh0, TDC_NONE, )
+        }
+        if (cur) {
+          const char* xh = s_x[bc];
+          const char* xl = s_x[bc] + IMG;
+          TDC_DIST(acc0, 1, TDC_NONE)
+        }
+      }
+      if (more) TDC_TILE_STORE(bn)
+      __syncthreads();
+      bc = bn;
+    }
+  } else {
+  int buf = 0;
+  for (int64_t r0 = a; r0 < b; r0 += TP) {
+    const bool more = r0 + TP < b;
+    // buffer buf ^ 1 was last read in the previous tile, before its barrier
+    if (more) TDC_TILE_LOAD(r0 + TP, buf ^ 1)
+    const char* xh = s_x[buf];
+    const char* xl = s_x[buf] + IMG;
+    // Software pipeline over the two 32-point halves, written out explicitly so that the
+    // membership VALU of one half issues between the MFMAs of the other (one wave per
+    // SIMD: nothing else hides it):
+    //   dist(0) | dist(1) + memberships(0) | W^T X(0) + memberships(1) | W^T X(1)
+    f32x16 acc0, acc1;
+    bf16x8 wh0[2], wh1[2];
+    f32x4 xq[4], iq[4];
     if constexpr (WAVES == 4) {
       TDC_DIST(acc0, 0, TDC_NONE)
       TDC_LOADQ(0)
@@ -747,33 +851,21 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
       TDC_WTX(0, wh0, TDC_MEMB1, )
       TDC_WTX(1, wh1, TDC_NONE, )
     } else {
-      // 8 waves: row statistics read from LDS per group of 4 elements (no xq/iq arrays
-      // live across the distance MFMAs: the 2-wave register budget is 256)
       const int sub = w >> 2;
       TDC_DIST(acc0, sub, TDC_NONE)
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int pt = sub * 32 + 8 * g4 + 4 * h;
-        xq[0] = *reinterpret_cast<const f32x4*>(&s_xx[buf][pt]);
-        iq[0] = *reinterpret_cast<const f32x4*>(&s_in[buf][pt]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 4 * g4 + e;
-          const float zf = ZERO_FLOOR * xq[0][e];
-          const float d2 = fmaxf(acc0[i] + xq[0][e], zf);
-          float u = mt<MODE>(d2, prm.expo) * iq[0][e];
-          if constexpr (!NZ) u = iq[0][e] < 0.f ? (d2 <= zf ? 1.f : 0.f) : u;
-          const float wv = mw<MODE>(u, prm.m);
-          const __bf16 bhv = (__bf16)wv;
-          wh0[i >> 3][i & 7] = bhv;
-          wsum += (float)bhv;
-        }
-      }
+      TDC_MEMB8(acc0, wh0, sub, buf)
       // early tile release: the tile's last transposed X reads are in registers, so the
       // next tile's row statistics and the barrier go before the last three W^T X MFMAs,
       // which then run under the next tile's first LDS reads (fcm10m -0.5 %)
       TDC_WTX(sub, wh0, TDC_NONE, { if (more) TDC_TILE_STORE(buf ^ 1) __syncthreads(); })
     }
+    if (WAVES == 4) {
+      if (more) TDC_TILE_STORE(buf ^ 1)
+      __syncthreads();
+    }
+    buf ^= 1;
+  }
+  }
 #undef TDC_NONE
 #undef TDC_MEMB0
 #undef TDC_MEMB1
@@ -782,12 +874,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
 #undef TDC_LOADQ
 #undef TDC_WTX
 #undef TDC_TRLD
-    if (WAVES == 4) {
-      if (more) TDC_TILE_STORE(buf ^ 1)
-      __syncthreads();
-    }
-    buf ^= 1;
-  }
+#undef TDC_MEMB8
 #undef TDC_TILE_LOAD
 #undef TDC_TILE_STORE
 
@@ -796,7 +883,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     // waves of the same centroid group through the (now idle) tile buffers
     static_assert(4 * 32 * DP * 4 <= (int)sizeof(s_x), "exchange fits the tile buffers");
     float* xo = reinterpret_cast<float*>(&s_x[0][0]) + cg * 32 * DP;
-    float* xw = &s_xx[0][0] + cg * 32;
+    float* xw = &s_rs[0][0][0] + cg * 32;
     __syncthreads();
     const float wpair = wsum + __shfl_xor(wsum, 32, 64);  // all lanes take part in the swap
     if (w >= 4) {
@@ -897,7 +984,7 @@ MParam make_mparam(double m, int nz) {
 template <int DP>
 int launch_mstats(const void* Xh, const void* Xl, const float* xx, int64_t N, const void* Ch,
                   const void* Cl, const float* cc, int K, int Kp, double m, int nz,
-                  int32_t* labels, float* rowinfo, hipStream_t s) {
+                  int32_t* labels, float* rowinfo, float* fix, hipStream_t s) {
   constexpr int WAVES = 8;
   const int64_t blocks = (N + WAVES * 32 - 1) / (WAVES * 32);
   const MParam p = make_mparam(m, nz);
@@ -908,7 +995,7 @@ int launch_mstats(const void* Xh, const void* Xl, const float* xx, int64_t N, co
 #define TDC_LS1(MODE)                                                                         \
   hipLaunchKernelGGL((fcm_mfma_stats1_kernel<DP, MODE, WAVES>), dim3((unsigned)blocks), dim3(WAVES * 64), 0, s, \
                      (const __bf16*)Xh, (const __bf16*)Xl, xx, N, (const __bf16*)Ch,          \
-                     (const __bf16*)Cl, cc, K, Kp / 64, p, labels, rowinfo)
+                     (const __bf16*)Cl, cc, K, Kp / 64, p, labels, rowinfo, (float4*)fix)
   // one product + fix-up from DP = 64 (fcm10m 19.05 -> 18.60 ms, profiles/fcm_stats1_ab_r04m.txt);
   // at DP = 32 the bf16x3 kernel's 6 MFMAs per tile are not what bounds it
   if constexpr (DP >= 64) {
@@ -935,7 +1022,7 @@ inline void accum_geometry(int64_t N, int K, int num_cus, int* nkt, int64_t* spl
 
 template <int DP>
 int launch_maccum(const void* Xh, const void* Xl, const float* xx, const float* rowinfo,
-                  int64_t N, const void* Ch, const void* Cl, const float* cc, int K, int Kp,
+                  const float* fix, int64_t N, const void* Ch, const void* Cl, const float* cc, int K, int Kp,
                   int D, double m, int nz, float* part, const float* mu, double* wx, double* ws,
                   int num_cus, hipStream_t s) {
   int nkt;
@@ -947,16 +1034,28 @@ int launch_maccum(const void* Xh, const void* Xl, const float* xx, const float* 
   const MParam p = make_mparam(m, nz);
   // 8 waves (2 per SIMD): one wave's epilogue VALU runs beside the other's MFMAs; the
   // one-wave software-pipelined WAVES=4 form measured slower (docs/PERF_NOTES.md)
-#define TDC_LA(MODE, NZV)                                                                     \
-  hipLaunchKernelGGL((fcm_mfma_accum_kernel<DP, MODE, NZV, 8>), dim3((unsigned)nb), dim3(512),   \
-                     0, s, (const __bf16*)Xh, (const __bf16*)Xl, xx, rowinfo, N,               \
-                     (const __bf16*)Ch, (const __bf16*)Cl, cc, K, nkt, rps, xcd, p, part,      \
+  // TDC_FCM_NOSTAG=1 selects the lockstep form (A/B of the stagger); the one-product form
+  // runs when the stats pass left its fix-up rows (DP >= 64)
+  static const bool stag = std::getenv("TDC_FCM_NOSTAG") == nullptr;
+#define TDC_LA(MODE, NZV, ST, ONEV)                                                           \
+  hipLaunchKernelGGL((fcm_mfma_accum_kernel<DP, MODE, NZV, 8, ST, ONEV>), dim3((unsigned)nb),  \
+                     dim3(512), 0, s, (const __bf16*)Xh, (const __bf16*)Xl, xx, rowinfo, fix,  \
+                     N, (const __bf16*)Ch, (const __bf16*)Cl, cc, K, nkt, rps, xcd, p, part,   \
                      part_ws, Kp)
-  if (m == 2.0) {
-    if (nz) TDC_LA(2, true); else TDC_LA(2, false);
-  } else {
-    if (nz) TDC_LA(0, true); else TDC_LA(0, false);
+  // (the bf16x3 form keeps the lockstep loop: staggered, its extra live registers spill --
+  // fcm10m 17.7 -> 19.7 ms; one product + stagger 16.0 ms, profiles/fcm10m_*_r05e.txt)
+#define TDC_LA2(MODE, NZV)                                                                    \
+  if (DP >= 64 && fix) {                                                                      \
+    if (stag) TDC_LA(MODE, NZV, true, DP >= 64); else TDC_LA(MODE, NZV, false, DP >= 64);     \
+  } else {                                                                                    \
+    TDC_LA(MODE, NZV, false, false);                                                          \
   }
+  if (m == 2.0) {
+    if (nz) { TDC_LA2(2, true) } else { TDC_LA2(2, false) }
+  } else {
+    if (nz) { TDC_LA2(0, true) } else { TDC_LA2(0, false) }
+  }
+#undef TDC_LA2
 #undef TDC_LA
   TDC_CHECK_LAUNCH();
   const int64_t tot = (int64_t)K * DP + K;
@@ -1390,19 +1489,29 @@ int64_t tdc_fcm_mfma_workspace(int64_t N, int K, int Kp, int DP, int num_cus) {
   return splits * (int64_t)Kp * (DP + 1);
 }
 
+int64_t tdc_fcm_mfma_rowinfo_len(int64_t N, int DP) {
+  return DP >= 64 ? ((N + 3) / 4) * 4 + 4 * N : N;
+}
 int tdc_fcm_mfma(int pass, const void* Xh, const void* Xl, const float* xx, int64_t N, int DP,
                  int D, const void* Ch, const void* Cl, const float* cc, int K, int Kp, double m,
-                 int nan_to_zero, int32_t* labels, float* rowinfo, double* wx, double* ws,
-                 float* work, const float* shift, int num_cus, hipStream_t s) {
+                 int nan_to_zero, int32_t* labels, float* rowinfo, int64_t rowinfo_len,
+                 double* wx, double* ws, float* work, const float* shift, int num_cus,
+                 hipStream_t s) {
   if (N <= 0 || K <= 0) return 0;
   if (Kp % 128 != 0 || Kp < K) return (int)hipErrorInvalidValue;
+  if (rowinfo_len < N) return (int)hipErrorInvalidValue;
+  // the fix-up rows follow the [N] statistics (16-byte aligned) when the caller sized
+  // rowinfo for them (tdc_fcm_mfma_rowinfo_len); without them the accumulate pass runs the
+  // bf16x3 distances
+  float* fix = (DP >= 64 && rowinfo_len >= tdc_fcm_mfma_rowinfo_len(N, DP))
+                   ? rowinfo + ((N + 3) / 4) * 4 : nullptr;
 #define TDC_FM(DPV)                                                                           \
   if (DP == DPV) {                                                                            \
     if (pass == 0)                                                                            \
       return launch_mstats<DPV>(Xh, Xl, xx, N, Ch, Cl, cc, K, Kp, m, nan_to_zero, labels,     \
-                                rowinfo, s);                                                  \
-    return launch_maccum<DPV>(Xh, Xl, xx, rowinfo, N, Ch, Cl, cc, K, Kp, D, m, nan_to_zero,   \
-                              work, shift, wx, ws, num_cus, s);                               \
+                                rowinfo, fix, s);                                             \
+    return launch_maccum<DPV>(Xh, Xl, xx, rowinfo, fix, N, Ch, Cl, cc, K, Kp, D, m,           \
+                              nan_to_zero, work, shift, wx, ws, num_cus, s);                  \
   }
   TDC_FM(32)
   TDC_FM(64)

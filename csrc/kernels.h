@@ -148,11 +148,16 @@ int tdc_fcm_split_rows(const float* src, int64_t rows, int64_t valid, int d, int
 // work: fp32 [tdc_fcm_mfma_workspace(...)] per-block partial slabs of pass 1; shift
 // (nullable, fp32 [D]): the vector subtracted from rows and centroids at the split, added
 // back as shift * sum w in the reduction.
+// rowinfo holds rowinfo_len floats: [N] row statistics, and from DP = 64, when rowinfo_len >=
+// tdc_fcm_mfma_rowinfo_len(N, DP), each row's two corrected nearest d2 after them (16-byte
+// aligned float4 {d2a, d2b, la, lb}); with them pass 1 runs one-product distances.
 int tdc_fcm_mfma(int pass, const void* Xh, const void* Xl, const float* xx, int64_t N, int DP,
                  int D, const void* Ch, const void* Cl, const float* cc, int K, int Kp, double m,
-                 int nan_to_zero, int32_t* labels, float* rowinfo, double* wx, double* ws,
-                 float* work, const float* shift, int num_cus, hipStream_t stream);
+                 int nan_to_zero, int32_t* labels, float* rowinfo, int64_t rowinfo_len,
+                 double* wx, double* ws, float* work, const float* shift, int num_cus,
+                 hipStream_t stream);
 int64_t tdc_fcm_mfma_workspace(int64_t N, int K, int Kp, int DP, int num_cus);
+int64_t tdc_fcm_mfma_rowinfo_len(int64_t N, int DP);
 // Wide D (DP in 128 ... 1024, multiples of 128), over a chunk of M rows with the [M, K]
 // block G (fp32): pass 0: G = d2 (hi/lo MFMA, distances within 2^-16 ||x||^2 of a centroid
 // stored as 0, the on-centroid rule of tdc_fcm_wide pass 1, which then turns G into w);

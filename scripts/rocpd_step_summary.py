@@ -10,7 +10,7 @@ sel = rows[first:]
 span = (sel[-1][2] - sel[0][1]) / 1e3 / nsteps
 agg = collections.defaultdict(lambda: [0, 0.0])
 for n, s, e in sel:
-    short = re.sub(r"\(.*", "", n)[:90]
+    short = re.sub(r"\(.*", "", n.replace("(anonymous namespace)::", ""))[:110]
     agg[short][0] += 1; agg[short][1] += (e - s) / 1e3
 tot = sum(v[1] for v in agg.values()) / nsteps
 print(f"per step: wall span {span:.1f} us, kernel busy {tot:.1f} us, {len(sel)/nsteps:.1f} launches")

@@ -1290,7 +1290,12 @@ class HipMfmaFCM(_LocalOpsBase):
             self.xh = torch.empty(n, self.dp, dtype=torch.bfloat16, device=dev)
             self.xl = torch.empty_like(self.xh)
             self.xx = torch.empty(n, dtype=torch.float32, device=dev)
-            self.rowinfo = torch.empty(n, dtype=torch.float32, device=dev)
+            self.rowinfo = None
+        # row statistics + (DP >= 64) the two corrected nearest d2 per row, which let the
+        # accumulate pass run one-product distances
+        ril = self._ri_len(n)
+        if self.rowinfo is None or self.rowinfo.numel() < ril:
+            self.rowinfo = torch.empty(ril, dtype=torch.float32, device=self.device)
         self.ops.fcm_split_rows(self._xsrc[:, : self.d], n, 0, self.xh[:n], self.xl[:n],
                                 self.xx[:n], self.mu)
         self._xsrc = None  # the hi/lo rows are the shard from here on
@@ -1316,10 +1321,24 @@ class HipMfmaFCM(_LocalOpsBase):
         n = self.n
         return self.xh[:n], self.xl[:n], self.xx[:n]
 
+    one_product = True  # class switch: False keeps bf16x3 distances in the accumulate pass
+
+    @property
+    def precision(self) -> str:
+        """What the step computes, in words (bench.py reports it)."""
+        if self.one_product and self.dp >= 64:
+            return FCM_PRECISION["bf16_one"]
+        return FCM_PRECISION["bf16"]
+
+    def _ri_len(self, n):
+        if not self.one_product:
+            return n
+        return int(self.ops.fcm_mfma_rowinfo_len(self.cc, n, self.dp))
+
     def step(self, C, labels, wx, ws):
         self.prepare(C)
         xh, xl, xx = self._ops_args()
-        ri = self.rowinfo[: self.n]
+        ri = self.rowinfo[: self._ri_len(self.n)]
         self.ops.fcm_mfma_stats(xh, xl, xx, self.ch, self.cl, self.cc, self.k, self.m,
                                 self.nan_to_zero, labels, ri)
         self.ops.fcm_mfma_accum(xh, xl, xx, ri, self.ch, self.cl, self.cc, self.k, self.m,
@@ -1355,6 +1374,8 @@ class HipMfmaWideFCM(HipMfmaFCM):
     name = "hip_fcm_mfma"
     chunk_elems = 1 << 27
     max_chunk_rows = 1 << 20  # keeps every per-split X offset of the W^T X pass in 32 bits
+
+    one_product = False  # no stats-pass fix-up rows on the wide path
 
     @staticmethod
     def _pick_dp(d: int) -> Optional[int]:
@@ -1453,7 +1474,12 @@ FCM_PRECISION = {
             "cores), fp64 memberships and sums",
     "fp32": "fp32 difference-form distances and memberships, fp64 sums",
     "bf16": "bf16x3 MFMA distances (fp32-faithful), fp32 memberships, bf16 weights in the "
-            "W^T X MFMAs, fp64 sums",
+            "W^T X MFMAs (hi+lo rows), fp64 sums",
+    # HipMfmaFCM from D = 64: both passes run one product and correct the two nearest
+    "bf16_one": "bf16 MFMA distances: one product (x_hi . c_hi, ~2^-9/sqrt(D) relative error "
+                "on x.c) for every centroid, each row's two nearest corrected to bf16x3 "
+                "(fp32-faithful); fp32 memberships, bf16 weights in the W^T X MFMAs (hi+lo "
+                "rows), fp64 sums",
 }
 
 

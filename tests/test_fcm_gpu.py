@@ -268,3 +268,34 @@ def test_fcm_mfma_blobs_accuracy(gpu, m):
     torch.testing.assert_close(ws.cpu()[ok], b[ok], rtol=1e-2 if m == 2.0 else 4e-2,
                                atol=1e-6 * float(b.max()))
     assert (lab.long().cpu() == lr.long()).double().mean().item() > 0.999
+
+
+@pytest.mark.parametrize("k,d", [(1024, 128), (257, 64)])
+@pytest.mark.parametrize("m", [2.0, 1.5])
+@pytest.mark.parametrize("nz", [True, False])
+def test_fcm_mfma_one_product_vs_bf16x3(gpu, k, d, m, nz):
+    """From D = 64 the accumulate pass runs one-product distances with the stats pass's
+    two-nearest fix-up (HipMfmaFCM.one_product); the bf16x3 form (one_product = False)
+    on the same data and centroids must agree with it to well inside the oracle
+    tolerance, and both must meet the oracle, and the precision string must say which."""
+    from tensorflow_distributed_clustering_amd.ops import FCM_PRECISION, HipMfmaFCM
+    n = 20001
+    x, c = _data(n, k, d, 11 * k + d)
+    xg, cg = x.float().to(gpu), c.float().to(gpu)
+    res = {}
+    for one in (True, False):
+        ops = HipMfmaFCM(xg, k, m, nz)
+        ops.one_product = one
+        lab = torch.empty(n, dtype=torch.int32, device=gpu)
+        wx = torch.zeros(k, d, dtype=torch.float64, device=gpu)
+        ws = torch.zeros(k, dtype=torch.float64, device=gpu)
+        ops.step(cg, lab, wx, ws)
+        assert ops.precision == FCM_PRECISION["bf16_one" if one else "bf16"]
+        _check(wx.cpu(), ws.cpu(), lab, xg.cpu(), cg.cpu(), m, nz, 2e-3 * m, 0.998)
+        res[one] = (wx.cpu(), ws.cpu(), lab.cpu())
+    (wx1, ws1, l1), (wx3, ws3, l3) = res[True], res[False]
+    ok = ws3 > 1e-12 * ws3.max()
+    assert float(((ws1 - ws3).abs() / ws3.clamp_min(1e-300))[ok].max()) < 2e-3
+    c1, c3 = wx1 / ws1.clamp_min(1e-300)[:, None], wx3 / ws3.clamp_min(1e-300)[:, None]
+    assert float((c1 - c3)[ok].abs().max()) < 1e-3 * float(c3[ok].abs().max())
+    assert (l1 == l3).double().mean().item() >= 0.999
