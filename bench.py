@@ -112,6 +112,9 @@ def parse(argv=None):
                          "changed between fp64 running totals (with a full re-sum every "
                          "--delta-refresh steps and after steps that moved > 40%% of the rows); "
                          "full re-sums every row every step; auto = delta where supported")
+    ap.add_argument("--comm-mode", default="auto", choices=["auto", "allreduce", "rsag"],
+                    help="partial-sum reduction (ClusterConfig.comm_mode); with "
+                         "TDC_FORCE_COLLECTIVES=1 a world-1 run issues the RCCL calls too")
     ap.add_argument("--delta-refresh", type=int, default=32,
                     help="delta update: full re-sum every this many steps (0: never)")
     ap.add_argument("--deterministic", action="store_true",
@@ -167,7 +170,8 @@ def main(argv=None):
     cfg = tdc.ClusterConfig(n_clusters=a.k, max_iter=a.steps, dtype=a.dtype, init=a.init,
                             seed=a.seed, compute_inertia=False, algorithm=a.algorithm,
                             fuzzifier=a.fuzzifier, update=a.update,
-                            delta_refresh=a.delta_refresh, deterministic=a.deterministic)
+                            delta_refresh=a.delta_refresh, deterministic=a.deterministic,
+                            comm_mode=a.comm_mode)
     if a.mode == "minibatch":
         from tensorflow_distributed_clustering_amd.models.minibatch import MiniBatchStepper
         eng = MiniBatchStepper(x, cfg.replace(batch_size=a.batch_size or (1 << 20)), comm,
@@ -259,7 +263,8 @@ def main(argv=None):
     check = None
     if not a.no_check and src_info is None:
         if a.method == "fcm":
-            check = fcm_witness(eng, x, n_global, s, e, comm, torch, a)
+            check = fcm_witness(eng, x, n_global, s, e, comm, torch, a,
+                                C0=snap["C"] if snap is not None else None)
         else:
             check = witness(eng, x, n_global, s, e, comm, torch, a)
     breakdown = None
@@ -302,6 +307,8 @@ def main(argv=None):
         }
         if update_info is not None:
             out["update"] = update_info
+        out["comm"] = {"mode": "rsag" if getattr(eng, "rsag", False) else "allreduce",
+                       "collective": bool(comm.collective), "backend": comm.backend}
         out["graph_replay"] = graph
         if check is not None:
             out["check"] = check
@@ -425,51 +432,74 @@ def phase_breakdown(eng, torch, dev, reps: int = 5):
 WITNESS_ROWS = 65536
 
 
-def fcm_witness(eng, x, n_global, s, e, comm, torch, a):
-    """FCM correctness witness, after the timed region: ONE FCM step from the final
-    centroids on a fixed sample of WITNESS_ROWS global rows (evenly spaced, world-size
-    invariant), computed by the same native tower the engine runs and by the fp64 oracle
-    (plain PyTorch difference-form distances, `scripts/distribuitedClustering.py:112-137`);
-    reported: the centroid error max|c - c_ref| / max|c_ref| and the worst relative error
-    of sum_i w_ik over the clusters holding >= 1e-6 of the total weight."""
+def fcm_witness(eng, x, n_global, s, e, comm, torch, a, C0=None):
+    """FCM correctness witness, after the timed region: ONE FCM step on a fixed sample of
+    WITNESS_ROWS global rows (evenly spaced, world-size invariant), computed by the same
+    native tower the engine runs and by the fp64 oracle (plain PyTorch difference-form
+    distances, `scripts/distribuitedClustering.py:112-137`); reported: the centroid error
+    max|c - c_ref| / max|c_ref| and the worst relative error of sum_i w_ik over the
+    clusters holding >= 1e-6 of the total weight -- from the final centroids, and (key
+    ``at_init``) from the init centroids C0.  FCM at m = 2 on well-mixed high-D data can
+    collapse every centroid onto the grand mean (distance concentration: u -> 1/K); the
+    final step is then trivially exact (w = K^-2 is a bf16 number), which
+    ``final_ws_spread`` = (max - min) / mean of sum_i w_ik shows, while the init step keeps
+    the memberships spread."""
     from tensorflow_distributed_clustering_amd.ops import FCM_PRECISION, make_fcm_ops
     from tensorflow_distributed_clustering_amd.ops import reference as ref
     dev = comm.device
-    C = eng.centers().double()
-    k, d = C.shape
     g = torch.arange(WITNESS_ROWS, dtype=torch.float64) * (n_global / WITNESS_ROWS)
     g = torch.unique(g.floor().long())
     loc = (g[(g >= s) & (g < e)] - s).to(dev)
-    xs = x.index_select(0, loc)[:, :d] if loc.numel() else x[:0, :d]
     nz = eng.cfg.fcm_nan_to_zero
-    wx = torch.zeros(k, d, dtype=torch.float64, device=dev)
-    ws = torch.zeros(k, dtype=torch.float64, device=dev)
-    wr = torch.zeros(k, d, dtype=torch.float64, device=dev)
-    wsr = torch.zeros(k, dtype=torch.float64, device=dev)
-    if xs.shape[0]:
-        ops = make_fcm_ops(xs.float() if eng.dtype_name != "fp64" else xs.double(), k,
-                           eng.dtype_name, eng.m, nz, eng.cfg.backend)
-        lab = torch.empty(xs.shape[0], dtype=torch.int32, device=dev)
-        ops.step(C.to(ops.c_dtype).contiguous(), lab, wx, ws)
-        step = max(1, (1 << 25) // max(1, k))
-        for r0 in range(0, xs.shape[0], step):
-            pa, pb, _ = ref.fcm_partial(xs[r0:r0 + step].double(), C, eng.m, nz,
-                                        acc_dtype=torch.float64)
-            wr += pa
-            wsr += pb
-    for t in (wx, ws, wr, wsr):
-        comm.allreduce_(t)
-    c_k = wx / ws.clamp_min(1e-300)[:, None]
-    c_r = wr / wsr.clamp_min(1e-300)[:, None]
-    ok = wsr > 1e-6 * float(wsr.sum())
-    cerr = float((c_k - c_r)[ok].abs().max()) / max(1e-300, float(c_r[ok].abs().max())) \
-        if bool(ok.any()) else 0.0
-    werr = float(((ws - wsr).abs() / wsr.clamp_min(1e-300))[ok].max()) if bool(ok.any()) else 0.0
-    return {"fcm_centroid_rel_err": cerr, "fcm_weight_sum_rel_err": werr,
-            "sample_rows": int(comm.sum_scalar(float(loc.numel()))),
-            "precision": (getattr(ops, "precision", None) if xs.shape[0] else None)
-            or FCM_PRECISION.get(eng.dtype_name, eng.dtype_name),
-            "backend": ops.name if xs.shape[0] else None}
+
+    def at(C):
+        C = C.double()
+        k, d = C.shape
+        xs = x.index_select(0, loc)[:, :d] if loc.numel() else x[:0, :d]
+        wx = torch.zeros(k, d, dtype=torch.float64, device=dev)
+        ws = torch.zeros(k, dtype=torch.float64, device=dev)
+        wr = torch.zeros(k, d, dtype=torch.float64, device=dev)
+        wsr = torch.zeros(k, dtype=torch.float64, device=dev)
+        ops = None
+        if xs.shape[0]:
+            # the engine's own operand dtype: a bf16 shard reaches the tower as bf16
+            xin = xs.double() if eng.dtype_name == "fp64" else (
+                xs if xs.dtype == torch.bfloat16 else xs.float())
+            ops = make_fcm_ops(xin, k, eng.dtype_name, eng.m, nz, eng.cfg.backend)
+            lab = torch.empty(xs.shape[0], dtype=torch.int32, device=dev)
+            ops.step(C.to(ops.c_dtype).contiguous(), lab, wx, ws)
+            step = max(1, (1 << 24) // max(1, k * d))
+            for r0 in range(0, xs.shape[0], step):
+                # exact difference form: a sampled row that IS a centroid (random-row init)
+                # is at distance exactly 0, the rule the native towers apply
+                pa, pb, _ = ref.fcm_partial(xs[r0:r0 + step].double(), C, eng.m, nz,
+                                            acc_dtype=torch.float64, exact=True)
+                wr += pa
+                wsr += pb
+        for t in (wx, ws, wr, wsr):
+            comm.allreduce_(t)
+        c_k = wx / ws.clamp_min(1e-300)[:, None]
+        c_r = wr / wsr.clamp_min(1e-300)[:, None]
+        ok = wsr > 1e-6 * float(wsr.sum())
+        cerr = float((c_k - c_r)[ok].abs().max()) / max(1e-300, float(c_r[ok].abs().max())) \
+            if bool(ok.any()) else 0.0
+        werr = float(((ws - wsr).abs() / wsr.clamp_min(1e-300))[ok].max()) \
+            if bool(ok.any()) else 0.0
+        spread = float((wsr.max() - wsr.min()) / wsr.mean().clamp_min(1e-300))
+        return {"fcm_centroid_rel_err": cerr, "fcm_weight_sum_rel_err": werr,
+                "ws_spread": spread,
+                "precision": (getattr(ops, "precision", None) if ops is not None else None)
+                or FCM_PRECISION.get(eng.dtype_name, eng.dtype_name),
+                "backend": ops.name if ops is not None else None}
+
+    out = at(eng.centers())
+    out["final_ws_spread"] = out.pop("ws_spread")
+    out["sample_rows"] = int(comm.sum_scalar(float(loc.numel())))
+    if C0 is not None:
+        ini = at(C0)
+        out["at_init"] = {kk: ini[kk] for kk in ("fcm_centroid_rel_err",
+                                                 "fcm_weight_sum_rel_err", "ws_spread")}
+    return out
 
 
 def witness(eng, x, n_global, s, e, comm, torch, a):

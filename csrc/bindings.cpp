@@ -461,7 +461,7 @@ void fcm_mfma_stats(const at::Tensor& Xh, const at::Tensor& Xl, const at::Tensor
   TORCH_CHECK(rowinfo.scalar_type() == at::kFloat && rowinfo.is_contiguous() && rowinfo.numel() >= N,
               "tdc.fcm_mfma_stats: rowinfo fp32 [N]");
   const DevGuard guard(Xh.device());
-  check(tdc_fcm_mfma(0, Xh.data_ptr(), Xl.data_ptr(), xx.data_ptr<float>(), N, (int)Xh.size(1), 0,
+  check(tdc_fcm_mfma(0, Xh.data_ptr(), Xl.data_ptr(), nullptr, xx.data_ptr<float>(), N, (int)Xh.size(1), 0,
                      Ch.data_ptr(), Cl.data_ptr(), cc.data_ptr<float>(), (int)K, (int)Ch.size(0),
                      m, nan_to_zero ? 1 : 0, labels.data_ptr<int32_t>(), rowinfo.data_ptr<float>(),
                      rowinfo.numel(), nullptr, nullptr, nullptr, nullptr,
@@ -472,8 +472,13 @@ void fcm_mfma_stats(const at::Tensor& Xh, const at::Tensor& Xl, const at::Tensor
 void fcm_mfma_accum(const at::Tensor& Xh, const at::Tensor& Xl, const at::Tensor& xx,
                     const at::Tensor& rowinfo, const at::Tensor& Ch, const at::Tensor& Cl,
                     const at::Tensor& cc, int64_t K, double m, bool nan_to_zero, at::Tensor& wx,
-                    at::Tensor& ws, at::Tensor& work, const std::optional<at::Tensor>& shift) {
+                    at::Tensor& ws, at::Tensor& work, const std::optional<at::Tensor>& shift,
+                    const std::optional<at::Tensor>& Xr) {
   check_mfma_fcm(Xh, Xl, xx, Ch, Cl, cc, K, m, "fcm_mfma_accum");
+  if (Xr.has_value() && Xr->defined())
+    TORCH_CHECK(Xr->scalar_type() == at::kBFloat16 && Xr->is_contiguous() &&
+                    Xr->sizes() == Xh.sizes(),
+                "tdc.fcm_mfma_accum: Xr bf16 [N, DP] like Xh");
   const int nc = num_cus(Xh.device().index());
   TORCH_CHECK(work.scalar_type() == at::kFloat && work.is_contiguous() &&
                   work.numel() >= tdc_fcm_mfma_workspace(Xh.size(0), (int)K, (int)Ch.size(0),
@@ -487,7 +492,7 @@ void fcm_mfma_accum(const at::Tensor& Xh, const at::Tensor& Xl, const at::Tensor
                   wx.size(1) <= Xh.size(1) && ws.numel() == K,
               "tdc.fcm_mfma_accum: wx [K, D] / ws [K] fp64");
   const DevGuard guard(Xh.device());
-  check(tdc_fcm_mfma(1, Xh.data_ptr(), Xl.data_ptr(), xx.data_ptr<float>(), N, (int)Xh.size(1),
+  check(tdc_fcm_mfma(1, Xh.data_ptr(), Xl.data_ptr(), opt_ptr(Xr), xx.data_ptr<float>(), N, (int)Xh.size(1),
                      (int)wx.size(1), Ch.data_ptr(), Cl.data_ptr(), cc.data_ptr<float>(), (int)K,
                      (int)Ch.size(0), m, nan_to_zero ? 1 : 0, nullptr,
                      const_cast<float*>(rowinfo.data_ptr<float>()), rowinfo.numel(), wx.data_ptr<double>(),
@@ -1152,7 +1157,7 @@ TORCH_LIBRARY(tdc, m) {
   m.def("fcm_mfma_wide(int stage, Tensor Xh, Tensor Xl, Tensor xx, Tensor Ch, Tensor Cl, Tensor cc, int K, int D, Tensor(a!) G, Tensor(b!)? work=None, Tensor? shift=None, Tensor(c!)? wx=None, Tensor(d!)? ws=None) -> ()");
   m.def("fcm_split_rows(Tensor src, int valid, int neg2, Tensor(a!) hi, Tensor(b!) lo, Tensor(c!)? norm, Tensor? shift=None) -> ()");
   m.def("fcm_mfma_stats(Tensor Xh, Tensor Xl, Tensor xx, Tensor Ch, Tensor Cl, Tensor cc, int K, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) rowinfo) -> ()");
-  m.def("fcm_mfma_accum(Tensor Xh, Tensor Xl, Tensor xx, Tensor rowinfo, Tensor Ch, Tensor Cl, Tensor cc, int K, float m, bool nan_to_zero, Tensor(a!) wx, Tensor(b!) ws, Tensor(c!) work, Tensor? shift=None) -> ()");
+  m.def("fcm_mfma_accum(Tensor Xh, Tensor Xl, Tensor xx, Tensor rowinfo, Tensor Ch, Tensor Cl, Tensor cc, int K, float m, bool nan_to_zero, Tensor(a!) wx, Tensor(b!) ws, Tensor(c!) work, Tensor? shift=None, Tensor? Xr=None) -> ()");
   m.def("fcm_mfma_workspace(Tensor like, int N, int K, int Kp, int DP) -> int");
   m.def("fcm_mfma_rowinfo_len(Tensor like, int N, int DP) -> int");
   m.def("assign_bigd_supported(ScalarType dtype, int DP) -> bool", &assign_bigd_supported);

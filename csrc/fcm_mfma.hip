@@ -28,7 +28,6 @@
 // 2^-17 ||x||^2): a point on a centroid keeps the reference's NaN -> 0 semantics.  Rows
 // and centroids are shifted by a fixed vector (the shard mean) before the split, so the
 // expansion's cancellation is relative to the data spread, not to its offset.
-#include <cstdlib>
 #include <type_traits>
 
 #include "tdc_common.h"
@@ -41,6 +40,7 @@ namespace {
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr float ZERO_FLOOR = 1.52587890625e-05f;  // 2^-16 (an exact hit computes ~2^-17 |x|^2)
@@ -369,9 +369,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats1_kernel(
   // register i = centroid (i&3)+8(i>>2)+4h of the half; the key is the UNclamped one-product
   // d2 with the register index in its low mantissa bits, and t is taken of the key itself
   // (2^-19 relative off d2), so the fix-up can take out exactly the term it added
+  // (the floor as an int32 max of the bits: zf >= 0, so every negative key maps to zf and
+  // the positive ones order as their bits -- fmaxf of the bit-cast key cost a canonicalising
+  // v_max_f32 per element on top of the max itself)
+  const int zfi = __float_as_int(zf);
   auto elem = [&](float a, int i, int& m, int& m2, float& sp) __attribute__((always_inline)) {
     const int pk = (int)((__float_as_uint(a + xn) & ~15u) | (unsigned)i);
-    sp += mt<MODE>(fmaxf(__int_as_float(pk), zf), prm.expo);
+    sp += mt<MODE>(__int_as_float(max(pk, zfi)), prm.expo);
     m2 = max(m, min(m2, pk));  // median of (m, m2, pk), m <= m2 kept
     m = min(m, pk);
   };
@@ -565,7 +569,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats1_kernel(
 // kept the runner-up's one-product term).  The memberships then use the same d2 as the
 // denominator sum_k t_k of the stats pass (up to the fp32 rounding of the two MFMA orders),
 // and the distance MFMAs drop from 3 x DP/16 to DP/16 per 32 x 32 tile.
-template <int DP, int MODE, bool NZ, int WAVES, bool STAG, bool ONE>
+//
+// RAW (with ONE): the second tile image holds the shard's own bf16 rows (unshifted) instead
+// of the lo halves; W^T X is then ONE product per tile, exact in its products (bf16 w times
+// bf16 x into fp32), and the reduction adds no shift back.  For bf16 data only (the rows
+// ARE those bf16 numbers; fp32 rows keep W^T Xh + W^T Xl).
+template <int DP, int MODE, bool NZ, int WAVES, bool STAG, bool ONE, bool RAW>
 __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     const __bf16* __restrict__ Xh, const __bf16* __restrict__ Xl, const float* __restrict__ xx,
     const float* __restrict__ rowinfo, const float* __restrict__ fix, int64_t N,
@@ -583,8 +592,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
   static_assert(WAVES == 4 || WAVES == 8, "4 or 8 waves");
   static_assert(!STAG || WAVES == 8, "the stagger pairs the two waves of a SIMD");
   static_assert(!ONE || WAVES == 8, "one-product form: 8 waves");
+  static_assert(!RAW || ONE, "raw rows in W^T X with one-product distances only");
   constexpr int NBUF = STAG ? 3 : 2;
-  constexpr int NRS = ONE ? 6 : 2;        // row statistics: xx, 1/S (+ d2a, d2b, la, lb)
+  // row statistics per tile row: xx, 1/S, the zero floor 2^-16 xx (+ d2a, d2b, la, lb)
+  constexpr int NRS = ONE ? 7 : 3;
   __shared__ __attribute__((aligned(16))) char s_x[NBUF][2 * IMG];
   __shared__ __attribute__((aligned(16))) float s_rs[NBUF][NRS][TP];
 
@@ -617,6 +628,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     ccl = cc[kc];
   }
 
+  const bf16x2 ONES2 = {(__bf16)1.0f, (__bf16)1.0f};
   f32x16 out[NDT];
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt)
@@ -661,9 +673,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
       /* wave w loads statistic w of the tile's rows; padded rows: a huge norm keeps t   \
          finite (rcp(0) * info 0 would be NaN), no fix-up centroid */                    \
       const int64_t gr = (R0_) + lane;                                                    \
-      if (w == 0) pv = gr < b ? xx[gr] : 1.0e30f;                                         \
-      else if (w == 1) pv = gr < b ? rowinfo[gr] : 0.f;                                   \
-      else pv = gr < b ? fix[gr * 4 + (w - 2)] : (w >= 4 ? __int_as_float(-1) : 0.f);     \
+      if (w == 0 || w == 2) {                                                             \
+        pv = gr < b ? xx[gr] : 1.0e30f;                                                   \
+        if (w == 2) pv *= ZERO_FLOOR;                                                     \
+      } else if (w == 1) pv = gr < b ? rowinfo[gr] : 0.f;                                 \
+      else pv = gr < b ? fix[gr * 4 + (w - 3)] : (w >= 5 ? __int_as_float(-1) : 0.f);     \
     }                                                                                     \
   }
 #define TDC_TILE_STORE(B_)                                                                \
@@ -731,8 +745,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     const int rA = (SUB) * 32 + 16 * s_ + 4 * (g >> 1) + q4;                              \
     const int oA = xoff<DP>(rA, c0 + (p4 >> 1)) + 8 * (p4 & 1);                           \
     const int oB = xoff<DP>(rA + 8, c0 + (p4 >> 1)) + 8 * (p4 & 1);                       \
-    H0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xh + oA));                  \
-    H1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xh + oB));                  \
+    if constexpr (!RAW) {                                                                 \
+      H0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xh + oA));                \
+      H1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xh + oB));                \
+    }                                                                                     \
     L0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xl + oA));                  \
     L1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xl + oB));                  \
   }
@@ -746,10 +762,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
       s16x4 nh0, nh1, nl0, nl1;                                                           \
       if (t + 1 < 2 * NDT) TDC_TRLD(SUB, t + 1, nh0, nh1, nl0, nl1)                       \
       const int s = t / NDT, dt = t % NDT;                                                \
-      const bf16x8 xbh = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7)); \
+      bf16x8 xbh;                                                                         \
+      if constexpr (!RAW) xbh = __builtin_bit_cast(bf16x8, __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7)); \
       const bf16x8 xbl = __builtin_bit_cast(bf16x8, __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7)); \
       if (t + 1 == 2 * NDT) { LAST }                                                      \
-      out[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(WH[s], xbh, out[dt], 0, 0, 0);    \
+      if constexpr (!RAW)                                                                 \
+        out[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(WH[s], xbh, out[dt], 0, 0, 0);  \
       out[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(WH[s], xbl, out[dt], 0, 0, 0);    \
       INTERLEAVE(t * EPW, EPW)                                                            \
       if (t + 1 < 2 * NDT) { h0 = nh0; h1 = nh1; l0 = nl0; l1 = nl1; }                   \
@@ -766,18 +784,20 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     const int pt = (SUB) * 32 + 8 * g4 + 4 * h;                                           \
     const f32x4 xq4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][0][pt]);                  \
     const f32x4 iq4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][1][pt]);                  \
+    const f32x4 zf4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][2][pt]);                  \
     f32x4 da4, db4;                                                                       \
     i32x4 la4, lb4;                                                                       \
     if constexpr (ONE) {                                                                  \
-      da4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][2][pt]);                            \
-      db4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][3][pt]);                            \
-      la4 = *reinterpret_cast<const i32x4*>(&s_rs[B_][4][pt]);                            \
-      lb4 = *reinterpret_cast<const i32x4*>(&s_rs[B_][5][pt]);                            \
+      da4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][3][pt]);                            \
+      db4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][4][pt]);                            \
+      la4 = *reinterpret_cast<const i32x4*>(&s_rs[B_][5][pt]);                            \
+      lb4 = *reinterpret_cast<const i32x4*>(&s_rs[B_][6][pt]);                            \
     }                                                                                     \
     _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                       \
       const int i = 4 * g4 + e;                                                           \
-      const float zf = ZERO_FLOOR * xq4[e];                                               \
-      float d2 = fmaxf(ACC[i] + xq4[e], zf);                                              \
+      const float zf = zf4[e];                                                            \
+      /* the floor as an int32 max (zf >= 0; fmaxf canonicalised the LDS operand) */     \
+      float d2 = __int_as_float(max(__float_as_int(ACC[i] + xq4[e]), __float_as_int(zf))); \
       if constexpr (ONE) {                                                                \
         d2 = kc == la4[e] ? da4[e] : d2;                                                  \
         d2 = kc == lb4[e] ? db4[e] : d2;                                                  \
@@ -787,7 +807,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
       const float wv = mw<MODE>(u, prm.m);                                                \
       const __bf16 bhv = (__bf16)wv;                                                      \
       WH[i >> 3][i & 7] = bhv;                                                            \
-      wsum += (float)bhv;                                                                 \
+      /* the rounded weights summed a pair at a time (v_dot2c with (1, 1)) */            \
+      if (e & 1) {                                                                        \
+        const bf16x2 pr_ = {WH[i >> 3][(i & 7) - 1], bhv};                                \
+        /* (inline asm: the builtin with a constant (1, 1) is folded back into two      \
+           converts and two adds) */                                                      \
+        asm("v_dot2c_f32_bf16 %0, %1, %2" : "+v"(wsum) : "v"(pr_), "v"(ONES2));          \
+      }                                                                                   \
     }                                                                                     \
   }
   if constexpr (STAG) {
@@ -1021,8 +1047,8 @@ inline void accum_geometry(int64_t N, int K, int num_cus, int* nkt, int64_t* spl
 }
 
 template <int DP>
-int launch_maccum(const void* Xh, const void* Xl, const float* xx, const float* rowinfo,
-                  const float* fix, int64_t N, const void* Ch, const void* Cl, const float* cc, int K, int Kp,
+int launch_maccum(const void* Xh, const void* Xl, const void* Xr, const float* xx,
+                  const float* rowinfo, const float* fix, int64_t N, const void* Ch, const void* Cl, const float* cc, int K, int Kp,
                   int D, double m, int nz, float* part, const float* mu, double* wx, double* ws,
                   int num_cus, hipStream_t s) {
   int nkt;
@@ -1034,21 +1060,22 @@ int launch_maccum(const void* Xh, const void* Xl, const float* xx, const float* 
   const MParam p = make_mparam(m, nz);
   // 8 waves (2 per SIMD): one wave's epilogue VALU runs beside the other's MFMAs; the
   // one-wave software-pipelined WAVES=4 form measured slower (docs/PERF_NOTES.md)
-  // TDC_FCM_NOSTAG=1 selects the lockstep form (A/B of the stagger); the one-product form
-  // runs when the stats pass left its fix-up rows (DP >= 64)
-  static const bool stag = std::getenv("TDC_FCM_NOSTAG") == nullptr;
-#define TDC_LA(MODE, NZV, ST, ONEV)                                                           \
-  hipLaunchKernelGGL((fcm_mfma_accum_kernel<DP, MODE, NZV, 8, ST, ONEV>), dim3((unsigned)nb),  \
-                     dim3(512), 0, s, (const __bf16*)Xh, (const __bf16*)Xl, xx, rowinfo, fix,  \
-                     N, (const __bf16*)Ch, (const __bf16*)Cl, cc, K, nkt, rps, xcd, p, part,   \
-                     part_ws, Kp)
-  // (the bf16x3 form keeps the lockstep loop: staggered, its extra live registers spill --
-  // fcm10m 17.7 -> 19.7 ms; one product + stagger 16.0 ms, profiles/fcm10m_*_r05e.txt)
+  // The one-product form runs when the stats pass left its fix-up rows (DP >= 64), always
+  // staggered (fcm10m 16.65 -> 16.02 ms, profiles/fcm10m_*_r05e.txt), with the raw bf16 rows
+  // as the W^T X operand when the caller has them (Xr); the bf16x3 form keeps the lockstep
+  // loop (staggered, its extra live registers spill: 17.7 -> 19.7 ms)
+  const void* X2 = Xr ? Xr : Xl;
+#define TDC_LA(MODE, NZV, ST, ONEV, RAWV)                                                     \
+  hipLaunchKernelGGL((fcm_mfma_accum_kernel<DP, MODE, NZV, 8, ST, ONEV, RAWV>),               \
+                     dim3((unsigned)nb), dim3(512), 0, s, (const __bf16*)Xh,                   \
+                     (const __bf16*)X2, xx, rowinfo, fix, N, (const __bf16*)Ch,                \
+                     (const __bf16*)Cl, cc, K, nkt, rps, xcd, p, part, part_ws, Kp)
 #define TDC_LA2(MODE, NZV)                                                                    \
   if (DP >= 64 && fix) {                                                                      \
-    if (stag) TDC_LA(MODE, NZV, true, DP >= 64); else TDC_LA(MODE, NZV, false, DP >= 64);     \
+    if (Xr) TDC_LA(MODE, NZV, DP >= 64, DP >= 64, DP >= 64);                                  \
+    else TDC_LA(MODE, NZV, DP >= 64, DP >= 64, false);                                        \
   } else {                                                                                    \
-    TDC_LA(MODE, NZV, false, false);                                                          \
+    TDC_LA(MODE, NZV, false, false, false);                                                   \
   }
   if (m == 2.0) {
     if (nz) { TDC_LA2(2, true) } else { TDC_LA2(2, false) }
@@ -1059,8 +1086,9 @@ int launch_maccum(const void* Xh, const void* Xl, const float* xx, const float* 
 #undef TDC_LA
   TDC_CHECK_LAUNCH();
   const int64_t tot = (int64_t)K * DP + K;
+  // (raw rows: the slabs hold sum w x of the unshifted rows, nothing to add back)
   hipLaunchKernelGGL(fcm_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, part,
-                     part_ws, splits, K, Kp, DP, D, mu, wx, ws);
+                     part_ws, splits, K, Kp, DP, D, (fix && DP >= 64 && Xr) ? nullptr : mu, wx, ws);
   TDC_CHECK_LAUNCH();
   return 0;
 }
@@ -1492,11 +1520,11 @@ int64_t tdc_fcm_mfma_workspace(int64_t N, int K, int Kp, int DP, int num_cus) {
 int64_t tdc_fcm_mfma_rowinfo_len(int64_t N, int DP) {
   return DP >= 64 ? ((N + 3) / 4) * 4 + 4 * N : N;
 }
-int tdc_fcm_mfma(int pass, const void* Xh, const void* Xl, const float* xx, int64_t N, int DP,
-                 int D, const void* Ch, const void* Cl, const float* cc, int K, int Kp, double m,
-                 int nan_to_zero, int32_t* labels, float* rowinfo, int64_t rowinfo_len,
-                 double* wx, double* ws, float* work, const float* shift, int num_cus,
-                 hipStream_t s) {
+int tdc_fcm_mfma(int pass, const void* Xh, const void* Xl, const void* Xr, const float* xx,
+                 int64_t N, int DP, int D, const void* Ch, const void* Cl, const float* cc, int K,
+                 int Kp, double m, int nan_to_zero, int32_t* labels, float* rowinfo,
+                 int64_t rowinfo_len, double* wx, double* ws, float* work, const float* shift,
+                 int num_cus, hipStream_t s) {
   if (N <= 0 || K <= 0) return 0;
   if (Kp % 128 != 0 || Kp < K) return (int)hipErrorInvalidValue;
   if (rowinfo_len < N) return (int)hipErrorInvalidValue;
@@ -1510,7 +1538,7 @@ int tdc_fcm_mfma(int pass, const void* Xh, const void* Xl, const float* xx, int6
     if (pass == 0)                                                                            \
       return launch_mstats<DPV>(Xh, Xl, xx, N, Ch, Cl, cc, K, Kp, m, nan_to_zero, labels,     \
                                 rowinfo, fix, s);                                             \
-    return launch_maccum<DPV>(Xh, Xl, xx, rowinfo, fix, N, Ch, Cl, cc, K, Kp, D, m,           \
+    return launch_maccum<DPV>(Xh, Xl, Xr, xx, rowinfo, fix, N, Ch, Cl, cc, K, Kp, D, m,       \
                               nan_to_zero, work, shift, wx, ws, num_cus, s);                  \
   }
   TDC_FM(32)

@@ -151,11 +151,13 @@ int tdc_fcm_split_rows(const float* src, int64_t rows, int64_t valid, int d, int
 // rowinfo holds rowinfo_len floats: [N] row statistics, and from DP = 64, when rowinfo_len >=
 // tdc_fcm_mfma_rowinfo_len(N, DP), each row's two corrected nearest d2 after them (16-byte
 // aligned float4 {d2a, d2b, la, lb}); with them pass 1 runs one-product distances.
-int tdc_fcm_mfma(int pass, const void* Xh, const void* Xl, const float* xx, int64_t N, int DP,
-                 int D, const void* Ch, const void* Cl, const float* cc, int K, int Kp, double m,
-                 int nan_to_zero, int32_t* labels, float* rowinfo, int64_t rowinfo_len,
-                 double* wx, double* ws, float* work, const float* shift, int num_cus,
-                 hipStream_t stream);
+// Xr (nullable, pass 1 with the fix-up rows): the shard's own bf16 rows [N, DP], unshifted,
+// zero padded -- W^T X then takes them as its one operand (bf16 data only: exact products).
+int tdc_fcm_mfma(int pass, const void* Xh, const void* Xl, const void* Xr, const float* xx,
+                 int64_t N, int DP, int D, const void* Ch, const void* Cl, const float* cc, int K,
+                 int Kp, double m, int nan_to_zero, int32_t* labels, float* rowinfo,
+                 int64_t rowinfo_len, double* wx, double* ws, float* work, const float* shift,
+                 int num_cus, hipStream_t stream);
 int64_t tdc_fcm_mfma_workspace(int64_t N, int K, int Kp, int DP, int num_cus);
 int64_t tdc_fcm_mfma_rowinfo_len(int64_t N, int DP);
 // Wide D (DP in 128 ... 1024, multiples of 128), over a chunk of M rows with the [M, K]

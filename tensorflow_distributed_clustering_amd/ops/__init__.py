@@ -1260,7 +1260,7 @@ class HipMfmaFCM(_LocalOpsBase):
         self.ch = torch.zeros(self.kp, self.dp, dtype=torch.bfloat16, device=dev)
         self.cl = torch.zeros_like(self.ch)
         self.cc = torch.zeros(self.kp, dtype=torch.float32, device=dev)
-        self.xh = self.xl = self.xx = self.rowinfo = None
+        self.xh = self.xl = self.xx = self.rowinfo = self.xr = None
         self.work = self.mu = None
         self._set_x(x)
 
@@ -1274,11 +1274,15 @@ class HipMfmaFCM(_LocalOpsBase):
             self.work = torch.empty(need, dtype=torch.float32, device=self.device)
         return self.work
 
-    def _set_x(self, x):
+    def _set_x(self, x, streamed: bool = False):
         """Hold the rows; they are split into hi/lo at the next step, once the shift (the
         mean of the first centroids -- replicated, so resident, streamed and every world
         size use the same one) is known."""
         self._xsrc = x if (x.dtype == torch.float32 and x.stride(1) == 1) else x.float().contiguous()
+        # bf16 rows are also the exact W^T X operand of the one-product accumulate (Xr);
+        # a streamed chunk is copied (its buffer is refilled while the step may still read)
+        self._xraw = x if x.dtype == torch.bfloat16 else None
+        self._xraw_alias = not streamed
         self.n = int(x.shape[0])
         self._dirty = True
         self.x = None
@@ -1299,12 +1303,21 @@ class HipMfmaFCM(_LocalOpsBase):
         self.ops.fcm_split_rows(self._xsrc[:, : self.d], n, 0, self.xh[:n], self.xl[:n],
                                 self.xx[:n], self.mu)
         self._xsrc = None  # the hi/lo rows are the shard from here on
+        self.xr = None
+        if self._xraw is not None and self._use_raw():
+            xr = self._xraw[:, : self.d]
+            if self.d == self.dp and xr.is_contiguous() and self._xraw_alias:
+                self.xr = xr  # the shard itself
+            else:
+                self.xr = torch.zeros(n, self.dp, dtype=torch.bfloat16, device=self.device)
+                self.xr[:, : self.d] = xr
+        self._xraw = None
         self._dirty = False
 
     def bind(self, x):
         if x.shape[1] != self.d:
             raise ValueError(f"chunk width {x.shape[1]} != {self.d}")
-        self._set_x(x)
+        self._set_x(x, streamed=True)
         return self
 
     def prepare(self, C):
@@ -1322,12 +1335,17 @@ class HipMfmaFCM(_LocalOpsBase):
         return self.xh[:n], self.xl[:n], self.xx[:n]
 
     one_product = True  # class switch: False keeps bf16x3 distances in the accumulate pass
+    raw_rows = True     # class switch: bf16 shards feed W^T X as they are (one product)
+
+    def _use_raw(self):
+        return self.raw_rows and self.one_product and self.dp >= 64
 
     @property
     def precision(self) -> str:
         """What the step computes, in words (bench.py reports it)."""
         if self.one_product and self.dp >= 64:
-            return FCM_PRECISION["bf16_one"]
+            return FCM_PRECISION["bf16_one_raw" if getattr(self, "xr", None) is not None
+                                 else "bf16_one"]
         return FCM_PRECISION["bf16"]
 
     def _ri_len(self, n):
@@ -1341,8 +1359,9 @@ class HipMfmaFCM(_LocalOpsBase):
         ri = self.rowinfo[: self._ri_len(self.n)]
         self.ops.fcm_mfma_stats(xh, xl, xx, self.ch, self.cl, self.cc, self.k, self.m,
                                 self.nan_to_zero, labels, ri)
+        xr = self.xr[: self.n] if self.xr is not None and self.one_product else None
         self.ops.fcm_mfma_accum(xh, xl, xx, ri, self.ch, self.cl, self.cc, self.k, self.m,
-                                self.nan_to_zero, wx, ws, self._work(), self.mu)
+                                self.nan_to_zero, wx, ws, self._work(), self.mu, xr)
 
     def assign(self, C, labels):
         self.prepare(C)
@@ -1480,6 +1499,11 @@ FCM_PRECISION = {
                 "on x.c) for every centroid, each row's two nearest corrected to bf16x3 "
                 "(fp32-faithful); fp32 memberships, bf16 weights in the W^T X MFMAs (hi+lo "
                 "rows), fp64 sums",
+    # ... on a bf16 shard: W^T X takes the bf16 rows themselves (exact products)
+    "bf16_one_raw": "bf16 MFMA distances: one product (x_hi . c_hi, ~2^-9/sqrt(D) relative "
+                    "error on x.c) for every centroid, each row's two nearest corrected to "
+                    "bf16x3 (fp32-faithful); fp32 memberships; W^T X = bf16 weights x the bf16 "
+                    "rows (exact products, fp32 accumulate), fp64 sums",
 }
 
 

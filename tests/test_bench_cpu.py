@@ -81,6 +81,10 @@ def test_bench_fcm_and_minibatch_presets():
     # FCM witness: one step of the engine's tower vs the fp64 oracle on the sample rows
     assert d["check"]["fcm_centroid_rel_err"] < 1e-9 and d["check"]["fcm_weight_sum_rel_err"] < 1e-9
     assert d["check"]["sample_rows"] == 30000 and "fp64" in d["precision"]
+    # ... also from the init centroids (random rows: the exact oracle's zero distances)
+    ini = d["check"]["at_init"]
+    assert ini["fcm_centroid_rel_err"] < 1e-9 and ini["fcm_weight_sum_rel_err"] < 1e-9
+    assert ini["ws_spread"] > 0 and d["check"]["final_ws_spread"] >= 0
     d = _run(["--preset", "minibatch1b", "--n-per-gpu", "50000", "--k", "32", "--batch-size", "4096",
               "--steps", "2", "--warmup", "1", "--dtype", "fp32"])
     assert d["config"]["model"] == "kmeans-minibatch" and d["config"]["global_batch"] == 4096
