@@ -376,8 +376,17 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats1_kernel(
   auto elem = [&](float a, int i, int& m, int& m2, float& sp) __attribute__((always_inline)) {
     const int pk = (int)((__float_as_uint(a + xn) & ~15u) | (unsigned)i);
     sp += mt<MODE>(__int_as_float(max(pk, zfi)), prm.expo);
-    m2 = max(m, min(m2, pk));  // median of (m, m2, pk), m <= m2 kept
+    // median of (m, m2, pk) with m <= m2 kept: one v_med3_i32 (the max(m, min(m2, pk))
+    // spelling compiled to a v_min + v_max pair)
+    int md;
+    asm("v_med3_i32 %0, %1, %2, %3" : "=v"(md) : "v"(m), "v"(m2), "v"(pk));
+    m2 = md;
     m = min(m, pk);
+  };
+  // two top-2 sets (m <= m2 each) -> one
+  auto merge2 = [](int& m, int& m2, int mo, int m2o) __attribute__((always_inline)) {
+    m2 = min(max(m, mo), min(m2, m2o));
+    m = min(m, mo);
   };
   // the MFMAs of half Q into acc; with EPI, the previous tile's epilogue (accp: all 32
   // centroids real) issues between them, 16/KS elements per MFMA: at one product the
@@ -401,20 +410,26 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats1_kernel(
 #pragma unroll
       for (int e = 0; e < 4; ++e) init[4 * g4 + e] = n4[e];
     }
-    int m = KINF, m2 = KINF;
-    float sp = 0.f;
+    // even and odd elements in two independent chains (running sum, top-2), merged once
+    // per phase: one chain serialised every v_add / v_min on its predecessor
+    int m = KINF, m2 = KINF, mo = KINF, m2o = KINF;
+    float sp = 0.f, spo = 0.f;
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) {
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[kk], bh[kk], kk == 0 ? init : acc, 0, 0, 0);
       if constexpr (EPI) {
 #pragma unroll
         for (int i = 0; i < 16; ++i)
-          if (i * KS / 16 == kk) elem(accp[i], i, m, m2, sp);
+          if (i * KS / 16 == kk) {
+            if (i & 1) elem(accp[i], i, mo, m2o, spo);
+            else elem(accp[i], i, m, m2, sp);
+          }
         __builtin_amdgcn_sched_barrier(0);
       }
     }
     if constexpr (EPI) {
-      S += sp;
+      S += sp + spo;
+      merge2(m, m2, mo, m2o);
       fold(m, m2, ttp);
     }
   };
@@ -696,7 +711,21 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
   constexpr int EPK = 16 / KS;          // membership elements per distance k-step
   constexpr int EPW = 16 / (2 * NDT);   // membership elements per W^T X (s, dt) step
 #define TDC_DIST(ACC, SUB, INTERLEAVE)                                                    \
-  {                                                                                       \
+  if constexpr (ONE) {                                                                    \
+    /* one product: the A fragments read two k-steps ahead (an LDS read outlives one    \
+       32-cycle MFMA; the registers of the lo fragments pay for the deeper ring) */     \
+    _Pragma("unroll") for (int i = 0; i < 16; ++i) ACC[i] = ccl;                         \
+    const int prow = (SUB) * 32 + r;                                                      \
+    bf16x8 af[KS];                                                                        \
+    _Pragma("unroll") for (int kk = 0; kk < 2 && kk < KS; ++kk)                           \
+      af[kk] = as_bf16x8(*reinterpret_cast<const uint4*>(xh + xoff<DP>(prow, h * (CPR / 2) + kk))); \
+    _Pragma("unroll") for (int kk = 0; kk < KS; ++kk) {                                   \
+      if (kk + 2 < KS)                                                                    \
+        af[kk + 2] = as_bf16x8(*reinterpret_cast<const uint4*>(xh + xoff<DP>(prow, h * (CPR / 2) + kk + 2))); \
+      ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk], ch[kk], ACC, 0, 0, 0);        \
+      INTERLEAVE(kk * EPK, EPK)                                                           \
+    }                                                                                     \
+  } else {                                                                                \
     _Pragma("unroll") for (int i = 0; i < 16; ++i) ACC[i] = ccl;                         \
     const int prow = (SUB) * 32 + r;                                                      \
     bf16x8 ah = as_bf16x8(*reinterpret_cast<const uint4*>(xh + xoff<DP>(prow, h * (CPR / 2)))); \
@@ -755,7 +784,21 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
   // W^T X of half SUB (weights WH, bf16): A = W (row = centroid, k = points), B = X^T hi and
   // lo via transposed reads (T10), prefetched one (s, dt) step ahead; INTERLEAVE runs between
 #define TDC_WTX(SUB, WH, INTERLEAVE, LAST)                                            \
-  {                                                                                       \
+  if constexpr (RAW) {                                                                    \
+    /* one product per (s, dt) step: the transposed reads run three steps ahead */       \
+    constexpr int NSTEP = 2 * NDT, PFW = 3;                                               \
+    s16x4 lr0[NSTEP], lr1[NSTEP], hdum0, hdum1;                                           \
+    _Pragma("unroll") for (int t = 0; t < PFW && t < NSTEP; ++t)                          \
+      TDC_TRLD(SUB, t, hdum0, hdum1, lr0[t], lr1[t])                                      \
+    _Pragma("unroll") for (int t = 0; t < NSTEP; ++t) {                                   \
+      if (t + PFW < NSTEP) TDC_TRLD(SUB, t + PFW, hdum0, hdum1, lr0[t + PFW], lr1[t + PFW]) \
+      const int s = t / NDT, dt = t % NDT;                                                \
+      const bf16x8 xb = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lr0[t], lr1[t], 0, 1, 2, 3, 4, 5, 6, 7)); \
+      if (t + 1 == NSTEP) { LAST }                                                        \
+      out[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(WH[s], xb, out[dt], 0, 0, 0);     \
+      INTERLEAVE(t * EPW, EPW)                                                            \
+    }                                                                                     \
+  } else {                                                                                \
     s16x4 h0, h1, l0, l1;                                                                 \
     TDC_TRLD(SUB, 0, h0, h1, l0, l1)                                                      \
     _Pragma("unroll") for (int t = 0; t < 2 * NDT; ++t) {                                 \

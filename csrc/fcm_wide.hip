@@ -396,9 +396,16 @@ __global__ __launch_bounds__(256, 1) void fcm_wide_wtx_f64m_kernel(
   __shared__ double s_x[2][F64S * PW];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = w >> 1, wc = w & 1;
-  const int kt = (int)(blockIdx.x % nkt);
-  const int dt = (int)((blockIdx.x / nkt) % ndt);
-  const int64_t split = blockIdx.x / ((int64_t)nkt * ndt);
+  // XCD-aware order: the nkt x ndt tile blocks of one row split are consecutive on one XCD,
+  // so its W and X rows come from HBM once into that XCD's L2
+  int64_t L = blockIdx.x;
+  {
+    const int64_t per = (int64_t)gridDim.x / 8;
+    if (per * 8 == (int64_t)gridDim.x) L = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+  }
+  const int kt = (int)(L % nkt);
+  const int dt = (int)((L / nkt) % ndt);
+  const int64_t split = L / ((int64_t)nkt * ndt);
   const int k0 = kt * F64T, d0 = dt * F64T;
   const int64_t a = split * rows_per_split;
   const int64_t b = min(M, a + rows_per_split);
@@ -454,9 +461,11 @@ __global__ __launch_bounds__(256, 1) void fcm_wide_wtx_f64m_kernel(
         for (int tj = 0; tj < 4; ++tj)
           acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ti], bv[tj], acc[ti][tj], 0, 0, 0);
     }
-    if (dt == 0 && tid < F64T) {
+    // sum_r W[r, k]: stage s of the split goes to feature tile s % ndt, all four waves
+    // (thread t: column t & 127, rows of half t >> 7) -- one tile's waves alone carried it
+    if ((int)(((rs - a) / F64S) % ndt) == dt) {
 #pragma unroll
-      for (int r = 0; r < F64S; ++r) wsum += s_w[buf][r * PW + tid];
+      for (int r = 0; r < F64S / 2; ++r) wsum += s_w[buf][((tid >> 7) * (F64S / 2) + r) * PW + (tid & 127)];
     }
     if (more) store(buf ^ 1);
     __syncthreads();
@@ -474,7 +483,27 @@ __global__ __launch_bounds__(256, 1) void fcm_wide_wtx_f64m_kernel(
         if (k < K && d < D && v != 0.0) atomicAdd(&wx[(int64_t)k * D + d], v);
       }
     }
-  if (dt == 0 && tid < F64T && k0 + tid < K && wsum != 0.0) atomicAdd(&ws[k0 + tid], wsum);
+  if (k0 + (tid & 127) < K && wsum != 0.0) atomicAdd(&ws[k0 + (tid & 127)], wsum);
+}
+
+// row splits of the fp64 W^T X pass: one 256-thread block per CU at a time, so the grid
+// (splits x tiles blocks) should fill whole rounds of num_cus blocks -- 11 splits x 48
+// tiles at D = 768, K = 1024 ran 2.06 rounds, i.e. three; pick the split count in
+// [base, 4 base] with the least rounds x rows per block
+inline int64_t wtx_f64_splits(int64_t stages, int64_t tiles, int num_cus) {
+  int64_t base = ((int64_t)num_cus * 2 + tiles - 1) / tiles;
+  if (base < 1) base = 1;
+  int64_t best = base;
+  double best_cost = 1e300;
+  for (int64_t sp = base; sp <= 4 * base && sp <= stages; ++sp) {
+    const int64_t rounds = (sp * tiles + num_cus - 1) / num_cus;
+    const double cost = (double)rounds * (double)((stages + sp - 1) / sp) * (1.0 + 1e-3 * sp);
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = sp;
+    }
+  }
+  return best < stages ? best : (stages > 0 ? stages : 1);
 }
 
 template <typename T>
@@ -494,9 +523,7 @@ int launch_wide(int pass, const void* X, int64_t M, int64_t ldx, int D, const vo
     if (pass == 2) {
       const int nkt = (K + F64T - 1) / F64T, ndt = (D + F64T - 1) / F64T;
       const int64_t stages = (M + F64S - 1) / F64S;
-      int64_t splits = ((int64_t)num_cus * 2 + (int64_t)nkt * ndt - 1) / ((int64_t)nkt * ndt);
-      if (splits > stages) splits = stages;
-      if (splits < 1) splits = 1;
+      int64_t splits = wtx_f64_splits(stages, (int64_t)nkt * ndt, num_cus);
       const int64_t rps = ((stages + splits - 1) / splits) * F64S;
       splits = (M + rps - 1) / rps;
       hipLaunchKernelGGL(fcm_wide_wtx_f64m_kernel, dim3((unsigned)(splits * nkt * ndt)), dim3(256),

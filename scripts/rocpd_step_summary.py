@@ -1,12 +1,16 @@
 # Per-step kernel summary from a rocprofv3 --kernel-trace SQLite database:
-#   python scripts/rocpd_step_summary.py run_results.db <kernel name marking one step> <steps>
+#   python scripts/rocpd_step_summary.py run_results.db <kernel name marking one step> <steps> [end]
+# The marker is the first kernel of a step, or with "end" its last (e.g. finalize_kernel):
+# the window is then the nsteps steps that end at the last nsteps markers.
 import sqlite3, sys, re, collections
 db, marker, nsteps = sys.argv[1], sys.argv[2], int(sys.argv[3])
 c = sqlite3.connect(db)
 rows = list(c.execute("select name, start, end from kernels order by start"))
 idx = [i for i, r in enumerate(rows) if marker in r[0]]
-first = idx[len(idx) - nsteps]
-sel = rows[first:]
+if len(sys.argv) > 4 and sys.argv[4] == "end":
+    sel = rows[idx[len(idx) - nsteps - 1] + 1: idx[-1] + 1]
+else:
+    sel = rows[idx[len(idx) - nsteps]:]
 span = (sel[-1][2] - sel[0][1]) / 1e3 / nsteps
 agg = collections.defaultdict(lambda: [0, 0.0])
 for n, s, e in sel:

@@ -1446,7 +1446,10 @@ class HipWideFCM(_LocalOpsBase):
     per chunk, no library GEMM.  Takes over from fcm_tower (D <= 256) and the MFMA tower
     (fp32, D <= 128) past their register / LDS budgets."""
     name = "hip_fcm_wide"
-    chunk_elems = 1 << 27
+    # [rows, K] block per chunk (2 GiB in fp64): each chunk's W^T X pass flushes its
+    # partial tiles with atomics and ends in a partial round of blocks, so fewer, larger
+    # chunks; HBM is 288 GB per GPU
+    chunk_elems = 1 << 28
 
     def __init__(self, x, k, dtype="fp64", m=2.0, nan_to_zero=True):
         super().__init__(x, k, "keep")

@@ -12,6 +12,11 @@
 //      pieces and fragment reads)
 //   2: s_setprio(1) around every MFMA cluster (guide T5)
 //   4: index tags carry the stage within a super-stage of 16 (8 tag bits)
+//   8: half-P software pipeline inside each phase: the MFMAs of point tiles 0..P/2-1 run
+//      with the tag + min epilogue of tiles P/2..P-1 of the previous phase between them,
+//      then the MFMAs of tiles P/2.. with the epilogue of tiles 0..P/2-1 of this phase
+//      (no extra accumulators: each half's registers are read before they are rewritten),
+//      instead of 32 MFMAs and then a 48-VALU epilogue burst
 // Data: Gaussian blobs around K uniform(-10,10) centres (splitmix64 + Box-Muller).
 #include <hip/hip_runtime.h>
 
@@ -59,6 +64,8 @@ void ring3x_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
   // QT=4), so the per-stage compare / select of the running best becomes one v_min_f32
   // per point tile, and the compare / select runs once per super-stage
   constexpr bool STAGETAG = (VAR & 4) != 0;
+  constexpr bool HALFP = (VAR & 8) != 0;
+  static_assert(!HALFP || (P % 2 == 0 && !STAGETAG && !SPREAD && KS == 4), "half-P form");
   static_assert(!STAGETAG || QT == 4, "stage tags: 4 (q, reg) bits + 4 stage bits");
   if (STAGETAG && ntiles > 16) return;  // experiment covers K <= 1024
   constexpr unsigned EMB = STAGETAG ? 255u : (QT * 4 <= 16 ? 15u : 31u);
@@ -146,8 +153,56 @@ void ring3x_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
 #pragma unroll
     for (int p = 0; p < P; ++p) m[p] = STAGETAG ? best[p] : INFINITY;
     const unsigned stag = STAGETAG ? (unsigned)((t & 15) << 4) : 0u;
+    if constexpr (HALFP) {
+      constexpr int H = P / 2;
+      f32x4 acc[P];
+      auto epi1 = [&](int p, int q) __attribute__((always_inline)) {
 #pragma unroll
-    for (int q = 0; q < QT; ++q) {
+        for (int i = 0; i < 4; ++i) {
+          const float v = __uint_as_float((__float_as_uint(acc[p][i]) & ~EMB) | (unsigned)(q * 4 + i));
+          m[p] = __builtin_fminf(m[p], v);
+        }
+      };
+      bf16x8 a[KS];
+#pragma unroll
+      for (int q = 0; q < QT; ++q) {
+        f32x4 n4;
+        asm volatile("ds_read_b128 %0, %1 offset:%2"
+                     : "=v"(n4) : "v"(noff), "i"(slot * STAGE_B + q * 16 * 4));
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk)
+          asm volatile("ds_read_b128 %0, %1 offset:%2"
+                       : "=v"(a[kk]) : "v"(aoff[kk]), "i"(slot * STAGE_B + q * 16 * DP * 2));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        // tiles 0..H-1 of phase q, with the epilogue of tiles H.. of phase q-1
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+#pragma unroll
+          for (int p = 0; p < H; ++p)
+            acc[p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk], bq[p][kk], kk == 0 ? n4 : acc[p], 0, 0, 0);
+          if (q > 0) {
+#pragma unroll
+            for (int p = H + kk * H / KS; p < H + (kk + 1) * H / KS; ++p) epi1(p, q - 1);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        // tiles H.. of phase q, with the epilogue of tiles 0..H-1 of phase q
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+#pragma unroll
+          for (int p = H; p < P; ++p)
+            acc[p] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk], bq[p][kk], kk == 0 ? n4 : acc[p], 0, 0, 0);
+#pragma unroll
+          for (int p = kk * H / KS; p < (kk + 1) * H / KS; ++p) epi1(p, q);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#pragma unroll
+      for (int p = H; p < P; ++p) epi1(p, QT - 1);
+    }
+#pragma unroll
+    for (int q = 0; q < (HALFP ? 0 : QT); ++q) {
       auto afrag = [&](int kk) __attribute__((always_inline)) {
         bf16x8 a;
         asm volatile("ds_read_b128 %0, %1 offset:%2"
@@ -374,6 +429,7 @@ int main(int argc, char** argv) {
   TRY("prod P4 NST3", prod4)
   TRY("stage tags P8", var<8, 2, 4, 4>)
   TRY("stage tags P4 NST3", var<4, 3, 4, 4>)
+  TRY("half-P pipeline P8", var<8, 2, 4, 8>)
   const double flop = 2.0 * (double)N * Kp * DP;
   for (int round = 0; round < 3; ++round) {
     const float t0 = timeit([&] { prod(b0, 0); }, reps);
@@ -381,9 +437,10 @@ int main(int argc, char** argv) {
     const float t3 = timeit([&] { var<8, 2, 4, 4>(b1, 0); }, reps);
     const float t5 = timeit([&] { prod4(b1, 0); }, reps);
     const float t6 = timeit([&] { var<4, 3, 4, 4>(b1, 0); }, reps);
+    const float t7 = timeit([&] { var<8, 2, 4, 8>(b1, 0); }, reps);
     printf("round %d: prod P8 %.3f ms (%.0f TF/s) | copy P8 %.3f | stagetag P8 %.3f | "
-           "prod P4N3 %.3f | stagetag P4N3 %.3f\n",
-           round, t0, flop / t0 / 1e9, t1, t3, t5, t6);
+           "prod P4N3 %.3f | stagetag P4N3 %.3f | half-P P8 %.3f\n",
+           round, t0, flop / t0 / 1e9, t1, t3, t5, t6, t7);
     fflush(stdout);
   }
   return 0;
