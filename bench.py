@@ -56,11 +56,12 @@ PRESETS = {
                        dtype="fp64", method="fcm"),
     "embed50m_fp8": dict(n_per_gpu=50_000_000, dim=768, k=65536, scaling="strong", mode="lloyd",
                          dtype="fp8"),
-    # FCM at the headline shape on the MFMA tower: bf16x3 distances, fp32 memberships, bf16
-    # weights in W^T X (ops.FCM_PRECISION; --dtype fp32 runs the exact fp32 tower), m = 2
-    # (the reference's m = D = 128 would underflow every u^m)
+    # FCM at the headline shape on the MFMA tower: one-product distances with the two
+    # nearest corrected (--fcm-distances x3: bf16x3), fp32 memberships, bf16 weights x the
+    # bf16 rows in W^T X (ops.FCM_PRECISION, reported with the witness; --dtype fp32 runs
+    # the exact fp32 tower), m = 2 (the reference's m = D = 128 would underflow every u^m)
     "fcm10m": dict(n_per_gpu=10_000_000, dim=128, k=1024, scaling="weak", mode="lloyd",
-                   dtype="bf16", method="fcm", fuzzifier=2.0),
+                   dtype="bf16", method="fcm", fuzzifier=2.0, fcm_distances="one"),
 }
 
 
@@ -112,6 +113,9 @@ def parse(argv=None):
                          "changed between fp64 running totals (with a full re-sum every "
                          "--delta-refresh steps and after steps that moved > 40%% of the rows); "
                          "full re-sums every row every step; auto = delta where supported")
+    ap.add_argument("--fcm-distances", default="x3", choices=["one", "x3"],
+                    help="bf16 FCM distances: one product + two-nearest fix-up, or bf16x3 "
+                         "(ClusterConfig.fcm_distances)")
     ap.add_argument("--comm-mode", default="auto", choices=["auto", "allreduce", "rsag"],
                     help="partial-sum reduction (ClusterConfig.comm_mode); with "
                          "TDC_FORCE_COLLECTIVES=1 a world-1 run issues the RCCL calls too")
@@ -171,7 +175,7 @@ def main(argv=None):
                             seed=a.seed, compute_inertia=False, algorithm=a.algorithm,
                             fuzzifier=a.fuzzifier, update=a.update,
                             delta_refresh=a.delta_refresh, deterministic=a.deterministic,
-                            comm_mode=a.comm_mode)
+                            comm_mode=a.comm_mode, fcm_distances=a.fcm_distances)
     if a.mode == "minibatch":
         from tensorflow_distributed_clustering_amd.models.minibatch import MiniBatchStepper
         eng = MiniBatchStepper(x, cfg.replace(batch_size=a.batch_size or (1 << 20)), comm,
@@ -465,7 +469,8 @@ def fcm_witness(eng, x, n_global, s, e, comm, torch, a, C0=None):
             # the engine's own operand dtype: a bf16 shard reaches the tower as bf16
             xin = xs.double() if eng.dtype_name == "fp64" else (
                 xs if xs.dtype == torch.bfloat16 else xs.float())
-            ops = make_fcm_ops(xin, k, eng.dtype_name, eng.m, nz, eng.cfg.backend)
+            ops = make_fcm_ops(xin, k, eng.dtype_name, eng.m, nz, eng.cfg.backend,
+                               eng.cfg.fcm_distances)
             lab = torch.empty(xs.shape[0], dtype=torch.int32, device=dev)
             ops.step(C.to(ops.c_dtype).contiguous(), lab, wx, ws)
             step = max(1, (1 << 24) // max(1, k * d))

@@ -257,7 +257,11 @@ __global__ __launch_bounds__(256) void fcm_wide_wtx_kernel(const T* __restrict__
 // ---------------------------------------------------------------------------------------
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 constexpr int F64T = 128;  // output tile edge
-constexpr int F64S = 16;   // reduction depth per LDS stage
+// reduction depth per LDS stage: 16 in the distance pass, 32 in W^T X (half its register-
+// staged stores and barriers per MFMA, 46.3 -> 43.9 ms per D=768 step; the distance pass
+// went 40.9 -> 44.1 ms at 32, profiles/fcm_fp64_d768_kernel_stats_r05l.txt)
+constexpr int F64S_D = 16;
+constexpr int F64S_W = 32;
 
 // G[r, k] = d2 for rows [0, M) x centroids (grid: XCD-grouped (row tile, centroid tile)).
 // The norms are summed from the staged tiles (the kernel sees every feature of its rows
@@ -268,7 +272,7 @@ constexpr int F64S = 16;   // reduction depth per LDS stage
 __global__ __launch_bounds__(256, 1) void fcm_wide_d2_f64m_kernel(
     const double* __restrict__ X, int64_t M, int64_t ldx, int D, const double* __restrict__ C,
     int K, int nct, double* __restrict__ G) {
-  constexpr int PX = F64S + 2;  // 144-B rows: each 32-lane half of a b64 fragment read covers 64 banks once
+  constexpr int PX = F64S_D + 2;  // 144-B rows: each 32-lane half of a b64 fragment read covers 64 banks once
   __shared__ double s_x[2][F64T * PX];
   __shared__ double s_c[2][F64T * PX];
   __shared__ double s_xn[F64T], s_cn[F64T];
@@ -282,8 +286,9 @@ __global__ __launch_bounds__(256, 1) void fcm_wide_d2_f64m_kernel(
   const int ct = (int)(L % nct);
   const int64_t r0 = (L / nct) * F64T;
   const int k0 = ct * F64T;
-  // staging: thread t loads 4 features (chunk t & 3) of rows (t >> 2) and (t >> 2) + 64
-  const int srow = tid >> 2, sch = (tid & 3) * 4;
+  // staging: thread t loads F64S_D / 4 features (chunk t & 3) of rows (t >> 2) and (t >> 2) + 64
+  constexpr int FPT = F64S_D / 4;
+  const int srow = tid >> 2, sch = (tid & 3) * FPT;
   const double* xr[2];
   const double* cr[2];
 #pragma unroll
@@ -293,14 +298,14 @@ __global__ __launch_bounds__(256, 1) void fcm_wide_d2_f64m_kernel(
     xr[j] = X + rr * ldx;
     cr[j] = C + (int64_t)kk * D;
   }
-  double vx[2][4], vc[2][4];
+  double vx[2][FPT], vc[2][FPT];
   double nx[2] = {0.0, 0.0}, nc[2] = {0.0, 0.0};
   auto load = [&](int st) __attribute__((always_inline)) {
-    const int d0 = st * F64S + sch;
+    const int d0 = st * F64S_D + sch;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
+      for (int e = 0; e < FPT; ++e) {
         const bool ok = d0 + e < D;
         vx[j][e] = ok ? xr[j][d0 + e] : 0.0;
         vc[j][e] = ok ? cr[j][d0 + e] : 0.0;
@@ -310,7 +315,7 @@ __global__ __launch_bounds__(256, 1) void fcm_wide_d2_f64m_kernel(
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
+      for (int e = 0; e < FPT; ++e) {
         s_x[buf][(srow + 64 * j) * PX + sch + e] = vx[j][e];
         s_c[buf][(srow + 64 * j) * PX + sch + e] = vc[j][e];
         nx[j] = fma(vx[j][e], vx[j][e], nx[j]);
@@ -322,7 +327,7 @@ __global__ __launch_bounds__(256, 1) void fcm_wide_d2_f64m_kernel(
   for (int ti = 0; ti < 4; ++ti)
 #pragma unroll
     for (int tj = 0; tj < 4; ++tj) acc[ti][tj] = f64x4{0.0, 0.0, 0.0, 0.0};
-  const int nst = (D + F64S - 1) / F64S;
+  const int nst = (D + F64S_D - 1) / F64S_D;
   load(0);
   store(0);
   __syncthreads();
@@ -333,7 +338,7 @@ __global__ __launch_bounds__(256, 1) void fcm_wide_d2_f64m_kernel(
     const double* sx = s_x[buf] + (wr * 64 + fr) * PX + fk;
     const double* sc = s_c[buf] + (wc * 64 + fr) * PX + fk;
 #pragma unroll
-    for (int kk = 0; kk < F64S / 4; ++kk) {
+    for (int kk = 0; kk < F64S_D / 4; ++kk) {
       double a[4], b[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -392,8 +397,8 @@ __global__ __launch_bounds__(256, 1) void fcm_wide_wtx_f64m_kernel(
     double* __restrict__ ws) {
   constexpr int PW = F64T + 16;  // 1152-B rows (= 128 mod 256): the two 16-lane groups of a
                                  // b64 fragment read fall on disjoint bank halves
-  __shared__ double s_w[2][F64S * PW];
-  __shared__ double s_x[2][F64S * PW];
+  __shared__ double s_w[2][F64S_W * PW];
+  __shared__ double s_x[2][F64S_W * PW];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = w >> 1, wc = w & 1;
   // XCD-aware order: the nkt x ndt tile blocks of one row split are consecutive on one XCD,
@@ -409,25 +414,31 @@ __global__ __launch_bounds__(256, 1) void fcm_wide_wtx_f64m_kernel(
   const int k0 = kt * F64T, d0 = dt * F64T;
   const int64_t a = split * rows_per_split;
   const int64_t b = min(M, a + rows_per_split);
-  // staging: thread t loads 8 consecutive columns (t & 15) * 8 of stage row t >> 4
+  // staging: thread t loads 8 consecutive columns (t & 15) * 8 of stage rows (t >> 4) + 16 j
+  constexpr int RPT = F64S_W / 16;
   const int srow = tid >> 4, scol = (tid & 15) * 8;
-  double vw[8], vx[8];
+  double vw[RPT][8], vx[RPT][8];
   auto load = [&](int64_t rs) __attribute__((always_inline)) {
-    const int64_t r = rs + srow;
-    const bool rok = r < b;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int k = k0 + scol + e, d = d0 + scol + e;
-      vw[e] = (rok && k < K) ? W[r * (int64_t)K + k] : 0.0;
-      vx[e] = (rok && d < D) ? X[r * ldx + d] : 0.0;
+    for (int j = 0; j < RPT; ++j) {
+      const int64_t r = rs + srow + 16 * j;
+      const bool rok = r < b;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k = k0 + scol + e, d = d0 + scol + e;
+        vw[j][e] = (rok && k < K) ? W[r * (int64_t)K + k] : 0.0;
+        vx[j][e] = (rok && d < D) ? X[r * ldx + d] : 0.0;
+      }
     }
   };
   auto store = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      s_w[buf][srow * PW + scol + e] = vw[e];
-      s_x[buf][srow * PW + scol + e] = vx[e];
-    }
+    for (int j = 0; j < RPT; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s_w[buf][(srow + 16 * j) * PW + scol + e] = vw[j][e];
+        s_x[buf][(srow + 16 * j) * PW + scol + e] = vx[j][e];
+      }
   };
   f64x4 acc[4][4];
 #pragma unroll
@@ -442,13 +453,13 @@ __global__ __launch_bounds__(256, 1) void fcm_wide_wtx_f64m_kernel(
   __syncthreads();
   const int fr = lane & 15, fk = lane >> 4;
   int buf = 0;
-  for (int64_t rs = a; rs < b; rs += F64S) {
-    const bool more = rs + F64S < b;
-    if (more) load(rs + F64S);
+  for (int64_t rs = a; rs < b; rs += F64S_W) {
+    const bool more = rs + F64S_W < b;
+    if (more) load(rs + F64S_W);
     const double* sw = s_w[buf] + fk * PW + wr * 64 + fr;
     const double* sx = s_x[buf] + fk * PW + wc * 64 + fr;
 #pragma unroll
-    for (int kk = 0; kk < F64S / 4; ++kk) {
+    for (int kk = 0; kk < F64S_W / 4; ++kk) {
       double av[4], bv[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -463,9 +474,9 @@ __global__ __launch_bounds__(256, 1) void fcm_wide_wtx_f64m_kernel(
     }
     // sum_r W[r, k]: stage s of the split goes to feature tile s % ndt, all four waves
     // (thread t: column t & 127, rows of half t >> 7) -- one tile's waves alone carried it
-    if ((int)(((rs - a) / F64S) % ndt) == dt) {
+    if ((int)(((rs - a) / F64S_W) % ndt) == dt) {
 #pragma unroll
-      for (int r = 0; r < F64S / 2; ++r) wsum += s_w[buf][((tid >> 7) * (F64S / 2) + r) * PW + (tid & 127)];
+      for (int r = 0; r < F64S_W / 2; ++r) wsum += s_w[buf][((tid >> 7) * (F64S_W / 2) + r) * PW + (tid & 127)];
     }
     if (more) store(buf ^ 1);
     __syncthreads();
@@ -522,9 +533,9 @@ int launch_wide(int pass, const void* X, int64_t M, int64_t ldx, int D, const vo
     }
     if (pass == 2) {
       const int nkt = (K + F64T - 1) / F64T, ndt = (D + F64T - 1) / F64T;
-      const int64_t stages = (M + F64S - 1) / F64S;
+      const int64_t stages = (M + F64S_W - 1) / F64S_W;
       int64_t splits = wtx_f64_splits(stages, (int64_t)nkt * ndt, num_cus);
-      const int64_t rps = ((stages + splits - 1) / splits) * F64S;
+      const int64_t rps = ((stages + splits - 1) / splits) * F64S_W;
       splits = (M + rps - 1) / rps;
       hipLaunchKernelGGL(fcm_wide_wtx_f64m_kernel, dim3((unsigned)(splits * nkt * ndt)), dim3(256),
                          0, s, (const double*)G, (const double*)X, M, ldx, D, K, nkt, ndt, rps,

@@ -21,6 +21,7 @@ ALGORITHMS = ("lloyd", "bounded")
 COMM_MODES = ("auto", "allreduce", "rsag")
 UPDATE_MODES = ("auto", "full", "delta")
 EXACT_ASSIGN = ("auto", "mfma", "simt")
+FCM_DISTANCES = ("one", "x3")
 
 
 @dataclass(frozen=True)
@@ -41,6 +42,13 @@ class ClusterConfig:
     fuzzifier       FCM m. ``None`` = compat value D (`:121,129`).
     fcm_nan_to_zero compat: membership NaN (point on a centroid) -> 0 (`:125-126`);
                     False gives the correct one-hot membership.
+    fcm_distances   bf16 FCM on the matrix cores (D >= 64): 'x3' (default) runs the
+                    fp32-faithful bf16x3 distances in the accumulate pass; 'one' runs ONE
+                    bf16 product per distance with each row's two nearest centroids
+                    corrected to bf16x3 (0.87x the step at fcm10m, but at a random-row
+                    init on that data the centroid error against the fp64 oracle is
+                    9.4e-3 ('one') vs 9.0e-4 ('x3') of max|c|, profiles/bench_fcm10m_*_r05h;
+                    the stats pass runs one product + fix-up either way).
     empty_cluster   'keep' (default) | 'nan' (globally empty -> NaN, the segment-sum
                     notebook) | 'nan_any' (empty on ANY rank -> NaN, the script's
                     reduce_mean poisoning) | 'reseed' | 'zero'
@@ -86,6 +94,7 @@ class ClusterConfig:
     seed: int = 0
     fuzzifier: Optional[float] = None
     fcm_nan_to_zero: bool = True
+    fcm_distances: str = "x3"
     empty_cluster: str = "keep"
     backend: str = "auto"
     deterministic: bool = False
@@ -135,6 +144,8 @@ class ClusterConfig:
             raise ValueError(f"comm_mode must be one of {COMM_MODES}")
         if self.update not in UPDATE_MODES:
             raise ValueError(f"update must be one of {UPDATE_MODES}")
+        if self.fcm_distances not in FCM_DISTANCES:
+            raise ValueError(f"fcm_distances must be one of {FCM_DISTANCES}")
         if self.exact_assign not in EXACT_ASSIGN:
             raise ValueError(f"exact_assign must be one of {EXACT_ASSIGN}")
         if self.delta_refresh < 0 or not (0.0 <= self.delta_theta <= 1.0):

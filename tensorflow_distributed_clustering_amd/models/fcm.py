@@ -90,13 +90,15 @@ class FcmEngine(OomGuard):
             print(f"[fcm] fuzzifier m={self.m:g} with K={k}: weights u^m ~ K^-m underflow fp32; "
                   f"computing in fp64", flush=True)
         if isinstance(source, torch.Tensor) and not chunk_rows:
-            self.local = make_fcm_ops(source, k, dt_name, self.m, cfg.fcm_nan_to_zero, cfg.backend)
+            self.local = make_fcm_ops(source, k, dt_name, self.m, cfg.fcm_nan_to_zero, cfg.backend,
+                                      cfg.fcm_distances)
             self.source = None
         else:
             if isinstance(source, torch.Tensor):  # device-resident shard, walked in chunks
                 source = ResidentSource(source.to(tdt), (tdt, d), row_offset)
             probe = torch.zeros(1, d, dtype=tdt, device=dev)
-            self.local = make_fcm_ops(probe, k, dt_name, self.m, cfg.fcm_nan_to_zero, cfg.backend)
+            self.local = make_fcm_ops(probe, k, dt_name, self.m, cfg.fcm_nan_to_zero, cfg.backend,
+                                      cfg.fcm_distances)
             self.source = source
         self.chunk_rows = chunk_rows
         self.streamed = self.source is not None
@@ -356,7 +358,7 @@ class FuzzyCMeans:
         x = torch.as_tensor(x)
         d = int(x.shape[1])
         ops = make_fcm_ops(x, self.cfg.n_clusters, self.cfg.dtype, self.fuzzifier(d),
-                           self.cfg.fcm_nan_to_zero, self.cfg.backend)
+                           self.cfg.fcm_nan_to_zero, self.cfg.backend, self.cfg.fcm_distances)
         labels = torch.empty(int(x.shape[0]), dtype=torch.int32, device=x.device)
         ops.assign(self._centers_on(x.device, ops.c_dtype), labels)
         return labels

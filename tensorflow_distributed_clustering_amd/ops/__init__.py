@@ -1334,7 +1334,8 @@ class HipMfmaFCM(_LocalOpsBase):
         n = self.n
         return self.xh[:n], self.xl[:n], self.xx[:n]
 
-    one_product = True  # class switch: False keeps bf16x3 distances in the accumulate pass
+    # one-product accumulate (ClusterConfig.fcm_distances = 'one'); off: bf16x3 distances
+    one_product = False
     raw_rows = True     # class switch: bf16 shards feed W^T X as they are (one product)
 
     def _use_raw(self):
@@ -1511,14 +1512,16 @@ FCM_PRECISION = {
 
 
 def make_fcm_ops(x: torch.Tensor, k: int, dtype: str = "fp64", m: float = 2.0,
-                 nan_to_zero: bool = True, backend: str = "auto"):
+                 nan_to_zero: bool = True, backend: str = "auto", distances: str = "x3"):
     """FCM tower for (dtype, K, D).  fp64 / fp32: the exact difference-form towers (fused
     small-K*D kernel, SIMT tower up to D = 256, wide tower above) -- the reference's
     memberships come from exact differences (`scripts/distribuitedClustering.py:112-129`).
     bf16 (and fp8): the MFMA towers (fp32 rows split into bf16 hi/lo, bf16x3 distances,
     memberships in fp32, W = u^m rounded to bf16 for the W^T X MFMAs; centroid error
     ~1e-3 of max|c| against the fp64 oracle, FCM_PRECISION) for 16 < D <= 1024, K >= 32;
-    other shapes fall back to the exact fp32 towers."""
+    other shapes fall back to the exact fp32 towers.  ``distances`` (ClusterConfig
+    .fcm_distances): 'one' = one-product distances + two-nearest fix-up in both passes
+    (D >= 64), 'x3' = bf16x3 distances in the accumulate pass."""
     d = x.shape[1]
     mfma = dtype in ("bf16", "fp8")
     if mfma:
@@ -1530,7 +1533,9 @@ def make_fcm_ops(x: torch.Tensor, k: int, dtype: str = "fp64", m: float = 2.0,
         return HipSmallFCM(x, k, dtype, m, nan_to_zero)
     if mfma and d > 16 and k >= FCM_MFMA_MIN_K:
         if fcm_mfma_dim(d) is not None:
-            return HipMfmaFCM(x, k, m, nan_to_zero)
+            ops = HipMfmaFCM(x, k, m, nan_to_zero)
+            ops.one_product = distances != "x3"
+            return ops
         if fcm_mfma_wide_dim(d) is not None:
             return HipMfmaWideFCM(x, k, m, nan_to_zero)
     if d <= 256:

@@ -118,6 +118,9 @@ def test_config_validation():
         tdc.ClusterConfig(n_clusters=3, dtype="fp16")
     with pytest.raises(ValueError):
         tdc.ClusterConfig(n_clusters=3, init="bogus")
+    with pytest.raises(ValueError):
+        tdc.ClusterConfig(n_clusters=3, fcm_distances="bf16x9")
+    assert tdc.ClusterConfig(n_clusters=3).fcm_distances == "x3"
 
 
 def test_kmeans_parallel_init_quality():

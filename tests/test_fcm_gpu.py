@@ -323,6 +323,7 @@ def test_fcm_mfma_bf16_rows_raw_wtx(gpu, k, d, m, nz):
     res = {}
     for raw in (True, False):
         ops = HipMfmaFCM(xg, k, m, nz)
+        ops.one_product = True
         ops.raw_rows = raw
         lab = torch.empty(n, dtype=torch.int32, device=gpu)
         wx = torch.zeros(k, d, dtype=torch.float64, device=gpu)
@@ -342,3 +343,28 @@ def test_fcm_mfma_bf16_rows_raw_wtx(gpu, k, d, m, nz):
     # fp32 accumulation order differs
     torch.testing.assert_close(ws1, ws2, rtol=1e-6, atol=0)
     assert bool(((c1 - c2).abs() <= 1e-5 * (1 + c2.abs()))[ok].all())
+
+
+def test_fcm_distances_config_selects_form(gpu):
+    """ClusterConfig.fcm_distances reaches the MFMA tower: 'x3' runs the bf16x3 accumulate
+    (precision string and engine attribute), 'one' the one-product form; both fits stay
+    within the MFMA tower's tolerance of each other."""
+    import tensorflow_distributed_clustering_amd as tdc
+    from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs
+    from tensorflow_distributed_clustering_amd.ops import FCM_PRECISION
+    x = gaussian_blobs(30000, 128, 64, seed=3, dtype=torch.float32, device=gpu)
+    cen = {}
+    for mode in ("one", "x3"):
+        cfg = tdc.ClusterConfig(n_clusters=64, max_iter=3, dtype="bf16", fuzzifier=2.0, seed=2,
+                                fcm_distances=mode)
+        f = tdc.FuzzyCMeans(cfg).fit(x)
+        loc = f.engine_.local
+        assert loc.one_product == (mode == "one")
+        assert loc.precision == FCM_PRECISION["bf16_one" if mode == "one" else "bf16"]
+        cen[mode] = torch.as_tensor(f.result_.centers, dtype=torch.float64)
+    # the one-product form moves the centroid of a fuzzy cluster: after 3 iterations on
+    # this data by up to 1.5 % of max|c| (the rest agree to ~1e-5), the size of the
+    # at-init witness gap of the fcm10m bench (9.4e-3 vs 9.0e-4)
+    diff = (cen["one"] - cen["x3"]).abs().max(1).values
+    assert float(diff.max()) < 3e-2 * float(cen["x3"].abs().max())
+    assert float(diff.median()) < 1e-3 * float(cen["x3"].abs().max())
