@@ -290,7 +290,7 @@ def test_fcm_mfma_one_product_vs_bf16x3(gpu, k, d, m, nz):
         wx = torch.zeros(k, d, dtype=torch.float64, device=gpu)
         ws = torch.zeros(k, dtype=torch.float64, device=gpu)
         ops.step(cg, lab, wx, ws)
-        assert ops.precision == FCM_PRECISION["bf16_one" if one else "bf16"]
+        assert ops.precision == FCM_PRECISION["bf16_one" if one else "bf16"]  # fp32 rows
         _check(wx.cpu(), ws.cpu(), lab, xg.cpu(), cg.cpu(), m, nz, 2e-3 * m, 0.998)
         res[one] = (wx.cpu(), ws.cpu(), lab.cpu())
     (wx1, ws1, l1), (wx3, ws3, l3) = res[True], res[False]
@@ -360,7 +360,7 @@ def test_fcm_distances_config_selects_form(gpu):
         f = tdc.FuzzyCMeans(cfg).fit(x)
         loc = f.engine_.local
         assert loc.one_product == (mode == "one")
-        assert loc.precision == FCM_PRECISION["bf16_one" if mode == "one" else "bf16"]
+        assert loc.precision == FCM_PRECISION["bf16_one" if mode == "one" else "bf16"]  # fp32
         cen[mode] = torch.as_tensor(f.result_.centers, dtype=torch.float64)
     # the one-product form moves the centroid of a fuzzy cluster: after 3 iterations on
     # this data by up to 1.5 % of max|c| (the rest agree to ~1e-5), the size of the
@@ -368,3 +368,57 @@ def test_fcm_distances_config_selects_form(gpu):
     diff = (cen["one"] - cen["x3"]).abs().max(1).values
     assert float(diff.max()) < 3e-2 * float(cen["x3"].abs().max())
     assert float(diff.median()) < 1e-3 * float(cen["x3"].abs().max())
+
+
+@pytest.mark.parametrize("k,d", [(1024, 128), (300, 100)])
+@pytest.mark.parametrize("nz", [True, False])
+def test_fcm_mfma_bf16x3_raw_wtx(gpu, k, d, nz):
+    """bf16x3 distances (the default form) on a bf16 shard: the tile holds xh | xl | xr and
+    W^T X takes the raw rows (one product); against the hi/lo W^T X of the same form the
+    weights are identical and the centroids agree to the split's 2^-17."""
+    from tensorflow_distributed_clustering_amd.ops import FCM_PRECISION, HipMfmaFCM
+    n, m = 20001, 2.0
+    x, c = _data(n, k, d, 17 * k + d)
+    xb = x.to(torch.bfloat16)
+    c[min(3, k - 1)] = xb[7].double()
+    xg, cg = xb.to(gpu), c.float().to(gpu)
+    res = {}
+    for raw in (True, False):
+        ops = HipMfmaFCM(xg, k, m, nz)
+        ops.raw_rows = raw
+        lab = torch.empty(n, dtype=torch.int32, device=gpu)
+        wx = torch.zeros(k, d, dtype=torch.float64, device=gpu)
+        ws = torch.zeros(k, dtype=torch.float64, device=gpu)
+        ops.step(cg, lab, wx, ws)
+        assert ops.precision == FCM_PRECISION["bf16_raw" if raw else "bf16"]
+        # (the stats pass's one-product normaliser on bf16-rounded rows: this seed's worst
+        # cluster sum is 0.41 % off at m = 2 in both W^T X forms)
+        _check(wx.cpu(), ws.cpu(), lab, xb.double(), cg.cpu(), m, nz, 3e-3 * m, 0.998)
+        res[raw] = (wx.cpu(), ws.cpu())
+    (wx1, ws1), (wx2, ws2) = res[True], res[False]
+    ok = ws2 > 1e-12 * ws2.max()
+    torch.testing.assert_close(ws1, ws2, rtol=1e-6, atol=0)
+    c1, c2 = wx1 / ws1.clamp_min(1e-300)[:, None], wx2 / ws2.clamp_min(1e-300)[:, None]
+    assert bool(((c1 - c2).abs() <= 1e-5 * (1 + c2.abs()))[ok].all())
+
+
+@pytest.mark.parametrize("k,d", [(1024, 128), (257, 64), (300, 100)])
+@pytest.mark.parametrize("m", [2.0, 3.0])
+@pytest.mark.parametrize("nz", [True, False])
+def test_fcm_mfma_f8x_matches_oracle(gpu, k, d, m, nz):
+    """fcm_distances='f8x' on a bf16 shard: one bf16 product + the cross terms on the fp8
+    cores (2^8-scaled lo halves, E8M0 rescale) + the two-nearest fix-up -- held to the
+    bf16x3 tolerance of the oracle tests (2e-3 m), unlike 'one'."""
+    from tensorflow_distributed_clustering_amd.ops import FCM_PRECISION, make_fcm_ops
+    n = 20001
+    x, c = _data(n, k, d, 19 * k + d)
+    xb = x.to(torch.bfloat16)
+    c[min(3, k - 1)] = xb[7].double()
+    xg, cg = xb.to(gpu), c.float().to(gpu)
+    ops = make_fcm_ops(xg, k, "bf16", m, nz, "auto", "f8x")
+    lab = torch.empty(n, dtype=torch.int32, device=gpu)
+    wx = torch.zeros(k, d, dtype=torch.float64, device=gpu)
+    ws = torch.zeros(k, dtype=torch.float64, device=gpu)
+    ops.step(cg, lab, wx, ws)
+    assert ops.precision == FCM_PRECISION["bf16_one_f8x"]
+    _check(wx.cpu(), ws.cpu(), lab, xb.double(), cg.cpu(), m, nz, 2e-3 * m, 0.998)
