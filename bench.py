@@ -113,7 +113,7 @@ def parse(argv=None):
                          "changed between fp64 running totals (with a full re-sum every "
                          "--delta-refresh steps and after steps that moved > 40%% of the rows); "
                          "full re-sums every row every step; auto = delta where supported")
-    ap.add_argument("--fcm-distances", default="x3", choices=["one", "x3", "f8x"],
+    ap.add_argument("--fcm-distances", default="x3", choices=["one", "x3"],
                     help="bf16 FCM distances: one product + two-nearest fix-up, or bf16x3 "
                          "(ClusterConfig.fcm_distances)")
     ap.add_argument("--comm-mode", default="auto", choices=["auto", "allreduce", "rsag"],

@@ -407,7 +407,7 @@ void fcm_mfma_wide(int64_t pass, const at::Tensor& Xh, const at::Tensor& Xl, con
 
 void fcm_split_rows(const at::Tensor& src, int64_t valid, int64_t neg2, at::Tensor& hi,
                     at::Tensor& lo, const std::optional<at::Tensor>& norm,
-                    const std::optional<at::Tensor>& shift, const std::optional<at::Tensor>& f8) {
+                    const std::optional<at::Tensor>& shift) {
   check_cuda(src, "src");
   TORCH_CHECK(src.scalar_type() == at::kFloat && src.dim() == 2 && src.stride(1) == 1,
               "tdc.fcm_split_rows: src fp32 rows");
@@ -424,15 +424,11 @@ void fcm_split_rows(const at::Tensor& src, int64_t valid, int64_t neg2, at::Tens
   if (shift.has_value() && shift->defined())
     TORCH_CHECK(shift->scalar_type() == at::kFloat && shift->is_contiguous() &&
                     shift->numel() >= src.size(1), "tdc.fcm_split_rows: shift fp32 [d]");
-  if (f8.has_value() && f8->defined())
-    TORCH_CHECK(f8->scalar_type() == at::kByte && f8->is_contiguous() &&
-                    f8->numel() >= rows * 2 * DP,
-                "tdc.fcm_split_rows: f8 uint8 [rows, 2 DP]");
   const DevGuard guard(src.device());
   check(tdc_fcm_split_rows(src.data_ptr<float>(), rows, valid, (int)src.size(1), src.stride(0), DP,
                            (int)neg2, static_cast<const float*>(opt_ptr(shift)), hi.data_ptr(),
                            lo.data_ptr(),
-                           static_cast<float*>(opt_ptr(norm)), opt_ptr(f8), cur_stream()),
+                           static_cast<float*>(opt_ptr(norm)), cur_stream()),
         "fcm_split_rows");
 }
 
@@ -465,7 +461,7 @@ void fcm_mfma_stats(const at::Tensor& Xh, const at::Tensor& Xl, const at::Tensor
   TORCH_CHECK(rowinfo.scalar_type() == at::kFloat && rowinfo.is_contiguous() && rowinfo.numel() >= N,
               "tdc.fcm_mfma_stats: rowinfo fp32 [N]");
   const DevGuard guard(Xh.device());
-  check(tdc_fcm_mfma(0, Xh.data_ptr(), Xl.data_ptr(), nullptr, nullptr, nullptr, xx.data_ptr<float>(), N, (int)Xh.size(1), 0,
+  check(tdc_fcm_mfma(0, Xh.data_ptr(), Xl.data_ptr(), nullptr, xx.data_ptr<float>(), N, (int)Xh.size(1), 0,
                      Ch.data_ptr(), Cl.data_ptr(), cc.data_ptr<float>(), (int)K, (int)Ch.size(0),
                      m, nan_to_zero ? 1 : 0, labels.data_ptr<int32_t>(), rowinfo.data_ptr<float>(),
                      rowinfo.numel(), nullptr, nullptr, nullptr, nullptr,
@@ -477,21 +473,12 @@ void fcm_mfma_accum(const at::Tensor& Xh, const at::Tensor& Xl, const at::Tensor
                     const at::Tensor& rowinfo, const at::Tensor& Ch, const at::Tensor& Cl,
                     const at::Tensor& cc, int64_t K, double m, bool nan_to_zero, at::Tensor& wx,
                     at::Tensor& ws, at::Tensor& work, const std::optional<at::Tensor>& shift,
-                    const std::optional<at::Tensor>& Xr, const std::optional<at::Tensor>& A8,
-                    const std::optional<at::Tensor>& B8) {
+                    const std::optional<at::Tensor>& Xr) {
   check_mfma_fcm(Xh, Xl, xx, Ch, Cl, cc, K, m, "fcm_mfma_accum");
   if (Xr.has_value() && Xr->defined())
     TORCH_CHECK(Xr->scalar_type() == at::kBFloat16 && Xr->is_contiguous() &&
                     Xr->sizes() == Xh.sizes(),
                 "tdc.fcm_mfma_accum: Xr bf16 [N, DP] like Xh");
-  const bool f8x = A8.has_value() && A8->defined();
-  TORCH_CHECK(f8x == (B8.has_value() && B8->defined()), "tdc.fcm_mfma_accum: A8 and B8 together");
-  if (f8x)
-    TORCH_CHECK(A8->scalar_type() == at::kByte && B8->scalar_type() == at::kByte &&
-                    A8->is_contiguous() && B8->is_contiguous() &&
-                    A8->numel() >= Xh.size(0) * 2 * Xh.size(1) &&
-                    B8->numel() >= Ch.size(0) * 2 * Ch.size(1) && Xr.has_value() && Xr->defined(),
-                "tdc.fcm_mfma_accum: A8 uint8 [N, 2 DP], B8 uint8 [Kp, 2 DP], with Xr");
   const int nc = num_cus(Xh.device().index());
   TORCH_CHECK(work.scalar_type() == at::kFloat && work.is_contiguous() &&
                   work.numel() >= tdc_fcm_mfma_workspace(Xh.size(0), (int)K, (int)Ch.size(0),
@@ -505,7 +492,7 @@ void fcm_mfma_accum(const at::Tensor& Xh, const at::Tensor& Xl, const at::Tensor
                   wx.size(1) <= Xh.size(1) && ws.numel() == K,
               "tdc.fcm_mfma_accum: wx [K, D] / ws [K] fp64");
   const DevGuard guard(Xh.device());
-  check(tdc_fcm_mfma(1, Xh.data_ptr(), Xl.data_ptr(), opt_ptr(Xr), opt_ptr(A8), opt_ptr(B8), xx.data_ptr<float>(), N, (int)Xh.size(1),
+  check(tdc_fcm_mfma(1, Xh.data_ptr(), Xl.data_ptr(), opt_ptr(Xr), xx.data_ptr<float>(), N, (int)Xh.size(1),
                      (int)wx.size(1), Ch.data_ptr(), Cl.data_ptr(), cc.data_ptr<float>(), (int)K,
                      (int)Ch.size(0), m, nan_to_zero ? 1 : 0, nullptr,
                      const_cast<float*>(rowinfo.data_ptr<float>()), rowinfo.numel(), wx.data_ptr<double>(),
@@ -1168,9 +1155,9 @@ TORCH_LIBRARY(tdc, m) {
   m.def("fcm_wide_rows(Tensor(a!) G, int K, float m, bool nan_to_zero, Tensor(b!) labels, bool write_w) -> ()");
   m.def("fcm_mfma_wide_workspace(Tensor like, int M, int Kp, int DP) -> int");
   m.def("fcm_mfma_wide(int stage, Tensor Xh, Tensor Xl, Tensor xx, Tensor Ch, Tensor Cl, Tensor cc, int K, int D, Tensor(a!) G, Tensor(b!)? work=None, Tensor? shift=None, Tensor(c!)? wx=None, Tensor(d!)? ws=None) -> ()");
-  m.def("fcm_split_rows(Tensor src, int valid, int neg2, Tensor(a!) hi, Tensor(b!) lo, Tensor(c!)? norm, Tensor? shift=None, Tensor(d!)? f8=None) -> ()");
+  m.def("fcm_split_rows(Tensor src, int valid, int neg2, Tensor(a!) hi, Tensor(b!) lo, Tensor(c!)? norm, Tensor? shift=None) -> ()");
   m.def("fcm_mfma_stats(Tensor Xh, Tensor Xl, Tensor xx, Tensor Ch, Tensor Cl, Tensor cc, int K, float m, bool nan_to_zero, Tensor(a!) labels, Tensor(b!) rowinfo) -> ()");
-  m.def("fcm_mfma_accum(Tensor Xh, Tensor Xl, Tensor xx, Tensor rowinfo, Tensor Ch, Tensor Cl, Tensor cc, int K, float m, bool nan_to_zero, Tensor(a!) wx, Tensor(b!) ws, Tensor(c!) work, Tensor? shift=None, Tensor? Xr=None, Tensor? A8=None, Tensor? B8=None) -> ()");
+  m.def("fcm_mfma_accum(Tensor Xh, Tensor Xl, Tensor xx, Tensor rowinfo, Tensor Ch, Tensor Cl, Tensor cc, int K, float m, bool nan_to_zero, Tensor(a!) wx, Tensor(b!) ws, Tensor(c!) work, Tensor? shift=None, Tensor? Xr=None) -> ()");
   m.def("fcm_mfma_workspace(Tensor like, int N, int K, int Kp, int DP) -> int");
   m.def("fcm_mfma_rowinfo_len(Tensor like, int N, int DP) -> int");
   m.def("assign_bigd_supported(ScalarType dtype, int DP) -> bool", &assign_bigd_supported);

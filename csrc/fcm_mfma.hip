@@ -41,7 +41,6 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr float ZERO_FLOOR = 1.52587890625e-05f;  // 2^-16 (an exact hit computes ~2^-17 |x|^2)
@@ -591,23 +590,14 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats1_kernel(
 // no shift back.  For bf16 data only (the rows ARE those bf16 numbers; fp32 rows keep
 // W^T Xh + W^T Xl).  With ONE the tile holds [xh | xr]; with the bf16x3 distances
 // [xh | xl | xr] (NIMG = 3).
-//
-// F8X (with ONE, RAW, STAG): the distances add the cross terms xl.ch + xh.cl on the fp8 matrix
-// cores after the bf16 xh.ch -- A8 = [e4m3(xl 2^8) | e4m3(xh)] per row, B8 = [e4m3(ch) |
-// e4m3(cl 2^8)] per centroid, the 2^-8 applied exactly by the MFMA's E8M0 block scales --
-// which leaves ~2^-13 / sqrt(D) of |x||c| instead of one product's 2^-9 / sqrt(D)
-// (tools/fcm_precision_model.py: with the nearest-two fix-up as accurate as bf16x3).  LDS:
-// xh and A8 in two tile buffers (only the distances read them, in the tile's own
-// interval), xr in three, the block's 128 B8 rows once.
-template <int DP, int MODE, bool NZ, int WAVES, bool STAG, bool ONE, bool RAW, bool F8X = false>
+template <int DP, int MODE, bool NZ, int WAVES, bool STAG, bool ONE, bool RAW>
 __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     const __bf16* __restrict__ Xh, const __bf16* __restrict__ Xl, const float* __restrict__ xx,
     const float* __restrict__ rowinfo, const float* __restrict__ fix, int64_t N,
     const __bf16* __restrict__ Xr, const __bf16* __restrict__ Ch,
     const __bf16* __restrict__ Cl, const float* __restrict__ cc, int K, int nkt,
     int64_t rows_per_split, int xcd_map, MParam prm, float* __restrict__ part,
-    float* __restrict__ part_ws, int KP, const unsigned char* __restrict__ A8,
-    const unsigned char* __restrict__ B8) {
+    float* __restrict__ part_ws, int KP) {
   constexpr int TP = 64;                  // points per LDS tile (two 32-point sub-tiles)
   constexpr int CPR = DP / 8;
   constexpr int KS = DP / 16;
@@ -621,9 +611,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
   // tile images: xh, then xl (bf16x3 distances, or W^T X's lo operand), then xr (RAW)
   constexpr int NIMG = (RAW && !ONE) ? 3 : 2;
   constexpr int NBUF = STAG ? 3 : 2;
-  static_assert(!F8X || (ONE && RAW && STAG), "fp8 cross terms: one-product staggered raw form");
-  // F8X layout: xh[2] | A8[2] | xr[3] | B8 (128 rows = 2 images)
-  constexpr int SXB = F8X ? 9 * IMG : NBUF * NIMG * IMG;
+  constexpr int SXB = NBUF * NIMG * IMG;
   // row statistics per tile row: xx, 1/S, the zero floor 2^-16 xx (+ d2a, d2b, la, lb)
   constexpr int NRS = ONE ? 7 : 3;
   __shared__ __attribute__((aligned(16))) char s_xf[SXB];
@@ -673,9 +661,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
   // the 2 x 64 row statistics still go through registers (padded rows get special
   // values).
   constexpr int PPI = IMG / 1024;               // 1-KiB pieces per (hi or lo) image
-  constexpr int TIMG = F8X ? 3 : NIMG;          // images per tile
-  constexpr int PPW = TIMG * PPI / WAVES;       // pieces per wave per tile
-  static_assert(IMG % 1024 == 0 && (TIMG * PPI) % WAVES == 0, "tile pieces");
+  constexpr int PPW = NIMG * PPI / WAVES;       // pieces per wave per tile
+  static_assert(IMG % 1024 == 0 && (NIMG * PPI) % WAVES == 0, "tile pieces");
   const int wu = __builtin_amdgcn_readfirstlane(w);  // wave index in SGPRs (DMA destinations)
   int prow[PPW];
   unsigned pcol[PPW];
@@ -717,59 +704,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                      \
     if (tid < NRS * TP) s_rs[B_][w][lane] = pv;                                          \
   }
-  // F8X: the tile's three images (0 xh -> it & 1, 1 xr -> it % 3, 2 A8 -> it & 1); every
-  // row is 2 DP bytes in all three, so one swizzle and one piece geometry serve them
-#define TDC_X8_OFF(IM_, IT_)                                                              \
-  ((IM_) == 0 ? (int)((IT_) & 1) * IMG                                                    \
-              : (IM_) == 2 ? 2 * IMG + (int)((IT_) & 1) * IMG : 4 * IMG + (int)((IT_) % 3) * IMG)
-#define TDC_TILE_LOAD8(R0_, IT_)                                                          \
-  {                                                                                       \
-    const int last_ = (int)(b - 1 - (R0_));                                               \
-    _Pragma("unroll") for (int i = 0; i < PPW; ++i) {                                     \
-      const int pc_ = wu * PPW + i;                                                       \
-      const int im_ = pc_ / PPI;                                                          \
-      const unsigned char* base_ = (im_ == 0 ? (const unsigned char*)Xh                   \
-                                   : im_ == 1 ? (const unsigned char*)Xr : A8) +          \
-                                   (R0_) * (DP * 2);                                      \
-      const int rr_ = prow[i] < last_ ? prow[i] : last_;                                  \
-      const unsigned dst_ = lds_x + TDC_X8_OFF(im_, IT_) + (pc_ % PPI) * 1024;            \
-      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"                  \
-                   :: "s"(__builtin_amdgcn_readfirstlane(dst_)),                          \
-                      "v"((unsigned)(rr_ * DP * 2) + pcol[i]), "s"(uniform_ptr(base_))    \
-                   : "memory", "m0");                                                     \
-    }                                                                                     \
-    if (tid < NRS * TP) {                                                                 \
-      const int64_t gr = (R0_) + lane;                                                    \
-      if (w == 0 || w == 2) {                                                             \
-        pv = gr < b ? xx[gr] : 1.0e30f;                                                   \
-        if (w == 2) pv *= ZERO_FLOOR;                                                     \
-      } else if (w == 1) pv = gr < b ? rowinfo[gr] : 0.f;                                 \
-      else pv = gr < b ? fix[gr * 4 + (w - 3)] : (w >= 5 ? __int_as_float(-1) : 0.f);     \
-    }                                                                                     \
-  }
-  if constexpr (F8X) {
-    // the block's 128 B8 rows, once (they land before the first tile's barrier)
-    constexpr int BPW = 2 * PPI / WAVES;
-    const unsigned char* bsrc = B8 + (int64_t)kt * 128 * (DP * 2);
-#pragma unroll
-    for (int i = 0; i < BPW; ++i) {
-      const int pc = wu * BPW + i;
-      const int q = (pc % PPI) * 64 + lane;
-      const int row = (pc / PPI) * 64 + q / CPR;
-      const unsigned col = (unsigned)(xoff<DP>(row & 63, q % CPR) - (row & 63) * DP * 2);
-      const unsigned dst = lds_x + 7 * IMG + pc * 1024;
-      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
-                   :: "s"(__builtin_amdgcn_readfirstlane(dst)),
-                      "v"((unsigned)(row * DP * 2) + col), "s"(uniform_ptr(bsrc))
-                   : "memory", "m0");
-    }
-  }
   if (a < b) {
-    if constexpr (F8X) {
-      TDC_TILE_LOAD8(a, 0)
-    } else {
-      TDC_TILE_LOAD(a, 0)
-    }
+    TDC_TILE_LOAD(a, 0)
     TDC_TILE_STORE(0)
   }
   __syncthreads();
@@ -792,26 +728,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
         af[kk + 2] = as_bf16x8(*reinterpret_cast<const uint4*>(xh + xoff<DP>(prow, h * (CPR / 2) + kk + 2))); \
       ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk], ch[kk], ACC, 0, 0, 0);        \
       INTERLEAVE(kk * EPK, EPK)                                                           \
-    }                                                                                     \
-    if constexpr (F8X) {                                                                  \
-      /* cross terms on the fp8 cores: step s covers row bytes [64 s, 64 s + 64): lane     \
-         (r, h) holds chunks 4 s + h and 4 s + 2 + h (assign_bigd.hip's probed layout);   \
-         the xl / cl halves carry 2^8, taken back by E8M0 scale 119 = 2^-8 */             \
-      constexpr int NS8 = DP / 32;                                                        \
-      const char* b8 = s_xf + 7 * IMG;                                                    \
-      const int crow = cg * 32 + r;                                                       \
-      _Pragma("unroll") for (int s8 = 0; s8 < NS8; ++s8) {                                \
-        const uint4 a0_ = *reinterpret_cast<const uint4*>(a8 + xoff<DP>(prow, 4 * s8 + h));     \
-        const uint4 a1_ = *reinterpret_cast<const uint4*>(a8 + xoff<DP>(prow, 4 * s8 + 2 + h)); \
-        const uint4 b0_ = *reinterpret_cast<const uint4*>(b8 + xoff<DP>(crow, 4 * s8 + h));     \
-        const uint4 b1_ = *reinterpret_cast<const uint4*>(b8 + xoff<DP>(crow, 4 * s8 + 2 + h)); \
-        const i32x8 av_ = {(int)a0_.x, (int)a0_.y, (int)a0_.z, (int)a0_.w,                \
-                           (int)a1_.x, (int)a1_.y, (int)a1_.z, (int)a1_.w};               \
-        const i32x8 bv_ = {(int)b0_.x, (int)b0_.y, (int)b0_.z, (int)b0_.w,                \
-                           (int)b1_.x, (int)b1_.y, (int)b1_.z, (int)b1_.w};               \
-        const int sa_ = s8 < NS8 / 2 ? 119 : 127, sb_ = s8 < NS8 / 2 ? 127 : 119;         \
-        ACC = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(av_, bv_, ACC, 0, 0, 0, sa_, 0, sb_); \
-      }                                                                                   \
     }                                                                                     \
   } else {                                                                                \
     _Pragma("unroll") for (int i = 0; i < 16; ++i) ACC[i] = ccl;                         \
@@ -959,25 +875,17 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     for (int64_t it = 0; it <= ntile; ++it) {
       const bool cur = it < ntile, more = it + 1 < ntile;
       const int bn = bc == 2 ? 0 : bc + 1, bp = bc == 0 ? 2 : bc - 1;
-      if (more) {
-        if constexpr (F8X) {
-          TDC_TILE_LOAD8(a + (it + 1) * TP, it + 1)
-        } else {
-          TDC_TILE_LOAD(a + (it + 1) * TP, bn)
-        }
-      }
+      if (more) TDC_TILE_LOAD(a + (it + 1) * TP, bn)
       // image pointers of tile it (cur) and it - 1 (the lagging waves' W^T X)
-      const char* xh_c = F8X ? s_xf + TDC_X8_OFF(0, it) : s_x(bc);
-      const char* xl_c = F8X ? xh_c : s_x(bc) + IMG;
-      const char* xw_c = F8X ? s_xf + TDC_X8_OFF(1, it) : s_x(bc) + (NIMG - 1) * IMG;
-      const char* a8_c = F8X ? s_xf + TDC_X8_OFF(2, it) : nullptr;
-      const char* xw_p = F8X ? s_xf + TDC_X8_OFF(1, it + 2) : s_x(bp) + (NIMG - 1) * IMG;
+      const char* xh_c = s_x(bc);
+      const char* xl_c = s_x(bc) + IMG;
+      const char* xw_c = s_x(bc) + (NIMG - 1) * IMG;
+      const char* xw_p = s_x(bp) + (NIMG - 1) * IMG;
       if (sub == 0) {
         if (cur) {
           const char* xh = xh_c;
           const char* xl = xl_c;
           const char* xw = xw_c;
-          const char* a8 = a8_c;
           TDC_DIST(acc0, 0, TDC_NONE)
           TDC_MEMB8(acc0, wh0, 0, bc)
           TDC_WTX(0, wh0, TDC_NONE, )
@@ -985,7 +893,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
       } else {
         if (it > 0) {
           // (W^T X reads xh only without RAW, when the tile is [xh | xl])
-          const char* xh = F8X ? xw_p : s_x(bp);
+          const char* xh = s_x(bp);
           const char* xl = xw_p;
           const char* xw = xw_p;
           TDC_MEMB8(acc0, wh0, 1, bp)
@@ -995,7 +903,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
           const char* xh = xh_c;
           const char* xl = xl_c;
           const char* xw = xw_c;
-          const char* a8 = a8_c;
           TDC_DIST(acc0, 1, TDC_NONE)
         }
       }
@@ -1011,7 +918,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     if (more) TDC_TILE_LOAD(r0 + TP, buf ^ 1)
     const char* xh = s_x(buf);
     const char* xl = s_x(buf) + IMG;
-    const char* a8 = nullptr;
     const char* xw = s_x(buf) + (NIMG - 1) * IMG;
     // Software pipeline over the two 32-point halves, written out explicitly so that the
     // membership VALU of one half issues between the MFMAs of the other (one wave per
@@ -1129,8 +1035,7 @@ __global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict
                                                          int neg2, const float* __restrict__ shift,
                                                          __bf16* __restrict__ hi,
                                                          __bf16* __restrict__ lo,
-                                                         float* __restrict__ norm,
-                                                         unsigned char* __restrict__ f8) {
+                                                         float* __restrict__ norm) {
   const int lane = threadIdx.x & 63;
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows;
        row += (int64_t)gridDim.x * 4) {
@@ -1143,15 +1048,6 @@ __global__ __launch_bounds__(256) void split_rows_kernel(const float* __restrict
       const __bf16 vl = (__bf16)(t - (float)vh);
       hi[row * DP + c] = vh;
       lo[row * DP + c] = vl;
-      if (f8) {
-        // the fp8 cross-term operands (fcm_mfma_accum F8X): rows [e4m3(lo 2^8) | e4m3(hi)],
-        // centroids [e4m3(hi) | e4m3(lo 2^8)] -- 2 DP bytes per row
-        const unsigned char eh = (unsigned char)(__builtin_amdgcn_cvt_pk_fp8_f32((float)vh, 0.f, 0, false) & 0xff);
-        const unsigned char el =
-            (unsigned char)(__builtin_amdgcn_cvt_pk_fp8_f32((float)vl * 256.f, 0.f, 0, false) & 0xff);
-        f8[row * 2 * DP + c] = neg2 ? eh : el;
-        f8[row * 2 * DP + DP + c] = neg2 ? el : eh;
-      }
     }
     s = wave_sum(s);
     // centroid pad rows: a huge norm keeps their distances (and memberships) negligible
@@ -1209,8 +1105,7 @@ inline void accum_geometry(int64_t N, int K, int num_cus, int* nkt, int64_t* spl
 }
 
 template <int DP>
-int launch_maccum(const void* Xh, const void* Xl, const void* Xr, const void* A8,
-                  const void* B8, const float* xx,
+int launch_maccum(const void* Xh, const void* Xl, const void* Xr, const float* xx,
                   const float* rowinfo, const float* fix, int64_t N, const void* Ch, const void* Cl, const float* cc, int K, int Kp,
                   int D, double m, int nz, float* part, const float* mu, double* wx, double* ws,
                   int num_cus, hipStream_t s) {
@@ -1230,21 +1125,20 @@ int launch_maccum(const void* Xh, const void* Xl, const void* Xr, const void* A8
   // (one product + raw rows: the tile is [xh | xr], so xr rides in the second image slot)
   const bool one = DP >= 64 && fix;
   const void* X2 = (one && Xr) ? Xr : Xl;
-#define TDC_LA(MODE, NZV, ST, ONEV, RAWV, F8V)                                                \
-  hipLaunchKernelGGL((fcm_mfma_accum_kernel<DP, MODE, NZV, 8, ST, ONEV, RAWV, F8V>),          \
+#define TDC_LA(MODE, NZV, ST, ONEV, RAWV)                                                     \
+  hipLaunchKernelGGL((fcm_mfma_accum_kernel<DP, MODE, NZV, 8, ST, ONEV, RAWV>),               \
                      dim3((unsigned)nb), dim3(512), 0, s, (const __bf16*)Xh,                   \
                      (const __bf16*)X2, xx, rowinfo, fix, N, (const __bf16*)Xr,                \
                      (const __bf16*)Ch, (const __bf16*)Cl, cc, K, nkt, rps, xcd, p, part,      \
-                     part_ws, Kp, (const unsigned char*)A8, (const unsigned char*)B8)
+                     part_ws, Kp)
 #define TDC_LA2(MODE, NZV)                                                                    \
   if (one) {                                                                                  \
-    if (Xr && A8 && B8) TDC_LA(MODE, NZV, DP >= 64, DP >= 64, DP >= 64, DP >= 64);            \
-    else if (Xr) TDC_LA(MODE, NZV, DP >= 64, DP >= 64, DP >= 64, false);                      \
-    else TDC_LA(MODE, NZV, DP >= 64, DP >= 64, false, false);                                 \
+    if (Xr) TDC_LA(MODE, NZV, DP >= 64, DP >= 64, DP >= 64);                                  \
+    else TDC_LA(MODE, NZV, DP >= 64, DP >= 64, false);                                        \
   } else if (Xr && DP >= 64) {                                                                \
-    TDC_LA(MODE, NZV, false, false, DP >= 64, false);                                         \
+    TDC_LA(MODE, NZV, false, false, DP >= 64);                                                \
   } else {                                                                                    \
-    TDC_LA(MODE, NZV, false, false, false, false);                                            \
+    TDC_LA(MODE, NZV, false, false, false);                                                   \
   }
   if (m == 2.0) {
     if (nz) { TDC_LA2(2, true) } else { TDC_LA2(2, false) }
@@ -1614,12 +1508,12 @@ using namespace tdc;
 
 int tdc_fcm_split_rows(const float* src, int64_t rows, int64_t valid, int d, int64_t ld, int DP,
                        int neg2, const float* shift, void* hi, void* lo, float* norm,
-                       void* f8, hipStream_t s) {
+                       hipStream_t s) {
   if (rows <= 0) return 0;
   int64_t blocks = (rows + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(split_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, s, src, rows, valid,
-                     d, ld, DP, neg2, shift, (__bf16*)hi, (__bf16*)lo, norm, (unsigned char*)f8);
+                     d, ld, DP, neg2, shift, (__bf16*)hi, (__bf16*)lo, norm);
   TDC_CHECK_LAUNCH();
   return 0;
 }
@@ -1689,8 +1583,7 @@ int64_t tdc_fcm_mfma_workspace(int64_t N, int K, int Kp, int DP, int num_cus) {
 int64_t tdc_fcm_mfma_rowinfo_len(int64_t N, int DP) {
   return DP >= 64 ? ((N + 3) / 4) * 4 + 4 * N : N;
 }
-int tdc_fcm_mfma(int pass, const void* Xh, const void* Xl, const void* Xr, const void* A8,
-                 const void* B8, const float* xx,
+int tdc_fcm_mfma(int pass, const void* Xh, const void* Xl, const void* Xr, const float* xx,
                  int64_t N, int DP, int D, const void* Ch, const void* Cl, const float* cc, int K,
                  int Kp, double m, int nan_to_zero, int32_t* labels, float* rowinfo,
                  int64_t rowinfo_len, double* wx, double* ws, float* work, const float* shift,
@@ -1708,7 +1601,7 @@ int tdc_fcm_mfma(int pass, const void* Xh, const void* Xl, const void* Xr, const
     if (pass == 0)                                                                            \
       return launch_mstats<DPV>(Xh, Xl, xx, N, Ch, Cl, cc, K, Kp, m, nan_to_zero, labels,     \
                                 rowinfo, fix, s);                                             \
-    return launch_maccum<DPV>(Xh, Xl, Xr, A8, B8, xx, rowinfo, fix, N, Ch, Cl, cc, K, Kp, D, m, \
+    return launch_maccum<DPV>(Xh, Xl, Xr, xx, rowinfo, fix, N, Ch, Cl, cc, K, Kp, D, m,       \
                               nan_to_zero, work, shift, wx, ws, num_cus, s);                  \
   }
   TDC_FM(32)

@@ -144,7 +144,7 @@ int tdc_fcm_wide(int pass, int dtype, const void* X, int64_t M, int64_t ldx, int
 // shift (nullable, fp32 [d]) is subtracted from every row first.
 int tdc_fcm_split_rows(const float* src, int64_t rows, int64_t valid, int d, int64_t ld, int DP,
                        int neg2, const float* shift, void* hi, void* lo, float* norm,
-                       void* f8, hipStream_t stream);
+                       hipStream_t stream);
 // work: fp32 [tdc_fcm_mfma_workspace(...)] per-block partial slabs of pass 1; shift
 // (nullable, fp32 [D]): the vector subtracted from rows and centroids at the split, added
 // back as shift * sum w in the reduction.
@@ -153,10 +153,7 @@ int tdc_fcm_split_rows(const float* src, int64_t rows, int64_t valid, int d, int
 // aligned float4 {d2a, d2b, la, lb}); with them pass 1 runs one-product distances.
 // Xr (nullable, pass 1 with the fix-up rows): the shard's own bf16 rows [N, DP], unshifted,
 // zero padded -- W^T X then takes them as its one operand (bf16 data only: exact products).
-// A8 / B8 (nullable, with Xr): the fp8 cross-term operands of fcm_split_rows' f8 output
-// (rows / centroids, 2 DP bytes each) -- pass 1 then adds xl.ch + xh.cl on the fp8 cores.
-int tdc_fcm_mfma(int pass, const void* Xh, const void* Xl, const void* Xr, const void* A8,
-                 const void* B8, const float* xx,
+int tdc_fcm_mfma(int pass, const void* Xh, const void* Xl, const void* Xr, const float* xx,
                  int64_t N, int DP, int D, const void* Ch, const void* Cl, const float* cc, int K,
                  int Kp, double m, int nan_to_zero, int32_t* labels, float* rowinfo,
                  int64_t rowinfo_len, double* wx, double* ws, float* work, const float* shift,

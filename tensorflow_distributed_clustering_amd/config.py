@@ -21,7 +21,7 @@ ALGORITHMS = ("lloyd", "bounded")
 COMM_MODES = ("auto", "allreduce", "rsag")
 UPDATE_MODES = ("auto", "full", "delta")
 EXACT_ASSIGN = ("auto", "mfma", "simt")
-FCM_DISTANCES = ("one", "x3", "f8x")
+FCM_DISTANCES = ("one", "x3")
 
 
 @dataclass(frozen=True)
@@ -48,8 +48,7 @@ class ClusterConfig:
                     corrected to bf16x3 (0.87x the step at fcm10m, but at a random-row
                     init on that data the centroid error against the fp64 oracle is
                     9.4e-3 ('one') vs 9.0e-4 ('x3') of max|c|, profiles/bench_fcm10m_*_r05h;
-                    the stats pass runs one product + fix-up either way); 'f8x' adds
-                    the cross terms to 'one' on the fp8 matrix cores (bf16 shards).
+                    the stats pass runs one product + fix-up either way).
     empty_cluster   'keep' (default) | 'nan' (globally empty -> NaN, the segment-sum
                     notebook) | 'nan_any' (empty on ANY rank -> NaN, the script's
                     reduce_mean poisoning) | 'reseed' | 'zero'

@@ -1260,7 +1260,7 @@ class HipMfmaFCM(_LocalOpsBase):
         self.ch = torch.zeros(self.kp, self.dp, dtype=torch.bfloat16, device=dev)
         self.cl = torch.zeros_like(self.ch)
         self.cc = torch.zeros(self.kp, dtype=torch.float32, device=dev)
-        self.xh = self.xl = self.xx = self.rowinfo = self.xr = self.a8 = self.b8 = None
+        self.xh = self.xl = self.xx = self.rowinfo = self.xr = None
         self.work = self.mu = None
         self._set_x(x)
 
@@ -1300,15 +1300,8 @@ class HipMfmaFCM(_LocalOpsBase):
         ril = self._ri_len(n)
         if self.rowinfo is None or self.rowinfo.numel() < ril:
             self.rowinfo = torch.empty(ril, dtype=torch.float32, device=self.device)
-        f8 = None
-        if self._xraw is not None and self._use_f8x():
-            if getattr(self, "a8", None) is None or self.a8.shape[0] < n:
-                self.a8 = torch.empty(n, 2 * self.dp, dtype=torch.uint8, device=self.device)
-            f8 = self.a8[:n]
-        else:
-            self.a8 = None
         self.ops.fcm_split_rows(self._xsrc[:, : self.d], n, 0, self.xh[:n], self.xl[:n],
-                                self.xx[:n], self.mu, f8)
+                                self.xx[:n], self.mu)
         self._xsrc = None  # the hi/lo rows are the shard from here on
         self.xr = None
         if self._xraw is not None and self._use_raw():
@@ -1333,12 +1326,7 @@ class HipMfmaFCM(_LocalOpsBase):
             # fixed shift: distances are shift-invariant and the expansion's cancellation
             # error scales with |x - mu|^2 instead of |x|^2
             self.mu = Cf.double().mean(0).float()
-        b8 = None
-        if self._use_f8x():
-            if getattr(self, "b8", None) is None:
-                self.b8 = torch.empty(self.kp, 2 * self.dp, dtype=torch.uint8, device=self.device)
-            b8 = self.b8
-        self.ops.fcm_split_rows(Cf, self.k, 1, self.ch, self.cl, self.cc, self.mu, b8)
+        self.ops.fcm_split_rows(Cf, self.k, 1, self.ch, self.cl, self.cc, self.mu)
         if self._dirty:
             self._split_x()
 
@@ -1346,24 +1334,18 @@ class HipMfmaFCM(_LocalOpsBase):
         n = self.n
         return self.xh[:n], self.xl[:n], self.xx[:n]
 
-    # one-product accumulate (ClusterConfig.fcm_distances = 'one' / 'f8x'); off: bf16x3
+    # one-product accumulate (ClusterConfig.fcm_distances = 'one'); off: bf16x3 distances
     one_product = False
     raw_rows = True     # class switch: bf16 shards feed W^T X as they are (one product)
-    f8_cross = False    # + the cross terms on the fp8 cores ('f8x'; bf16 shards, D >= 64)
 
     def _use_raw(self):
         return self.raw_rows and self.dp >= 64
-
-    def _use_f8x(self):
-        return self.f8_cross and self.one_product and self._use_raw()
 
     @property
     def precision(self) -> str:
         """What the step computes, in words (bench.py reports it)."""
         raw = getattr(self, "xr", None) is not None
         if self.one_product and self.dp >= 64:
-            if raw and getattr(self, "a8", None) is not None:
-                return FCM_PRECISION["bf16_one_f8x"]
             return FCM_PRECISION["bf16_one_raw" if raw else "bf16_one"]
         return FCM_PRECISION["bf16_raw" if raw else "bf16"]
 
@@ -1379,11 +1361,8 @@ class HipMfmaFCM(_LocalOpsBase):
         self.ops.fcm_mfma_stats(xh, xl, xx, self.ch, self.cl, self.cc, self.k, self.m,
                                 self.nan_to_zero, labels, ri)
         xr = self.xr[: self.n] if self.xr is not None else None
-        a8 = b8 = None
-        if xr is not None and getattr(self, "a8", None) is not None and self._use_f8x():
-            a8, b8 = self.a8[: self.n], self.b8
         self.ops.fcm_mfma_accum(xh, xl, xx, ri, self.ch, self.cl, self.cc, self.k, self.m,
-                                self.nan_to_zero, wx, ws, self._work(), self.mu, xr, a8, b8)
+                                self.nan_to_zero, wx, ws, self._work(), self.mu, xr)
 
     def assign(self, C, labels):
         self.prepare(C)
@@ -1527,12 +1506,6 @@ FCM_PRECISION = {
                 "on x.c) for every centroid, each row's two nearest corrected to bf16x3 "
                 "(fp32-faithful); fp32 memberships, bf16 weights in the W^T X MFMAs (hi+lo "
                 "rows), fp64 sums",
-    # ... + the cross terms x_lo.c_hi + x_hi.c_lo on the fp8 cores
-    "bf16_one_f8x": "bf16 MFMA distances: x_hi . c_hi (bf16) + x_lo . c_hi + x_hi . c_lo "
-                    "(fp8 e4m3 operands, 2^8-scaled lo halves, exact E8M0 rescale; ~2^-13/"
-                    "sqrt(D) relative error on x.c), each row's two nearest corrected to "
-                    "bf16x3; fp32 memberships; W^T X = bf16 weights x the bf16 rows (exact "
-                    "products), fp64 sums",
     # ... on a bf16 shard: W^T X takes the bf16 rows themselves (exact products)
     "bf16_one_raw": "bf16 MFMA distances: one product (x_hi . c_hi, ~2^-9/sqrt(D) relative "
                     "error on x.c) for every centroid, each row's two nearest corrected to "
@@ -1564,8 +1537,7 @@ def make_fcm_ops(x: torch.Tensor, k: int, dtype: str = "fp64", m: float = 2.0,
     if mfma and d > 16 and k >= FCM_MFMA_MIN_K:
         if fcm_mfma_dim(d) is not None:
             ops = HipMfmaFCM(x, k, m, nan_to_zero)
-            ops.one_product = distances != "x3"
-            ops.f8_cross = distances == "f8x"
+            ops.one_product = distances == "one"
             return ops
         if fcm_mfma_wide_dim(d) is not None:
             return HipMfmaWideFCM(x, k, m, nan_to_zero)

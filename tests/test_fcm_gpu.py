@@ -401,24 +401,3 @@ def test_fcm_mfma_bf16x3_raw_wtx(gpu, k, d, nz):
     c1, c2 = wx1 / ws1.clamp_min(1e-300)[:, None], wx2 / ws2.clamp_min(1e-300)[:, None]
     assert bool(((c1 - c2).abs() <= 1e-5 * (1 + c2.abs()))[ok].all())
 
-
-@pytest.mark.parametrize("k,d", [(1024, 128), (257, 64), (300, 100)])
-@pytest.mark.parametrize("m", [2.0, 3.0])
-@pytest.mark.parametrize("nz", [True, False])
-def test_fcm_mfma_f8x_matches_oracle(gpu, k, d, m, nz):
-    """fcm_distances='f8x' on a bf16 shard: one bf16 product + the cross terms on the fp8
-    cores (2^8-scaled lo halves, E8M0 rescale) + the two-nearest fix-up -- held to the
-    bf16x3 tolerance of the oracle tests (2e-3 m), unlike 'one'."""
-    from tensorflow_distributed_clustering_amd.ops import FCM_PRECISION, make_fcm_ops
-    n = 20001
-    x, c = _data(n, k, d, 19 * k + d)
-    xb = x.to(torch.bfloat16)
-    c[min(3, k - 1)] = xb[7].double()
-    xg, cg = xb.to(gpu), c.float().to(gpu)
-    ops = make_fcm_ops(xg, k, "bf16", m, nz, "auto", "f8x")
-    lab = torch.empty(n, dtype=torch.int32, device=gpu)
-    wx = torch.zeros(k, d, dtype=torch.float64, device=gpu)
-    ws = torch.zeros(k, dtype=torch.float64, device=gpu)
-    ops.step(cg, lab, wx, ws)
-    assert ops.precision == FCM_PRECISION["bf16_one_f8x"]
-    _check(wx.cpu(), ws.cpu(), lab, xb.double(), cg.cpu(), m, nz, 2e-3 * m, 0.998)
