@@ -288,8 +288,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats1_kernel(
   constexpr int KS = DP / 16;
   constexpr int HALF = DP / 2;
   constexpr int IMGB = BN * DP * 2;           // bytes of one hi stage image
-  __shared__ __attribute__((aligned(16))) char s_c[2][IMGB];
-  __shared__ __attribute__((aligned(16))) float s_n[2][BN];
+  // stage ring: a stage's compute (~1K cycles per SIMD) is shorter than its DMA's latency
+  // from L2 under load, so stage t + NSTS - 1 is issued while stage t computes (with two
+  // slots the pass waited out every stage: ~4.8K cycles per 64-centroid stage, SQ_WAIT_ANY
+  // 26 % + SQ_WAIT_INST_ANY 39 % of wave cycles, profiles/pmc_fcm10m_one_vs_x3_r05h.txt)
+  constexpr int NSTS = 4;
+  __shared__ __attribute__((aligned(16))) char s_c[NSTS][IMGB];
+  __shared__ __attribute__((aligned(16))) float s_n[NSTS][BN];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
@@ -333,7 +338,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats1_kernel(
                       "s"(uniform_ptr(base))
                    : "memory", "m0");
     }
-    if (wu == 0 && lane < BN / 4) {
+    // every wave loads the stage's norms (identical bytes to the same slot), so every wave
+    // issues PPW + 1 DMAs per stage and the ring's vmcnt waits are exact for all of them
+    if (lane < BN / 4) {
       const float* nb = cc + (int64_t)T * BN;
       const unsigned nd = lds_n + B * BN * 4;
       asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
@@ -341,8 +348,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats1_kernel(
                       "s"(uniform_ptr(nb)) : "memory", "m0");
     }
   };
-  stage_load(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  constexpr int VPS = PPW + 1;
+  // (stages past the end reload the last one into a free slot: uniform DMA counts)
+#pragma unroll
+  for (int t = 0; t < NSTS - 1; ++t) stage_load(t < nstages ? t : nstages - 1, t);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NSTS - 2) * VPS) : "memory");  // stage 0 landed
   __syncthreads();
 
   // keys: the tagged d2 bits compared as int32 (no canonicalising v_max per v_min_f32; all
@@ -456,8 +466,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats1_kernel(
 
   f32x16 acc0, acc1;
   for (int t = 0; t < nstages; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < nstages) stage_load(t + 1, buf ^ 1);
+    const int buf = t % NSTS;
+    {
+      // slot (t + NSTS - 1) % NSTS was last read in stage t - 1, before its barrier
+      const int tn = t + NSTS - 1;
+      stage_load(tn < nstages ? tn : nstages - 1, tn % NSTS);
+    }
     const char* cb = s_c[buf];
     const float* ns = s_n[buf];
     bf16x8 ah0[KS], ah1[KS];
@@ -476,9 +490,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats1_kernel(
       phase(acc1, 1, ah1, ns, acc0, 0, WITHOUT{});
       epi(acc0, 0, t);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NSTS - 2) * VPS) : "memory");  // stage t + 1 landed
     __syncthreads();
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   {
     const bf16x8* sl = reinterpret_cast<const bf16x8*>(Xl + row * DP + h * HALF);
 #pragma unroll
@@ -610,13 +625,22 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
   static_assert(!ONE || WAVES == 8, "one-product form: 8 waves");
   // tile images: xh, then xl (bf16x3 distances, or W^T X's lo operand), then xr (RAW)
   constexpr int NIMG = (RAW && !ONE) ? 3 : 2;
-  constexpr int NBUF = STAG ? 3 : 2;
+  // STAG: a 4-slot tile ring with two tiles in flight (tile it + 2 loads while tile it
+  // computes and tile it - 1 finishes its lagging W^T X): one interval's work (~1.8K cycles
+  // per SIMD) is shorter than a 32-KB tile's DMA latency under load.  The row statistics
+  // then arrive by LDS-DMA too (no register staging to wait on), the zero floor is taken
+  // of xx in the membership step, and a partial last tile's padded rows are patched in LDS
+  // after their DMA lands.
+  constexpr int NBUF = STAG ? 4 : 2;
   constexpr int SXB = NBUF * NIMG * IMG;
-  // row statistics per tile row: xx, 1/S, the zero floor 2^-16 xx (+ d2a, d2b, la, lb)
-  constexpr int NRS = ONE ? 7 : 3;
+  // row statistics per tile row: xx, 1/S, (non-STAG: the zero floor 2^-16 xx,) + (ONE)
+  // d2a, d2b, la, lb
+  constexpr int RSF = STAG ? 2 : 3;       // index of d2a
+  constexpr int NRS = ONE ? RSF + 4 : 3;
   __shared__ __attribute__((aligned(16))) char s_xf[SXB];
 #define s_x(B_) (s_xf + (B_) * NIMG * IMG)
   __shared__ __attribute__((aligned(16))) float s_rs[NBUF][NRS][TP];
+  __shared__ __attribute__((aligned(16))) float s_rsdummy[STAG ? TP : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
@@ -673,6 +697,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     pcol[i] = (unsigned)(xoff<DP>(prow[i], q % CPR) - prow[i] * DP * 2);  // = source chunk
   }
   const unsigned lds_x = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)&s_xf[0];
+  const unsigned lds_rs = (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)&s_rs[0][0][0];
+  const unsigned lds_dummy = (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)&s_rsdummy[0];
   float pv = 0.f;
 #define TDC_TILE_LOAD(R0_, B_)                                                            \
   {                                                                                       \
@@ -699,12 +725,56 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
       else pv = gr < b ? fix[gr * 4 + (w - 3)] : (w >= 5 ? __int_as_float(-1) : 0.f);     \
     }                                                                                     \
   }
+  // STAG: images and statistics of one tile by LDS-DMA, VPS = PPW + 1 per wave: wave w < NRS
+  // brings statistic w of the 64 rows (rows past the range clamped, patched later); the
+  // others a dummy copy into scratch, so every wave's vmcnt count is the same
+  constexpr int VPS = PPW + 1;
+#define TDC_TILE_DMA(R0_, B_)                                                             \
+  {                                                                                       \
+    const int last_ = (int)(b - 1 - (R0_));                                               \
+    _Pragma("unroll") for (int i = 0; i < PPW; ++i) {                                     \
+      const int pc_ = wu * PPW + i;                                                       \
+      const int im_ = pc_ / PPI;                                                          \
+      const __bf16* base_ = (im_ == 0 ? Xh : (im_ == 1 ? Xl : Xr)) + (R0_) * DP;          \
+      const int rr_ = prow[i] < last_ ? prow[i] : last_;                                  \
+      const unsigned dst_ = lds_x + (B_) * NIMG * IMG + im_ * IMG + (pc_ % PPI) * 1024;   \
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"                  \
+                   :: "s"(__builtin_amdgcn_readfirstlane(dst_)),                          \
+                      "v"((unsigned)(rr_ * DP * 2) + pcol[i]), "s"(uniform_ptr(base_))    \
+                   : "memory", "m0");                                                     \
+    }                                                                                     \
+    {                                                                                     \
+      const int st_ = wu < NRS ? wu : wu - NRS;                                           \
+      const int lr_ = lane < last_ ? lane : last_;                                        \
+      const float* sb_ = st_ == 0 ? xx + (R0_) : st_ == 1 ? rowinfo + (R0_)               \
+                                                          : fix + (R0_) * 4 + (st_ - RSF); \
+      const unsigned so_ = st_ < RSF ? (unsigned)lr_ * 4u : (unsigned)lr_ * 16u;           \
+      const unsigned sd_ = wu < NRS ? lds_rs + ((B_) * NRS + wu) * TP * 4 : lds_dummy;    \
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, %2"                    \
+                   :: "s"(__builtin_amdgcn_readfirstlane(sd_)), "v"(so_),                 \
+                      "s"(uniform_ptr(sb_)) : "memory", "m0");                            \
+    }                                                                                     \
+  }
+  // rows of a partial tile past the range: a huge norm keeps t finite (rcp(0) * info 0
+  // would be NaN), no fix-up centroid (after this wave's own statistics DMA landed)
+#define TDC_TILE_PATCH(R0_, B_)                                                           \
+  if ((R0_) + TP > b && w < NRS) {                                                        \
+    const int valid_ = (int)(b - (R0_));                                                  \
+    if (lane >= valid_)                                                                   \
+      s_rs[B_][w][lane] = w == 0 ? 1.0e30f : (w >= RSF + 2 ? __int_as_float(-1) : 0.f);   \
+  }
 #define TDC_TILE_STORE(B_)                                                                \
   {                                                                                       \
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                      \
     if (tid < NRS * TP) s_rs[B_][w][lane] = pv;                                          \
   }
-  if (a < b) {
+  if constexpr (STAG) {
+    // tiles 0 and 1 in flight, wait for tile 0 (every block has >= 1 tile: a < b)
+    TDC_TILE_DMA(a, 0)
+    TDC_TILE_DMA(a + TP < b ? a + TP : a, 1)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VPS) : "memory");
+    TDC_TILE_PATCH(a, 0)
+  } else if (a < b) {
     TDC_TILE_LOAD(a, 0)
     TDC_TILE_STORE(0)
   }
@@ -831,14 +901,16 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     const int pt = (SUB) * 32 + 8 * g4 + 4 * h;                                           \
     const f32x4 xq4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][0][pt]);                  \
     const f32x4 iq4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][1][pt]);                  \
-    const f32x4 zf4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][2][pt]);                  \
+    f32x4 zf4;                                                                            \
+    if constexpr (STAG) zf4 = xq4 * ZERO_FLOOR;                                           \
+    else zf4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][2][pt]);                         \
     f32x4 da4, db4;                                                                       \
     i32x4 la4, lb4;                                                                       \
     if constexpr (ONE) {                                                                  \
-      da4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][3][pt]);                            \
-      db4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][4][pt]);                            \
-      la4 = *reinterpret_cast<const i32x4*>(&s_rs[B_][5][pt]);                            \
-      lb4 = *reinterpret_cast<const i32x4*>(&s_rs[B_][6][pt]);                            \
+      da4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][RSF][pt]);                          \
+      db4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][RSF + 1][pt]);                      \
+      la4 = *reinterpret_cast<const i32x4*>(&s_rs[B_][RSF + 2][pt]);                      \
+      lb4 = *reinterpret_cast<const i32x4*>(&s_rs[B_][RSF + 3][pt]);                      \
     }                                                                                     \
     _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                       \
       const int i = 4 * g4 + e;                                                           \
@@ -864,19 +936,21 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     }                                                                                     \
   }
   if constexpr (STAG) {
-    // interval it: tile it is in buffer it % 3 (loaded during interval it - 1), tile it + 1
-    // loads into the next buffer, tile it - 1 (the lagging waves' memberships and W^T X)
-    // stays in the previous one
+    // interval it: tile it in slot it % 4 (landed at the end of interval it - 1), tile
+    // it - 1 (the lagging waves' memberships and W^T X) in slot (it + 3) % 4, tile it + 1
+    // landing, tile it + 2 loading into the slot tile it - 2 left
     const int sub = w >> 2;
     const int64_t ntile = (b - a + TP - 1) / TP;
     f32x16 acc0;
     bf16x8 wh0[2];
-    int bc = 0;
     for (int64_t it = 0; it <= ntile; ++it) {
-      const bool cur = it < ntile, more = it + 1 < ntile;
-      const int bn = bc == 2 ? 0 : bc + 1, bp = bc == 0 ? 2 : bc - 1;
-      if (more) TDC_TILE_LOAD(a + (it + 1) * TP, bn)
-      // image pointers of tile it (cur) and it - 1 (the lagging waves' W^T X)
+      const bool cur = it < ntile;
+      const int bc = (int)(it & 3), bp = (int)((it + 3) & 3), bl2 = (int)((it + 2) & 3);
+      {
+        // (past the end: the last tile again into the free slot -- uniform DMA counts)
+        const int64_t t2 = it + 2 < ntile ? it + 2 : ntile - 1;
+        TDC_TILE_DMA(a + t2 * TP, bl2)
+      }
       const char* xh_c = s_x(bc);
       const char* xl_c = s_x(bc) + IMG;
       const char* xw_c = s_x(bc) + (NIMG - 1) * IMG;
@@ -906,10 +980,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
           TDC_DIST(acc0, 1, TDC_NONE)
         }
       }
-      if (more) TDC_TILE_STORE(bn)
+      // tile it + 1 landed (only tile it + 2's DMAs may still be in flight)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VPS) : "memory");
+      if (it + 1 < ntile) TDC_TILE_PATCH(a + (it + 1) * TP, (int)((it + 1) & 3))
       __syncthreads();
-      bc = bn;
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the reloads past the end
+    __syncthreads();
   } else {
   int buf = 0;
   for (int64_t r0 = a; r0 < b; r0 += TP) {

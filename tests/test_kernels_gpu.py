@@ -542,18 +542,23 @@ def test_assign_exact_wide_d(gpu, dt, n, d, k):
                                atol=1e-9)
 
 
-@pytest.mark.parametrize("dtype,d,backend", [("fp64", 48, "hip_exact_tiled"),
-                                             ("fp32", 96, "hip_exact_tiled"),
-                                             ("bf16", 768, "hip_bf16_wide"),
-                                             ("bf16", 900, "hip_bf16_wide"),
-                                             ("bf16", 1100, "hip_exact_tiled")])
-def test_wide_d_lloyd_is_native(gpu, dtype, d, backend):
-    """fp64 D > 32 and fp32 D > 64 run the native exact kernels (no GEMM); bf16 runs
-    the wide MFMA kernel up to D=1024, above it the exact tiles."""
+@pytest.mark.parametrize("dtype,d,backend,exact", [("fp64", 48, "hip_x3_mfma", "auto"),
+                                                   ("fp32", 96, "hip_x3_mfma", "auto"),
+                                                   ("fp64", 48, "hip_exact_tiled", "simt"),
+                                                   ("fp32", 96, "hip_exact_tiled", "simt"),
+                                                   ("bf16", 768, "hip_bf16_wide", "auto"),
+                                                   ("bf16", 900, "hip_bf16_wide", "auto"),
+                                                   ("bf16", 1100, "hip_exact_tiled", "auto")])
+def test_wide_d_lloyd_is_native(gpu, dtype, d, backend, exact):
+    """fp64 D > 32 and fp32 D > 64 run native exact-argmin kernels (no library GEMM): the
+    bf16x3 MFMA path with its exact re-check by default, the difference-form SIMT tiles
+    with exact_assign='simt'; bf16 runs the wide MFMA kernel up to D=1024, above it the
+    exact tiles."""
     import tensorflow_distributed_clustering_amd as tdc
     from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs
     x = gaussian_blobs(20000, d, 20, seed=3, dtype=torch.float64, device=gpu)
-    r = tdc.KMeans(tdc.ClusterConfig(n_clusters=20, max_iter=3, dtype=dtype, seed=2)).fit(x).result_
+    r = tdc.KMeans(tdc.ClusterConfig(n_clusters=20, max_iter=3, dtype=dtype, seed=2,
+                                     exact_assign=exact)).fit(x).result_
     assert r.backend == backend
     mfma = backend == "hip_bf16_wide"
     # the MFMA path keeps the shard in bf16: the oracle clusters the same rounded rows
