@@ -631,16 +631,20 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
   // then arrive by LDS-DMA too (no register staging to wait on), the zero floor is taken
   // of xx in the membership step, and a partial last tile's padded rows are patched in LDS
   // after their DMA lands.
+  // (the bf16x3 8-wave form measured the same with a 3-slot ring of this kind -- 16.6 vs
+  // 16.2-16.8 ms, profiles/bench_fcm10m_x3_r05r.json.log -- and spilled 7 VGPRs: it keeps
+  // its double buffer with register-staged statistics)
+  constexpr bool RING = STAG;
   constexpr int NBUF = STAG ? 4 : 2;
   constexpr int SXB = NBUF * NIMG * IMG;
   // row statistics per tile row: xx, 1/S, (non-STAG: the zero floor 2^-16 xx,) + (ONE)
   // d2a, d2b, la, lb
-  constexpr int RSF = STAG ? 2 : 3;       // index of d2a
-  constexpr int NRS = ONE ? RSF + 4 : 3;
+  constexpr int RSF = RING ? 2 : 3;       // index of d2a
+  constexpr int NRS = ONE ? RSF + 4 : (RING ? 2 : 3);
   __shared__ __attribute__((aligned(16))) char s_xf[SXB];
 #define s_x(B_) (s_xf + (B_) * NIMG * IMG)
   __shared__ __attribute__((aligned(16))) float s_rs[NBUF][NRS][TP];
-  __shared__ __attribute__((aligned(16))) float s_rsdummy[STAG ? TP : 1];
+  __shared__ __attribute__((aligned(16))) float s_rsdummy[RING ? TP : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
@@ -744,7 +748,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
                    : "memory", "m0");                                                     \
     }                                                                                     \
     {                                                                                     \
-      const int st_ = wu < NRS ? wu : wu - NRS;                                           \
+      /* (the dummy copies re-read xx: fix is null without the one-product form) */       \
+      const int st_ = wu < NRS ? wu : 0;                                                  \
       const int lr_ = lane < last_ ? lane : last_;                                        \
       const float* sb_ = st_ == 0 ? xx + (R0_) : st_ == 1 ? rowinfo + (R0_)               \
                                                           : fix + (R0_) * 4 + (st_ - RSF); \
@@ -768,7 +773,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                      \
     if (tid < NRS * TP) s_rs[B_][w][lane] = pv;                                          \
   }
-  if constexpr (STAG) {
+  if constexpr (RING) {
     // tiles 0 and 1 in flight, wait for tile 0 (every block has >= 1 tile: a < b)
     TDC_TILE_DMA(a, 0)
     TDC_TILE_DMA(a + TP < b ? a + TP : a, 1)
@@ -902,7 +907,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     const f32x4 xq4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][0][pt]);                  \
     const f32x4 iq4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][1][pt]);                  \
     f32x4 zf4;                                                                            \
-    if constexpr (STAG) zf4 = xq4 * ZERO_FLOOR;                                           \
+    if constexpr (RING) zf4 = xq4 * ZERO_FLOOR;                                           \
     else zf4 = *reinterpret_cast<const f32x4*>(&s_rs[B_][2][pt]);                         \
     f32x4 da4, db4;                                                                       \
     i32x4 la4, lb4;                                                                       \
@@ -988,6 +993,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the reloads past the end
     __syncthreads();
   } else {
+  {
   int buf = 0;
   for (int64_t r0 = a; r0 < b; r0 += TP) {
     const bool more = r0 + TP < b;
@@ -1024,6 +1030,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_accum_kernel(
       __syncthreads();
     }
     buf ^= 1;
+  }
   }
   }
 #undef TDC_NONE
