@@ -1309,7 +1309,12 @@ class HipMfmaFCM(_LocalOpsBase):
             if self.d == self.dp and xr.is_contiguous() and self._xraw_alias:
                 self.xr = xr  # the shard itself
             else:
-                self.xr = torch.zeros(n, self.dp, dtype=torch.bfloat16, device=self.device)
+                # an owned, zero-padded copy (reused by the next streamed chunk)
+                buf = getattr(self, "_xr_buf", None)
+                if buf is None or buf.shape[0] < n:
+                    buf = self._xr_buf = torch.zeros(n, self.dp, dtype=torch.bfloat16,
+                                                     device=self.device)
+                self.xr = buf[:n]
                 self.xr[:, : self.d] = xr
         self._xraw = None
         self._dirty = False

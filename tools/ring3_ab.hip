@@ -430,6 +430,7 @@ int main(int argc, char** argv) {
   TRY("stage tags P8", var<8, 2, 4, 4>)
   TRY("stage tags P4 NST3", var<4, 3, 4, 4>)
   TRY("half-P pipeline P8", var<8, 2, 4, 8>)
+  TRY("copy P8 NST3", var<8, 3, 4, 0>)
   const double flop = 2.0 * (double)N * Kp * DP;
   for (int round = 0; round < 3; ++round) {
     const float t0 = timeit([&] { prod(b0, 0); }, reps);
@@ -438,9 +439,10 @@ int main(int argc, char** argv) {
     const float t5 = timeit([&] { prod4(b1, 0); }, reps);
     const float t6 = timeit([&] { var<4, 3, 4, 4>(b1, 0); }, reps);
     const float t7 = timeit([&] { var<8, 2, 4, 8>(b1, 0); }, reps);
+    const float t8 = timeit([&] { var<8, 3, 4, 0>(b1, 0); }, reps);
     printf("round %d: prod P8 %.3f ms (%.0f TF/s) | copy P8 %.3f | stagetag P8 %.3f | "
-           "prod P4N3 %.3f | stagetag P4N3 %.3f | half-P P8 %.3f\n",
-           round, t0, flop / t0 / 1e9, t1, t3, t5, t6, t7);
+           "prod P4N3 %.3f | stagetag P4N3 %.3f | half-P P8 %.3f | copy P8 NST3 %.3f\n",
+           round, t0, flop / t0 / 1e9, t1, t3, t5, t6, t7, t8);
     fflush(stdout);
   }
   return 0;
