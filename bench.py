@@ -375,8 +375,10 @@ def precision_of(eng, a):
             return own
         return FCM_PRECISION.get(getattr(eng, "dtype_name", a.dtype), a.dtype)
     if name == "hip_x3_mfma":
-        return (f"{a.dtype} exact-argmin labels: bf16x3 MFMA scores + exact {a.dtype} re-check "
-                f"of the rows the error bound cannot certify; {a.dtype} rows in the update")
+        pre = ("one-product bf16 MFMA prefilter certifying rows by its own bound, then "
+               if getattr(eng.local, "pre", None) is not None and eng.local.prefilter else "")
+        return (f"{a.dtype} exact-argmin labels: {pre}bf16x3 MFMA scores + exact {a.dtype} "
+                f"re-check of the rows the error bound cannot certify; {a.dtype} rows in the update")
     if a.dtype == "fp8":
         return "fp8 e4m3 block-scaled MFMA distances; sums from the bf16 rows"
     if a.dtype == "bf16":
@@ -561,6 +563,8 @@ def witness(eng, x, n_global, s, e, comm, torch, a):
         # fp32/fp64 MFMA path: rows of the last label pass re-checked exactly
         out["recheck_rows_frac"] = comm.sum_scalar(float(amb())) / max(1, n_global)
         out["rescan_rows_frac"] = comm.sum_scalar(float(eng.local.rescanned_rows())) / max(1, n_global)
+        # rows the one-product prefilter could not certify (the three-product pass's share)
+        out["x3_rows_frac"] = comm.sum_scalar(float(eng.local.prefilter_rows())) / max(1, n_global)
     if a.dtype != "fp8":
         # fp64 argmin over the kernel's own operands (bf16 rows, bf16-rounded centroids)
         out["agree_fp64_kernel_operands"] = comm.sum_scalar(agree_op) / max(1.0, tot)

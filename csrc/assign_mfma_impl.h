@@ -242,6 +242,30 @@ void assign_mfma_bf16_ring2_kernel(const __bf16* __restrict__ X, int64_t N, int6
 // ------------------------------------------------------------------------------------
 // TOP2: also track the second-smallest distance (mind2): one v_med3 + one v_min per
 // score instead of half a v_min3 (bounds-based pruning, models/bounded.py).
+//
+// cstat (TOP2 only, nullable): the one-product prefilter of the fp32 / fp64 assignment
+// (assign_x3.hip).  X is then the bf16 hi term xh of the data rows and Cm2 the hi term th of
+// t = -2c, so a score leaves out xh.(t - th) + (x - xh).t; x1_eps bounds that per row from
+// ||xh|| (x - xh <= 2^-8 |xh| componentwise, RNE) and the centroid maxima cstat, plus the
+// accumulation / norm / tag terms of the x3 bound.  A row whose gap s2 - s1 exceeds 2 eps has
+// the exact argmin as its label here; every other row gets its label with the sign bit set
+// (x3_compact_kernel lists them for the three-product kernel: appending here took one
+// same-address atomic per 16 rows and serialised the kernel's tail).
+__device__ __forceinline__ float x1_eps(float hx, const float* cstat, int KS) {
+  const float cn = cstat[0];
+  const float Hc = sqrtf(cstat[1]) * 1.0001f, Lc = sqrtf(cstat[2]) * 1.0001f;
+  constexpr float R8 = 0.00392157f;              // 2^-8 / (1 - 2^-8): |tr| <= R8 |tl|
+  const float Tc = Lc * (1.f + R8);              // ||t - th||
+  const float dx = hx * (0.00390625f + 1.5259e-5f);  // ||x - xh|| (+2^-16: fp64 -> fp32 -> bf16)
+  const float e_split = hx * Tc + dx * (Hc + Tc);
+  const float s_main = hx * Hc;
+  constexpr float U8 = 8.f * 1.1920929e-7f;      // per-MFMA accumulation (probe_mfma_acc)
+  const float e_acc = U8 * ((float)KS * cn + (float)(KS + 1) * s_main);
+  const float e_cn = 1.1920929e-7f * cn;
+  const float e_tag = 3.8146973e-6f * (cn + s_main);  // 5 tag bits: 2^-18
+  return (e_split + e_acc + e_cn + e_tag) * 1.001f + 1e-30f;
+}
+
 template <int DP, int P, int NST, int WAVES, int QT, bool TOP2 = false>
 __global__ __launch_bounds__(WAVES * 64, ((DP >= 128 && P >= 8) ? 2 : WAVES == 6 ? 3 : (WAVES % 4 == 0 ? (WAVES / 4 > 1 ? WAVES / 4 : 3) : 2)))
 void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
@@ -249,7 +273,8 @@ void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int6
                                    int ntiles, int32_t* __restrict__ labels,
                                    float* __restrict__ mind,
                                    const int32_t* __restrict__ rowidx = nullptr,
-                                   float* __restrict__ mind2 = nullptr) {
+                                   float* __restrict__ mind2 = nullptr,
+                                   const float* __restrict__ cstat = nullptr) {
   constexpr int BNL = 16 * QT;                     // centroids per stage
   constexpr int CPR = DP / 8;
   constexpr int KS = DP / 32;                      // 32-deep k-steps
@@ -293,7 +318,7 @@ void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int6
   }
   // ||x||^2 only feeds the optional min-distance output: skip its ~5 VALU per element
   // when the caller does not ask for it (uniform branch)
-  if (mind || mind2) {
+  if (mind || mind2 || (TOP2 && cstat)) {
 #pragma unroll
     for (int p = 0; p < P; ++p) {
       float s = 0.f;
@@ -425,8 +450,18 @@ void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int6
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float v = __uint_as_float((__float_as_uint(acc[p][i]) & ~EMB) | (unsigned)(q * 4 + i));
-          if constexpr (TOP2) m2[p] = __builtin_amdgcn_fmed3f(m[p], m2[p], v);  // m <= m2 kept
-          m[p] = __builtin_fminf(m[p], v);
+          if constexpr (TOP2) {
+            // m <= m2 kept.  asm: the builtins canonicalised the tagged v first (one more VALU
+            // per score: 855 -> 639 per loop trip); v is never a signalling NaN (tag bits
+            // only in normal values, NaN rows end with v2 - v1 = NaN and are flagged)
+            float r1, r2;
+            asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r2) : "v"(m[p]), "v"(m2[p]), "v"(v));
+            asm("v_min_f32 %0, %1, %2" : "=v"(r1) : "v"(m[p]), "v"(v));
+            m2[p] = r2;
+            m[p] = r1;
+          } else {
+            m[p] = __builtin_fminf(m[p], v);
+          }
         }
       }
     }
@@ -466,6 +501,12 @@ void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int6
       const bool other = (ov < v) || (ov == v && ol < lab);
       v = other ? ov : v;
       lab = other ? ol : lab;
+    }
+    if constexpr (TOP2) {
+      if (cstat) {  // uniform branch: the prefilter flags its uncertified rows
+        const float eps2 = 2.f * x1_eps(sqrtf(xn[p]) * 1.0001f, cstat, KS);
+        if (!(v2 - v > eps2)) lab |= (int)0x80000000;
+      }
     }
     const int64_t row = pbase + p * 16 + r;
     if (g == 0 && row < N) {

@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256) void x3_split_kernel(const T* __restrict__ src
 __global__ __launch_bounds__(1024) void x3_prep_kernel(const float* __restrict__ cnorm,
                                                        const float2* __restrict__ nhl, int K,
                                                        float* __restrict__ cstat,
-                                                       int* __restrict__ amb_count) {
+                                                       int* __restrict__ amb_count, int nzero) {
   __shared__ float red[3][16];
   float m = 0.f, mh = 0.f, ml = 0.f;
   for (int k = threadIdx.x; k < K; k += 1024) {
@@ -119,6 +119,7 @@ __global__ __launch_bounds__(1024) void x3_prep_kernel(const float* __restrict__
       cstat[2] = v2;
       amb_count[0] = 0;
       amb_count[1] = 0;
+      if (nzero > 2) amb_count[2] = 0;  // the prefilter's list
     }
   }
 }
@@ -207,7 +208,8 @@ __global__ __launch_bounds__(256, 2) void assign_x3_ring_kernel(
     const __bf16* __restrict__ Ch, const __bf16* __restrict__ Cl, const float* __restrict__ cnorm,
     int ntiles, const float* __restrict__ cstat, int32_t* __restrict__ labels,
     float* __restrict__ mind, int2* __restrict__ amb, int* __restrict__ ambF,
-    int* __restrict__ amb_count) {
+    int* __restrict__ amb_count, const int32_t* __restrict__ rowidx,
+    const int* __restrict__ nrows) {
   constexpr int WAVES = 4;
   constexpr int BNL = 16 * QT;                 // centroids per stage
   constexpr int CPR = DP / 8;
@@ -231,6 +233,12 @@ __global__ __launch_bounds__(256, 2) void assign_x3_ring_kernel(
   const int w = tid >> 6;
   const int r = lane & 15;
   const int g = lane >> 4;
+  // listed mode (after the one-product prefilter): point i is row rowidx[i], the count is
+  // read on the device and the workgroups past it leave before any load
+  if (nrows) {
+    N = *nrows;
+    if ((int64_t)blockIdx.x * (WAVES * P * 16) >= N) return;
+  }
   const int64_t pbase = (int64_t)blockIdx.x * (WAVES * P * 16) + (int64_t)w * (P * 16);
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
 
@@ -239,6 +247,7 @@ __global__ __launch_bounds__(256, 2) void assign_x3_ring_kernel(
   for (int p = 0; p < P; ++p) {
     int64_t row = pbase + p * 16 + r;
     if (row >= N) row = N - 1;
+    if (rowidx) row = rowidx[row];
     const __bf16* sh = Xh + row * DP + g * 8;
     const __bf16* sl = Xl + row * DP + g * 8;
 #pragma unroll
@@ -434,8 +443,9 @@ __global__ __launch_bounds__(256, 2) void assign_x3_ring_kernel(
     for (int o = 16; o <= 32; o <<= 1)
       top3_merge(v1, l1, v2, l2, v3, __shfl_xor(v1, o, 64), __shfl_xor(l1, o, 64),
                  __shfl_xor(v2, o, 64), __shfl_xor(l2, o, 64), __shfl_xor(v3, o, 64));
-    const int64_t row = pbase + p * 16 + r;
-    const bool valid = g == 0 && row < N;
+    const int64_t lrow = pbase + p * 16 + r;
+    const bool valid = g == 0 && lrow < N;
+    const int64_t row = rowidx ? (int64_t)rowidx[lrow < N ? lrow : N - 1] : lrow;
     const float eps2 = 2.f * x3_eps(sqrtf(sh) * 1.0001f, sqrtf(sl) * 1.0001f, cstat, KS);
     if (mind) {  // + ||xh + xl||^2 turns the score into a distance (uniform branch)
       float sx = 0.f;
@@ -550,17 +560,55 @@ __global__ __launch_bounds__(256) void x3_recheck_kernel(const T* __restrict__ X
   }
 }
 
+// the prefilter's flagged rows (label sign bit set) -> compact list pre (count *n): RPB rows
+// per workgroup, one ballot per 64 rows and ONE atomic per workgroup (the labels of the
+// listed rows are rewritten by the listed x3 pass)
+constexpr int X3_COMPACT_RPB = 4096;
+__global__ __launch_bounds__(256) void x3_compact_kernel(const int32_t* __restrict__ labels,
+                                                         int64_t N, int32_t* __restrict__ list,
+                                                         int* __restrict__ n) {
+  constexpr int RPW = X3_COMPACT_RPB / 4, J = RPW / 64;
+  __shared__ int s_cnt[4];
+  __shared__ int s_base;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * X3_COMPACT_RPB + (int64_t)w * RPW;
+  unsigned long long m[J];
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int64_t row = r0 + j * 64 + lane;
+    m[j] = __ballot(row < N && labels[row] < 0);
+    c += __popcll(m[j]);
+  }
+  if (lane == 0) s_cnt[w] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int t = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+    s_base = t ? atomicAdd(n, t) : 0;
+  }
+  __syncthreads();
+  int base = s_base;
+  for (int v = 0; v < w; ++v) base += s_cnt[v];
+  const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    if ((m[j] >> lane) & 1ull) list[base + __popcll(m[j] & below)] = (int)(r0 + j * 64 + lane);
+    base += __popcll(m[j]);
+  }
+}
+
 template <int DP, int P, int NST, int QT>
 int launch_x3(const void* Xh, const void* Xl, int64_t N, const void* Ch, const void* Cl,
               const float* cnorm, int Kp, const float* cstat, int32_t* labels,
-              float* mind, int2* amb, int* ambF, int* amb_count, hipStream_t s) {
+              float* mind, int2* amb, int* ambF, int* amb_count, const int32_t* rowidx,
+              const int* nrows, hipStream_t s) {
   constexpr int BNL = 16 * QT;
   if (Kp % BNL != 0) return (int)hipErrorInvalidValue;
   const int64_t per = 4 * P * 16;
   hipLaunchKernelGGL((assign_x3_ring_kernel<DP, P, NST, QT>), dim3((unsigned)((N + per - 1) / per)),
                      dim3(256), 0, s, (const __bf16*)Xh, (const __bf16*)Xl, N, (const __bf16*)Ch,
                      (const __bf16*)Cl, cnorm, Kp / BNL, cstat, labels, mind, amb, ambF,
-                     amb_count);
+                     amb_count, rowidx, nrows);
   TDC_CHECK_LAUNCH();
   return 0;
 }
@@ -591,9 +639,9 @@ int tdc_x3_split(int src_dtype, const void* src, int64_t rows, int64_t valid, in
 }
 
 int tdc_x3_prep(const float* cnorm, const float* nhl, int K, float* cstat, int* amb_count,
-                hipStream_t s) {
+                hipStream_t s, int nzero) {
   hipLaunchKernelGGL(x3_prep_kernel, dim3(1), dim3(1024), 0, s, cnorm, (const float2*)nhl, K,
-                     cstat, amb_count);
+                     cstat, amb_count, nzero);
   TDC_CHECK_LAUNCH();
   return 0;
 }
@@ -601,19 +649,52 @@ int tdc_x3_prep(const float* cnorm, const float* nhl, int K, float* cstat, int* 
 // amb: int32 [3 cap] = list2 (int2 [cap]) | listF (int32 [cap]); amb_count int32 [2]
 int tdc_assign_x3(const void* Xh, const void* Xl, int64_t N, int DP, const void* Ch, const void* Cl,
                   const float* cnorm, int Kp, const float* cstat, int32_t* labels,
-                  float* mind, int32_t* amb, int64_t cap, int* amb_count, hipStream_t s) {
+                  float* mind, int32_t* amb, int64_t cap, int* amb_count, hipStream_t s,
+                  const int32_t* rowidx, const int* nrows) {
   if (N <= 0) return 0;
   if (N >= ((int64_t)1 << 31) || cap < N) return (int)hipErrorInvalidValue;
+  if ((rowidx == nullptr) != (nrows == nullptr)) return (int)hipErrorInvalidValue;
   int2* l2 = reinterpret_cast<int2*>(amb);
   int* lf = amb + 2 * cap;
   switch (DP) {
     // LDS per stage: 2 images x 64 centroids x DP x 2 B; two workgroups (8 waves) per CU
-    case 32: return launch_x3<32, 6, 3, 4>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cstat, labels, mind, l2, lf, amb_count, s);
-    case 64: return launch_x3<64, 6, 3, 4>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cstat, labels, mind, l2, lf, amb_count, s);
-    case 128: return launch_x3<128, 4, 2, 4>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cstat, labels, mind, l2, lf, amb_count, s);
-    case 256: return launch_x3<256, 2, 2, 2>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cstat, labels, mind, l2, lf, amb_count, s);
+    case 32: return launch_x3<32, 6, 3, 4>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cstat, labels, mind, l2, lf, amb_count, rowidx, nrows, s);
+    case 64: return launch_x3<64, 6, 3, 4>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cstat, labels, mind, l2, lf, amb_count, rowidx, nrows, s);
+    case 128: return launch_x3<128, 4, 2, 4>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cstat, labels, mind, l2, lf, amb_count, rowidx, nrows, s);
+    case 256: return launch_x3<256, 2, 2, 2>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cstat, labels, mind, l2, lf, amb_count, rowidx, nrows, s);
   }
   return (int)hipErrorInvalidValue;
+}
+
+// One-product prefilter (assign_mfma_impl.h x1_eps): bf16 ring3 top-2 over (xh, th) with the
+// exact labels of the certified rows, the others flagged and then listed in pre (count in
+// *npre) by x3_compact_kernel for tdc_assign_x3's listed mode.  DP 64 / 128 / 256.
+int tdc_x3_prefilter(const void* Xh, int64_t N, int DP, const void* Ch, const float* cnorm, int Kp,
+                     const float* cstat, int32_t* labels, int32_t* pre, int* npre, hipStream_t s) {
+  if (N <= 0) return 0;
+  if (Kp % 64 != 0 || N >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
+  const __bf16* x = (const __bf16*)Xh;
+  const __bf16* c = (const __bf16*)Ch;
+  const dim3 grid((unsigned)((N + 255) / 256));
+  if (DP == 64)  // P = 4 (P = 8 spills with the top-2 registers)
+    hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<64, 4, 3, 4, 4, true>), grid, dim3(256), 0,
+                       s, x, N, (int64_t)DP, c, cnorm, Kp / 64, labels, nullptr, nullptr, nullptr,
+                       cstat);
+  else if (DP == 128)
+    hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<128, 4, 3, 4, 4, true>), grid, dim3(256), 0,
+                       s, x, N, (int64_t)DP, c, cnorm, Kp / 64, labels, nullptr, nullptr, nullptr,
+                       cstat);
+  else if (DP == 256)
+    hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<256, 4, 2, 4, 4, true>), grid, dim3(256), 0,
+                       s, x, N, (int64_t)DP, c, cnorm, Kp / 64, labels, nullptr, nullptr, nullptr,
+                       cstat);
+  else
+    return (int)hipErrorInvalidValue;
+  TDC_CHECK_LAUNCH();
+  int64_t blocks = (N + X3_COMPACT_RPB - 1) / X3_COMPACT_RPB;
+  hipLaunchKernelGGL(x3_compact_kernel, dim3((unsigned)blocks), dim3(256), 0, s, labels, N, pre, npre);
+  TDC_CHECK_LAUNCH();
+  return 0;
 }
 
 int tdc_x3_rows(const float* G, int64_t M, int K, int64_t row0, const float* xx, const float* cstat,

@@ -713,7 +713,8 @@ void x3_recheck(const at::Tensor& X, const at::Tensor& C, at::Tensor& labels, co
 void x3_assign(const at::Tensor& X, const at::Tensor& Xh, const at::Tensor& Xl, const at::Tensor& Ch,
                const at::Tensor& Cl, const at::Tensor& cnorm, const at::Tensor& cnhl,
                const at::Tensor& C, at::Tensor& labels, const std::optional<at::Tensor>& mind,
-               at::Tensor& amb, at::Tensor& cstat, at::Tensor& amb_count, bool recheck) {
+               at::Tensor& amb, at::Tensor& cstat, at::Tensor& amb_count, bool recheck,
+               const std::optional<at::Tensor>& pre) {
   check_cuda(Xh, "Xh");
   TORCH_CHECK(Xh.scalar_type() == at::kBFloat16 && Xl.scalar_type() == at::kBFloat16 &&
                   Ch.scalar_type() == at::kBFloat16 && Cl.scalar_type() == at::kBFloat16,
@@ -748,15 +749,28 @@ void x3_assign(const at::Tensor& X, const at::Tensor& Xh, const at::Tensor& Xl, 
                     C.scalar_type() == X.scalar_type() && C.is_contiguous(),
                 "tdc.x3_assign: X / C fp32 or fp64 (same dtype)");
   }
+  int32_t* pl = nullptr;
+  if (pre.has_value() && pre->defined()) {
+    TORCH_CHECK(pre->scalar_type() == at::kInt && pre->is_contiguous() && pre->numel() >= N &&
+                    amb_count.numel() >= 3 && (DP == 64 || DP == 128 || DP == 256) && md == nullptr,
+                "tdc.x3_assign: pre int32 [>= N] needs amb_count int32 [3], DP 64/128/256 and no mind");
+    pl = pre->data_ptr<int32_t>();
+  }
   const DevGuard guard(Xh.device());
   hipStream_t s = cur_stream();
   int32_t* list = amb.data_ptr<int>();
+  int* cnt = amb_count.data_ptr<int>();
   check(tdc_x3_prep(cnorm.data_ptr<float>(), cnhl.data_ptr<float>(), K, cstat.data_ptr<float>(),
-                    amb_count.data_ptr<int>(), s),
+                    cnt, s, pl ? 3 : 2),
         "x3_prep");
+  if (pl)  // one-product prefilter, then the three products over the rows it could not certify
+    check(tdc_x3_prefilter(Xh.data_ptr(), N, DP, Ch.data_ptr(), cnorm.data_ptr<float>(), Kp,
+                           cstat.data_ptr<float>(), labels.data_ptr<int32_t>(), pl, cnt + 2, s),
+          "x3_prefilter");
   check(tdc_assign_x3(Xh.data_ptr(), Xl.data_ptr(), N, DP, Ch.data_ptr(), Cl.data_ptr(),
                       cnorm.data_ptr<float>(), Kp, cstat.data_ptr<float>(),
-                      labels.data_ptr<int32_t>(), md, list, cap, amb_count.data_ptr<int>(), s),
+                      labels.data_ptr<int32_t>(), md, list, cap, cnt, s, pl,
+                      pl ? cnt + 2 : nullptr),
         "assign_x3");
   if (recheck)
     check(tdc_x3_recheck(dcode(X.scalar_type()), X.data_ptr(), X.stride(0), (int)C.size(1), C.data_ptr(),
@@ -1177,7 +1191,7 @@ TORCH_LIBRARY(tdc, m) {
   m.def("sculley_update(Tensor sums, Tensor counts, Tensor(a!) C, Tensor(b!) v, Tensor(c!)? shift, Tensor(d!)? Cm2, Tensor(e!)? cnorm) -> ()");
   m.def("x3_split(Tensor src, int valid, int neg2, Tensor(a!) hi, Tensor(b!) lo, Tensor(c!)? norm, Tensor(d!)? nhl=None) -> ()");
   m.def("x3_prep(Tensor cnorm, Tensor? nhl, int K, Tensor(a!) cstat, Tensor(b!) amb_count) -> ()");
-  m.def("x3_assign(Tensor X, Tensor Xh, Tensor Xl, Tensor Ch, Tensor Cl, Tensor cnorm, Tensor cnhl, Tensor C, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!) amb, Tensor(d!) cstat, Tensor(e!) amb_count, bool recheck=True) -> ()");
+  m.def("x3_assign(Tensor X, Tensor Xh, Tensor Xl, Tensor Ch, Tensor Cl, Tensor cnorm, Tensor cnhl, Tensor C, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!) amb, Tensor(d!) cstat, Tensor(e!) amb_count, bool recheck=True, Tensor(f!)? pre=None) -> ()");
   m.def("x3_rows(Tensor G, int row0, Tensor xx, Tensor cstat, int DP, Tensor(a!) labels, Tensor(b!) amb, Tensor(c!) amb_count) -> ()");
   m.def("x3_recheck(Tensor X, Tensor C, Tensor(a!) labels, Tensor amb, Tensor amb_count) -> ()");
 }

@@ -55,14 +55,22 @@ int tdc_bounds_scatter(const int32_t* active, const int* count, int64_t cap,
 //   assign (DP in 32/64/128/256, Kp % 64 == 0 -- % 32 at DP 256): labels, optional mind;
 //   rows  (wide D): top-3 over a chunk's raw d2 block G [M, K] (tdc_fcm_mfma_wide pass 1),
 //          xx [M] = ||x||^2, list rows offset by row0;
-//   recheck: exact difference form in the data's dtype (X/C both f32 or f64, D <= 1024).
+//   recheck: exact difference form in the data's dtype (X/C both f32 or f64, D <= 1024);
+//   prefilter (DP 64/128/256): one bf16 product (xh . th) with top-2 and a per-row bound:
+//          labels of the certified rows, the others listed in pre (count *npre, zeroed by
+//          prep with nzero = 3 into amb_count[2]) for assign's listed mode (rowidx / nrows:
+//          point i is row rowidx[i], count read on the device; grid sized by N).
 int tdc_x3_split(int src_dtype, const void* src, int64_t rows, int64_t valid, int d, int64_t ld,
                  int DP, int neg2, void* hi, void* lo, float* norm, float* nhl, hipStream_t stream);
 int tdc_x3_prep(const float* cnorm, const float* nhl, int K, float* cstat, int* amb_count,
-                hipStream_t stream);
+                hipStream_t stream, int nzero = 2);
+int tdc_x3_prefilter(const void* Xh, int64_t N, int DP, const void* Ch, const float* cnorm, int Kp,
+                     const float* cstat, int32_t* labels, int32_t* pre, int* npre,
+                     hipStream_t stream);
 int tdc_assign_x3(const void* Xh, const void* Xl, int64_t N, int DP, const void* Ch, const void* Cl,
                   const float* cnorm, int Kp, const float* cstat, int32_t* labels,
-                  float* mind, int32_t* amb, int64_t cap, int* amb_count, hipStream_t stream);
+                  float* mind, int32_t* amb, int64_t cap, int* amb_count, hipStream_t stream,
+                  const int32_t* rowidx = nullptr, const int* nrows = nullptr);
 int tdc_x3_rows(const float* G, int64_t M, int K, int64_t row0, const float* xx, const float* cstat,
                 int DP, int32_t* labels, int32_t* amb, int64_t cap, int* amb_count,
                 hipStream_t stream);

@@ -405,6 +405,10 @@ __device__ __forceinline__ f32x2 pk_sub_hi(f32x2 xp, f32x2 c) {
 template <typename T> struct ExactCfg { static constexpr int MR = 8; };
 template <> struct ExactCfg<double> { static constexpr int MR = 4; };
 
+// A listed re-scan (rowidx / nptr below) of at most this many rows runs on
+// assign_exact_few_kernel instead: the 128-row tiles would leave all but a handful of CUs idle.
+constexpr int EXACT_FEW_MAX = 32768;
+
 // rowidx (nullable): row i of the launch is row rowidx[i] of X (and of labels / mind), with
 // the row count read from the device (nptr) -- the full re-scan of the rows the fp32/fp64
 // MFMA assignment could not certify (assign_x3.hip), sized on the device
@@ -423,7 +427,10 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(const T* __restrict__
   __shared__ __attribute__((aligned(16))) T s_c[DC][PC];
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
   constexpr bool F32 = sizeof(T) == 4;
-  if (nptr) N = *nptr;
+  if (nptr) {
+    N = *nptr;
+    if (N <= EXACT_FEW_MAX) return;  // assign_exact_few_kernel has them
+  }
   for (int64_t r0 = (int64_t)blockIdx.x * R; r0 < N; r0 += (int64_t)gridDim.x * R) {
     T best[MR];
     int bk[MR];
@@ -528,11 +535,153 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(const T* __restrict__
   }
 }
 
+// The listed re-scan when it is short (<= EXACT_FEW_MAX rows; the x3 path lists ~0.02% of N):
+// RB rows per workgroup with one centroid of each 256-centroid chunk per thread, so a few
+// thousand rows still spread over every CU (on the 128-row tiles 1.7k rows kept 14 CUs busy
+// for 0.5 ms).  Same fma chain in ascending d from 0 as assign_exact_kernel (zero padding adds
+// fma(0, 0, acc) = acc), so the distances are bit-identical; ties go to the lower index.
+template <typename T>
+__global__ __launch_bounds__(256) void assign_exact_few_kernel(const T* __restrict__ X, int64_t ldx,
+                                                               int D, const T* __restrict__ C, int K,
+                                                               int32_t* __restrict__ labels,
+                                                               T* __restrict__ mind,
+                                                               const int32_t* __restrict__ rowidx,
+                                                               const int* __restrict__ nptr) {
+  constexpr int RB = 8, KT = 256, DC = 32;
+  __shared__ __attribute__((aligned(16))) T s_x[DC][RB];
+  __shared__ T s_c[DC][KT + 1];
+  __shared__ T s_rb[4][RB];
+  __shared__ int s_rk[4][RB];
+  const int n = *nptr;
+  if (n > EXACT_FEW_MAX) return;  // assign_exact_kernel has them
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // (k0, dc) chunks in one flat sequence; the next chunk's centroid slice (16-B loads when
+  // rows allow) and row values are loaded into registers while the current one is computed
+  constexpr int VEC = 16 / (int)sizeof(T), VPR = DC / VEC, NV = KT * DC / VEC / 256;
+  typedef T vecT __attribute__((ext_vector_type(VEC)));
+  const int nd = (D + DC - 1) / DC, nchunks = nd * ((K + KT - 1) / KT);
+  const bool vec_ok = D % VEC == 0 && ((uintptr_t)C % 16) == 0;
+  vecT cv[NV];
+  T xv;
+  auto load = [&](int64_t r0, int ci) __attribute__((always_inline)) {
+    const int k0 = (ci / nd) * KT, dc = (ci % nd) * DC;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int e = tid + 256 * i, r = e / VPR, d = dc + (e % VPR) * VEC;
+      const T* src = C + (int64_t)(k0 + r) * D + d;
+      if (k0 + r < K && vec_ok && d + VEC <= D) {
+        cv[i] = *reinterpret_cast<const vecT*>(src);
+      } else {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) cv[i][j] = (k0 + r < K && d + j < D) ? src[j] : (T)0;
+      }
+    }
+    const int r = tid / DC, d = dc + tid % DC;  // RB x DC = 256 entries
+    const int64_t row = r0 + r;
+    xv = (row < n && d < D) ? X[(int64_t)rowidx[row] * ldx + d] : (T)0;
+  };
+  for (int64_t r0 = (int64_t)blockIdx.x * RB; r0 < n; r0 += (int64_t)gridDim.x * RB) {
+    T best[RB];
+    int bk[RB];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      best[i] = (T)INFINITY;
+      bk[i] = 0;
+    }
+    T acc[RB];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) acc[i] = (T)0;
+    load(r0, 0);
+    for (int ci = 0; ci < nchunks; ++ci) {
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int e = tid + 256 * i, r = e / VPR, d = (e % VPR) * VEC;
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) s_c[d + j][r] = cv[i][j];
+      }
+      s_x[tid % DC][tid / DC] = xv;
+      __syncthreads();
+      if (ci + 1 < nchunks) load(r0, ci + 1);
+#pragma unroll 4
+      for (int d = 0; d < DC; ++d) {
+        const T c = s_c[d][tid];
+#pragma unroll
+        for (int i = 0; i < RB; ++i) {
+          const T df = s_x[d][i] - c;
+          acc[i] = fma(df, df, acc[i]);
+        }
+      }
+      if (ci % nd == nd - 1) {  // a 256-centroid chunk is complete
+        const int k = (ci / nd) * KT + tid;
+        if (k < K) {
+#pragma unroll
+          for (int i = 0; i < RB; ++i)
+            if (acc[i] < best[i]) {  // ascending k per thread: strict < keeps the first
+              best[i] = acc[i];
+              bk[i] = k;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < RB; ++i) acc[i] = (T)0;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const T ob = __shfl_xor(best[i], o, 64);
+        const int ok = __shfl_xor(bk[i], o, 64);
+        if (ob < best[i] || (ob == best[i] && ok < bk[i])) {
+          best[i] = ob;
+          bk[i] = ok;
+        }
+      }
+      if (lane == 0) {
+        s_rb[w][i] = best[i];
+        s_rk[w][i] = bk[i];
+      }
+    }
+    __syncthreads();
+    if (tid < RB && r0 + tid < n) {
+      T b = s_rb[0][tid];
+      int k = s_rk[0][tid];
+#pragma unroll
+      for (int v = 1; v < 4; ++v)
+        if (s_rb[v][tid] < b || (s_rb[v][tid] == b && s_rk[v][tid] < k)) {
+          b = s_rb[v][tid];
+          k = s_rk[v][tid];
+        }
+      const int64_t orow = rowidx[r0 + tid];
+      labels[orow] = k;
+      if (mind) mind[orow] = b;
+    }
+  }
+}
+
 int tdc_assign_exact(int dtype, const void* X, int64_t N, int64_t ldx, int D, const void* C, int K,
                      int32_t* labels, void* mind, int num_cus, hipStream_t s,
                      const int32_t* rowidx, const int* nptr) {
   if (N <= 0) return 0;
-  (void)num_cus;
+  if (nptr) {
+    if (!rowidx) return (int)hipErrorInvalidValue;
+    // both launches read the listed count; exactly one of them has work
+    int64_t fb = ((N < EXACT_FEW_MAX ? N : EXACT_FEW_MAX) + 7) / 8;
+    const int64_t cap = (int64_t)(num_cus > 0 ? num_cus : 256) * 4;
+    if (fb > cap) fb = cap;
+    if (dtype == TDC_F32)
+      hipLaunchKernelGGL(assign_exact_few_kernel<float>, dim3((unsigned)fb), dim3(256), 0, s,
+                         (const float*)X, ldx, D, (const float*)C, K, labels, (float*)mind, rowidx,
+                         nptr);
+    else if (dtype == TDC_F64)
+      hipLaunchKernelGGL(assign_exact_few_kernel<double>, dim3((unsigned)fb), dim3(256), 0, s,
+                         (const double*)X, ldx, D, (const double*)C, K, labels, (double*)mind,
+                         rowidx, nptr);
+    else
+      return (int)hipErrorInvalidValue;
+    TDC_CHECK_LAUNCH();
+    if (N <= EXACT_FEW_MAX) return 0;
+  }
   const int64_t rows_per_tile = 16 * (dtype == TDC_F64 ? ExactCfg<double>::MR : ExactCfg<float>::MR);
   int64_t blocks = (N + rows_per_tile - 1) / rows_per_tile;
   // grid-stride over row tiles with the blocks resident at once (no partial 2nd round)

@@ -937,10 +937,22 @@ class HipX3Lloyd(_LocalOpsBase):
     the vector rate.  D <= 256 keeps the point fragments in registers (the ring3
     pipeline); 256 < D <= 1024 runs the bf16x3 distance GEMM into a row-chunk block and a
     top-3 row pass.  The update, the all-reduce and the finalize use the fp32 / fp64 rows
-    (NativeUpdate), as on the exact path."""
+    (NativeUpdate), as on the exact path.
+
+    ``prefilter`` (D 33..256): a one-product pass first (xh . th, the bf16 ring3 kernel with
+    top-2 and its own per-row bound, assign_mfma_impl.h x1_eps) labels every row whose gap
+    certifies its winner and lists the rest; the three products then run over the listed
+    rows only.  On clustered data most rows certify, so the step costs ~1/3 + the listed
+    share of the full x3 pass; on data where nothing certifies it would cost ~4/3, so the
+    listed count comes back to the host asynchronously (pinned copy + event, read when it
+    has landed, never waited on) and a listed share above ``PRE_MAX_FRAC`` turns the
+    prefilter off for ``PRE_RETRY`` assignments."""
     name = "hip_x3_mfma"
     chunk_elems = 1 << 27           # wide path: [rows, K] fp32 block per chunk
     max_chunk_rows = 1 << 20
+    prefilter = True
+    PRE_MAX_FRAC = 0.6   # listed share above which the one-product pass costs more than it saves
+    PRE_RETRY = 16
 
     def __init__(self, x, k, dtype="fp32", empty_cluster="keep"):
         super().__init__(x, k, empty_cluster)
@@ -957,8 +969,9 @@ class HipX3Lloyd(_LocalOpsBase):
         self.cnorm = torch.zeros(self.kp, dtype=torch.float32, device=dev)
         self.cnhl = torch.zeros(self.kp, 2, dtype=torch.float32, device=dev)  # ||th||^2, ||tl||^2
         self.cstat = torch.zeros(3, dtype=torch.float32, device=dev)  # maxima of cnorm / cnhl
-        self.amb_count = torch.zeros(2, dtype=torch.int32, device=dev)
-        self.xh = self.xl = self.xx = self.amb = self.G = None
+        # [0] two-candidate list, [1] full re-scan list, [2] the prefilter's listed rows
+        self.amb_count = torch.zeros(3, dtype=torch.int32, device=dev)
+        self.xh = self.xl = self.xx = self.amb = self.G = self.pre = None
         self.x = None
         self._set_x(x)
         self.update = NativeUpdate(self.ops, self.n, k, self.d, self.c_dtype, dev)
@@ -974,6 +987,8 @@ class HipX3Lloyd(_LocalOpsBase):
             self.xx = torch.empty(max(n, 1), dtype=torch.float32, device=dev) if self.wide else None
             # re-check lists: int2 {row, runner-up} entries | full re-scan rows
             self.amb = torch.empty(3 * max(n, 1), dtype=torch.int32, device=dev)
+            self.pre = (torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+                        if self.dp in (64, 128, 256) else None)
         self.x = x
         self.n = n
         if n:
@@ -1008,8 +1023,17 @@ class HipX3Lloyd(_LocalOpsBase):
         Cx = C if (C.dtype == self.c_dtype and C.is_contiguous()) else C.to(self.c_dtype).contiguous()
         amb = self.amb[: 3 * n]  # the lists' layout follows their capacity: n rows
         if not self.wide:
+            pre = self.pre if self._want_prefilter() else None
+            self._pre_ran = pre is not None
             self.ops.x3_assign(self.x, self.xh[:n], self.xl[:n], self.ch, self.cl, self.cnorm,
-                               self.cnhl, Cx, labels, None, amb, self.cstat, self.amb_count, True)
+                               self.cnhl, Cx, labels, None, amb, self.cstat, self.amb_count, True,
+                               pre)
+            if pre is not None and self._pre_ev is None and \
+                    not torch.cuda.is_current_stream_capturing():
+                self._pre_host.copy_(self.amb_count[2:3], non_blocking=True)
+                self._pre_ev = torch.cuda.Event()
+                self._pre_ev.record()
+                self._pre_n = n
         else:
             self.ops.x3_prep(self.cnorm, self.cnhl, self.k, self.cstat, self.amb_count)
             rows = self._chunk_rows()
@@ -1024,9 +1048,33 @@ class HipX3Lloyd(_LocalOpsBase):
         if mind is not None:
             _exact_mind(self.x, C, labels, mind, self.d)
 
+    def _want_prefilter(self) -> bool:
+        if not self.prefilter or self.pre is None:
+            return False
+        if not hasattr(self, "_pre_ev"):
+            self._pre_ev, self._pre_off, self._pre_n = None, 0, 0
+            self._pre_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        if torch.cuda.is_current_stream_capturing():
+            return self._pre_off == 0  # a captured step keeps the current choice
+        if self._pre_off > 0:
+            self._pre_off -= 1
+            return False
+        ev = self._pre_ev
+        if ev is not None and ev.query():  # the count of an earlier assignment has landed
+            self._pre_ev = None
+            if int(self._pre_host[0]) > self.PRE_MAX_FRAC * max(1, self._pre_n):
+                self._pre_off = self.PRE_RETRY - 1
+                return False
+        return True
+
     def ambiguous_rows(self) -> int:
         """Rows the last assignment re-checked exactly (host read; diagnostics)."""
-        return int(self.amb_count.sum().item())
+        return int(self.amb_count[:2].sum().item())
+
+    def prefilter_rows(self) -> int:
+        """Rows the last assignment's one-product prefilter left to the three-product pass
+        (0 when the prefilter did not run; host read; diagnostics)."""
+        return int(self.amb_count[2].item()) if getattr(self, "_pre_ran", False) else 0
 
     def rescanned_rows(self) -> int:
         """... of which re-scanned over all K (a third candidate within the bound)."""
@@ -1059,10 +1107,11 @@ def lloyd_row_extra(dtype: str, d: int, delta: bool = True) -> int:
     """Device bytes per row a Lloyd shard holds besides its layout row (the HBM planner's
     per_row_extra): labels + min distances + the sorted update's permutation (16), the delta
     update's prev / moved-list / event permutation (20), and on the fp32 / fp64 MFMA path
-    the bf16 hi/lo rows (4 x padded D) + the re-check list entry (8)."""
+    the bf16 hi/lo rows (4 x padded D) + the re-check list entries (12) + the prefilter's
+    list entry (4)."""
     extra = 16 + (20 if delta else 0)
     if dtype in ("fp32", "fp64") and d > X3_MIN_D and x3_dim(d) is not None:
-        extra += 4 * x3_dim(d) + 8
+        extra += 4 * x3_dim(d) + 16
     return extra
 
 

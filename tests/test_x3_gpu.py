@@ -195,3 +195,92 @@ def test_x3_streamed_and_delta(gpu):
     np.testing.assert_allclose(res.centers, st.centers, rtol=1e-5, atol=1e-5)
     full = tdc.KMeans(cfg.replace(update="full")).fit(x.to(gpu)).result_
     np.testing.assert_allclose(res.centers, full.centers, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("m", [1, 1700, 40000])
+def test_listed_rescan_matches_exact(gpu, dtype, m):
+    """The listed full re-scan (x3_recheck's listF part): short lists run on the few-rows
+    kernel (<= 32768 rows), long ones on the 128-row tiles; both give the labels of the
+    full exact tiles on the listed rows and leave the other rows alone."""
+    from tensorflow_distributed_clustering_amd import _native
+    ops = _native.require()
+    n, d, k = 60000, 100, 300
+    x, c = _blobs(n, d, k, seed=m, dtype=dtype)
+    xg, C = x.to(gpu), c.to(gpu).contiguous()
+    want = torch.empty(n, dtype=torch.int32, device=gpu)
+    ops.assign_exact(xg, C, want, None)
+    rows = torch.randperm(n, generator=torch.Generator().manual_seed(m))[:m].to(torch.int32)
+    cap = n
+    amb = torch.zeros(3 * cap, dtype=torch.int32, device=gpu)
+    amb[2 * cap: 2 * cap + m] = rows.to(gpu)
+    count = torch.tensor([0, m], dtype=torch.int32, device=gpu)
+    labels = torch.full((n,), -1, dtype=torch.int32, device=gpu)
+    ops.x3_recheck(xg, C, labels, amb, count)
+    torch.cuda.synchronize()
+    got = labels.cpu()
+    listed = torch.zeros(n, dtype=torch.bool)
+    listed[rows.long()] = True
+    assert torch.equal(got[listed], want.cpu()[listed])
+    assert bool((got[~listed] == -1).all())
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+@pytest.mark.parametrize("n,d,k,offset", [(50000, 128, 1024, 0.0), (30000, 64, 200, 0.0),
+                                          (6000, 256, 64, 0.0), (40000, 128, 256, 200.0)])
+def test_x3_prefilter_same_labels(gpu, dtype, n, d, k, offset):
+    """The one-product prefilter only decides rows its own bound certifies: the labels are
+    those of the plain three-product pass (both exact up to the dtype's rounding).  The
+    offset case (|x| >> the cluster gaps) leaves most rows to the three products."""
+    tdt = torch.float32 if dtype == "fp32" else torch.float64
+    x, c = _blobs(n, d, k, seed=d + k, dtype=tdt)
+    x, c = x + offset, c + offset
+    xg, C = x.to(gpu), c.to(gpu).contiguous()
+    lo = _x3(xg, k, dtype)
+    assert lo.pre is not None and lo.prefilter
+    lo.prepare(C)
+    la = torch.full((n,), -1, dtype=torch.int32, device=gpu)
+    lo.assign(C, la, None)
+    listed = lo.prefilter_rows()
+    lo.prefilter = False
+    lb = torch.full((n,), -1, dtype=torch.int32, device=gpu)
+    lo.assign(C, lb, None)
+    assert lo.prefilter_rows() == 0
+    rel = 1e-6 if dtype == "fp32" else 1e-12
+    bad, _ = _tie_ok(x.double(), c.double(), la, rel)
+    assert bad == 0
+    diff = (la != lb).nonzero().flatten().cpu()
+    if diff.numel():  # only exact ties may differ
+        d64 = ref.pairwise_sqdist(x[diff].double(), c.double(), exact=True)
+        da = d64.gather(1, la.cpu()[diff].long()[:, None]).squeeze(1)
+        db = d64.gather(1, lb.cpu()[diff].long()[:, None]).squeeze(1)
+        assert torch.all((da - db).abs() <= rel * db.abs() + 1e-30)
+    if offset == 0.0:
+        assert listed < 0.5 * n, listed  # blob data: most rows certify on one product
+    else:
+        assert listed > 0
+
+
+def test_x3_prefilter_backs_off(gpu):
+    """Data where the one-product bound certifies almost nothing (|x| >> the cluster gaps):
+    once the listed count has come back, the prefilter is skipped for PRE_RETRY
+    assignments, and the labels stay exact either way."""
+    n, d, k = 20000, 128, 128
+    x, c = _blobs(n, d, k, seed=9, dtype=torch.float32)
+    x, c = x + 300.0, c + 300.0
+    xg, C = x.to(gpu), c.to(gpu).contiguous()
+    lo = _x3(xg, k, "fp32")
+    lo.prepare(C)
+    labels = torch.empty(n, dtype=torch.int32, device=gpu)
+    lo.assign(C, labels, None)
+    assert lo.prefilter_rows() > lo.PRE_MAX_FRAC * n
+    torch.cuda.synchronize()
+    lo.assign(C, labels, None)
+    assert lo.prefilter_rows() == 0  # skipped: the first count was read
+    for _ in range(lo.PRE_RETRY - 1):
+        lo.assign(C, labels, None)
+    assert lo.prefilter_rows() == 0
+    lo.assign(C, labels, None)
+    assert lo.prefilter_rows() > 0  # tried again after PRE_RETRY skipped assignments
+    bad, _ = _tie_ok(x.double(), c.double(), labels, 1e-6)
+    assert bad == 0
