@@ -116,6 +116,9 @@ def parse(argv=None):
     ap.add_argument("--fcm-distances", default="x3", choices=["one", "x3"],
                     help="bf16 FCM distances: one product + two-nearest fix-up, or bf16x3 "
                          "(ClusterConfig.fcm_distances)")
+    ap.add_argument("--no-x3-prefilter", action="store_true",
+                    help="fp32/fp64 K-Means: run the bf16x3 pass over every row (no one-product "
+                         "prefilter; A/B of HipX3Lloyd.prefilter)")
     ap.add_argument("--comm-mode", default="auto", choices=["auto", "allreduce", "rsag"],
                     help="partial-sum reduction (ClusterConfig.comm_mode); with "
                          "TDC_FORCE_COLLECTIVES=1 a world-1 run issues the RCCL calls too")
@@ -196,6 +199,8 @@ def main(argv=None):
         else:
             eng = LloydEngine(x, cfg, comm, n_global, s, defer_init=True)
         points_per_step = n_global
+    if a.no_x3_prefilter and hasattr(getattr(eng, "local", None), "prefilter"):
+        eng.local.prefilter = False
     init_s = None
     if hasattr(eng, "init_centroids") and getattr(eng, "c0", None) is None:
         # the centroid init, timed on its own (never inside the timed steps)

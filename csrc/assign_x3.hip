@@ -202,7 +202,7 @@ __device__ __forceinline__ void x3_append(bool amb, bool two, int64_t row, int l
 // point tile.  At D=128 a score costs 3 MFMAs (48 matrix cycles) against ~4.75 epilogue
 // VALU, so the kernel is MFMA-bound where the bf16 ring3 is issue-bound.
 // ------------------------------------------------------------------------------------
-template <int DP, int P, int NST, int QT>
+template <int DP, int P, int NST, int QT, bool LISTED = false>
 __global__ __launch_bounds__(256, 2) void assign_x3_ring_kernel(
     const __bf16* __restrict__ Xh, const __bf16* __restrict__ Xl, int64_t N,
     const __bf16* __restrict__ Ch, const __bf16* __restrict__ Cl, const float* __restrict__ cnorm,
@@ -234,20 +234,22 @@ __global__ __launch_bounds__(256, 2) void assign_x3_ring_kernel(
   const int r = lane & 15;
   const int g = lane >> 4;
   // listed mode (after the one-product prefilter): point i is row rowidx[i], the count is
-  // read on the device and the workgroups past it leave before any load
-  if (nrows) {
+  // read on the device and the workgroups past it leave before any load.  (A grid-stride
+  // loop on the resident workgroups instead: 1.28 -> 1.44 ms at the headline's 14 % listed,
+  // 0.31 -> 0.28 ms at N=2M; profiles/headline_fp32_prefilter_kernel_stats_r05w.txt.)
+  if (LISTED) {
     N = *nrows;
     if ((int64_t)blockIdx.x * (WAVES * P * 16) >= N) return;
   }
-  const int64_t pbase = (int64_t)blockIdx.x * (WAVES * P * 16) + (int64_t)w * (P * 16);
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  const int64_t pbase = (int64_t)blockIdx.x * (WAVES * P * 16) + (int64_t)w * (P * 16);
 
   bf16x8 bh[P][KS], bl[P][KS];
 #pragma unroll
   for (int p = 0; p < P; ++p) {
     int64_t row = pbase + p * 16 + r;
     if (row >= N) row = N - 1;
-    if (rowidx) row = rowidx[row];
+    if (LISTED) row = rowidx[row];
     const __bf16* sh = Xh + row * DP + g * 8;
     const __bf16* sl = Xl + row * DP + g * 8;
 #pragma unroll
@@ -384,9 +386,15 @@ __global__ __launch_bounds__(256, 2) void assign_x3_ring_kernel(
         for (int i = 0; i < 4; ++i) {
           const float v = __uint_as_float((__float_as_uint(acc[p][i] + acx[p][i]) & ~EMB) |
                                           (unsigned)(q * 4 + i));
-          m3[p] = __builtin_amdgcn_fmed3f(m2[p], m3[p], v);
-          m2[p] = __builtin_amdgcn_fmed3f(m1[p], m2[p], v);
-          m1[p] = __builtin_fminf(m1[p], v);
+          // asm: the builtins canonicalised the tagged v first (one more VALU per score);
+          // v is never a signalling NaN (see assign_mfma_impl.h's top-2)
+          float n1, n2, n3;
+          asm("v_med3_f32 %0, %1, %2, %3" : "=v"(n3) : "v"(m2[p]), "v"(m3[p]), "v"(v));
+          asm("v_med3_f32 %0, %1, %2, %3" : "=v"(n2) : "v"(m1[p]), "v"(m2[p]), "v"(v));
+          asm("v_min_f32 %0, %1, %2" : "=v"(n1) : "v"(m1[p]), "v"(v));
+          m3[p] = n3;
+          m2[p] = n2;
+          m1[p] = n1;
         }
       }
     }
@@ -445,7 +453,7 @@ __global__ __launch_bounds__(256, 2) void assign_x3_ring_kernel(
                  __shfl_xor(v2, o, 64), __shfl_xor(l2, o, 64), __shfl_xor(v3, o, 64));
     const int64_t lrow = pbase + p * 16 + r;
     const bool valid = g == 0 && lrow < N;
-    const int64_t row = rowidx ? (int64_t)rowidx[lrow < N ? lrow : N - 1] : lrow;
+    const int64_t row = LISTED ? (int64_t)rowidx[lrow < N ? lrow : N - 1] : lrow;
     const float eps2 = 2.f * x3_eps(sqrtf(sh) * 1.0001f, sqrtf(sl) * 1.0001f, cstat, KS);
     if (mind) {  // + ||xh + xl||^2 turns the score into a distance (uniform branch)
       float sx = 0.f;
@@ -605,10 +613,18 @@ int launch_x3(const void* Xh, const void* Xl, int64_t N, const void* Ch, const v
   constexpr int BNL = 16 * QT;
   if (Kp % BNL != 0) return (int)hipErrorInvalidValue;
   const int64_t per = 4 * P * 16;
-  hipLaunchKernelGGL((assign_x3_ring_kernel<DP, P, NST, QT>), dim3((unsigned)((N + per - 1) / per)),
-                     dim3(256), 0, s, (const __bf16*)Xh, (const __bf16*)Xl, N, (const __bf16*)Ch,
-                     (const __bf16*)Cl, cnorm, Kp / BNL, cstat, labels, mind, amb, ambF,
-                     amb_count, rowidx, nrows);
+  int64_t blocks = (N + per - 1) / per;
+  if (nrows) {  // listed: sized by N, the workgroups past the device-side count leave
+    hipLaunchKernelGGL((assign_x3_ring_kernel<DP, P, NST, QT, true>), dim3((unsigned)blocks),
+                       dim3(256), 0, s, (const __bf16*)Xh, (const __bf16*)Xl, N, (const __bf16*)Ch,
+                       (const __bf16*)Cl, cnorm, Kp / BNL, cstat, labels, mind, amb, ambF,
+                       amb_count, rowidx, nrows);
+  } else {
+    hipLaunchKernelGGL((assign_x3_ring_kernel<DP, P, NST, QT>), dim3((unsigned)blocks),
+                       dim3(256), 0, s, (const __bf16*)Xh, (const __bf16*)Xl, N, (const __bf16*)Ch,
+                       (const __bf16*)Cl, cnorm, Kp / BNL, cstat, labels, mind, amb, ambF,
+                       amb_count, nullptr, nullptr);
+  }
   TDC_CHECK_LAUNCH();
   return 0;
 }
