@@ -246,17 +246,21 @@ void assign_mfma_bf16_ring2_kernel(const __bf16* __restrict__ X, int64_t N, int6
 // cstat (TOP2 only, nullable): the one-product prefilter of the fp32 / fp64 assignment
 // (assign_x3.hip).  X is then the bf16 hi term xh of the data rows and Cm2 the hi term th of
 // t = -2c, so a score leaves out xh.(t - th) + (x - xh).t; x1_eps bounds that per row from
-// ||xh|| (x - xh <= 2^-8 |xh| componentwise, RNE) and the centroid maxima cstat, plus the
-// accumulation / norm / tag terms of the x3 bound.  A row whose gap s2 - s1 exceeds 2 eps has
+// ||xh||, ||x - xh|| and the centroid maxima cstat, plus the accumulation / norm / tag terms
+// of the x3 bound.  ||x - xh|| comes from the row's ||xl|| (xnhl, written once per bound
+// shard by the split; x - xh = xl + xr with |xr| <= R8 |xl|), or without it from
+// x - xh <= 2^-8 |xh| componentwise (RNE; +2^-16 for fp64 -> fp32 -> bf16) -- the per-row
+// residual is ~0.6x that worst case and certifies ~1/6 more of the listed rows.  A row whose gap s2 - s1 exceeds 2 eps has
 // the exact argmin as its label here; every other row gets its label with the sign bit set
 // (x3_compact_kernel lists them for the three-product kernel: appending here took one
 // same-address atomic per 16 rows and serialised the kernel's tail).
-__device__ __forceinline__ float x1_eps(float hx, const float* cstat, int KS) {
+__device__ __forceinline__ float x1_eps(float hx, float lx, const float* cstat, int KS) {
   const float cn = cstat[0];
   const float Hc = sqrtf(cstat[1]) * 1.0001f, Lc = sqrtf(cstat[2]) * 1.0001f;
   constexpr float R8 = 0.00392157f;              // 2^-8 / (1 - 2^-8): |tr| <= R8 |tl|
   const float Tc = Lc * (1.f + R8);              // ||t - th||
-  const float dx = hx * (0.00390625f + 1.5259e-5f);  // ||x - xh|| (+2^-16: fp64 -> fp32 -> bf16)
+  const float dx = lx >= 0.f ? lx * (1.f + R8)   // ||x - xh||
+                             : hx * (0.00390625f + 1.5259e-5f);
   const float e_split = hx * Tc + dx * (Hc + Tc);
   const float s_main = hx * Hc;
   constexpr float U8 = 8.f * 1.1920929e-7f;      // per-MFMA accumulation (probe_mfma_acc)
@@ -274,7 +278,8 @@ void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int6
                                    float* __restrict__ mind,
                                    const int32_t* __restrict__ rowidx = nullptr,
                                    float* __restrict__ mind2 = nullptr,
-                                   const float* __restrict__ cstat = nullptr) {
+                                   const float* __restrict__ cstat = nullptr,
+                                   const float2* __restrict__ xnhl = nullptr) {
   constexpr int BNL = 16 * QT;                     // centroids per stage
   constexpr int CPR = DP / 8;
   constexpr int KS = DP / 32;                      // 32-deep k-steps
@@ -504,7 +509,9 @@ void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int6
     }
     if constexpr (TOP2) {
       if (cstat) {  // uniform branch: the prefilter flags its uncertified rows
-        const float eps2 = 2.f * x1_eps(sqrtf(xn[p]) * 1.0001f, cstat, KS);
+        const int64_t rr = pbase + p * 16 + r;
+        const float lx = xnhl ? sqrtf(xnhl[rr < N ? rr : N - 1].y) * 1.0001f : -1.f;
+        const float eps2 = 2.f * x1_eps(sqrtf(xn[p]) * 1.0001f, lx, cstat, KS);
         if (!(v2 - v > eps2)) lab |= (int)0x80000000;
       }
     }

@@ -686,7 +686,9 @@ int tdc_assign_x3(const void* Xh, const void* Xl, int64_t N, int DP, const void*
 // exact labels of the certified rows, the others flagged and then listed in pre (count in
 // *npre) by x3_compact_kernel for tdc_assign_x3's listed mode.  DP 64 / 128 / 256.
 int tdc_x3_prefilter(const void* Xh, int64_t N, int DP, const void* Ch, const float* cnorm, int Kp,
-                     const float* cstat, int32_t* labels, int32_t* pre, int* npre, hipStream_t s) {
+                     const float* cstat, int32_t* labels, int32_t* pre, int* npre, hipStream_t s,
+                     const float* xnhl) {
+  const float2* xn2 = reinterpret_cast<const float2*>(xnhl);
   if (N <= 0) return 0;
   if (Kp % 64 != 0 || N >= ((int64_t)1 << 31)) return (int)hipErrorInvalidValue;
   const __bf16* x = (const __bf16*)Xh;
@@ -695,15 +697,15 @@ int tdc_x3_prefilter(const void* Xh, int64_t N, int DP, const void* Ch, const fl
   if (DP == 64)  // P = 4 (P = 8 spills with the top-2 registers)
     hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<64, 4, 3, 4, 4, true>), grid, dim3(256), 0,
                        s, x, N, (int64_t)DP, c, cnorm, Kp / 64, labels, nullptr, nullptr, nullptr,
-                       cstat);
+                       cstat, xn2);
   else if (DP == 128)
     hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<128, 4, 3, 4, 4, true>), grid, dim3(256), 0,
                        s, x, N, (int64_t)DP, c, cnorm, Kp / 64, labels, nullptr, nullptr, nullptr,
-                       cstat);
+                       cstat, xn2);
   else if (DP == 256)
     hipLaunchKernelGGL((assign_mfma_bf16_ring3_kernel<256, 4, 2, 4, 4, true>), grid, dim3(256), 0,
                        s, x, N, (int64_t)DP, c, cnorm, Kp / 64, labels, nullptr, nullptr, nullptr,
-                       cstat);
+                       cstat, xn2);
   else
     return (int)hipErrorInvalidValue;
   TDC_CHECK_LAUNCH();

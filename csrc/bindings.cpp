@@ -714,7 +714,7 @@ void x3_assign(const at::Tensor& X, const at::Tensor& Xh, const at::Tensor& Xl, 
                const at::Tensor& Cl, const at::Tensor& cnorm, const at::Tensor& cnhl,
                const at::Tensor& C, at::Tensor& labels, const std::optional<at::Tensor>& mind,
                at::Tensor& amb, at::Tensor& cstat, at::Tensor& amb_count, bool recheck,
-               const std::optional<at::Tensor>& pre) {
+               const std::optional<at::Tensor>& pre, const std::optional<at::Tensor>& xnhl) {
   check_cuda(Xh, "Xh");
   TORCH_CHECK(Xh.scalar_type() == at::kBFloat16 && Xl.scalar_type() == at::kBFloat16 &&
                   Ch.scalar_type() == at::kBFloat16 && Cl.scalar_type() == at::kBFloat16,
@@ -756,6 +756,12 @@ void x3_assign(const at::Tensor& X, const at::Tensor& Xh, const at::Tensor& Xl, 
                 "tdc.x3_assign: pre int32 [>= N] needs amb_count int32 [3], DP 64/128/256 and no mind");
     pl = pre->data_ptr<int32_t>();
   }
+  const float* xn2 = nullptr;
+  if (pl && xnhl.has_value() && xnhl->defined()) {
+    TORCH_CHECK(xnhl->scalar_type() == at::kFloat && xnhl->is_contiguous() && xnhl->numel() >= 2 * N,
+                "tdc.x3_assign: xnhl fp32 [>= N, 2] (the rows' hi/lo norms from x3_split)");
+    xn2 = xnhl->data_ptr<float>();
+  }
   const DevGuard guard(Xh.device());
   hipStream_t s = cur_stream();
   int32_t* list = amb.data_ptr<int>();
@@ -765,7 +771,8 @@ void x3_assign(const at::Tensor& X, const at::Tensor& Xh, const at::Tensor& Xl, 
         "x3_prep");
   if (pl)  // one-product prefilter, then the three products over the rows it could not certify
     check(tdc_x3_prefilter(Xh.data_ptr(), N, DP, Ch.data_ptr(), cnorm.data_ptr<float>(), Kp,
-                           cstat.data_ptr<float>(), labels.data_ptr<int32_t>(), pl, cnt + 2, s),
+                           cstat.data_ptr<float>(), labels.data_ptr<int32_t>(), pl, cnt + 2, s,
+                           xn2),
           "x3_prefilter");
   check(tdc_assign_x3(Xh.data_ptr(), Xl.data_ptr(), N, DP, Ch.data_ptr(), Cl.data_ptr(),
                       cnorm.data_ptr<float>(), Kp, cstat.data_ptr<float>(),
@@ -1191,7 +1198,7 @@ TORCH_LIBRARY(tdc, m) {
   m.def("sculley_update(Tensor sums, Tensor counts, Tensor(a!) C, Tensor(b!) v, Tensor(c!)? shift, Tensor(d!)? Cm2, Tensor(e!)? cnorm) -> ()");
   m.def("x3_split(Tensor src, int valid, int neg2, Tensor(a!) hi, Tensor(b!) lo, Tensor(c!)? norm, Tensor(d!)? nhl=None) -> ()");
   m.def("x3_prep(Tensor cnorm, Tensor? nhl, int K, Tensor(a!) cstat, Tensor(b!) amb_count) -> ()");
-  m.def("x3_assign(Tensor X, Tensor Xh, Tensor Xl, Tensor Ch, Tensor Cl, Tensor cnorm, Tensor cnhl, Tensor C, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!) amb, Tensor(d!) cstat, Tensor(e!) amb_count, bool recheck=True, Tensor(f!)? pre=None) -> ()");
+  m.def("x3_assign(Tensor X, Tensor Xh, Tensor Xl, Tensor Ch, Tensor Cl, Tensor cnorm, Tensor cnhl, Tensor C, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!) amb, Tensor(d!) cstat, Tensor(e!) amb_count, bool recheck=True, Tensor(f!)? pre=None, Tensor? xnhl=None) -> ()");
   m.def("x3_rows(Tensor G, int row0, Tensor xx, Tensor cstat, int DP, Tensor(a!) labels, Tensor(b!) amb, Tensor(c!) amb_count) -> ()");
   m.def("x3_recheck(Tensor X, Tensor C, Tensor(a!) labels, Tensor amb, Tensor amb_count) -> ()");
 }

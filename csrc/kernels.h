@@ -56,7 +56,8 @@ int tdc_bounds_scatter(const int32_t* active, const int* count, int64_t cap,
 //   rows  (wide D): top-3 over a chunk's raw d2 block G [M, K] (tdc_fcm_mfma_wide pass 1),
 //          xx [M] = ||x||^2, list rows offset by row0;
 //   recheck: exact difference form in the data's dtype (X/C both f32 or f64, D <= 1024);
-//   prefilter (DP 64/128/256): one bf16 product (xh . th) with top-2 and a per-row bound:
+//   prefilter (DP 64/128/256): one bf16 product (xh . th) with top-2 and a per-row bound
+//          (xnhl nullable: the rows' split norms from split, for the row's own ||xl||):
 //          labels of the certified rows, the others listed in pre (count *npre, zeroed by
 //          prep with nzero = 3 into amb_count[2]) for assign's listed mode (rowidx / nrows:
 //          point i is row rowidx[i], count read on the device; grid sized by N).
@@ -66,7 +67,7 @@ int tdc_x3_prep(const float* cnorm, const float* nhl, int K, float* cstat, int* 
                 hipStream_t stream, int nzero = 2);
 int tdc_x3_prefilter(const void* Xh, int64_t N, int DP, const void* Ch, const float* cnorm, int Kp,
                      const float* cstat, int32_t* labels, int32_t* pre, int* npre,
-                     hipStream_t stream);
+                     hipStream_t stream, const float* xnhl = nullptr);
 int tdc_assign_x3(const void* Xh, const void* Xl, int64_t N, int DP, const void* Ch, const void* Cl,
                   const float* cnorm, int Kp, const float* cstat, int32_t* labels,
                   float* mind, int32_t* amb, int64_t cap, int* amb_count, hipStream_t stream,

@@ -971,7 +971,7 @@ class HipX3Lloyd(_LocalOpsBase):
         self.cstat = torch.zeros(3, dtype=torch.float32, device=dev)  # maxima of cnorm / cnhl
         # [0] two-candidate list, [1] full re-scan list, [2] the prefilter's listed rows
         self.amb_count = torch.zeros(3, dtype=torch.int32, device=dev)
-        self.xh = self.xl = self.xx = self.amb = self.G = self.pre = None
+        self.xh = self.xl = self.xx = self.amb = self.G = self.pre = self.xnhl = None
         self.x = None
         self._set_x(x)
         self.update = NativeUpdate(self.ops, self.n, k, self.d, self.c_dtype, dev)
@@ -987,13 +987,16 @@ class HipX3Lloyd(_LocalOpsBase):
             self.xx = torch.empty(max(n, 1), dtype=torch.float32, device=dev) if self.wide else None
             # re-check lists: int2 {row, runner-up} entries | full re-scan rows
             self.amb = torch.empty(3 * max(n, 1), dtype=torch.int32, device=dev)
-            self.pre = (torch.empty(max(n, 1), dtype=torch.int32, device=dev)
-                        if self.dp in (64, 128, 256) else None)
+            pre_ok = self.dp in (64, 128, 256)
+            self.pre = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if pre_ok else None
+            # ||xh||^2, ||xl||^2 per row: the prefilter's bound takes the row's own residual
+            self.xnhl = torch.empty(max(n, 1), 2, dtype=torch.float32, device=dev) if pre_ok else None
         self.x = x
         self.n = n
         if n:
             self.ops.x3_split(x[:, : self.d], n, 0, self.xh[:n], self.xl[:n],
-                              self.xx[:n] if self.wide else None)
+                              self.xx[:n] if self.wide else None,
+                              self.xnhl[:n] if self.xnhl is not None else None)
 
     @property
     def layout(self):
@@ -1027,7 +1030,7 @@ class HipX3Lloyd(_LocalOpsBase):
             self._pre_ran = pre is not None
             self.ops.x3_assign(self.x, self.xh[:n], self.xl[:n], self.ch, self.cl, self.cnorm,
                                self.cnhl, Cx, labels, None, amb, self.cstat, self.amb_count, True,
-                               pre)
+                               pre, self.xnhl[:n] if pre is not None else None)
             if pre is not None and self._pre_ev is None and \
                     not torch.cuda.is_current_stream_capturing():
                 self._pre_host.copy_(self.amb_count[2:3], non_blocking=True)
@@ -1108,10 +1111,10 @@ def lloyd_row_extra(dtype: str, d: int, delta: bool = True) -> int:
     per_row_extra): labels + min distances + the sorted update's permutation (16), the delta
     update's prev / moved-list / event permutation (20), and on the fp32 / fp64 MFMA path
     the bf16 hi/lo rows (4 x padded D) + the re-check list entries (12) + the prefilter's
-    list entry (4)."""
+    list entry and the row's split norms (12)."""
     extra = 16 + (20 if delta else 0)
     if dtype in ("fp32", "fp64") and d > X3_MIN_D and x3_dim(d) is not None:
-        extra += 4 * x3_dim(d) + 16
+        extra += 4 * x3_dim(d) + 24
     return extra
 
 
