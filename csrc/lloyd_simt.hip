@@ -407,7 +407,7 @@ template <> struct ExactCfg<double> { static constexpr int MR = 4; };
 
 // A listed re-scan (rowidx / nptr below) of at most this many rows runs on
 // assign_exact_few_kernel instead: the 128-row tiles would leave all but a handful of CUs idle.
-constexpr int EXACT_FEW_MAX = 32768;
+constexpr int EXACT_FEW_MAX = 32768, EXACT_FEW_MAXD = 1024;
 
 // rowidx (nullable): row i of the launch is row rowidx[i] of X (and of labels / mind), with
 // the row count read from the device (nptr) -- the full re-scan of the rows the fp32/fp64
@@ -419,7 +419,8 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(const T* __restrict__
                                                            int32_t* __restrict__ labels,
                                                            T* __restrict__ mind,
                                                            const int32_t* __restrict__ rowidx,
-                                                           const int* __restrict__ nptr) {
+                                                           const int* __restrict__ nptr,
+                                                           int few_max) {
   constexpr int MR = ExactCfg<T>::MR;
   constexpr int R = 16 * MR, KT = 128, DC = 32;
   constexpr int PX = R + 4, PC = KT + 4;  // row pitch (16-B aligned, spreads the store banks)
@@ -429,7 +430,7 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(const T* __restrict__
   constexpr bool F32 = sizeof(T) == 4;
   if (nptr) {
     N = *nptr;
-    if (N <= EXACT_FEW_MAX) return;  // assign_exact_few_kernel has them
+    if (N <= few_max) return;  // assign_exact_few_kernel has them
   }
   for (int64_t r0 = (int64_t)blockIdx.x * R; r0 < N; r0 += (int64_t)gridDim.x * R) {
     T best[MR];
@@ -548,7 +549,9 @@ __global__ __launch_bounds__(256) void assign_exact_few_kernel(const T* __restri
                                                                const int32_t* __restrict__ rowidx,
                                                                const int* __restrict__ nptr) {
   constexpr int RB = 8, KT = 256, DC = 32;
-  __shared__ __attribute__((aligned(16))) T s_x[DC][RB];
+  // the row group's rows, staged once (D <= EXACT_FEW_MAXD, zero-padded to the chunk): a
+  // per-chunk slice had put two dependent global loads (index, row) on every chunk
+  __shared__ __attribute__((aligned(16))) T s_x[EXACT_FEW_MAXD][RB];
   __shared__ T s_c[DC][KT + 1];
   __shared__ T s_rb[4][RB];
   __shared__ int s_rk[4][RB];
@@ -562,7 +565,7 @@ __global__ __launch_bounds__(256) void assign_exact_few_kernel(const T* __restri
   const int nd = (D + DC - 1) / DC, nchunks = nd * ((K + KT - 1) / KT);
   const bool vec_ok = D % VEC == 0 && ((uintptr_t)C % 16) == 0;
   vecT cv[NV];
-  T xv;
+  const int Dp = nd * DC;
   auto load = [&](int64_t r0, int ci) __attribute__((always_inline)) {
     const int k0 = (ci / nd) * KT, dc = (ci % nd) * DC;
 #pragma unroll
@@ -576,9 +579,6 @@ __global__ __launch_bounds__(256) void assign_exact_few_kernel(const T* __restri
         for (int j = 0; j < VEC; ++j) cv[i][j] = (k0 + r < K && d + j < D) ? src[j] : (T)0;
       }
     }
-    const int r = tid / DC, d = dc + tid % DC;  // RB x DC = 256 entries
-    const int64_t row = r0 + r;
-    xv = (row < n && d < D) ? X[(int64_t)rowidx[row] * ldx + d] : (T)0;
   };
   for (int64_t r0 = (int64_t)blockIdx.x * RB; r0 < n; r0 += (int64_t)gridDim.x * RB) {
     T best[RB];
@@ -592,6 +592,12 @@ __global__ __launch_bounds__(256) void assign_exact_few_kernel(const T* __restri
 #pragma unroll
     for (int i = 0; i < RB; ++i) acc[i] = (T)0;
     load(r0, 0);
+    __syncthreads();  // the previous group's reads of s_x are done
+    for (int e = tid; e < RB * Dp; e += 256) {
+      const int r = e / Dp, d = e % Dp;
+      const int64_t row = r0 + r;
+      s_x[d][r] = (row < n && d < D) ? X[(int64_t)rowidx[row] * ldx + d] : (T)0;
+    }
     for (int ci = 0; ci < nchunks; ++ci) {
       __syncthreads();
 #pragma unroll
@@ -600,15 +606,15 @@ __global__ __launch_bounds__(256) void assign_exact_few_kernel(const T* __restri
 #pragma unroll
         for (int j = 0; j < VEC; ++j) s_c[d + j][r] = cv[i][j];
       }
-      s_x[tid % DC][tid / DC] = xv;
       __syncthreads();
       if (ci + 1 < nchunks) load(r0, ci + 1);
+      const int dc = (ci % nd) * DC;
 #pragma unroll 4
       for (int d = 0; d < DC; ++d) {
         const T c = s_c[d][tid];
 #pragma unroll
         for (int i = 0; i < RB; ++i) {
-          const T df = s_x[d][i] - c;
+          const T df = s_x[dc + d][i] - c;
           acc[i] = fma(df, df, acc[i]);
         }
       }
@@ -663,7 +669,8 @@ int tdc_assign_exact(int dtype, const void* X, int64_t N, int64_t ldx, int D, co
                      int32_t* labels, void* mind, int num_cus, hipStream_t s,
                      const int32_t* rowidx, const int* nptr) {
   if (N <= 0) return 0;
-  if (nptr) {
+  const bool few = nptr && D <= EXACT_FEW_MAXD;
+  if (few) {
     if (!rowidx) return (int)hipErrorInvalidValue;
     // both launches read the listed count; exactly one of them has work
     int64_t fb = ((N < EXACT_FEW_MAX ? N : EXACT_FEW_MAX) + 7) / 8;
@@ -692,11 +699,11 @@ int tdc_assign_exact(int dtype, const void* X, int64_t N, int64_t ldx, int D, co
   if (dtype == TDC_F32)
     hipLaunchKernelGGL(assign_exact_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s,
                        (const float*)X, N, ldx, D, (const float*)C, K, labels, (float*)mind,
-                       rowidx, nptr);
+                       rowidx, nptr, few ? EXACT_FEW_MAX : -1);
   else if (dtype == TDC_F64)
     hipLaunchKernelGGL(assign_exact_kernel<double>, dim3((unsigned)blocks), dim3(256), 0, s,
                        (const double*)X, N, ldx, D, (const double*)C, K, labels, (double*)mind,
-                       rowidx, nptr);
+                       rowidx, nptr, few ? EXACT_FEW_MAX : -1);
   else
     return (int)hipErrorInvalidValue;
   TDC_CHECK_LAUNCH();
