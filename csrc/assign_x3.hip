@@ -202,14 +202,14 @@ __device__ __forceinline__ void x3_append(bool amb, bool two, int64_t row, int l
 // point tile.  At D=128 a score costs 3 MFMAs (48 matrix cycles) against ~4.75 epilogue
 // VALU, so the kernel is MFMA-bound where the bf16 ring3 is issue-bound.
 // ------------------------------------------------------------------------------------
-template <int DP, int P, int NST, int QT, bool LISTED = false>
+template <int DP, int P, int NST, int QT, int LISTED = 0>
 __global__ __launch_bounds__(256, 2) void assign_x3_ring_kernel(
     const __bf16* __restrict__ Xh, const __bf16* __restrict__ Xl, int64_t N,
     const __bf16* __restrict__ Ch, const __bf16* __restrict__ Cl, const float* __restrict__ cnorm,
     int ntiles, const float* __restrict__ cstat, int32_t* __restrict__ labels,
     float* __restrict__ mind, int2* __restrict__ amb, int* __restrict__ ambF,
     int* __restrict__ amb_count, const int32_t* __restrict__ rowidx,
-    const int* __restrict__ nrows) {
+    const int* __restrict__ nrows, int64_t blk0) {
   constexpr int WAVES = 4;
   constexpr int BNL = 16 * QT;                 // centroids per stage
   constexpr int CPR = DP / 8;
@@ -228,21 +228,28 @@ __global__ __launch_bounds__(256, 2) void assign_x3_ring_kernel(
   constexpr unsigned EMB = 15u;
   __shared__ __attribute__((aligned(16))) char smem[NST * STAGE_B];
 
-  const int tid = threadIdx.x;
+  // listed modes (after the one-product prefilter): point i is row rowidx[i], the count is
+  // read on the device.  LISTED = 1: one point block per workgroup from block blk0 on, the
+  // launch sized by the caller's estimate of the count (the previous step's); the
+  // workgroups past the count leave before any load.  LISTED = 2: the overflow beyond such
+  // a launch, a grid-stride loop on the resident workgroups (normally empty).  Sized by N
+  // instead, the one-shot launch had ~35K empty workgroups at the headline shape (~0.3 ms);
+  // the grid-stride loop over every block was slower (1.28 -> 1.44 ms,
+  // profiles/headline_fp32_prefilter_kernel_stats_r05w.txt).
+  if (LISTED) N = *nrows;
+  for (int64_t blk = blk0 + blockIdx.x; blk * (WAVES * P * 16) < N; blk += gridDim.x) {
+  if (LISTED == 2 && blk != blk0 + blockIdx.x) __syncthreads();  // the ring's slots are free
+  // LISTED = 2: an opaque zero (asm volatile) rebuilds the lane constants per point block
+  // instead of holding them through the loop (spills otherwise)
+  unsigned oz = 0;
+  if (LISTED == 2) asm volatile("v_mov_b32 %0, 0" : "=v"(oz));
+  const int tid = (int)(threadIdx.x + oz);
   const int lane = tid & 63;
   const int w = tid >> 6;
   const int r = lane & 15;
   const int g = lane >> 4;
-  // listed mode (after the one-product prefilter): point i is row rowidx[i], the count is
-  // read on the device and the workgroups past it leave before any load.  (A grid-stride
-  // loop on the resident workgroups instead: 1.28 -> 1.44 ms at the headline's 14 % listed,
-  // 0.31 -> 0.28 ms at N=2M; profiles/headline_fp32_prefilter_kernel_stats_r05w.txt.)
-  if (LISTED) {
-    N = *nrows;
-    if ((int64_t)blockIdx.x * (WAVES * P * 16) >= N) return;
-  }
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-  const int64_t pbase = (int64_t)blockIdx.x * (WAVES * P * 16) + (int64_t)w * (P * 16);
+  const int64_t pbase = blk * (WAVES * P * 16) + (int64_t)w * (P * 16);
 
   bf16x8 bh[P][KS], bl[P][KS];
 #pragma unroll
@@ -471,6 +478,8 @@ __global__ __launch_bounds__(256, 2) void assign_x3_ring_kernel(
     if (valid) labels[row] = l1;
     x3_append(valid && !(v2 - v1 > eps2), v3 - v1 > eps2, row, l2, amb, ambF, amb_count);
   }
+  if (LISTED != 2) break;  // one point block per workgroup
+  }  // point blocks
 }
 
 // ------------------------------------------------------------------------------------
@@ -609,21 +618,34 @@ template <int DP, int P, int NST, int QT>
 int launch_x3(const void* Xh, const void* Xl, int64_t N, const void* Ch, const void* Cl,
               const float* cnorm, int Kp, const float* cstat, int32_t* labels,
               float* mind, int2* amb, int* ambF, int* amb_count, const int32_t* rowidx,
-              const int* nrows, hipStream_t s) {
+              const int* nrows, int64_t est_rows, hipStream_t s) {
   constexpr int BNL = 16 * QT;
   if (Kp % BNL != 0) return (int)hipErrorInvalidValue;
   const int64_t per = 4 * P * 16;
-  int64_t blocks = (N + per - 1) / per;
-  if (nrows) {  // listed: sized by N, the workgroups past the device-side count leave
-    hipLaunchKernelGGL((assign_x3_ring_kernel<DP, P, NST, QT, true>), dim3((unsigned)blocks),
+  const int64_t blocks = (N + per - 1) / per;
+  if (nrows) {
+    // est_rows (> 0): the caller's estimate of the listed count; the one-shot launch covers
+    // it, a small grid-stride launch covers anything beyond (normally nothing to do)
+    int64_t b1 = est_rows > 0 ? (est_rows + per - 1) / per : blocks;
+    if (b1 > blocks) b1 = blocks;
+    hipLaunchKernelGGL((assign_x3_ring_kernel<DP, P, NST, QT, 1>), dim3((unsigned)b1),
                        dim3(256), 0, s, (const __bf16*)Xh, (const __bf16*)Xl, N, (const __bf16*)Ch,
                        (const __bf16*)Cl, cnorm, Kp / BNL, cstat, labels, mind, amb, ambF,
-                       amb_count, rowidx, nrows);
+                       amb_count, rowidx, nrows, (int64_t)0);
+    if (b1 < blocks) {
+      TDC_CHECK_LAUNCH();
+      static const int res = resident_blocks(assign_x3_ring_kernel<DP, P, NST, QT, 2>, 256);
+      const int64_t b2 = blocks - b1 < res ? blocks - b1 : res;
+      hipLaunchKernelGGL((assign_x3_ring_kernel<DP, P, NST, QT, 2>), dim3((unsigned)b2),
+                         dim3(256), 0, s, (const __bf16*)Xh, (const __bf16*)Xl, N,
+                         (const __bf16*)Ch, (const __bf16*)Cl, cnorm, Kp / BNL, cstat, labels,
+                         mind, amb, ambF, amb_count, rowidx, nrows, b1);
+    }
   } else {
     hipLaunchKernelGGL((assign_x3_ring_kernel<DP, P, NST, QT>), dim3((unsigned)blocks),
                        dim3(256), 0, s, (const __bf16*)Xh, (const __bf16*)Xl, N, (const __bf16*)Ch,
                        (const __bf16*)Cl, cnorm, Kp / BNL, cstat, labels, mind, amb, ambF,
-                       amb_count, nullptr, nullptr);
+                       amb_count, nullptr, nullptr, (int64_t)0);
   }
   TDC_CHECK_LAUNCH();
   return 0;
@@ -666,7 +688,7 @@ int tdc_x3_prep(const float* cnorm, const float* nhl, int K, float* cstat, int* 
 int tdc_assign_x3(const void* Xh, const void* Xl, int64_t N, int DP, const void* Ch, const void* Cl,
                   const float* cnorm, int Kp, const float* cstat, int32_t* labels,
                   float* mind, int32_t* amb, int64_t cap, int* amb_count, hipStream_t s,
-                  const int32_t* rowidx, const int* nrows) {
+                  const int32_t* rowidx, const int* nrows, int64_t est_rows) {
   if (N <= 0) return 0;
   if (N >= ((int64_t)1 << 31) || cap < N) return (int)hipErrorInvalidValue;
   if ((rowidx == nullptr) != (nrows == nullptr)) return (int)hipErrorInvalidValue;
@@ -674,10 +696,10 @@ int tdc_assign_x3(const void* Xh, const void* Xl, int64_t N, int DP, const void*
   int* lf = amb + 2 * cap;
   switch (DP) {
     // LDS per stage: 2 images x 64 centroids x DP x 2 B; two workgroups (8 waves) per CU
-    case 32: return launch_x3<32, 6, 3, 4>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cstat, labels, mind, l2, lf, amb_count, rowidx, nrows, s);
-    case 64: return launch_x3<64, 6, 3, 4>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cstat, labels, mind, l2, lf, amb_count, rowidx, nrows, s);
-    case 128: return launch_x3<128, 4, 2, 4>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cstat, labels, mind, l2, lf, amb_count, rowidx, nrows, s);
-    case 256: return launch_x3<256, 2, 2, 2>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cstat, labels, mind, l2, lf, amb_count, rowidx, nrows, s);
+    case 32: return launch_x3<32, 6, 3, 4>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cstat, labels, mind, l2, lf, amb_count, rowidx, nrows, est_rows, s);
+    case 64: return launch_x3<64, 6, 3, 4>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cstat, labels, mind, l2, lf, amb_count, rowidx, nrows, est_rows, s);
+    case 128: return launch_x3<128, 4, 2, 4>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cstat, labels, mind, l2, lf, amb_count, rowidx, nrows, est_rows, s);
+    case 256: return launch_x3<256, 2, 2, 2>(Xh, Xl, N, Ch, Cl, cnorm, Kp, cstat, labels, mind, l2, lf, amb_count, rowidx, nrows, est_rows, s);
   }
   return (int)hipErrorInvalidValue;
 }

@@ -714,7 +714,8 @@ void x3_assign(const at::Tensor& X, const at::Tensor& Xh, const at::Tensor& Xl, 
                const at::Tensor& Cl, const at::Tensor& cnorm, const at::Tensor& cnhl,
                const at::Tensor& C, at::Tensor& labels, const std::optional<at::Tensor>& mind,
                at::Tensor& amb, at::Tensor& cstat, at::Tensor& amb_count, bool recheck,
-               const std::optional<at::Tensor>& pre, const std::optional<at::Tensor>& xnhl) {
+               const std::optional<at::Tensor>& pre, const std::optional<at::Tensor>& xnhl,
+               int64_t pre_est) {
   check_cuda(Xh, "Xh");
   TORCH_CHECK(Xh.scalar_type() == at::kBFloat16 && Xl.scalar_type() == at::kBFloat16 &&
                   Ch.scalar_type() == at::kBFloat16 && Cl.scalar_type() == at::kBFloat16,
@@ -777,7 +778,7 @@ void x3_assign(const at::Tensor& X, const at::Tensor& Xh, const at::Tensor& Xl, 
   check(tdc_assign_x3(Xh.data_ptr(), Xl.data_ptr(), N, DP, Ch.data_ptr(), Cl.data_ptr(),
                       cnorm.data_ptr<float>(), Kp, cstat.data_ptr<float>(),
                       labels.data_ptr<int32_t>(), md, list, cap, cnt, s, pl,
-                      pl ? cnt + 2 : nullptr),
+                      pl ? cnt + 2 : nullptr, pre_est),
         "assign_x3");
   if (recheck)
     check(tdc_x3_recheck(dcode(X.scalar_type()), X.data_ptr(), X.stride(0), (int)C.size(1), C.data_ptr(),
@@ -1198,7 +1199,7 @@ TORCH_LIBRARY(tdc, m) {
   m.def("sculley_update(Tensor sums, Tensor counts, Tensor(a!) C, Tensor(b!) v, Tensor(c!)? shift, Tensor(d!)? Cm2, Tensor(e!)? cnorm) -> ()");
   m.def("x3_split(Tensor src, int valid, int neg2, Tensor(a!) hi, Tensor(b!) lo, Tensor(c!)? norm, Tensor(d!)? nhl=None) -> ()");
   m.def("x3_prep(Tensor cnorm, Tensor? nhl, int K, Tensor(a!) cstat, Tensor(b!) amb_count) -> ()");
-  m.def("x3_assign(Tensor X, Tensor Xh, Tensor Xl, Tensor Ch, Tensor Cl, Tensor cnorm, Tensor cnhl, Tensor C, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!) amb, Tensor(d!) cstat, Tensor(e!) amb_count, bool recheck=True, Tensor(f!)? pre=None, Tensor? xnhl=None) -> ()");
+  m.def("x3_assign(Tensor X, Tensor Xh, Tensor Xl, Tensor Ch, Tensor Cl, Tensor cnorm, Tensor cnhl, Tensor C, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!) amb, Tensor(d!) cstat, Tensor(e!) amb_count, bool recheck=True, Tensor(f!)? pre=None, Tensor? xnhl=None, int pre_est=-1) -> ()");
   m.def("x3_rows(Tensor G, int row0, Tensor xx, Tensor cstat, int DP, Tensor(a!) labels, Tensor(b!) amb, Tensor(c!) amb_count) -> ()");
   m.def("x3_recheck(Tensor X, Tensor C, Tensor(a!) labels, Tensor amb, Tensor amb_count) -> ()");
 }

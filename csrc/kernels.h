@@ -60,7 +60,8 @@ int tdc_bounds_scatter(const int32_t* active, const int* count, int64_t cap,
 //          (xnhl nullable: the rows' split norms from split, for the row's own ||xl||):
 //          labels of the certified rows, the others listed in pre (count *npre, zeroed by
 //          prep with nzero = 3 into amb_count[2]) for assign's listed mode (rowidx / nrows:
-//          point i is row rowidx[i], count read on the device; grid sized by N).
+//          point i is row rowidx[i], count read on the device; est_rows > 0 sizes the launch
+//          for that many rows, with a grid-stride launch for any overflow).
 int tdc_x3_split(int src_dtype, const void* src, int64_t rows, int64_t valid, int d, int64_t ld,
                  int DP, int neg2, void* hi, void* lo, float* norm, float* nhl, hipStream_t stream);
 int tdc_x3_prep(const float* cnorm, const float* nhl, int K, float* cstat, int* amb_count,
@@ -71,7 +72,8 @@ int tdc_x3_prefilter(const void* Xh, int64_t N, int DP, const void* Ch, const fl
 int tdc_assign_x3(const void* Xh, const void* Xl, int64_t N, int DP, const void* Ch, const void* Cl,
                   const float* cnorm, int Kp, const float* cstat, int32_t* labels,
                   float* mind, int32_t* amb, int64_t cap, int* amb_count, hipStream_t stream,
-                  const int32_t* rowidx = nullptr, const int* nrows = nullptr);
+                  const int32_t* rowidx = nullptr, const int* nrows = nullptr,
+                  int64_t est_rows = -1);
 int tdc_x3_rows(const float* G, int64_t M, int K, int64_t row0, const float* xx, const float* cstat,
                 int DP, int32_t* labels, int32_t* amb, int64_t cap, int* amb_count,
                 hipStream_t stream);

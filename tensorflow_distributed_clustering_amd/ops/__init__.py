@@ -1028,9 +1028,13 @@ class HipX3Lloyd(_LocalOpsBase):
         if not self.wide:
             pre = self.pre if self._want_prefilter() else None
             self._pre_ran = pre is not None
+            # the listed launch is sized from the last listed share that came back (+25 %
+            # and a margin; anything beyond goes to a small grid-stride launch)
+            frac = getattr(self, "_pre_frac", None)
+            est = -1 if frac is None else min(n, int(frac * n * 1.25) + 16384)
             self.ops.x3_assign(self.x, self.xh[:n], self.xl[:n], self.ch, self.cl, self.cnorm,
                                self.cnhl, Cx, labels, None, amb, self.cstat, self.amb_count, True,
-                               pre, self.xnhl[:n] if pre is not None else None)
+                               pre, self.xnhl[:n] if pre is not None else None, est)
             if pre is not None and self._pre_ev is None and \
                     not torch.cuda.is_current_stream_capturing():
                 self._pre_host.copy_(self.amb_count[2:3], non_blocking=True)
@@ -1065,6 +1069,7 @@ class HipX3Lloyd(_LocalOpsBase):
         ev = self._pre_ev
         if ev is not None and ev.query():  # the count of an earlier assignment has landed
             self._pre_ev = None
+            self._pre_frac = int(self._pre_host[0]) / max(1, self._pre_n)
             if int(self._pre_host[0]) > self.PRE_MAX_FRAC * max(1, self._pre_n):
                 self._pre_off = self.PRE_RETRY - 1
                 return False

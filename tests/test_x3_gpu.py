@@ -284,3 +284,23 @@ def test_x3_prefilter_backs_off(gpu):
     assert lo.prefilter_rows() > 0  # tried again after PRE_RETRY skipped assignments
     bad, _ = _tie_ok(x.double(), c.double(), labels, 1e-6)
     assert bad == 0
+
+
+@pytest.mark.parametrize("frac", [0.0, 1.0])
+def test_x3_listed_launch_estimate(gpu, frac):
+    """The listed bf16x3 launch is sized from the previous listed share: a low estimate
+    leaves the rest to the grid-stride overflow launch, a high one to workgroups that
+    leave at once; the labels are exact either way."""
+    n, d, k = 60000, 128, 128
+    x, c = _blobs(n, d, k, seed=21, dtype=torch.float32)
+    x, c = x + 300.0, c + 300.0  # almost every row listed
+    xg, C = x.to(gpu), c.to(gpu).contiguous()
+    lo = _x3(xg, k, "fp32")
+    lo.prepare(C)
+    lo.PRE_MAX_FRAC = 2.0  # never back off here
+    lo._pre_frac = frac
+    labels = torch.full((n,), -1, dtype=torch.int32, device=gpu)
+    lo.assign(C, labels, None)
+    assert lo.prefilter_rows() > 40000
+    bad, _ = _tie_ok(x.double(), c.double(), labels, 1e-6)
+    assert bad == 0
