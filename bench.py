@@ -119,6 +119,9 @@ def parse(argv=None):
     ap.add_argument("--no-x3-prefilter", action="store_true",
                     help="fp32/fp64 K-Means: run the bf16x3 pass over every row (no one-product "
                          "prefilter; A/B of HipX3Lloyd.prefilter)")
+    ap.add_argument("--x3-full-grid", action="store_true",
+                    help="fp32/fp64 K-Means: size the listed bf16x3 launch by N instead of the "
+                         "last listed share (A/B of HipX3Lloyd.listed_estimate)")
     ap.add_argument("--comm-mode", default="auto", choices=["auto", "allreduce", "rsag"],
                     help="partial-sum reduction (ClusterConfig.comm_mode); with "
                          "TDC_FORCE_COLLECTIVES=1 a world-1 run issues the RCCL calls too")
@@ -201,6 +204,8 @@ def main(argv=None):
         points_per_step = n_global
     if a.no_x3_prefilter and hasattr(getattr(eng, "local", None), "prefilter"):
         eng.local.prefilter = False
+    if a.x3_full_grid and hasattr(getattr(eng, "local", None), "listed_estimate"):
+        eng.local.listed_estimate = False
     init_s = None
     if hasattr(eng, "init_centroids") and getattr(eng, "c0", None) is None:
         # the centroid init, timed on its own (never inside the timed steps)

@@ -951,6 +951,7 @@ class HipX3Lloyd(_LocalOpsBase):
     chunk_elems = 1 << 27           # wide path: [rows, K] fp32 block per chunk
     max_chunk_rows = 1 << 20
     prefilter = True
+    listed_estimate = True  # size the listed launch from the last listed share (A/B knob)
     PRE_MAX_FRAC = 0.6   # listed share above which the one-product pass costs more than it saves
     PRE_RETRY = 16
 
@@ -1030,7 +1031,7 @@ class HipX3Lloyd(_LocalOpsBase):
             self._pre_ran = pre is not None
             # the listed launch is sized from the last listed share that came back (+25 %
             # and a margin; anything beyond goes to a small grid-stride launch)
-            frac = getattr(self, "_pre_frac", None)
+            frac = getattr(self, "_pre_frac", None) if self.listed_estimate else None
             est = -1 if frac is None else min(n, int(frac * n * 1.25) + 16384)
             self.ops.x3_assign(self.x, self.xh[:n], self.xl[:n], self.ch, self.cl, self.cnorm,
                                self.cnhl, Cx, labels, None, amb, self.cstat, self.amb_count, True,
