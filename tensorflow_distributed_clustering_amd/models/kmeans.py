@@ -186,6 +186,11 @@ class OomGuard:
         self.C.copy_(c0)
         self.local.prepare(self.C)
         self.n_iter = n0
+        # the delta update's running totals now describe the discarded step's assignment:
+        # timed iteration 1 must re-sum every row, as the reference's first iteration does
+        # (`scripts/distribuitedClustering.py:277-280`), not take a delta over a warm-up
+        if getattr(self, "delta", None) is not None:
+            self.delta.reset()
 
     def rollback(self, step: int) -> np.ndarray:
         """Centroids at the start of ``step`` (replicated, host fp64); resets n_iter."""

@@ -25,6 +25,7 @@ Variants (picked by :func:`make_lloyd_ops`):
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -1604,6 +1605,11 @@ def make_fcm_ops(x: torch.Tensor, k: int, dtype: str = "fp64", m: float = 2.0,
             return ops
         if fcm_mfma_wide_dim(d) is not None:
             return HipMfmaWideFCM(x, k, m, nan_to_zero)
+    force = os.environ.get("TDC_FCM_PATH", "")  # A/B only: tower | wide | wide64
+    if force == "tower" and d <= 256:
+        return HipTowerFCM(x, k, dtype, m, nan_to_zero)
+    if force in ("wide", "wide64"):
+        return HipWideFCM(x, k, "fp64" if force == "wide64" else dtype, m, nan_to_zero)
     if d <= 256:
         return HipTowerFCM(x, k, dtype, m, nan_to_zero)
     return HipWideFCM(x, k, dtype, m, nan_to_zero)

@@ -197,3 +197,28 @@ def test_warmup_step_leaves_no_trace(method):
         a.step()
         b.step()
     assert torch.equal(a.C, b.C) and a.n_iter == b.n_iter == 3
+
+
+def test_warmup_does_not_prepay_the_first_full_update():
+    """After the untimed warm-up, timed iteration 1 is a FULL update (every row re-summed),
+    as the reference's computation_time includes its first iteration's full work
+    (`scripts/distribuitedClustering.py:277-280`), and the run matches a cold engine."""
+    from tensorflow_distributed_clustering_amd.models.kmeans import LloydEngine
+    from tensorflow_distributed_clustering_amd.parallel.dist import init_comm
+    comm = init_comm("cpu")
+    x = gaussian_blobs(3000, 4, 6, seed=5, dtype=torch.float64)
+    cfg = tdc.ClusterConfig(n_clusters=6, max_iter=5, dtype="fp64", seed=3, update="delta",
+                            delta_refresh=0)
+    a, b = LloydEngine(x, cfg, comm, 3000, 0), LloydEngine(x, cfg, comm, 3000, 0)
+    assert a.delta is not None
+    a.warmup(force=True)
+    s0 = a.update_stats()
+    a.step()
+    s1 = a.update_stats()
+    assert s1["full_steps"] - s0["full_steps"] == 1, (s0, s1)
+    for _ in range(2):
+        a.step()
+    for _ in range(3):
+        b.step()
+    torch.testing.assert_close(a.C, b.C)
+    assert a.update_stats()["full_steps"] - s0["full_steps"] == b.update_stats()["full_steps"]
