@@ -60,8 +60,13 @@ PRESETS = {
     # nearest corrected (--fcm-distances x3: bf16x3), fp32 memberships, bf16 weights x the
     # bf16 rows in W^T X (ops.FCM_PRECISION, reported with the witness; --dtype fp32 runs
     # the exact fp32 tower), m = 2 (the reference's m = D = 128 would underflow every u^m)
+    # cluster_std 0.25: at the blob generator's default 1.0, m=2 FCM at D=128, K=1024 pulls
+    # every centroid onto the grand mean within the timed steps (distance concentration;
+    # the final-state witness was then vacuous, final_ws_spread 0.0); at 0.25 the clusters
+    # keep their structure (tests/test_bench_cpu.py::test_fcm10m_preset_keeps_structure)
     "fcm10m": dict(n_per_gpu=10_000_000, dim=128, k=1024, scaling="weak", mode="lloyd",
-                   dtype="bf16", method="fcm", fuzzifier=2.0, fcm_distances="one"),
+                   dtype="bf16", method="fcm", fuzzifier=2.0, fcm_distances="one",
+                   cluster_std=0.25),
 }
 
 
@@ -78,6 +83,9 @@ def parse(argv=None):
                     help="strong: --n-per-gpu is the total N split over the ranks; weak: "
                          "every rank owns --n-per-gpu rows")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cluster-std", type=float, default=1.0,
+                    help="standard deviation of the synthetic Gaussian blobs (centres "
+                         "uniform in [-10, 10]^D)")
     ap.add_argument("--preset", default="headline", choices=sorted(PRESETS),
                     help="BASELINE config: headline (N=10M total D=128 K=1024, strong "
                          "scaling, default), headline_weak (10M per GPU), "
@@ -176,7 +184,8 @@ def main(argv=None):
     if a.source == "host":
         x, src_info = host_shard(a, e - s, s, dev, torch)
     else:
-        x = gaussian_blobs(e - s, a.dim, a.k, seed=a.seed, row_offset=s, dtype=dt, device=dev)
+        x = gaussian_blobs(e - s, a.dim, a.k, seed=a.seed, row_offset=s, dtype=dt, device=dev,
+                           cluster_std=a.cluster_std)
     cfg = tdc.ClusterConfig(n_clusters=a.k, max_iter=a.steps, dtype=a.dtype, init=a.init,
                             seed=a.seed, compute_inertia=False, algorithm=a.algorithm,
                             fuzzifier=a.fuzzifier, update=a.update,
@@ -308,7 +317,8 @@ def main(argv=None):
                                         else BASELINE_POINTS_PER_SEC),
             "dtype": a.dtype,
             "precision": precision_of(eng, a),
-            "data": "synthetic gaussian blobs (on-device, counter-based), random-row init",
+            "data": "synthetic gaussian blobs (on-device, counter-based, std "
+                    f"{a.cluster_std:g}), random-row init",
             "preset": a.preset,
             "init": {"method": a.init, "seconds": init_s},
             "iters_per_sec": 1e3 / ms,

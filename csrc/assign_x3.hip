@@ -54,13 +54,16 @@ __global__ __launch_bounds__(256) void x3_split_kernel(const T* __restrict__ src
                                                        int neg2, __bf16* __restrict__ hi,
                                                        __bf16* __restrict__ lo,
                                                        float* __restrict__ norm,
-                                                       float2* __restrict__ nhl) {
+                                                       float2* __restrict__ nhl,
+                                                       const T* __restrict__ shift) {
   const int lane = threadIdx.x & 63;
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows;
        row += (int64_t)gridDim.x * 4) {
     double s = 0.0, sh = 0.0, sl = 0.0;
     for (int c = lane; c < DP; c += 64) {
-      const T v = (row < valid && c < d) ? src[row * ld + c] : (T)0;
+      // shift (nullable): the split terms and norms are of v - shift (argmin-invariant);
+      // the bounds then scale with the spread of the data instead of its offset
+      const T v = (row < valid && c < d) ? src[row * ld + c] - (shift ? shift[c] : (T)0) : (T)0;
       s += (double)v * (double)v;
       const T t = neg2 ? (T)-2 * v : v;
       const __bf16 th = (__bf16)(float)t;
@@ -657,7 +660,8 @@ int launch_x3(const void* Xh, const void* Xl, int64_t N, const void* Ch, const v
 using namespace tdc;
 
 int tdc_x3_split(int src_dtype, const void* src, int64_t rows, int64_t valid, int d, int64_t ld,
-                 int DP, int neg2, void* hi, void* lo, float* norm, float* nhl, hipStream_t s) {
+                 int DP, int neg2, void* hi, void* lo, float* norm, float* nhl, hipStream_t s,
+                 const void* shift) {
   if (rows <= 0) return 0;
   if (d > DP || DP % 32 != 0) return (int)hipErrorInvalidValue;
   int64_t blocks = (rows + 3) / 4;
@@ -665,11 +669,11 @@ int tdc_x3_split(int src_dtype, const void* src, int64_t rows, int64_t valid, in
   if (src_dtype == TDC_F32)
     hipLaunchKernelGGL(x3_split_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s,
                        (const float*)src, rows, valid, d, ld, DP, neg2, (__bf16*)hi, (__bf16*)lo, norm,
-                       (float2*)nhl);
+                       (float2*)nhl, (const float*)shift);
   else if (src_dtype == TDC_F64)
     hipLaunchKernelGGL(x3_split_kernel<double>, dim3((unsigned)blocks), dim3(256), 0, s,
                        (const double*)src, rows, valid, d, ld, DP, neg2, (__bf16*)hi, (__bf16*)lo, norm,
-                       (float2*)nhl);
+                       (float2*)nhl, (const double*)shift);
   else
     return (int)hipErrorInvalidValue;
   TDC_CHECK_LAUNCH();

@@ -635,7 +635,8 @@ void update_sorted_indexed(const at::Tensor& X, const at::Tensor& rowidx, const 
 
 // ---- fp32 / fp64 assignment on the matrix cores (kernels.h tdc_x3_*) ----
 void x3_split(const at::Tensor& src, int64_t valid, int64_t neg2, at::Tensor& hi, at::Tensor& lo,
-              const std::optional<at::Tensor>& norm, const std::optional<at::Tensor>& nhl) {
+              const std::optional<at::Tensor>& norm, const std::optional<at::Tensor>& nhl,
+              const std::optional<at::Tensor>& shift) {
   check_cuda(src, "src");
   check_rows(src, "src");
   TORCH_CHECK(src.scalar_type() == at::kFloat || src.scalar_type() == at::kDouble,
@@ -652,11 +653,15 @@ void x3_split(const at::Tensor& src, int64_t valid, int64_t neg2, at::Tensor& hi
   if (nhl.has_value() && nhl->defined())
     TORCH_CHECK(nhl->scalar_type() == at::kFloat && nhl->is_contiguous() && nhl->numel() >= 2 * rows,
                 "tdc.x3_split: nhl fp32 [rows, 2]");
+  if (shift.has_value() && shift->defined())
+    TORCH_CHECK(shift->scalar_type() == src.scalar_type() && shift->is_contiguous() &&
+                    shift->numel() >= src.size(1) && shift->device() == src.device(),
+                "tdc.x3_split: shift [d] of src's dtype");
   const DevGuard guard(src.device());
   check(tdc_x3_split(dcode(src.scalar_type()), src.data_ptr(), rows, valid, (int)src.size(1),
                      src.stride(0), DP, (int)neg2, hi.data_ptr(), lo.data_ptr(),
                      static_cast<float*>(opt_ptr(norm)), static_cast<float*>(opt_ptr(nhl)),
-                     cur_stream()),
+                     cur_stream(), opt_ptr(shift)),
         "x3_split");
 }
 
@@ -1197,7 +1202,7 @@ TORCH_LIBRARY(tdc, m) {
   m.def("delta_update(Tensor X, Tensor labels, Tensor(a!) prev, Tensor(b!) sums, Tensor(c!) counts, Tensor(d!) work, Tensor(e!) ctrl, Tensor(f!)? cnt_hi=None, Tensor(g!)? cnt_lo=None, Tensor(h!)? moved=None, Tensor(i!)? zero_first=None, float fixed_scale=0.0, bool work_clean=False) -> ()");
   m.def("delta_finalize(Tensor sums, Tensor counts, Tensor? cnt_hi, Tensor? cnt_lo, Tensor? moved, Tensor(a!) G, Tensor(b!) C, int policy, Tensor(c!)? shift, Tensor(d!)? Cm2, Tensor(e!)? cnorm, Tensor(f!) ctrl, Tensor(g!)? stats, int refresh, float theta_n, float fixed_scale=0.0) -> ()");
   m.def("sculley_update(Tensor sums, Tensor counts, Tensor(a!) C, Tensor(b!) v, Tensor(c!)? shift, Tensor(d!)? Cm2, Tensor(e!)? cnorm) -> ()");
-  m.def("x3_split(Tensor src, int valid, int neg2, Tensor(a!) hi, Tensor(b!) lo, Tensor(c!)? norm, Tensor(d!)? nhl=None) -> ()");
+  m.def("x3_split(Tensor src, int valid, int neg2, Tensor(a!) hi, Tensor(b!) lo, Tensor(c!)? norm, Tensor(d!)? nhl=None, Tensor? shift=None) -> ()");
   m.def("x3_prep(Tensor cnorm, Tensor? nhl, int K, Tensor(a!) cstat, Tensor(b!) amb_count) -> ()");
   m.def("x3_assign(Tensor X, Tensor Xh, Tensor Xl, Tensor Ch, Tensor Cl, Tensor cnorm, Tensor cnhl, Tensor C, Tensor(a!) labels, Tensor(b!)? mind, Tensor(c!) amb, Tensor(d!) cstat, Tensor(e!) amb_count, bool recheck=True, Tensor(f!)? pre=None, Tensor? xnhl=None, int pre_est=-1) -> ()");
   m.def("x3_rows(Tensor G, int row0, Tensor xx, Tensor cstat, int DP, Tensor(a!) labels, Tensor(b!) amb, Tensor(c!) amb_count) -> ()");

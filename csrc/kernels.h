@@ -63,7 +63,8 @@ int tdc_bounds_scatter(const int32_t* active, const int* count, int64_t cap,
 //          point i is row rowidx[i], count read on the device; est_rows > 0 sizes the launch
 //          for that many rows, with a grid-stride launch for any overflow).
 int tdc_x3_split(int src_dtype, const void* src, int64_t rows, int64_t valid, int d, int64_t ld,
-                 int DP, int neg2, void* hi, void* lo, float* norm, float* nhl, hipStream_t stream);
+                 int DP, int neg2, void* hi, void* lo, float* norm, float* nhl, hipStream_t stream,
+                 const void* shift = nullptr);  // shift: [d] of src's dtype, subtracted first
 int tdc_x3_prep(const float* cnorm, const float* nhl, int K, float* cstat, int* amb_count,
                 hipStream_t stream, int nzero = 2);
 int tdc_x3_prefilter(const void* Xh, int64_t N, int DP, const void* Ch, const float* cnorm, int Kp,

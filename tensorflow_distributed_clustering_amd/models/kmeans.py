@@ -662,6 +662,13 @@ class LloydEngine(OomGuard):
         self.C.copy_(snapshot[0])
         self.local.prepare(self.C)
         self.n_iter = snapshot[1]
+        if self.delta is not None:
+            self.delta.reset()  # the warm-up's assignment is not this state's (as warmup())
+        settle = getattr(self.local, "settle", None)
+        if settle is not None:
+            # host-side choices a replay cannot revisit (the x3 prefilter and its listed
+            # launch size) are made from the warm-up step's measured state
+            settle()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self._eager_step()
@@ -803,7 +810,7 @@ class KMeans:
             # fp32 MFMA path's hi/lo rows): a shard that fits only without them streams
             delta = cfg.update != "full"
             extra = lloyd_row_extra(cfg.dtype, d, delta)
-            fixed = lloyd_fixed_extra(cfg.n_clusters, d, delta)
+            fixed = lloyd_fixed_extra(cfg.n_clusters, d, delta, cfg.dtype, xn.shape[0])
             chunk = want or plan_chunk_rows(xn.shape[0], row_bytes, cfg.n_clusters, d, dev,
                                             cfg.hbm_budget_gb, per_row_extra=extra,
                                             extra_fixed=fixed)

@@ -974,7 +974,7 @@ class HipX3Lloyd(_LocalOpsBase):
         # [0] two-candidate list, [1] full re-scan list, [2] the prefilter's listed rows
         self.amb_count = torch.zeros(3, dtype=torch.int32, device=dev)
         self.xh = self.xl = self.xx = self.amb = self.G = self.pre = self.xnhl = None
-        self.x = None
+        self.x = self.mu = None
         self._set_x(x)
         self.update = NativeUpdate(self.ops, self.n, k, self.d, self.c_dtype, dev)
 
@@ -995,10 +995,21 @@ class HipX3Lloyd(_LocalOpsBase):
             self.xnhl = torch.empty(max(n, 1), 2, dtype=torch.float32, device=dev) if pre_ok else None
         self.x = x
         self.n = n
+        if self.mu is None and n >= 2:
+            # fixed shift (this rank's first rows' mean; a streamed engine's one-row probe:
+            # the first centroids' mean, set in prepare): rows and centroids are split as
+            # v - mu, so the error bounds scale with the data's spread, not its offset
+            # (uncentred data otherwise fails the bound and re-scans exactly); the argmin
+            # is shift-invariant and the exact re-check reads the unshifted rows
+            self.mu = x[:, : self.d].double().mean(0).to(self.c_dtype).contiguous()
+        self._split_rows()
+
+    def _split_rows(self):
+        n, x = self.n, self.x
         if n:
             self.ops.x3_split(x[:, : self.d], n, 0, self.xh[:n], self.xl[:n],
                               self.xx[:n] if self.wide else None,
-                              self.xnhl[:n] if self.xnhl is not None else None)
+                              self.xnhl[:n] if self.xnhl is not None else None, self.mu)
 
     @property
     def layout(self):
@@ -1012,8 +1023,11 @@ class HipX3Lloyd(_LocalOpsBase):
         return self
 
     def prepare(self, C):
-        self.ops.x3_split(C.to(self.c_dtype).contiguous(), self.k, 1, self.ch, self.cl, self.cnorm,
-                          self.cnhl)
+        Cx = C.to(self.c_dtype).contiguous()
+        if self.mu is None:
+            self.mu = Cx[: self.k, : self.d].double().mean(0).to(self.c_dtype).contiguous()
+            self._split_rows()  # rows already split without it
+        self.ops.x3_split(Cx, self.k, 1, self.ch, self.cl, self.cnorm, self.cnhl, self.mu)
 
     def _chunk_rows(self):
         rows = max(1, min(self.n, self.chunk_elems // max(1, self.k), self.max_chunk_rows))
@@ -1077,6 +1091,15 @@ class HipX3Lloyd(_LocalOpsBase):
                 return False
         return True
 
+    def settle(self):
+        """Wait for the last assignment's listed count and take it in (before a graph
+        capture: the replay keeps the prefilter choice and sizes the listed launch from
+        this share, instead of the full-size launch of an unknown share)."""
+        ev = getattr(self, "_pre_ev", None)
+        if ev is not None:
+            ev.synchronize()
+            self._want_prefilter()
+
     def ambiguous_rows(self) -> int:
         """Rows the last assignment re-checked exactly (host read; diagnostics)."""
         return int(self.amb_count[:2].sum().item())
@@ -1125,10 +1148,20 @@ def lloyd_row_extra(dtype: str, d: int, delta: bool = True) -> int:
     return extra
 
 
-def lloyd_fixed_extra(k: int, d: int, delta: bool = True) -> int:
+def lloyd_fixed_extra(k: int, d: int, delta: bool = True, dtype: Optional[str] = None,
+                      n: Optional[int] = None) -> int:
     """Device bytes a Lloyd shard holds independent of its rows beyond the planner's
-    default: the delta update's fp64 running totals."""
-    return (k * d + k) * 8 if delta else 0
+    default: the delta update's fp64 running totals; on the wide fp32 / fp64 MFMA path
+    (HipX3Lloyd, D > 256) the [rows, K] fp32 score block of a row chunk; and the
+    inertia pass's difference block (_exact_mind, 2^28 bytes)."""
+    extra = (k * d + k) * 8 if delta else 0
+    if dtype in ("fp32", "fp64") and d > X3_MIN_D and x3_dim(d) is not None:
+        if x3_dim(d) > X3_DIMS[-1]:
+            rows = min(n if n is not None else HipX3Lloyd.max_chunk_rows,
+                       HipX3Lloyd.chunk_elems // max(1, k), HipX3Lloyd.max_chunk_rows)
+            extra += max(1, rows) * k * 4
+        extra += 1 << 28
+    return extra
 
 
 def lloyd_layout(dtype: str, d: int):
@@ -1296,7 +1329,8 @@ def fcm_mfma_dim(d: int) -> Optional[int]:
 
 
 class HipMfmaFCM(_LocalOpsBase):
-    """fp32 FCM on bf16 matrix cores (csrc/fcm_mfma.hip): the shard is split once into
+    """bf16 / fp8 FCM (``--dtype bf16``) on bf16 matrix cores (csrc/fcm_mfma.hip); fp32 and
+    fp64 FCM run the exact towers instead (make_fcm_ops).  The shard is split once into
     hi/lo bf16 rows (+ fp32 norms), the centroids every iteration; a stats pass (row
     normaliser + label) and an accumulate pass (distances -> w -> W^T X, all on MFMA)."""
     name = "hip_fcm_mfma"
@@ -1449,7 +1483,7 @@ def fcm_mfma_wide_dim(d: int) -> Optional[int]:
 
 
 class HipMfmaWideFCM(HipMfmaFCM):
-    """fp32 FCM for 128 < D <= 1024 on bf16 matrix cores (csrc/fcm_mfma.hip wide_*): the
+    """bf16 / fp8 FCM for 128 < D <= 1024 on bf16 matrix cores (csrc/fcm_mfma.hip wide_*): the
     tower's hi/lo operands no longer fit a wave's registers, so each row chunk runs
     three native kernels with its [rows, K] block G in HBM, like HipWideFCM, but with both
     products on MFMA: distances (xh ch + xh cl + xl ch) into G, memberships w = u^m in
@@ -1560,21 +1594,28 @@ FCM_PRECISION = {
     "fp64": "fp64 distances (difference form; D > 256: the GEMM expansion on the fp64 matrix "
             "cores), fp64 memberships and sums",
     "fp32": "fp32 difference-form distances and memberships, fp64 sums",
-    "bf16": "bf16x3 MFMA distances (fp32-faithful), fp32 memberships, bf16 weights in the "
-            "W^T X MFMAs (hi+lo rows), fp64 sums",
+    # HipMfmaFCM, fcm_distances='x3' (default).  Measured against the fp64 oracle at m=2
+    # (tests/test_fcm_gpu.py): sum_i w within 2e-3*m (hi+lo rows) / 3e-3*m (bf16 rows) --
+    # NOT fp32-faithful: the stats pass's row normaliser keeps one-product terms for all
+    # but the two nearest centroids
+    "bf16": "stats pass (row normaliser, label): one bf16 product (x_hi . c_hi) per "
+            "centroid, each row's two nearest corrected to bf16x3 (D >= 64; bf16x3 for all "
+            "below); accumulate pass: bf16x3 distances; fp32 memberships, bf16 weights in the "
+            "W^T X MFMAs (hi+lo rows), fp64 sums; sum w within ~2e-3*m of fp64",
     # ... on a bf16 shard from D = 64: W^T X takes the bf16 rows themselves (exact products)
-    "bf16_raw": "bf16x3 MFMA distances (fp32-faithful), fp32 memberships; W^T X = bf16 "
-                "weights x the bf16 rows (exact products, fp32 accumulate), fp64 sums",
-    # HipMfmaFCM from D = 64: both passes run one product and correct the two nearest
-    "bf16_one": "bf16 MFMA distances: one product (x_hi . c_hi, ~2^-9/sqrt(D) relative error "
-                "on x.c) for every centroid, each row's two nearest corrected to bf16x3 "
-                "(fp32-faithful); fp32 memberships, bf16 weights in the W^T X MFMAs (hi+lo "
-                "rows), fp64 sums",
+    "bf16_raw": "stats pass: one bf16 product per centroid, each row's two nearest corrected "
+                "to bf16x3; accumulate pass: bf16x3 distances; fp32 memberships; W^T X = bf16 "
+                "weights x the bf16 rows (exact products, fp32 accumulate), fp64 sums; sum w "
+                "within ~3e-3*m of fp64",
+    # HipMfmaFCM from D = 64, fcm_distances='one': both passes one product + the fix-up
+    "bf16_one": "both passes: one bf16 product (x_hi . c_hi, ~2^-9/sqrt(D) relative error "
+                "on x.c) per centroid, each row's two nearest corrected to bf16x3; fp32 "
+                "memberships, bf16 weights in the W^T X MFMAs (hi+lo rows), fp64 sums",
     # ... on a bf16 shard: W^T X takes the bf16 rows themselves (exact products)
-    "bf16_one_raw": "bf16 MFMA distances: one product (x_hi . c_hi, ~2^-9/sqrt(D) relative "
-                    "error on x.c) for every centroid, each row's two nearest corrected to "
-                    "bf16x3 (fp32-faithful); fp32 memberships; W^T X = bf16 weights x the bf16 "
-                    "rows (exact products, fp32 accumulate), fp64 sums",
+    "bf16_one_raw": "both passes: one bf16 product (x_hi . c_hi, ~2^-9/sqrt(D) relative "
+                    "error on x.c) per centroid, each row's two nearest corrected to bf16x3; "
+                    "fp32 memberships; W^T X = bf16 weights x the bf16 rows (exact products, "
+                    "fp32 accumulate), fp64 sums",
 }
 
 

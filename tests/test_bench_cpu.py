@@ -116,3 +116,16 @@ def test_bench_from_init_equals_fit():
             assert d["timed_from"] == "init" and d["ms_per_step_steady"] is None
             outs.append(np.load(out))
     np.testing.assert_allclose(outs[0], outs[1], rtol=1e-12, atol=1e-12)
+
+
+def test_fcm10m_preset_keeps_structure():
+    """The fcm10m preset's data (blobs at cluster_std 0.25) keeps cluster structure under
+    m = 2 FCM at D = 128, K = 1024: the final-state witness is informative
+    (final_ws_spread > 0.1, per-cluster weight sums differ) instead of the collapsed,
+    trivially exact state of round 5 (all centroids on the grand mean, spread 0.0).
+    Reduced N and the exact fp32 path here; the preset's D, K, m and generator."""
+    d = _run(["--preset", "fcm10m", "--n-per-gpu", "20000", "--dtype", "fp32", "--steps", "6",
+              "--warmup", "0", "--no-steady"], timeout=900)
+    assert d["config"]["D"] == 128 and d["config"]["K"] == 1024
+    assert d["config"]["fuzzifier"] == 2.0 and "std 0.25" in d["data"]
+    assert d["check"]["final_ws_spread"] > 0.1, d["check"]

@@ -231,7 +231,10 @@ def test_listed_rescan_matches_exact(gpu, dtype, m):
 def test_x3_prefilter_same_labels(gpu, dtype, n, d, k, offset):
     """The one-product prefilter only decides rows its own bound certifies: the labels are
     those of the plain three-product pass (both exact up to the dtype's rounding).  The
-    offset case (|x| >> the cluster gaps) leaves most rows to the three products."""
+    offset case (|x| >> the cluster gaps): the split subtracts a fixed shift (the rows'
+    mean), so the bounds scale with the spread and the offset data certifies as well as
+    centred data (before the shift it left most rows to the three products and the exact
+    re-scan)."""
     tdt = torch.float32 if dtype == "fp32" else torch.float64
     x, c = _blobs(n, d, k, seed=d + k, dtype=tdt)
     x, c = x + offset, c + offset
@@ -255,19 +258,29 @@ def test_x3_prefilter_same_labels(gpu, dtype, n, d, k, offset):
         da = d64.gather(1, la.cpu()[diff].long()[:, None]).squeeze(1)
         db = d64.gather(1, lb.cpu()[diff].long()[:, None]).squeeze(1)
         assert torch.all((da - db).abs() <= rel * db.abs() + 1e-30)
-    if offset == 0.0:
-        assert listed < 0.5 * n, listed  # blob data: most rows certify on one product
-    else:
-        assert listed > 0
+    assert listed < 0.5 * n, listed  # blob data: most rows certify on one product
+    assert lo.ambiguous_rows() <= 0.2 * n  # ... and on three
+
+
+def _near_ties(n, d, k, seed, dtype, delta=1e-3):
+    """Rows between two random centroids at t = 0.5 +- delta: a distance gap of ~4 delta
+    ||c_a - c_b||^2, below the one-product bound (~2^-8 |x||c|) and far above the
+    three-product one, at any shift."""
+    g = torch.Generator().manual_seed(seed)
+    c = torch.randn(k, d, generator=g, dtype=torch.float64) * 4
+    a = torch.randint(0, k, (n,), generator=g)
+    b = (a + 1 + torch.randint(0, k - 1, (n,), generator=g)) % k
+    t = 0.5 + (torch.rand(n, generator=g, dtype=torch.float64) - 0.5) * 2 * delta
+    x = c[a] * t[:, None] + c[b] * (1 - t[:, None])
+    return x.to(dtype), c.to(dtype)
 
 
 def test_x3_prefilter_backs_off(gpu):
-    """Data where the one-product bound certifies almost nothing (|x| >> the cluster gaps):
-    once the listed count has come back, the prefilter is skipped for PRE_RETRY
-    assignments, and the labels stay exact either way."""
+    """Data where the one-product bound certifies almost nothing (rows near ties of two
+    centroids): once the listed count has come back, the prefilter is skipped for
+    PRE_RETRY assignments, and the labels stay exact either way."""
     n, d, k = 20000, 128, 128
-    x, c = _blobs(n, d, k, seed=9, dtype=torch.float32)
-    x, c = x + 300.0, c + 300.0
+    x, c = _near_ties(n, d, k, seed=9, dtype=torch.float32)
     xg, C = x.to(gpu), c.to(gpu).contiguous()
     lo = _x3(xg, k, "fp32")
     lo.prepare(C)
@@ -292,8 +305,7 @@ def test_x3_listed_launch_estimate(gpu, frac):
     leaves the rest to the grid-stride overflow launch, a high one to workgroups that
     leave at once; the labels are exact either way."""
     n, d, k = 60000, 128, 128
-    x, c = _blobs(n, d, k, seed=21, dtype=torch.float32)
-    x, c = x + 300.0, c + 300.0  # almost every row listed
+    x, c = _near_ties(n, d, k, seed=21, dtype=torch.float32)  # almost every row listed
     xg, C = x.to(gpu), c.to(gpu).contiguous()
     lo = _x3(xg, k, "fp32")
     lo.prepare(C)
@@ -302,5 +314,31 @@ def test_x3_listed_launch_estimate(gpu, frac):
     labels = torch.full((n,), -1, dtype=torch.int32, device=gpu)
     lo.assign(C, labels, None)
     assert lo.prefilter_rows() > 40000
+    bad, _ = _tie_ok(x.double(), c.double(), labels, 1e-6)
+    assert bad == 0
+
+
+def test_x3_listed_overflow_multiblock(gpu):
+    """The listed launch's grid-stride overflow kernel (LISTED = 2) with several point
+    blocks per workgroup: the LDS ring is reused across blocks (the __syncthreads before
+    each later block) and the lane constants are rebuilt per block.  ~1M listed rows against
+    a one-shot launch sized for 16K (the estimate of a share of 0) leave the overflow grid
+    (<= the resident workgroups, 256 rows each) >= 3 blocks per workgroup; the labels are
+    the fp64 argmin."""
+    from tensorflow_distributed_clustering_amd import _native
+    n, d, k = 1_000_000, 128, 64
+    x, c = _near_ties(n, d, k, seed=33, dtype=torch.float32)
+    xg, C = x.to(gpu), c.to(gpu).contiguous()
+    lo = _x3(xg, k, "fp32")
+    lo.prepare(C)
+    lo.PRE_MAX_FRAC = 2.0
+    lo._pre_frac = 0.0
+    labels = torch.full((n,), -1, dtype=torch.int32, device=gpu)
+    lo.assign(C, labels, None)
+    torch.cuda.synchronize()
+    listed = lo.prefilter_rows()
+    cus = torch.cuda.get_device_properties(gpu).multi_processor_count
+    assert listed - 16384 > 3 * (4 * cus) * 256, (listed, cus)  # >= 3 blocks per workgroup
+    assert int(labels.min()) >= 0
     bad, _ = _tie_ok(x.double(), c.double(), labels, 1e-6)
     assert bad == 0
