@@ -335,6 +335,46 @@ void fcm_wide(int64_t pass, const at::Tensor& X, const at::Tensor& C, double m, 
         "fcm_wide");
 }
 
+// fp64 FCM with fused row statistics (kernels.h tdc_fcm_f64t): pass 0 G = t, rowinfo,
+// labels; pass 1 wx / ws += W^T X / sum W with w from G and rowinfo
+void fcm_f64t(int64_t pass, const at::Tensor& X, const at::Tensor& C, double m, bool nan_to_zero,
+              at::Tensor& G, at::Tensor& rowinfo, const std::optional<at::Tensor>& labels,
+              const std::optional<at::Tensor>& wx, const std::optional<at::Tensor>& ws) {
+  check_cuda(X, "X");
+  check_rows(X, "X");
+  TORCH_CHECK(X.scalar_type() == at::kDouble, "tdc.fcm_f64t: X fp64");
+  TORCH_CHECK(C.scalar_type() == at::kDouble && C.is_contiguous() && C.dim() == 2 &&
+                  C.size(1) == X.size(1), "tdc.fcm_f64t: C [K, D] fp64");
+  const int64_t M = X.size(0), K = C.size(0);
+  TORCH_CHECK(G.scalar_type() == at::kDouble && G.is_contiguous() && G.numel() >= M * K,
+              "tdc.fcm_f64t: G [M, K] fp64");
+  TORCH_CHECK(rowinfo.scalar_type() == at::kDouble && rowinfo.is_contiguous() &&
+                  rowinfo.numel() >= M, "tdc.fcm_f64t: rowinfo fp64 [M]");
+  TORCH_CHECK(m > 1.0, "tdc.fcm_f64t: fuzzifier must be > 1");
+  TORCH_CHECK(pass == 0 || pass == 1, "tdc.fcm_f64t: pass 0 or 1");
+  int32_t* lab = nullptr;
+  double *pwx = nullptr, *pws = nullptr;
+  if (pass == 0) {
+    TORCH_CHECK(labels.has_value() && labels->defined() && labels->scalar_type() == at::kInt &&
+                    labels->is_contiguous() && labels->numel() >= M,
+                "tdc.fcm_f64t: labels int32 [M]");
+    lab = labels->data_ptr<int32_t>();
+  } else {
+    TORCH_CHECK(wx.has_value() && ws.has_value() && wx->scalar_type() == at::kDouble &&
+                    ws->scalar_type() == at::kDouble && wx->is_contiguous() &&
+                    ws->is_contiguous() && wx->numel() == C.numel() && ws->numel() == K,
+                "tdc.fcm_f64t: wx [K, D] / ws [K] fp64");
+    pwx = wx->data_ptr<double>();
+    pws = ws->data_ptr<double>();
+  }
+  const DevGuard guard(X.device());
+  check(tdc_fcm_f64t((int)pass, X.data_ptr<double>(), M, X.stride(0), (int)X.size(1),
+                     C.data_ptr<double>(), (int)K, m, nan_to_zero ? 1 : 0, G.data_ptr<double>(),
+                     rowinfo.data_ptr<double>(), lab, pwx, pws, num_cus(X.device().index()),
+                     cur_stream()),
+        "fcm_f64t");
+}
+
 // the row pass of the wide towers alone (G [M, K] of d2 -> labels, and w in place)
 void fcm_wide_rows(at::Tensor& G, int64_t K, double m, bool nan_to_zero, at::Tensor& labels,
                    bool write_w) {
@@ -1180,6 +1220,7 @@ TORCH_LIBRARY(tdc, m) {
   m.def("fcm_tower_accum(Tensor X, Tensor C, float m, bool nan_to_zero, Tensor rowinfo, Tensor(a!) wx, Tensor(b!) ws) -> ()");
   m.def("fcm_wide(int stage, Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!) G, Tensor(b!)? labels=None, Tensor(c!)? wx=None, Tensor(d!)? ws=None) -> ()");
   m.def("fcm_wide_rows(Tensor(a!) G, int K, float m, bool nan_to_zero, Tensor(b!) labels, bool write_w) -> ()");
+  m.def("fcm_f64t(int stage, Tensor X, Tensor C, float m, bool nan_to_zero, Tensor(a!) G, Tensor(b!) rowinfo, Tensor(c!)? labels=None, Tensor(d!)? wx=None, Tensor(e!)? ws=None) -> ()");
   m.def("fcm_mfma_wide_workspace(Tensor like, int M, int Kp, int DP) -> int");
   m.def("fcm_mfma_wide(int stage, Tensor Xh, Tensor Xl, Tensor xx, Tensor Ch, Tensor Cl, Tensor cc, int K, int D, Tensor(a!) G, Tensor(b!)? work=None, Tensor? shift=None, Tensor(c!)? wx=None, Tensor(d!)? ws=None) -> ()");
   m.def("fcm_split_rows(Tensor src, int valid, int neg2, Tensor(a!) hi, Tensor(b!) lo, Tensor(c!)? norm, Tensor? shift=None) -> ()");
@@ -1226,6 +1267,7 @@ TORCH_LIBRARY_IMPL(tdc, CUDA, m) {
   m.impl("fcm_tower_accum", &fcm_tower_accum);
   m.impl("fcm_wide", &fcm_wide);
   m.impl("fcm_wide_rows", &fcm_wide_rows);
+  m.impl("fcm_f64t", &fcm_f64t);
   m.impl("fcm_mfma_wide_workspace", &fcm_mfma_wide_workspace);
   m.impl("fcm_mfma_wide", &fcm_mfma_wide);
   m.impl("finalize", &finalize);

@@ -66,9 +66,19 @@ __device__ __forceinline__ float fm_t(float dd, float expo) {
   else if constexpr (FM == 5) return __builtin_amdgcn_rsqf(__builtin_sqrtf(dd));
   else return exp2f(log2f(dd) * expo);
 }
+// 1 / dd in fp64 for finite dd > 0: the v_rcp_f64 estimate refined by two Newton steps
+// (5 fp64 operations against root_rcp<1>'s ~9), with root_rcp's exponent split kept for
+// dd whose reciprocal leaves the normal range
+__device__ __forceinline__ double rcp_f64_nr(double dd) {
+  double y = __builtin_amdgcn_rcp(dd);
+  y = fma(y, fma(-dd, y, 1.0), y);
+  y = fma(y, fma(-dd, y, 1.0), y);
+  return (dd > 0x1p-1000 && dd < 0x1p1000) ? y : root_rcp<1>(dd);
+}
+
 template <int FM>
 __device__ __forceinline__ double fm_t(double dd, double expo) {
-  if constexpr (FM == 2) return root_rcp<1>(dd);
+  if constexpr (FM == 2) return rcp_f64_nr(dd);
   else if constexpr (FM == 5) return root_rcp<4>(dd);
   else return exp2(log2(dd) * expo);
 }

@@ -391,10 +391,17 @@ __global__ __launch_bounds__(256, 1) void fcm_wide_d2_f64m_kernel(
 
 // wx[k, d] += sum_r W[r, k] x[r, d] over one split's rows (128 x 128 output tile per block);
 // ws[k] += sum_r W[r, k] (feature-tile-0 blocks); one fp64 atomic per output per block
-__global__ __launch_bounds__(256, 1) void fcm_wide_wtx_f64m_kernel(
+// WT >= 0: G holds t (fcm_f64_tstats_kernel) and w = fm_w<WT>(t * rowinfo) is formed while
+// staging (rowinfo < 0: one-hot over the row's t = inf, == 0: all zero); WT < 0: G holds w
+template <int WT, int NW = 4>
+__global__ __launch_bounds__(NW * 64, 1) void fcm_wide_wtx_f64m_kernel(
     const double* __restrict__ W, const double* __restrict__ X, int64_t M, int64_t ldx, int D,
     int K, int nkt, int ndt, int64_t rows_per_split, double* __restrict__ wx,
-    double* __restrict__ ws) {
+    double* __restrict__ ws, const double* __restrict__ rowinfo = nullptr, double m = 2.0) {
+  // NW = 4: 2 x 2 waves of 64 x 64 outputs (acc[4][4]: one wave per SIMD); NW = 8: 4 x 2
+  // waves of 32 x 64 (acc[2][4]: two waves per SIMD, one hides the other's staging / barrier)
+  constexpr int NT = NW * 64;
+  constexpr int WRN = NW / 2, TI = F64T / WRN / 16;
   constexpr int PW = F64T + 16;  // 1152-B rows (= 128 mod 256): the two 16-lane groups of a
                                  // b64 fragment read fall on disjoint bank halves
   __shared__ double s_w[2][F64S_W * PW];
@@ -414,19 +421,26 @@ __global__ __launch_bounds__(256, 1) void fcm_wide_wtx_f64m_kernel(
   const int k0 = kt * F64T, d0 = dt * F64T;
   const int64_t a = split * rows_per_split;
   const int64_t b = min(M, a + rows_per_split);
-  // staging: thread t loads 8 consecutive columns (t & 15) * 8 of stage rows (t >> 4) + 16 j
-  constexpr int RPT = F64S_W / 16;
+  // staging: thread t loads 8 consecutive columns (t & 15) * 8 of stage rows (t >> 4) + j NT/16
+  constexpr int RPT = F64S_W * 16 / NT;
   const int srow = tid >> 4, scol = (tid & 15) * 8;
   double vw[RPT][8], vx[RPT][8];
   auto load = [&](int64_t rs) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < RPT; ++j) {
-      const int64_t r = rs + srow + 16 * j;
+      const int64_t r = rs + srow + (NT / 16) * j;
       const bool rok = r < b;
+      double info = 0.0;
+      if constexpr (WT >= 0) info = rok ? rowinfo[r] : 0.0;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int k = k0 + scol + e, d = d0 + scol + e;
-        vw[j][e] = (rok && k < K) ? W[r * (int64_t)K + k] : 0.0;
+        double v = (rok && k < K) ? W[r * (int64_t)K + k] : 0.0;
+        if constexpr (WT >= 0) {
+          const double u = info > 0.0 ? v * info : (info < 0.0 && v == (double)INFINITY ? -1.0 / info : 0.0);
+          v = u > 0.0 ? fm_w<WT>(u, m) : 0.0;
+        }
+        vw[j][e] = v;
         vx[j][e] = (rok && d < D) ? X[r * ldx + d] : 0.0;
       }
     }
@@ -436,13 +450,13 @@ __global__ __launch_bounds__(256, 1) void fcm_wide_wtx_f64m_kernel(
     for (int j = 0; j < RPT; ++j)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        s_w[buf][(srow + 16 * j) * PW + scol + e] = vw[j][e];
-        s_x[buf][(srow + 16 * j) * PW + scol + e] = vx[j][e];
+        s_w[buf][(srow + (NT / 16) * j) * PW + scol + e] = vw[j][e];
+        s_x[buf][(srow + (NT / 16) * j) * PW + scol + e] = vx[j][e];
       }
   };
-  f64x4 acc[4][4];
+  f64x4 acc[TI][4];
 #pragma unroll
-  for (int ti = 0; ti < 4; ++ti)
+  for (int ti = 0; ti < TI; ++ti)
 #pragma unroll
     for (int tj = 0; tj < 4; ++tj) acc[ti][tj] = f64x4{0.0, 0.0, 0.0, 0.0};
   double wsum = 0.0;
@@ -456,45 +470,209 @@ __global__ __launch_bounds__(256, 1) void fcm_wide_wtx_f64m_kernel(
   for (int64_t rs = a; rs < b; rs += F64S_W) {
     const bool more = rs + F64S_W < b;
     if (more) load(rs + F64S_W);
-    const double* sw = s_w[buf] + fk * PW + wr * 64 + fr;
+    const double* sw = s_w[buf] + fk * PW + wr * (TI * 16) + fr;
     const double* sx = s_x[buf] + fk * PW + wc * 64 + fr;
 #pragma unroll
     for (int kk = 0; kk < F64S_W / 4; ++kk) {
-      double av[4], bv[4];
+      double av[TI], bv[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        av[t] = sw[kk * 4 * PW + t * 16];
-        bv[t] = sx[kk * 4 * PW + t * 16];
-      }
+      for (int t = 0; t < TI; ++t) av[t] = sw[kk * 4 * PW + t * 16];
 #pragma unroll
-      for (int ti = 0; ti < 4; ++ti)
+      for (int t = 0; t < 4; ++t) bv[t] = sx[kk * 4 * PW + t * 16];
+#pragma unroll
+      for (int ti = 0; ti < TI; ++ti)
 #pragma unroll
         for (int tj = 0; tj < 4; ++tj)
           acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ti], bv[tj], acc[ti][tj], 0, 0, 0);
     }
-    // sum_r W[r, k]: stage s of the split goes to feature tile s % ndt, all four waves
-    // (thread t: column t & 127, rows of half t >> 7) -- one tile's waves alone carried it
+    // sum_r W[r, k]: stage s of the split goes to feature tile s % ndt, all waves (thread t:
+    // column t & 127, rows of group t >> 7) -- one tile's waves alone carried it
     if ((int)(((rs - a) / F64S_W) % ndt) == dt) {
+      constexpr int RG = F64S_W / (NT / 128);
 #pragma unroll
-      for (int r = 0; r < F64S_W / 2; ++r) wsum += s_w[buf][((tid >> 7) * (F64S_W / 2) + r) * PW + (tid & 127)];
+      for (int r = 0; r < RG; ++r) wsum += s_w[buf][((tid >> 7) * RG + r) * PW + (tid & 127)];
     }
     if (more) store(buf ^ 1);
     __syncthreads();
     buf ^= 1;
   }
 #pragma unroll
-  for (int ti = 0; ti < 4; ++ti)
+  for (int ti = 0; ti < TI; ++ti)
 #pragma unroll
     for (int tj = 0; tj < 4; ++tj) {
       const int d = d0 + wc * 64 + tj * 16 + fr;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int k = k0 + wr * 64 + ti * 16 + fk + 4 * q;
+        const int k = k0 + wr * (TI * 16) + ti * 16 + fk + 4 * q;
         const double v = acc[ti][tj][q];
         if (k < K && d < D && v != 0.0) atomicAdd(&wx[(int64_t)k * D + d], v);
       }
     }
   if (k0 + (tid & 127) < K && wsum != 0.0) atomicAdd(&ws[k0 + (tid & 127)], wsum);
+}
+
+// ---------------------------------------------------------------------------------------
+// fp64 FCM with the row statistics fused into the distance GEMM (round 6): the separate
+// row pass (fcm_wide_rows: read G, write w in place -- 2 x 8 B per element, 39 ms of a
+// 206 ms step at N=10M, D=128, K=1024) is gone.
+//   fcm_f64_tstats  one block = 128 rows x ALL centroid tiles (looped): per tile the f64-MFMA
+//                   distance expansion, then t = d2^(-1/(m-1)) (+inf on a centroid) written
+//                   to G, and the row's sum_k t, zero count and (d2, k) minimum carried
+//                   across tiles (16-lane DPP butterflies, one owner lane per row); at the
+//                   end rowinfo (fcm_wide_rows semantics) and the label
+//   fcm_wide_wtx_f64m_kernel<FM>  W^T X with w = (t * rowinfo)^m formed while staging
+// 8 waves x (16 rows x 128 centroids, acc[8]): a row's 128 tile columns live in one wave, and
+// the block fits two waves per SIMD; lane (fr, fk) holds rows fk + 4 q, columns 16 tj + fr.
+// ---------------------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+// one butterfly step over the 16 lanes of a DPP row: sum s, count z, min (d, k) by (d, k)
+template <int CTRL>
+__device__ __forceinline__ void row_step(double& s, int& z, double& d, int& k) {
+  s += dpp_f64<CTRL>(s);
+  z += dpp_i32<CTRL>(z);
+  const double od = dpp_f64<CTRL>(d);
+  const int ok = dpp_i32<CTRL>(k);
+  const bool take = od < d || (od == d && ok < k);
+  d = take ? od : d;
+  k = take ? ok : k;
+}
+
+template <int FM>
+__global__ __launch_bounds__(512, 1) void fcm_f64_tstats_kernel(
+    const double* __restrict__ X, int64_t M, int64_t ldx, int D, const double* __restrict__ C,
+    int K, int nct, double expo, int nz, double* __restrict__ G, double* __restrict__ rowinfo,
+    int32_t* __restrict__ labels) {
+  constexpr int PX = F64S_D + 2;
+  __shared__ double s_x[2][F64T * PX];
+  __shared__ double s_c[2][F64T * PX];
+  __shared__ double s_xn[F64T], s_cn[F64T], s_cs[F64T];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;  // 8 waves x 16 rows
+  const int64_t r0 = (int64_t)blockIdx.x * F64T;
+  constexpr int FPT = F64S_D / 4;
+  const int srow = tid >> 2, sch = (tid & 3) * FPT;  // staging: one X row + one C row
+  const double* xr = X + min(r0 + srow, M - 1) * ldx;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int nst = (D + F64S_D - 1) / F64S_D;
+  const double eb = (double)(3 * D + 4) * 0x1p-53;
+  // per-row state, owner lane fr = q of row 16 w + fk + 4 q (fr < 4)
+  double st_s = 0.0, st_d = INFINITY;
+  int st_z = 0, st_k = 0;
+  for (int ct = 0; ct < nct; ++ct) {
+    const int k0 = ct * F64T;
+    const double* cr = C + (int64_t)min(k0 + srow, K - 1) * D;
+    double vx[FPT], vc[FPT];
+    double nx = 0.0, nc = 0.0;
+    auto load = [&](int st) __attribute__((always_inline)) {
+      const int d0 = st * F64S_D + sch;
+#pragma unroll
+      for (int e = 0; e < FPT; ++e) {
+        const bool ok = d0 + e < D;
+        vx[e] = ok ? xr[d0 + e] : 0.0;
+        vc[e] = ok ? cr[d0 + e] : 0.0;
+      }
+    };
+    auto store = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+      for (int e = 0; e < FPT; ++e) {
+        s_x[buf][srow * PX + sch + e] = vx[e];
+        s_c[buf][srow * PX + sch + e] = vc[e];
+        nx = fma(vx[e], vx[e], nx);
+        nc = fma(vc[e], vc[e], nc);
+      }
+    };
+    f64x4 acc[8];
+#pragma unroll
+    for (int tj = 0; tj < 8; ++tj) acc[tj] = f64x4{0.0, 0.0, 0.0, 0.0};
+    load(0);
+    store(0);
+    __syncthreads();
+    for (int st = 0; st < nst; ++st) {
+      const int buf = st & 1;
+      if (st + 1 < nst) load(st + 1);
+      const double* sx = s_x[buf] + (w * 16 + fr) * PX + fk;
+      const double* sc = s_c[buf] + fr * PX + fk;
+#pragma unroll
+      for (int kk = 0; kk < F64S_D / 4; ++kk) {
+        const double a = sx[kk * 4];
+        double b[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) b[t] = sc[t * 16 * PX + kk * 4];
+#pragma unroll
+        for (int tj = 0; tj < 8; ++tj)
+          acc[tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b[tj], acc[tj], 0, 0, 0);
+      }
+      if (st + 1 < nst) store(buf ^ 1);
+      __syncthreads();
+    }
+    // norms: the four chunk threads of a row are lanes t, t^1, t^2, t^3 of one wave
+    nx += __shfl_xor(nx, 1, 64);
+    nx += __shfl_xor(nx, 2, 64);
+    nc += __shfl_xor(nc, 1, 64);
+    nc += __shfl_xor(nc, 2, 64);
+    if ((tid & 3) == 0) {
+      if (ct == 0) s_xn[srow] = nx;
+      s_cn[srow] = nc;
+      s_cs[srow] = sqrt(nc);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rl = w * 16 + fk + 4 * q;
+      const int64_t row = r0 + rl;
+      const double xn = s_xn[rl], xs = sqrt(xn);
+      double s = 0.0, bd = INFINITY;
+      int z = 0, bk = 0;
+#pragma unroll
+      for (int tj = 0; tj < 8; ++tj) {
+        const int kl = tj * 16 + fr, k = k0 + kl;
+        const double d2 = xn + s_cn[kl] - 2.0 * acc[tj][q];
+        const double sb = xs + s_cs[kl];
+        const bool zero = d2 <= eb * sb * sb;
+        const double t = zero ? (double)INFINITY : fm_t<FM>(d2, expo);
+        if (k < K) {
+          if (row < M) G[row * (int64_t)K + k] = t;
+          const double dd = zero ? 0.0 : d2;
+          z += zero ? 1 : 0;
+          s += zero ? 0.0 : t;
+          if (dd < bd) {  // ascending k per lane: the first minimum wins
+            bd = dd;
+            bk = k;
+          }
+        }
+      }
+      row_step<0xB1>(s, z, bd, bk);   // quad_perm [1,0,3,2]: lane ^ 1
+      row_step<0x4E>(s, z, bd, bk);   // quad_perm [2,3,0,1]: lane ^ 2
+      row_step<0x141>(s, z, bd, bk);  // row_half_mirror: quads 0 <-> 1, 2 <-> 3
+      row_step<0x140>(s, z, bd, bk);  // row_mirror: halves of the 16-lane row
+      if (fr == q) {
+        st_s += s;
+        st_z += z;
+        if (bd < st_d || (bd == st_d && bk < st_k)) {
+          st_d = bd;
+          st_k = bk;
+        }
+      }
+    }
+    __syncthreads();  // s_cn / the stage buffers are rewritten by the next tile
+  }
+  if (fr < 4) {
+    const int64_t row = r0 + w * 16 + fk + 4 * fr;
+    if (row < M) {
+      const bool on = st_z > 0;
+      // > 0: 1 / sum t;  == 0: every membership 0 (NaN -> 0);  < 0: one-hot over the zeros
+      rowinfo[row] = on ? (nz ? 0.0 : -(double)st_z) : 1.0 / st_s;
+      labels[row] = (on && nz) ? 0 : st_k;
+    }
+  }
 }
 
 // row splits of the fp64 W^T X pass: one 256-thread block per CU at a time, so the grid
@@ -537,7 +715,7 @@ int launch_wide(int pass, const void* X, int64_t M, int64_t ldx, int D, const vo
       int64_t splits = wtx_f64_splits(stages, (int64_t)nkt * ndt, num_cus);
       const int64_t rps = ((stages + splits - 1) / splits) * F64S_W;
       splits = (M + rps - 1) / rps;
-      hipLaunchKernelGGL(fcm_wide_wtx_f64m_kernel, dim3((unsigned)(splits * nkt * ndt)), dim3(256),
+      hipLaunchKernelGGL(fcm_wide_wtx_f64m_kernel<-1>, dim3((unsigned)(splits * nkt * ndt)), dim3(256),
                          0, s, (const double*)G, (const double*)X, M, ldx, D, K, nkt, ndt, rps,
                          wx, ws);
       TDC_CHECK_LAUNCH();
@@ -583,10 +761,57 @@ int launch_wide(int pass, const void* X, int64_t M, int64_t ldx, int D, const vo
   return 0;
 }
 
+int launch_f64t(int pass, const double* X, int64_t M, int64_t ldx, int D, const double* C, int K,
+                double m, int nz, double* G, double* rowinfo, int32_t* labels, double* wx,
+                double* ws, int num_cus, hipStream_t s) {
+  const int fm = fcm_fm(m);
+  if (pass == 0) {
+    const int nct = (K + F64T - 1) / F64T;
+    const dim3 grid((unsigned)((M + F64T - 1) / F64T));
+    const double expo = -1.0 / (m - 1.0);
+#define TDC_TS(FMV)                                                                             \
+  hipLaunchKernelGGL((fcm_f64_tstats_kernel<FMV>), grid, dim3(512), 0, s, X, M, ldx, D, C, K, nct, \
+                     expo, nz, G, rowinfo, labels)
+    switch (fm) {
+      case 2: TDC_TS(2); break;
+      case 5: TDC_TS(5); break;
+      default: TDC_TS(0);
+    }
+#undef TDC_TS
+    TDC_CHECK_LAUNCH();
+    return 0;
+  }
+  const int nkt = (K + F64T - 1) / F64T, ndt = (D + F64T - 1) / F64T;
+  const int64_t stages = (M + F64S_W - 1) / F64S_W;
+  int64_t splits = wtx_f64_splits(stages, (int64_t)nkt * ndt, num_cus);
+  const int64_t rps = ((stages + splits - 1) / splits) * F64S_W;
+  splits = (M + rps - 1) / rps;
+#define TDC_WT(FMV)                                                                               \
+  hipLaunchKernelGGL((fcm_wide_wtx_f64m_kernel<FMV, 8>), dim3((unsigned)(splits * nkt * ndt)), dim3(512), \
+                     0, s, G, X, M, ldx, D, K, nkt, ndt, rps, wx, ws, rowinfo, m)
+  switch (fm) {
+    case 2: TDC_WT(2); break;
+    case 5: TDC_WT(5); break;
+    default: TDC_WT(0);
+  }
+#undef TDC_WT
+  TDC_CHECK_LAUNCH();
+  return 0;
+}
+
 }  // namespace
 }  // namespace tdc
 
 using namespace tdc;
+
+int tdc_fcm_f64t(int pass, const double* X, int64_t M, int64_t ldx, int D, const double* C, int K,
+                 double m, int nan_to_zero, double* G, double* rowinfo, int32_t* labels, double* wx,
+                 double* ws, int num_cus, hipStream_t s) {
+  if (M <= 0 || K <= 0) return 0;
+  if (D < 1 || pass < 0 || pass > 1 || m <= 1.0) return (int)hipErrorInvalidValue;
+  return launch_f64t(pass, X, M, ldx, D, C, K, m, nan_to_zero, G, rowinfo, labels, wx, ws, num_cus,
+                     s);
+}
 
 int tdc_fcm_wide(int pass, int dtype, const void* X, int64_t M, int64_t ldx, int D, const void* C,
                  int K, double m, int nan_to_zero, void* G, int32_t* labels, double* wx, double* ws,

@@ -183,6 +183,13 @@ int tdc_fcm_mfma_wide(int pass, const void* Xh, const void* Xl, const float* xx,
                       int Kp, float* G, float* work, const float* shift, double* wx, double* ws,
                       int num_cus, hipStream_t stream);
 int64_t tdc_fcm_mfma_wide_workspace(int64_t M, int Kp, int DP, int num_cus);
+// fp64 FCM, row statistics fused into the f64-MFMA distance pass (fcm_wide.hip), over a chunk
+// of M rows with G [M, K] fp64: pass 0: G = t = d2^(-1/(m-1)) (+inf on a centroid), rowinfo
+// [M] (fcm_wide_rows semantics: 1/sum t, 0 or -zeros on a centroid) and labels [M]; pass 1:
+// wx [K, D] / ws [K] += W^T X / sum W with w = (t * rowinfo)^m formed while staging.
+int tdc_fcm_f64t(int pass, const double* X, int64_t M, int64_t ldx, int D, const double* C, int K,
+                 double m, int nan_to_zero, double* G, double* rowinfo, int32_t* labels, double* wx,
+                 double* ws, int num_cus, hipStream_t stream);
 
 // N3  finalize: C = sums/counts (empty policy), max shift^2 -> shift (float, atomic max),
 // optional bf16 prep of the next assignment (Cm2 [Kp, DP] = -2*bf16(c), cnorm [Kp]).

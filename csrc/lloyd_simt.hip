@@ -541,14 +541,32 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(const T* __restrict__
 // thousand rows still spread over every CU (on the 128-row tiles 1.7k rows kept 14 CUs busy
 // for 0.5 ms).  Same fma chain in ascending d from 0 as assign_exact_kernel (zero padding adds
 // fma(0, 0, acc) = acc), so the distances are bit-identical; ties go to the lower index.
+// K split (round 6): with few listed rows the row groups alone leave most of the grid idle
+// (~60 fp64 rows: 8 workgroups streaming all K, ~120 us), so each row group's 256-centroid
+// chunks are split over S workgroups, S = the idle share of the grid (the same on every
+// workgroup: it depends only on the device-side count), each writing its (min, index) to
+// part_d / part_k; exact_few_merge_kernel then takes the per-row minimum over the splits in
+// ascending k order (ties: the lower index, as the unsplit scan).
+constexpr int EXACT_FEW_RB = 8, EXACT_FEW_PARTS = 8192;
+__device__ __forceinline__ int exact_few_splits(int n, int nkc, int grid) {
+  const int rg = (n + EXACT_FEW_RB - 1) / EXACT_FEW_RB;
+  int sp = rg > 0 ? grid / rg : 1;
+  if (sp > nkc) sp = nkc;
+  if (sp < 1) sp = 1;
+  if ((int64_t)sp * rg * EXACT_FEW_RB > EXACT_FEW_PARTS) sp = 1;
+  return sp;
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void assign_exact_few_kernel(const T* __restrict__ X, int64_t ldx,
                                                                int D, const T* __restrict__ C, int K,
                                                                int32_t* __restrict__ labels,
                                                                T* __restrict__ mind,
                                                                const int32_t* __restrict__ rowidx,
-                                                               const int* __restrict__ nptr) {
-  constexpr int RB = 8, KT = 256, DC = 32;
+                                                               const int* __restrict__ nptr,
+                                                               T* __restrict__ part_d,
+                                                               int* __restrict__ part_k) {
+  constexpr int RB = EXACT_FEW_RB, KT = 256, DC = 32;
   // the row group's rows, staged once (D <= EXACT_FEW_MAXD, zero-padded to the chunk): a
   // per-chunk slice had put two dependent global loads (index, row) on every chunk
   __shared__ __attribute__((aligned(16))) T s_x[EXACT_FEW_MAXD][RB];
@@ -562,10 +580,13 @@ __global__ __launch_bounds__(256) void assign_exact_few_kernel(const T* __restri
   // rows allow) and row values are loaded into registers while the current one is computed
   constexpr int VEC = 16 / (int)sizeof(T), VPR = DC / VEC, NV = KT * DC / VEC / 256;
   typedef T vecT __attribute__((ext_vector_type(VEC)));
-  const int nd = (D + DC - 1) / DC, nchunks = nd * ((K + KT - 1) / KT);
+  const int nd = (D + DC - 1) / DC, nkc = (K + KT - 1) / KT;
   const bool vec_ok = D % VEC == 0 && ((uintptr_t)C % 16) == 0;
   vecT cv[NV];
   const int Dp = nd * DC;
+  const int S = part_d ? exact_few_splits(n, nkc, (int)gridDim.x) : 1;
+  const int kcs = (nkc + S - 1) / S;  // 256-centroid chunks per split
+  const int64_t items = (int64_t)((n + RB - 1) / RB) * S;
   auto load = [&](int64_t r0, int ci) __attribute__((always_inline)) {
     const int k0 = (ci / nd) * KT, dc = (ci % nd) * DC;
 #pragma unroll
@@ -580,7 +601,12 @@ __global__ __launch_bounds__(256) void assign_exact_few_kernel(const T* __restri
       }
     }
   };
-  for (int64_t r0 = (int64_t)blockIdx.x * RB; r0 < n; r0 += (int64_t)gridDim.x * RB) {
+  for (int64_t item = blockIdx.x; item < items; item += gridDim.x) {
+    const int64_t r0 = (item / S) * RB;
+    const int sp = (int)(item % S);
+    const int c0 = sp * kcs * nd;  // this split's (k0, dc) chunk range
+    const int c1 = min(nkc, (sp + 1) * kcs) * nd;
+    if (c0 >= c1) continue;  // uniform per workgroup
     T best[RB];
     int bk[RB];
 #pragma unroll
@@ -591,14 +617,14 @@ __global__ __launch_bounds__(256) void assign_exact_few_kernel(const T* __restri
     T acc[RB];
 #pragma unroll
     for (int i = 0; i < RB; ++i) acc[i] = (T)0;
-    load(r0, 0);
+    load(r0, c0);
     __syncthreads();  // the previous group's reads of s_x are done
     for (int e = tid; e < RB * Dp; e += 256) {
       const int r = e / Dp, d = e % Dp;
       const int64_t row = r0 + r;
       s_x[d][r] = (row < n && d < D) ? X[(int64_t)rowidx[row] * ldx + d] : (T)0;
     }
-    for (int ci = 0; ci < nchunks; ++ci) {
+    for (int ci = c0; ci < c1; ++ci) {
       __syncthreads();
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
@@ -607,7 +633,7 @@ __global__ __launch_bounds__(256) void assign_exact_few_kernel(const T* __restri
         for (int j = 0; j < VEC; ++j) s_c[d + j][r] = cv[i][j];
       }
       __syncthreads();
-      if (ci + 1 < nchunks) load(r0, ci + 1);
+      if (ci + 1 < c1) load(r0, ci + 1);
       const int dc = (ci % nd) * DC;
 #pragma unroll 4
       for (int d = 0; d < DC; ++d) {
@@ -658,11 +684,60 @@ __global__ __launch_bounds__(256) void assign_exact_few_kernel(const T* __restri
           b = s_rb[v][tid];
           k = s_rk[v][tid];
         }
-      const int64_t orow = rowidx[r0 + tid];
-      labels[orow] = k;
-      if (mind) mind[orow] = b;
+      if (S > 1) {
+        part_d[(r0 + tid) * S + sp] = b;
+        part_k[(r0 + tid) * S + sp] = k;
+      } else {
+        const int64_t orow = rowidx[r0 + tid];
+        labels[orow] = k;
+        if (mind) mind[orow] = b;
+      }
     }
   }
+}
+
+// the per-row minimum over the K splits of assign_exact_few_kernel (nothing to do at S = 1)
+template <typename T>
+__global__ __launch_bounds__(256) void exact_few_merge_kernel(int K, int few_grid,
+                                                              int32_t* __restrict__ labels,
+                                                              T* __restrict__ mind,
+                                                              const int32_t* __restrict__ rowidx,
+                                                              const int* __restrict__ nptr,
+                                                              const T* __restrict__ part_d,
+                                                              const int* __restrict__ part_k) {
+  const int n = *nptr;
+  if (n > EXACT_FEW_MAX) return;
+  const int S = exact_few_splits(n, (K + 255) / 256, few_grid);
+  if (S <= 1) return;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 256) {
+    T b = part_d[r * S];
+    int k = part_k[r * S];
+    for (int sp = 1; sp < S; ++sp) {  // ascending k: strict < keeps the lower index
+      const T v = part_d[r * S + sp];
+      if (v < b) {
+        b = v;
+        k = part_k[r * S + sp];
+      }
+    }
+    const int64_t orow = rowidx[r];
+    labels[orow] = k;
+    if (mind) mind[orow] = b;
+  }
+}
+
+// split scratch of the few-rows re-scan, one per device (allocated on first use, before
+// any graph capture: the engines run an eager step first)
+static void* few_parts(int dtype_bytes) {
+  static void* bufs[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!bufs[dev]) {
+    void* p = nullptr;
+    if (hipMalloc(&p, (size_t)EXACT_FEW_PARTS * (8 + 4)) != hipSuccess) return nullptr;
+    bufs[dev] = p;
+  }
+  (void)dtype_bytes;
+  return bufs[dev];
 }
 
 int tdc_assign_exact(int dtype, const void* X, int64_t N, int64_t ldx, int D, const void* C, int K,
@@ -673,19 +748,34 @@ int tdc_assign_exact(int dtype, const void* X, int64_t N, int64_t ldx, int D, co
   if (few) {
     if (!rowidx) return (int)hipErrorInvalidValue;
     // both launches read the listed count; exactly one of them has work
-    int64_t fb = ((N < EXACT_FEW_MAX ? N : EXACT_FEW_MAX) + 7) / 8;
     const int64_t cap = (int64_t)(num_cus > 0 ? num_cus : 256) * 4;
-    if (fb > cap) fb = cap;
-    if (dtype == TDC_F32)
+    int64_t fb;
+    // K split: the grid covers the row groups of up to EXACT_FEW_MAX rows or, when fewer are
+    // listed, their 256-centroid chunks (a few hundred workgroups either way)
+    fb = cap;
+    char* parts = (char*)few_parts(dtype == TDC_F64 ? 8 : 4);
+    if (!parts) return (int)hipErrorOutOfMemory;
+    int* part_k = (int*)(parts + (size_t)EXACT_FEW_PARTS * 8);
+    const int mb = (EXACT_FEW_PARTS + 255) / 256;
+    if (dtype == TDC_F32) {
       hipLaunchKernelGGL(assign_exact_few_kernel<float>, dim3((unsigned)fb), dim3(256), 0, s,
                          (const float*)X, ldx, D, (const float*)C, K, labels, (float*)mind, rowidx,
-                         nptr);
-    else if (dtype == TDC_F64)
+                         nptr, (float*)parts, part_k);
+      TDC_CHECK_LAUNCH();
+      hipLaunchKernelGGL(exact_few_merge_kernel<float>, dim3((unsigned)mb), dim3(256), 0, s, K,
+                         (int)fb, labels, (float*)mind, rowidx, nptr, (const float*)parts,
+                         (const int*)part_k);
+    } else if (dtype == TDC_F64) {
       hipLaunchKernelGGL(assign_exact_few_kernel<double>, dim3((unsigned)fb), dim3(256), 0, s,
                          (const double*)X, ldx, D, (const double*)C, K, labels, (double*)mind,
-                         rowidx, nptr);
-    else
+                         rowidx, nptr, (double*)parts, part_k);
+      TDC_CHECK_LAUNCH();
+      hipLaunchKernelGGL(exact_few_merge_kernel<double>, dim3((unsigned)mb), dim3(256), 0, s, K,
+                         (int)fb, labels, (double*)mind, rowidx, nptr, (const double*)parts,
+                         (const int*)part_k);
+    } else {
       return (int)hipErrorInvalidValue;
+    }
     TDC_CHECK_LAUNCH();
     if (N <= EXACT_FEW_MAX) return 0;
   }

@@ -232,9 +232,14 @@ class FuzzyCMeans:
             es = 8 if tdt == torch.float64 else 4
             # MFMA tower keeps hi/lo bf16 rows + norms + row info next to the chunk
             row_bytes = d * es + 4 * d + 16
-            # the wide towers (D > 128) hold a [rows, K] block of up to 2^27 elements
-            from ..ops import HipWideFCM
-            g_bytes = HipWideFCM.chunk_elems * es if d > 128 else 0
+            # the wide towers (D > 128) hold a [rows, K] block of up to 2^28 elements; the
+            # fused fp64 path (K >= FCM_F64_MFMA_MIN_K) an fp64 one, and fp32 rows promoted
+            from ..ops import HipWideFCM, fcm_f64_mfma
+            if fcm_f64_mfma(cfg.n_clusters, d) and cfg.dtype not in ("bf16", "fp8"):
+                g_bytes = HipWideFCM.chunk_elems * 8
+                row_bytes += 8 * d + 8 if es == 4 else 8
+            else:
+                g_bytes = HipWideFCM.chunk_elems * es if d > 128 else 0
             chunk = want or plan_chunk_rows(n, row_bytes, cfg.n_clusters, d, dev,
                                             cfg.hbm_budget_gb, extra_fixed=g_bytes)
             if chunk:

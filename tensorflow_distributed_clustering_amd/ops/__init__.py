@@ -1539,49 +1539,77 @@ class HipMfmaWideFCM(HipMfmaFCM):
 
 
 class HipWideFCM(_LocalOpsBase):
-    """FCM for any D in fp32 / fp64 (csrc/fcm_wide.hip): exact difference-form distances of a
-    row chunk into the [rows, K] block G (the only intermediate, up to ``chunk_elems``
-    elements), memberships w = u^m in place, then W^T X and sum W -- three native kernels
-    per chunk, no library GEMM.  Takes over from fcm_tower (D <= 256) and the MFMA tower
-    (fp32, D <= 128) past their register / LDS budgets."""
+    """FCM for any D in fp32 / fp64 (csrc/fcm_wide.hip) per row chunk, with the [rows, K]
+    block G (up to ``chunk_elems`` elements) as the only intermediate, no library GEMM.
+
+    fp64 (``fused``, the default): two kernels per chunk, both GEMM-shaped passes on the f64
+    matrix cores -- the distance expansion with an exact-zero bound, t = d^(-2/(m-1)) into G
+    and the row statistics (sum t, on-centroid count, label) in the same kernel, then
+    W^T X with w = (t / sum t)^m formed while staging.  Unfused fp64 / fp32: distances
+    into G, memberships w = u^m in place (fcm_wide_rows), W^T X -- three kernels per chunk
+    (fp32 on exact difference-form SIMT tiles)."""
     name = "hip_fcm_wide"
     # [rows, K] block per chunk (2 GiB in fp64): each chunk's W^T X pass flushes its
     # partial tiles with atomics and ends in a partial round of blocks, so fewer, larger
     # chunks; HBM is 288 GB per GPU
     chunk_elems = 1 << 28
+    fused = True  # class switch (A/B): fp64 row statistics fused into the distance pass
 
     def __init__(self, x, k, dtype="fp64", m=2.0, nan_to_zero=True):
         super().__init__(x, k, "keep")
         self.ops = _native.require()
         tdt = torch.float64 if dtype == "fp64" else torch.float32
+        self.promoted = tdt == torch.float64 and x.dtype != torch.float64
         self.x = x.to(tdt).contiguous()
         self.c_dtype = tdt
         self.m = float(m)
         self.nan_to_zero = bool(nan_to_zero)
         self.G = None
+        self.rowinfo = None
+
+    @property
+    def precision(self) -> str:
+        if self._fused():
+            return FCM_PRECISION["fp64_mfma"] + (" (fp32 rows promoted to fp64)"
+                                                 if self.promoted else "")
+        return FCM_PRECISION["fp64" if self.c_dtype == torch.float64 else "fp32"]
+
+    def _fused(self) -> bool:
+        return self.fused and self.c_dtype == torch.float64
 
     def _block(self):
         rows = max(1, min(self.n, self.chunk_elems // max(1, self.k)))
         if self.G is None or self.G.shape[0] < rows:
             self.G = torch.empty(rows, self.k, dtype=self.c_dtype, device=self.device)
+        if self._fused() and (self.rowinfo is None or self.rowinfo.numel() < rows):
+            self.rowinfo = torch.empty(rows, dtype=torch.float64, device=self.device)
         return rows
 
-    def step(self, C, labels, wx, ws):
-        C = C.to(self.c_dtype).contiguous()
+    def _chunks(self):
         rows = self._block()
         for s in range(0, self.n, rows):
             e = min(self.n, s + rows)
-            xs, g = self.x[s:e], self.G[: e - s]
+            yield s, e, self.x[s:e], self.G[: e - s]
+
+    def step(self, C, labels, wx, ws):
+        C = C.to(self.c_dtype).contiguous()
+        for s, e, xs, g in self._chunks():
+            if self._fused():
+                ri = self.rowinfo[: e - s]
+                self.ops.fcm_f64t(0, xs, C, self.m, self.nan_to_zero, g, ri, labels[s:e])
+                self.ops.fcm_f64t(1, xs, C, self.m, self.nan_to_zero, g, ri, None, wx, ws)
+                continue
             self.ops.fcm_wide(0, xs, C, self.m, self.nan_to_zero, g)
             self.ops.fcm_wide(1, xs, C, self.m, self.nan_to_zero, g, labels[s:e])
             self.ops.fcm_wide(2, xs, C, self.m, self.nan_to_zero, g, None, wx, ws)
 
     def assign(self, C, labels):
         C = C.to(self.c_dtype).contiguous()
-        rows = self._block()
-        for s in range(0, self.n, rows):
-            e = min(self.n, s + rows)
-            xs, g = self.x[s:e], self.G[: e - s]
+        for s, e, xs, g in self._chunks():
+            if self._fused():
+                self.ops.fcm_f64t(0, xs, C, self.m, self.nan_to_zero, g,
+                                  self.rowinfo[: e - s], labels[s:e])
+                continue
             self.ops.fcm_wide(0, xs, C, self.m, self.nan_to_zero, g)
             self.ops.fcm_wide(3, xs, C, self.m, self.nan_to_zero, g, labels[s:e])
 
@@ -1594,6 +1622,10 @@ FCM_PRECISION = {
     "fp64": "fp64 distances (difference form; D > 256: the GEMM expansion on the fp64 matrix "
             "cores), fp64 memberships and sums",
     "fp32": "fp32 difference-form distances and memberships, fp64 sums",
+    # HipWideFCM fused fp64 (also fp32 data promoted to it where make_fcm_ops routes so)
+    "fp64_mfma": "fp64 distances as the GEMM expansion on the fp64 matrix cores (exact-zero "
+                 "bound (3D+4) 2^-53 (|x|+|c|)^2), fp64 memberships, W^T X on the fp64 "
+                 "matrix cores, fp64 sums",
     # HipMfmaFCM, fcm_distances='x3' (default).  Measured against the fp64 oracle at m=2
     # (tests/test_fcm_gpu.py): sum_i w within 2e-3*m (hi+lo rows) / 3e-3*m (bf16 rows) --
     # NOT fp32-faithful: the stats pass's row normaliser keeps one-product terms for all
@@ -1621,9 +1653,11 @@ FCM_PRECISION = {
 
 def make_fcm_ops(x: torch.Tensor, k: int, dtype: str = "fp64", m: float = 2.0,
                  nan_to_zero: bool = True, backend: str = "auto", distances: str = "x3"):
-    """FCM tower for (dtype, K, D).  fp64 / fp32: the exact difference-form towers (fused
-    small-K*D kernel, SIMT tower up to D = 256, wide tower above) -- the reference's
-    memberships come from exact differences (`scripts/distribuitedClustering.py:112-129`).
+    """FCM tower for (dtype, K, D).  fp64 / fp32: the fused small-K*D kernel; from K = 128
+    (FCM_F64_MFMA_MIN_K) the fp64 f64-MFMA wide path with fused row statistics (fp32 rows
+    promoted -- faster than the fp32 SIMT tower and fp64-accurate, like the reference's fp64
+    FCM, `scripts/distribuitedClustering.py:112-137`); below it the exact difference-form
+    SIMT tower up to D = 256 and the wide tower above.
     bf16 (and fp8): the MFMA towers (fp32 rows split into bf16 hi/lo, bf16x3 distances,
     memberships in fp32, W = u^m rounded to bf16 for the W^T X MFMAs; centroid error
     ~1e-3 of max|c| against the fp64 oracle, FCM_PRECISION) for 16 < D <= 1024, K >= 32;
@@ -1651,6 +1685,19 @@ def make_fcm_ops(x: torch.Tensor, k: int, dtype: str = "fp64", m: float = 2.0,
         return HipTowerFCM(x, k, dtype, m, nan_to_zero)
     if force in ("wide", "wide64"):
         return HipWideFCM(x, k, "fp64" if force == "wide64" else dtype, m, nan_to_zero)
+    if fcm_f64_mfma(k, d):
+        # fp64 on the f64 matrix cores (fused row statistics); fp32 rows are promoted to it:
+        # faster than the fp32 SIMT tower there and more accurate (FCM_F64_MFMA_MIN_K)
+        return HipWideFCM(x, k, "fp64", m, nan_to_zero)
     if d <= 256:
         return HipTowerFCM(x, k, dtype, m, nan_to_zero)
     return HipWideFCM(x, k, dtype, m, nan_to_zero)
+
+
+# K from which fp32 / fp64 FCM run HipWideFCM's fused fp64 MFMA path (a 128-centroid tile
+# per block; measured against the SIMT towers in profiles/fcm_route_r06.txt)
+FCM_F64_MFMA_MIN_K = 128
+
+
+def fcm_f64_mfma(k: int, d: int) -> bool:
+    return k >= FCM_F64_MFMA_MIN_K

@@ -145,3 +145,18 @@ def test_update_mode_flag_same_fit(data, tmp_path):
         outs.append(np.loadtxt(cen, delimiter=","))
     np.testing.assert_allclose(outs[1], outs[0], rtol=1e-10, atol=1e-10)
     np.testing.assert_allclose(outs[2], outs[0], rtol=1e-10, atol=1e-10)
+
+
+def test_resolve_dtype_auto_follows_the_measured_routing():
+    """--dtype auto: K-Means fp64 up to D = 1024; FCM fp64 on the small fused kernel
+    (D <= 16) and on the fp64 matrix-core path (K >= 128, where fp32 is promoted anyway),
+    fp32 SIMT tower in between."""
+    from tensorflow_distributed_clustering_amd.cli import resolve_dtype
+    assert resolve_dtype("auto", 1024, 128) == "fp64"
+    assert resolve_dtype("auto", 64, 2048) == "fp32"
+    fcm = "distributedFuzzyCMeans"
+    assert resolve_dtype("auto", 3, 5, fcm) == "fp64"
+    assert resolve_dtype("auto", 1024, 128, fcm) == "fp64"
+    assert resolve_dtype("auto", 128, 768, fcm) == "fp64"
+    assert resolve_dtype("auto", 64, 128, fcm) == "fp32"
+    assert resolve_dtype("bf16", 64, 128, fcm) == "bf16"

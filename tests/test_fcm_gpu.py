@@ -194,7 +194,9 @@ def test_fcm_dispatch_native_up_to_1024(gpu):
                                                ("fp64", 6, 40, "hip_fcm_tower"),
                                                ("fp64", 64, 100, "hip_fcm_tower"),
                                                ("fp32", 12, 64, "hip_fcm_tower"),
-                                               ("fp32", 128, 256, "hip_fcm_tower"),
+                                               ("fp32", 128, 256, "hip_fcm_wide"),
+                                               ("fp64", 128, 256, "hip_fcm_wide"),
+                                               ("fp32", 64, 100, "hip_fcm_tower"),
                                                ("bf16", 128, 256, "hip_fcm_mfma")])
 def test_fcm_fit_native_backends(gpu, dtype, d, k, backend):
     """Every FCM shape class runs a native backend and follows the fp64 torch fit."""
@@ -401,3 +403,33 @@ def test_fcm_mfma_bf16x3_raw_wtx(gpu, k, d, nz):
     c1, c2 = wx1 / ws1.clamp_min(1e-300)[:, None], wx2 / ws2.clamp_min(1e-300)[:, None]
     assert bool(((c1 - c2).abs() <= 1e-5 * (1 + c2.abs()))[ok].all())
 
+
+
+@pytest.mark.parametrize("k,d", [(1024, 128), (130, 100), (300, 17), (64, 256), (40, 768)])
+@pytest.mark.parametrize("m", [2.0, 3.0, 5.0])
+@pytest.mark.parametrize("nz", [True, False])
+def test_fcm_f64_fused_matches_oracle(gpu, k, d, m, nz):
+    """fp64 wide path with the row statistics fused into the f64-MFMA distance pass
+    (fcm_f64t: t into G + rowinfo + labels, then W^T X with w formed while staging), over
+    several chunks with a ragged tail and a point exactly on a centroid: the fp64 oracle's
+    numbers, and the same labels / sums as the unfused three-kernel path."""
+    from tensorflow_distributed_clustering_amd.ops import HipWideFCM
+    n = 5003
+    x, c = _data(n, k, d, 11 * k + d)
+    xg, cg = x.to(gpu), c.to(gpu)
+    res = {}
+    for fused in (True, False):
+        ops = HipWideFCM(xg, k, "fp64", m, nz)
+        ops.fused = fused
+        ops.chunk_elems = 2000 * k  # 3 chunks, the last ragged
+        lab = torch.empty(n, dtype=torch.int32, device=gpu)
+        wx = torch.zeros(k, d, dtype=torch.float64, device=gpu)
+        ws = torch.zeros(k, dtype=torch.float64, device=gpu)
+        ops.step(cg, lab, wx, ws)
+        _check(wx.cpu(), ws.cpu(), lab, xg.cpu(), cg.cpu(), m, nz, 1e-9, 0.99999)
+        lab2 = torch.full_like(lab, -1)
+        ops.assign(cg, lab2)
+        assert torch.equal(lab, lab2)
+        res[fused] = (lab.cpu(), wx.cpu(), ws.cpu())
+    assert torch.equal(res[True][0], res[False][0])
+    torch.testing.assert_close(res[True][2], res[False][2], rtol=1e-11, atol=0)
