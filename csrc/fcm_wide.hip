@@ -424,23 +424,19 @@ __global__ __launch_bounds__(NW * 64, 1) void fcm_wide_wtx_f64m_kernel(
   // staging: thread t loads 8 consecutive columns (t & 15) * 8 of stage rows (t >> 4) + j NT/16
   constexpr int RPT = F64S_W * 16 / NT;
   const int srow = tid >> 4, scol = (tid & 15) * 8;
-  double vw[RPT][8], vx[RPT][8];
+  double vw[RPT][8], vx[RPT][8], vi[RPT];
+  // loads only (issued at a stage's start, consumed by store() after its MFMAs, so their
+  // latency hides under them); the t -> w transform runs in store()
   auto load = [&](int64_t rs) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < RPT; ++j) {
       const int64_t r = rs + srow + (NT / 16) * j;
       const bool rok = r < b;
-      double info = 0.0;
-      if constexpr (WT >= 0) info = rok ? rowinfo[r] : 0.0;
+      if constexpr (WT >= 0) vi[j] = rok ? rowinfo[r] : 0.0;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int k = k0 + scol + e, d = d0 + scol + e;
-        double v = (rok && k < K) ? W[r * (int64_t)K + k] : 0.0;
-        if constexpr (WT >= 0) {
-          const double u = info > 0.0 ? v * info : (info < 0.0 && v == (double)INFINITY ? -1.0 / info : 0.0);
-          v = u > 0.0 ? fm_w<WT>(u, m) : 0.0;
-        }
-        vw[j][e] = v;
+        vw[j][e] = (rok && k < K) ? W[r * (int64_t)K + k] : 0.0;
         vx[j][e] = (rok && d < D) ? X[r * ldx + d] : 0.0;
       }
     }
@@ -450,7 +446,13 @@ __global__ __launch_bounds__(NW * 64, 1) void fcm_wide_wtx_f64m_kernel(
     for (int j = 0; j < RPT; ++j)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        s_w[buf][(srow + (NT / 16) * j) * PW + scol + e] = vw[j][e];
+        double v = vw[j][e];
+        if constexpr (WT >= 0) {
+          const double info = vi[j];
+          const double u = info > 0.0 ? v * info : (info < 0.0 && v == (double)INFINITY ? -1.0 / info : 0.0);
+          v = u > 0.0 ? fm_w<WT>(u, m) : 0.0;
+        }
+        s_w[buf][(srow + (NT / 16) * j) * PW + scol + e] = v;
         s_x[buf][(srow + (NT / 16) * j) * PW + scol + e] = vx[j][e];
       }
   };
@@ -566,20 +568,25 @@ __global__ __launch_bounds__(512, 1) void fcm_f64_tstats_kernel(
   // per-row state, owner lane fr = q of row 16 w + fk + 4 q (fr < 4)
   double st_s = 0.0, st_d = INFINITY;
   int st_z = 0, st_k = 0;
+  double vx[FPT], vc[FPT];
+  auto load_c = [&](const double* cr, int st) __attribute__((always_inline)) {
+    const int d0 = st * F64S_D + sch;
+#pragma unroll
+    for (int e = 0; e < FPT; ++e) {
+      const bool ok = d0 + e < D;
+      vx[e] = ok ? xr[d0 + e] : 0.0;
+      vc[e] = ok ? cr[d0 + e] : 0.0;
+    }
+  };
+  load_c(C + (int64_t)min(srow, K - 1) * D, 0);
   for (int ct = 0; ct < nct; ++ct) {
     const int k0 = ct * F64T;
     const double* cr = C + (int64_t)min(k0 + srow, K - 1) * D;
-    double vx[FPT], vc[FPT];
+    // the next tile's first stage is loaded during this tile's last one, so its latency
+    // hides under those MFMAs and this tile's epilogue
+    const double* crn = C + (int64_t)min(k0 + F64T + srow, K - 1) * D;
     double nx = 0.0, nc = 0.0;
-    auto load = [&](int st) __attribute__((always_inline)) {
-      const int d0 = st * F64S_D + sch;
-#pragma unroll
-      for (int e = 0; e < FPT; ++e) {
-        const bool ok = d0 + e < D;
-        vx[e] = ok ? xr[d0 + e] : 0.0;
-        vc[e] = ok ? cr[d0 + e] : 0.0;
-      }
-    };
+    auto load = [&](int st) __attribute__((always_inline)) { load_c(cr, st); };
     auto store = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
       for (int e = 0; e < FPT; ++e) {
@@ -592,12 +599,12 @@ __global__ __launch_bounds__(512, 1) void fcm_f64_tstats_kernel(
     f64x4 acc[8];
 #pragma unroll
     for (int tj = 0; tj < 8; ++tj) acc[tj] = f64x4{0.0, 0.0, 0.0, 0.0};
-    load(0);
-    store(0);
+    store(0);  // stage 0 of this tile (loaded before the loop / during the previous tile)
     __syncthreads();
     for (int st = 0; st < nst; ++st) {
       const int buf = st & 1;
       if (st + 1 < nst) load(st + 1);
+      else if (ct + 1 < nct) load_c(crn, 0);
       const double* sx = s_x[buf] + (w * 16 + fr) * PX + fk;
       const double* sc = s_c[buf] + fr * PX + fk;
 #pragma unroll

@@ -188,16 +188,16 @@ def resolve_dtype(dtype: str, k: int, d: int, method: str = "distributedKMeans")
     fp64 path assigns on the matrix cores (bf16x3 scores) and re-checks every row the error
     bound cannot certify in fp64, so its labels are the fp64 argmin (ops.HipX3Lloyd); past
     D = 1024 it runs fp32 exact tiles.  FCM keeps fp64 up to D = 16 (fused small-K*D
-    kernel) and from K = 128 at any D (both GEMM-shaped passes on the fp64 matrix cores,
-    ops.fcm_f64_mfma: there fp32 data is promoted to the same path, so fp64 costs nothing
-    extra); between the two it runs the exact fp32 SIMT tower (~1.6x the fp64 tower's
-    speed).  Nothing is silently dropped to bf16: the resolved dtype is printed and
-    written to --extended_log."""
+    kernel) and from K = 64 at any D (both GEMM-shaped passes on the fp64 matrix cores,
+    ops.fcm_f64_mfma: from D = 64 fp32 data is promoted to the same path, so fp64 costs
+    nothing extra; at D = 32 it costs ~1.35x the fp32 tower); in between it runs the exact
+    fp32 SIMT tower (~1.6x the fp64 tower's speed).  Nothing is silently dropped to bf16:
+    the resolved dtype is printed and written to --extended_log."""
     if dtype != "auto":
         return dtype
     if method == "distributedFuzzyCMeans":
         from .ops import fcm_f64_mfma
-        return "fp64" if (d <= 16 or fcm_f64_mfma(k, d)) else "fp32"
+        return "fp64" if (d <= 16 or fcm_f64_mfma(k, d, "fp64")) else "fp32"
     return "fp64" if d <= 1024 else "fp32"
 
 

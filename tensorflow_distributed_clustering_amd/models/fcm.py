@@ -233,9 +233,10 @@ class FuzzyCMeans:
             # MFMA tower keeps hi/lo bf16 rows + norms + row info next to the chunk
             row_bytes = d * es + 4 * d + 16
             # the wide towers (D > 128) hold a [rows, K] block of up to 2^28 elements; the
-            # fused fp64 path (K >= FCM_F64_MFMA_MIN_K) an fp64 one, and fp32 rows promoted
+            # fused fp64 path (ops.fcm_f64_mfma) an fp64 one, and fp32 rows promoted
             from ..ops import HipWideFCM, fcm_f64_mfma
-            if fcm_f64_mfma(cfg.n_clusters, d) and cfg.dtype not in ("bf16", "fp8"):
+            if cfg.dtype not in ("bf16", "fp8") and fcm_f64_mfma(
+                    cfg.n_clusters, d, "fp64" if es == 8 else "fp32"):
                 g_bytes = HipWideFCM.chunk_elems * 8
                 row_bytes += 8 * d + 8 if es == 4 else 8
             else:

@@ -1577,6 +1577,23 @@ class HipWideFCM(_LocalOpsBase):
     def _fused(self) -> bool:
         return self.fused and self.c_dtype == torch.float64
 
+    def bind(self, x):
+        """A streamed chunk; fp32 chunks of a promoted shard are widened into an owned
+        fp64 buffer (the source refills its slot while the step may still read)."""
+        if x.shape[1] != self.d:
+            raise ValueError(f"chunk width {x.shape[1]} != {self.d}")
+        if x.dtype == self.c_dtype:
+            self.x = x
+        else:
+            buf = getattr(self, "_xbuf", None)
+            if buf is None or buf.shape[0] < x.shape[0]:
+                buf = self._xbuf = torch.empty(x.shape[0], self.d, dtype=self.c_dtype,
+                                               device=self.device)
+            self.x = buf[: x.shape[0]]
+            self.x.copy_(x)
+        self.n = x.shape[0]
+        return self
+
     def _block(self):
         rows = max(1, min(self.n, self.chunk_elems // max(1, self.k)))
         if self.G is None or self.G.shape[0] < rows:
@@ -1653,11 +1670,11 @@ FCM_PRECISION = {
 
 def make_fcm_ops(x: torch.Tensor, k: int, dtype: str = "fp64", m: float = 2.0,
                  nan_to_zero: bool = True, backend: str = "auto", distances: str = "x3"):
-    """FCM tower for (dtype, K, D).  fp64 / fp32: the fused small-K*D kernel; from K = 128
-    (FCM_F64_MFMA_MIN_K) the fp64 f64-MFMA wide path with fused row statistics (fp32 rows
-    promoted -- faster than the fp32 SIMT tower and fp64-accurate, like the reference's fp64
-    FCM, `scripts/distribuitedClustering.py:112-137`); below it the exact difference-form
-    SIMT tower up to D = 256 and the wide tower above.
+    """FCM tower for (dtype, K, D).  fp64 / fp32: the fused small-K*D kernel; from K = 64
+    (fp32: and D = 64, fcm_f64_mfma) the fp64 f64-MFMA wide path with fused row statistics
+    (fp32 rows promoted -- faster than the fp32 SIMT tower and fp64-accurate, like the
+    reference's fp64 FCM, `scripts/distribuitedClustering.py:112-137`); below it the exact
+    difference-form SIMT tower up to D = 256 and the wide tower above.
     bf16 (and fp8): the MFMA towers (fp32 rows split into bf16 hi/lo, bf16x3 distances,
     memberships in fp32, W = u^m rounded to bf16 for the W^T X MFMAs; centroid error
     ~1e-3 of max|c| against the fp64 oracle, FCM_PRECISION) for 16 < D <= 1024, K >= 32;
@@ -1685,19 +1702,27 @@ def make_fcm_ops(x: torch.Tensor, k: int, dtype: str = "fp64", m: float = 2.0,
         return HipTowerFCM(x, k, dtype, m, nan_to_zero)
     if force in ("wide", "wide64"):
         return HipWideFCM(x, k, "fp64" if force == "wide64" else dtype, m, nan_to_zero)
-    if fcm_f64_mfma(k, d):
-        # fp64 on the f64 matrix cores (fused row statistics); fp32 rows are promoted to it:
-        # faster than the fp32 SIMT tower there and more accurate (FCM_F64_MFMA_MIN_K)
+    if fcm_f64_mfma(k, d, dtype):
+        # fp64 on the f64 matrix cores (fused row statistics); fp32 rows are promoted to it
+        # where that beats the fp32 SIMT tower (and is more accurate)
         return HipWideFCM(x, k, "fp64", m, nan_to_zero)
     if d <= 256:
         return HipTowerFCM(x, k, dtype, m, nan_to_zero)
     return HipWideFCM(x, k, dtype, m, nan_to_zero)
 
 
-# K from which fp32 / fp64 FCM run HipWideFCM's fused fp64 MFMA path (a 128-centroid tile
-# per block; measured against the SIMT towers in profiles/fcm_route_r06.txt)
-FCM_F64_MFMA_MIN_K = 128
+# Where fp32 / fp64 FCM run HipWideFCM's fused fp64 MFMA path instead of the SIMT towers
+# (N=1M, m=2, ms/iter, profiles/fcm_route_r06f.txt):
+#   D=32  K=32: fp64 tower 0.85 / f64-MFMA 1.23;  K=128: 1.63 / 1.45 (fp32 tower 1.08);
+#         K=1024: 10.6 / 9.78 (fp32 tower 7.25)
+#   D=128 K=64: 3.63 / 1.86 (fp32 tower 2.29);  K=128: 6.43 / 2.12 (4.12);  K=1024: 45.4 /
+#         14.0 (28.2);  D=256 K=1024: 128 / 25.3 (66.5)
+# fp64 from K = 64; fp32 (promoted) from K = 64 and D = 64 -- at D = 32 its SIMT tower wins
+FCM_F64_MFMA_MIN_K = 64
+FCM_F64_MFMA_MIN_D_FP32 = 64
 
 
-def fcm_f64_mfma(k: int, d: int) -> bool:
-    return k >= FCM_F64_MFMA_MIN_K
+def fcm_f64_mfma(k: int, d: int, dtype: str = "fp64") -> bool:
+    if k < FCM_F64_MFMA_MIN_K:
+        return False
+    return dtype == "fp64" or d >= FCM_F64_MFMA_MIN_D_FP32

@@ -149,7 +149,7 @@ def test_update_mode_flag_same_fit(data, tmp_path):
 
 def test_resolve_dtype_auto_follows_the_measured_routing():
     """--dtype auto: K-Means fp64 up to D = 1024; FCM fp64 on the small fused kernel
-    (D <= 16) and on the fp64 matrix-core path (K >= 128, where fp32 is promoted anyway),
+    (D <= 16) and on the fp64 matrix-core path (K >= 64, where fp32 is promoted from D = 64),
     fp32 SIMT tower in between."""
     from tensorflow_distributed_clustering_amd.cli import resolve_dtype
     assert resolve_dtype("auto", 1024, 128) == "fp64"
@@ -158,5 +158,6 @@ def test_resolve_dtype_auto_follows_the_measured_routing():
     assert resolve_dtype("auto", 3, 5, fcm) == "fp64"
     assert resolve_dtype("auto", 1024, 128, fcm) == "fp64"
     assert resolve_dtype("auto", 128, 768, fcm) == "fp64"
-    assert resolve_dtype("auto", 64, 128, fcm) == "fp32"
+    assert resolve_dtype("auto", 64, 128, fcm) == "fp64"
+    assert resolve_dtype("auto", 32, 128, fcm) == "fp32"
     assert resolve_dtype("bf16", 64, 128, fcm) == "bf16"

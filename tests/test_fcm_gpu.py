@@ -196,7 +196,9 @@ def test_fcm_dispatch_native_up_to_1024(gpu):
                                                ("fp32", 12, 64, "hip_fcm_tower"),
                                                ("fp32", 128, 256, "hip_fcm_wide"),
                                                ("fp64", 128, 256, "hip_fcm_wide"),
-                                               ("fp32", 64, 100, "hip_fcm_tower"),
+                                               ("fp32", 64, 100, "hip_fcm_wide"),
+                                               ("fp32", 32, 100, "hip_fcm_tower"),
+                                               ("fp64", 32, 40, "hip_fcm_tower"),
                                                ("bf16", 128, 256, "hip_fcm_mfma")])
 def test_fcm_fit_native_backends(gpu, dtype, d, k, backend):
     """Every FCM shape class runs a native backend and follows the fp64 torch fit."""

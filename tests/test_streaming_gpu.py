@@ -173,7 +173,8 @@ def test_bounded_lloyd_policies_and_spherical(gpu):
             np.testing.assert_allclose(a.centers, b.centers, rtol=0, atol=5e-2)
 
 
-@pytest.mark.parametrize("dtype,backend", [("bf16", "hip_fcm_mfma"), ("fp32", "hip_fcm_tower"), ("fp64", "hip_fcm_tower")])
+@pytest.mark.parametrize("dtype,backend", [("bf16", "hip_fcm_mfma"), ("fp32", "hip_fcm_wide"),
+                                           ("fp64", "hip_fcm_wide")])
 def test_fcm_hbm_budget_streams_and_matches_resident(gpu, dtype, backend):
     """FCM with --hbm_budget_gb below the shard: host-resident rows stream through HBM in
     chunks (fp32: native RowStreamer + hybrid residency; fp64: plain pinned slices) and
@@ -181,7 +182,7 @@ def test_fcm_hbm_budget_streams_and_matches_resident(gpu, dtype, backend):
     import numpy as np
     import tensorflow_distributed_clustering_amd as tdc
     from tensorflow_distributed_clustering_amd.data.synth import gaussian_blobs
-    n, d, k = 400_000, 64, 64
+    n, d, k = 400_000, 64, 64  # fp32 / fp64: the fused fp64 MFMA path (fp32 chunks widened)
     x = gaussian_blobs(n, d, k, seed=6, dtype=torch.float64).numpy()
     c0 = x[:k] + 0.3
     cfg = tdc.ClusterConfig(n_clusters=k, max_iter=4, dtype=dtype, init="given", fuzzifier=2.0)

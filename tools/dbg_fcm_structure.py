@@ -31,8 +31,14 @@ if iters:  # exact fp32 tower iterations from C: a realistic late-iteration cent
         C[keep] = wx[keep] / ws[keep, None]
     print(f"after {iters} exact iterations")
 wr, wsr, labr = ref.fcm_partial(x.double(), C, m, True, acc_dtype=torch.float64, exact=True)
-D2 = ref.pairwise_sqdist(x.double(), C, exact=True)
-top3 = D2.topk(3, dim=1, largest=False)
+tops, colmin = [], torch.full((k,), float("inf"), dtype=torch.float64, device=dev)
+for r0 in range(0, n, 8192):  # chunked: the [n, K, D] difference block would not fit
+    dd = ref.pairwise_sqdist(x[r0:r0 + 8192].double(), C, exact=True)
+    tops.append(dd.topk(3, dim=1, largest=False))
+    colmin = torch.minimum(colmin, dd.min(0).values)
+from types import SimpleNamespace
+top3 = SimpleNamespace(values=torch.cat([t.values for t in tops]),
+                       indices=torch.cat([t.indices for t in tops]))
 near1 = torch.bincount(top3.indices[:, 0], minlength=k)
 near2 = torch.bincount(top3.indices[:, 1], minlength=k)
 near3 = torch.bincount(top3.indices[:, 2], minlength=k)
@@ -66,4 +72,4 @@ for name, mk in (("tower fp32", lambda: HipTowerFCM(x.float(), k, "fp32", m, Tru
           f"centroid err {cerr:.3e}  label agree {float((lab == labr).double().mean()):.5f}")
     for j in worst.tolist():
         print(f"   k={j} wsr {float(wsr[j]):.4e} ws {float(ws[j]):.4e} near1 {int(near1[j])} "
-              f"near2 {int(near2[j])} near3 {int(near3[j])} min d2 {float(D2[:, j].min()):.3f}")
+              f"near2 {int(near2[j])} near3 {int(near3[j])} min d2 {float(colmin[j]):.3f}")

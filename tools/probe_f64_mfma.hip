@@ -25,25 +25,30 @@ __global__ __launch_bounds__(256) void probe(double* out, int iters, double a0, 
   if (s == 12345.678) out[0] = s;  // keep the chain live
 }
 
+template <int NACC>
+void run(double* out, int cus, int wps, int iters) {
+  const int blocks = cus * wps;  // 4 waves per block: one per SIMD per block
+  hipLaunchKernelGGL(probe<NACC>, dim3(blocks), dim3(256), 0, 0, out, iters, 1.0, 2.0);
+  (void)hipDeviceSynchronize();
+  for (int rep = 0; rep < 2; ++rep) {
+    auto t0 = std::chrono::steady_clock::now();
+    hipLaunchKernelGGL(probe<NACC>, dim3(blocks), dim3(256), 0, 0, out, iters, 1.0, 2.0);
+    (void)hipDeviceSynchronize();
+    auto t1 = std::chrono::steady_clock::now();
+    const double s = std::chrono::duration<double>(t1 - t0).count();
+    const double flop = (double)blocks * 4 * iters * NACC * 16 * 16 * 4 * 2;
+    printf("accumulators %2d, waves/SIMD %d: %.3f ms, %.1f TF/s fp64 MFMA\n", NACC, wps, s * 1e3,
+           flop / s / 1e12);
+  }
+}
+
 int main() {
   double* out;
-  hipMalloc(&out, 8);
+  (void)hipMalloc(&out, 8);
   int cus = 0;
-  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
-  const int iters = 4096;
-  for (int wps = 1; wps <= 2; ++wps) {
-    const int blocks = cus * wps;  // 4 waves per block: one per SIMD per block
-    hipLaunchKernelGGL(probe<8>, dim3(blocks), dim3(256), 0, 0, out, iters, 1.0, 2.0);
-    hipDeviceSynchronize();
-    for (int rep = 0; rep < 3; ++rep) {
-      auto t0 = std::chrono::steady_clock::now();
-      hipLaunchKernelGGL(probe<8>, dim3(blocks), dim3(256), 0, 0, out, iters, 1.0, 2.0);
-      hipDeviceSynchronize();
-      auto t1 = std::chrono::steady_clock::now();
-      const double s = std::chrono::duration<double>(t1 - t0).count();
-      const double flop = (double)blocks * 4 * iters * 8 * 16 * 16 * 4 * 2;
-      printf("waves/SIMD %d: %.3f ms, %.1f TF/s fp64 MFMA\n", wps, s * 1e3, flop / s / 1e12);
-    }
-  }
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+  for (int wps = 1; wps <= 4; ++wps) run<8>(out, cus, wps, 4096);
+  for (int wps = 1; wps <= 2; ++wps) run<16>(out, cus, wps, 2048);
+  run<4>(out, cus, 4, 8192);
   return 0;
 }
