@@ -1164,11 +1164,20 @@ int launch_mstats(const void* Xh, const void* Xl, const float* xx, int64_t N, co
   hipLaunchKernelGGL((fcm_mfma_stats1_kernel<DP, MODE, WAVES>), dim3((unsigned)blocks), dim3(WAVES * 64), 0, s, \
                      (const __bf16*)Xh, (const __bf16*)Xl, xx, N, (const __bf16*)Ch,          \
                      (const __bf16*)Cl, cc, K, Kp / 64, p, labels, rowinfo, (float4*)fix)
-  // one product + fix-up from DP = 64 (fcm10m 19.05 -> 18.60 ms, profiles/fcm_stats1_ab_r04m.txt);
+  // one product + fix-up from DP = 64 (fcm10m 19.05 -> 18.60 ms, profiles/fcm_stats1_ab_r04m.txt)
+  // only for the one-product form (fix rows requested): its row normaliser is wrong where a
+  // third centroid sits within the one-product error of the nearest two (duplicate
+  // centroids of a tight blob: sum w +55 % on clustered data, profiles/
+  // fcm_bf16_witness_diag_it10_r06g.txt), so the bf16x3 form keeps bf16x3 in both passes;
   // at DP = 32 the bf16x3 kernel's 6 MFMAs per tile are not what bounds it
+  bool done = false;
   if constexpr (DP >= 64) {
-    if (m == 2.0) TDC_LS1(2); else TDC_LS1(0);
-  } else {
+    if (fix) {
+      if (m == 2.0) TDC_LS1(2); else TDC_LS1(0);
+      done = true;
+    }
+  }
+  if (!done) {
     if (m == 2.0) TDC_LS(2); else TDC_LS(0);
   }
 #undef TDC_LS

@@ -244,7 +244,9 @@ def run(args) -> int:
                   file=sys.stderr)
         dtype = resolve_dtype(args.dtype, args.K, d, args.method_name)
         if comm.is_root and args.dtype != dtype:
-            print(f"note: --dtype {args.dtype} resolved to {dtype} (D={d}, {args.method_name})",
+            print(f"note: --dtype {args.dtype} resolved to {dtype} (D={d}, K={args.K}, "
+                  f"{args.method_name}; the reference's fp64 precision where it runs on the "
+                  f"matrix cores -- --dtype bf16 trades it for the bf16 MFMA rate)",
                   file=sys.stderr)
         init = "first_k" if args.compat else args.init
         empty = "nan_any" if args.compat else args.empty_cluster

@@ -1643,19 +1643,16 @@ FCM_PRECISION = {
     "fp64_mfma": "fp64 distances as the GEMM expansion on the fp64 matrix cores (exact-zero "
                  "bound (3D+4) 2^-53 (|x|+|c|)^2), fp64 memberships, W^T X on the fp64 "
                  "matrix cores, fp64 sums",
-    # HipMfmaFCM, fcm_distances='x3' (default).  Measured against the fp64 oracle at m=2
-    # (tests/test_fcm_gpu.py): sum_i w within 2e-3*m (hi+lo rows) / 3e-3*m (bf16 rows) --
-    # NOT fp32-faithful: the stats pass's row normaliser keeps one-product terms for all
-    # but the two nearest centroids
-    "bf16": "stats pass (row normaliser, label): one bf16 product (x_hi . c_hi) per "
-            "centroid, each row's two nearest corrected to bf16x3 (D >= 64; bf16x3 for all "
-            "below); accumulate pass: bf16x3 distances; fp32 memberships, bf16 weights in the "
-            "W^T X MFMAs (hi+lo rows), fp64 sums; sum w within ~2e-3*m of fp64",
+    # HipMfmaFCM, fcm_distances='x3' (default): bf16x3 in both passes.  bf16 hi + lo hold 16
+    # of fp32's 24 mantissa bits, so a product carries ~3 2^-16 |x||c| of error -- relative
+    # to a small d2 next to a centroid that is percent-level on tight, well-separated
+    # clusters (the fcm10m witness); sum w within ~2e-3*m of fp64 on the oracle tests
+    "bf16": "bf16x3 MFMA distances in both passes (|d2 error| ~ 3 2^-16 |x-mu||c-mu|), "
+            "fp32 memberships, bf16 weights in the W^T X MFMAs (hi+lo rows), fp64 sums",
     # ... on a bf16 shard from D = 64: W^T X takes the bf16 rows themselves (exact products)
-    "bf16_raw": "stats pass: one bf16 product per centroid, each row's two nearest corrected "
-                "to bf16x3; accumulate pass: bf16x3 distances; fp32 memberships; W^T X = bf16 "
-                "weights x the bf16 rows (exact products, fp32 accumulate), fp64 sums; sum w "
-                "within ~3e-3*m of fp64",
+    "bf16_raw": "bf16x3 MFMA distances in both passes (|d2 error| ~ 3 2^-16 "
+                "|x-mu||c-mu|), fp32 memberships; W^T X = bf16 weights x the bf16 rows (exact "
+                "products, fp32 accumulate), fp64 sums",
     # HipMfmaFCM from D = 64, fcm_distances='one': both passes one product + the fix-up
     "bf16_one": "both passes: one bf16 product (x_hi . c_hi, ~2^-9/sqrt(D) relative error "
                 "on x.c) per centroid, each row's two nearest corrected to bf16x3; fp32 "

@@ -192,7 +192,7 @@ def test_fcm_dispatch_native_up_to_1024(gpu):
                                                ("bf16", 768, 40, "hip_fcm_mfma"),
                                                ("fp32", 512, 64, "hip_fcm_wide"),
                                                ("fp64", 6, 40, "hip_fcm_tower"),
-                                               ("fp64", 64, 100, "hip_fcm_tower"),
+                                               ("fp64", 64, 100, "hip_fcm_wide"),
                                                ("fp32", 12, 64, "hip_fcm_tower"),
                                                ("fp32", 128, 256, "hip_fcm_wide"),
                                                ("fp64", 128, 256, "hip_fcm_wide"),

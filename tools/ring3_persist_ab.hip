@@ -269,6 +269,179 @@ void ring3p_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+
+// ring2x: the 32x32x16 shape with ring3's refinements (saddr-form LDS-DMA, stage-level
+// running minimum, early slot release, two waves per SIMD).  A 32x32x16 MFMA holds the
+// SIMD's issue for 8 of its 32 cycles (16x16x32: 8 of 16), so the tag + min epilogue
+// (16 scores per lane per tile) leaves slack where ring3 is issue-bound.
+template <int DP, int P, int NST, int WAVES, int QT>
+__global__ __launch_bounds__(WAVES * 64, 2)
+void ring2x_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
+                   const __bf16* __restrict__ Cm2, const float* __restrict__ cnorm, int ntiles,
+                   int32_t* __restrict__ labels) {
+  constexpr int BNL = 32 * QT;
+  constexpr int CPR = DP / 8;
+  constexpr int KS = DP / 16;
+  constexpr int HALF = DP / 2;
+  constexpr int TILE_B = BNL * DP * 2;
+  constexpr int NORM_B = BNL * 4;
+  constexpr int STAGE_B = TILE_B + NORM_B;
+  constexpr int PIECES = TILE_B / 1024;
+  constexpr int PPW = (PIECES + WAVES - 1) / WAVES;
+  constexpr int NCH = NORM_B / 16;
+  constexpr int NPW = (NCH + WAVES - 1) / WAVES;
+  constexpr int VPS = PPW + 1;
+  constexpr unsigned EMB = QT * 16 <= 32 ? 31u : 63u;
+  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE_B];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t pbase = (int64_t)blockIdx.x * (WAVES * P * 32) + (int64_t)w * (P * 32);
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  bf16x8 bq[P][KS];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    int64_t row = pbase + p * 32 + r;
+    if (row >= N) row = N - 1;
+    const bf16x8* src = reinterpret_cast<const bf16x8*>(X + row * ldx + h * HALF);
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) bq[p][kk] = src[kk];
+  }
+  unsigned voff[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int piece = (w * PPW + i) % PIECES;
+    const int L = piece * 64 + lane;
+    const int row = L / CPR, cp = L % CPR;
+    voff[i] = (unsigned)((row * DP + swz<DP>(row, cp) * 8) * 2);
+  }
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  auto issue = [&](int t, int slot) __attribute__((always_inline)) {
+    const __bf16* base = Cm2 + (int64_t)t * BNL * DP;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int piece = (wu * PPW + i) % PIECES;
+      const unsigned dst = lds0 + slot * STAGE_B + piece * 1024;
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, %2"
+                   :: "s"(__builtin_amdgcn_readfirstlane(dst)), "v"(voff[i]), "s"(base)
+                   : "memory", "m0");
+    }
+    const int nb = w * NPW < NCH - NPW ? w * NPW : NCH - NPW;
+    if (lane < NPW) {
+      const float* src = cnorm + (int64_t)t * BNL + (nb + lane) * 4;
+      __builtin_amdgcn_global_load_lds(
+          (const void*)src,
+          (__attribute__((address_space(3))) void*)(smem + slot * STAGE_B + TILE_B + nb * 16),
+          16, 0, 0);
+    }
+  };
+#pragma unroll
+  for (int t = 0; t < NST - 1; ++t) issue(t < ntiles ? t : ntiles - 1, t);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * VPS) : "memory");
+  __builtin_amdgcn_s_barrier();
+  float best[P];
+  int bt[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    best[p] = INFINITY;
+    bt[p] = 0;
+  }
+  unsigned aoff[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) aoff[kk] = lds0 + r * (DP * 2) + swz<DP>(r, h * (CPR / 2) + kk) * 16;
+  const unsigned noff = lds0 + TILE_B + 16 * h;
+  auto stage = [&](int t, auto slot_c) __attribute__((always_inline)) {
+    constexpr int slot = decltype(slot_c)::value;
+    {
+      const int tn = t + NST - 1;
+      issue(tn < ntiles ? tn : ntiles - 1, (slot + NST - 1) % NST);
+    }
+    float m[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) m[p] = INFINITY;
+#pragma unroll
+    for (int q = 0; q < QT; ++q) {
+      auto afrag = [&](int kk) __attribute__((always_inline)) {
+        bf16x8 a;
+        asm volatile("ds_read_b128 %0, %1 offset:%2"
+                     : "=v"(a) : "v"(aoff[kk]), "i"(slot * STAGE_B + q * 32 * DP * 2));
+        return a;
+      };
+      f32x4 n4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        asm volatile("ds_read_b128 %0, %1 offset:%2"
+                     : "=v"(n4[j]) : "v"(noff), "i"(slot * STAGE_B + (q * 32 + 8 * j) * 4));
+      bf16x8 a0 = afrag(0);
+      bf16x8 a1 = afrag(1);
+      f32x16 acc[P];
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        bf16x8 a2 = a1;
+        if (kk + 2 < KS) a2 = afrag(kk + 2);
+        if (kk + 2 < KS) asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");
+        else if (kk + 1 < KS) asm volatile("s_waitcnt lgkmcnt(1)" ::: "memory");
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (q == QT - 1 && kk == KS - 1) {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * VPS) : "memory");
+          __builtin_amdgcn_s_barrier();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+          if (kk == 0) {
+            f32x16 init;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              init[4 * j + 0] = n4[j][0];
+              init[4 * j + 1] = n4[j][1];
+              init[4 * j + 2] = n4[j][2];
+              init[4 * j + 3] = n4[j][3];
+            }
+            acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq[p][0], init, 0, 0, 0);
+          } else {
+            acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq[p][kk], acc[p], 0, 0, 0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        a0 = a1;
+        a1 = a2;
+      }
+#pragma unroll
+      for (int p = 0; p < P; ++p)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float v = __uint_as_float((__float_as_uint(acc[p][i]) & ~EMB) | (unsigned)(q * 16 + i));
+          m[p] = __builtin_fminf(m[p], v);
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const bool up = m[p] < best[p];
+      best[p] = up ? m[p] : best[p];
+      bt[p] = up ? t : bt[p];
+    }
+  };
+  for (int t0 = 0; t0 < ntiles; t0 += NST) {
+    stage(t0, std::integral_constant<int, 0>{});
+    if constexpr (NST > 1) if (t0 + 1 < ntiles) stage(t0 + 1, std::integral_constant<int, 1>{});
+    if constexpr (NST > 2) if (t0 + 2 < ntiles) stage(t0 + 2, std::integral_constant<int, 2 % NST>{});
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const float ob = __shfl_xor(best[p], 32, 64);
+    const int obt = __shfl_xor(bt[p], 32, 64);
+    const unsigned e0 = __float_as_uint(best[p]) & EMB, e1 = __float_as_uint(ob) & EMB;
+    const int l0 = bt[p] * BNL + (int)(e0 >> 4) * 32 + (int)(e0 & 3) + 8 * (int)((e0 & 15) >> 2) + 4 * h;
+    const int l1 = obt * BNL + (int)(e1 >> 4) * 32 + (int)(e1 & 3) + 8 * (int)((e1 & 15) >> 2) + 4 * (1 - h);
+    const float v0 = __uint_as_float(__float_as_uint(best[p]) & ~EMB);
+    const float v1 = __uint_as_float(__float_as_uint(ob) & ~EMB);
+    const bool other = (v1 < v0) || (v1 == v0 && l1 < l0);
+    const int64_t row = pbase + p * 32 + r;
+    if (h == 0 && row < N) labels[row] = other ? l1 : l0;
+  }
+}
+
 static uint64_t sm64(uint64_t& s) {
   uint64_t z = (s += 0x9e3779b97f4a7c15ull);
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -316,6 +489,13 @@ static void var(const Bufs& b, hipStream_t s, int stagger, int slots = 2) {
   hipLaunchKernelGGL((ring3p_kernel<128, 8, 2, 4, 4, PERSIST, RELOAD>), dim3((unsigned)grid),
                      dim3(256), 0, s, b.x, b.n, (int64_t)DP, b.c, b.cn, b.kp / 64, b.lab, nblk,
                      stagger, g_cus * 2);
+}
+
+template <int P, int NST, int QT>
+static void r2x(const Bufs& b, hipStream_t s) {
+  const int64_t per = 4 * P * 32;
+  hipLaunchKernelGGL((ring2x_kernel<128, P, NST, 4, QT>), dim3((unsigned)((b.n + per - 1) / per)),
+                     dim3(256), 0, s, b.x, b.n, (int64_t)DP, b.c, b.cn, b.kp / (32 * QT), b.lab);
 }
 
 template <typename F>
@@ -396,26 +576,22 @@ int main(int argc, char** argv) {
   CK(hipMemset(l1, 0xff, N * 4));          \
   __VA_ARGS__;                             \
   check(NAME);
-  TRY("copy", (var<false, false>(b1, 0, 0)))
-  TRY("copy + stagger 100", (var<false, false>(b1, 0, 100)))
-  TRY("persist", (var<true, false>(b1, 0, 0)))
+  TRY("ring2x P4 NST2 QT2", (r2x<4, 2, 2>(b1, 0)))
+  TRY("ring2x P4 NST3 QT2", (r2x<4, 3, 2>(b1, 0)))
+  TRY("ring2x P4 NST2 QT1", (r2x<4, 2, 1>(b1, 0)))
+  TRY("ring2x P2 NST3 QT2", (r2x<2, 3, 2>(b1, 0)))
   TRY("persist + reload", (var<true, true>(b1, 0, 0)))
-  TRY("persist + reload + stagger", (var<true, true>(b1, 0, 100)))
   const double flop = 2.0 * (double)N * Kp * DP;
   for (int round = 0; round < 3; ++round) {
     const float t0 = timeit([&] { prod(b0, 0); }, reps);
-    const float t1 = timeit([&] { var<false, false>(b1, 0, 0); }, reps);
-    const float t2 = timeit([&] { var<false, false>(b1, 0, 50); }, reps);
-    const float t3 = timeit([&] { var<false, false>(b1, 0, 100); }, reps);
-    const float t4 = timeit([&] { var<true, false>(b1, 0, 0); }, reps);
-    const float t5 = timeit([&] { var<true, false>(b1, 0, 100); }, reps);
-    const float t6 = timeit([&] { var<true, true>(b1, 0, 0); }, reps);
-    const float t7 = timeit([&] { var<true, true>(b1, 0, 50); }, reps);
-    const float t8 = timeit([&] { var<true, true>(b1, 0, 100); }, reps);
-    printf("round %d: prod %.3f ms (%.0f TF/s) | copy %.3f | stag50 %.3f | stag100 %.3f | "
-           "persist %.3f | persist+stag100 %.3f | reload %.3f | reload+stag50 %.3f | "
-           "reload+stag100 %.3f\n",
-           round, t0, flop / t0 / 1e9, t1, t2, t3, t4, t5, t6, t7, t8);
+    const float t1 = timeit([&] { r2x<4, 2, 2>(b1, 0); }, reps);
+    const float t2 = timeit([&] { r2x<4, 3, 2>(b1, 0); }, reps);
+    const float t3 = timeit([&] { r2x<4, 2, 1>(b1, 0); }, reps);
+    const float t4 = timeit([&] { r2x<2, 3, 2>(b1, 0); }, reps);
+    const float t5 = timeit([&] { var<false, false>(b1, 0, 0); }, reps);
+    printf("round %d: prod ring3 %.3f ms (%.0f TF/s) | ring2x P4N2Q2 %.3f | P4N3Q2 %.3f | "
+           "P4N2Q1 %.3f | P2N3Q2 %.3f | ring3 copy %.3f\n",
+           round, t0, flop / t0 / 1e9, t1, t2, t3, t4, t5);
     fflush(stdout);
   }
   return 0;
