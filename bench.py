@@ -56,16 +56,18 @@ PRESETS = {
                        dtype="fp64", method="fcm"),
     "embed50m_fp8": dict(n_per_gpu=50_000_000, dim=768, k=65536, scaling="strong", mode="lloyd",
                          dtype="fp8"),
-    # FCM at the headline shape on the MFMA tower: one-product distances with the two
-    # nearest corrected (--fcm-distances x3: bf16x3), fp32 memberships, bf16 weights x the
-    # bf16 rows in W^T X (ops.FCM_PRECISION, reported with the witness; --dtype fp32 runs
-    # the exact fp32 tower), m = 2 (the reference's m = D = 128 would underflow every u^m)
+    # FCM at the headline shape on the bf16 MFMA tower: bf16x3 distances in both passes
+    # (the library default; --fcm-distances one: one product + two-nearest fix-up, ~20 %
+    # faster but 4 % off in the centroids on this data, profiles/bench_fcm10m_one_std025_r06h),
+    # fp32 memberships, bf16 weights x the bf16 rows in W^T X (ops.FCM_PRECISION, reported
+    # with the witness; --dtype fp32 / fp64 run the fp64 matrix-core path), m = 2 (the
+    # reference's m = D = 128 would underflow every u^m).
     # cluster_std 0.25: at the blob generator's default 1.0, m=2 FCM at D=128, K=1024 pulls
     # every centroid onto the grand mean within the timed steps (distance concentration;
     # the final-state witness was then vacuous, final_ws_spread 0.0); at 0.25 the clusters
     # keep their structure (tests/test_bench_cpu.py::test_fcm10m_preset_keeps_structure)
     "fcm10m": dict(n_per_gpu=10_000_000, dim=128, k=1024, scaling="weak", mode="lloyd",
-                   dtype="bf16", method="fcm", fuzzifier=2.0, fcm_distances="one",
+                   dtype="bf16", method="fcm", fuzzifier=2.0, fcm_distances="x3",
                    cluster_std=0.25),
 }
 

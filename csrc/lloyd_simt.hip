@@ -569,7 +569,10 @@ __global__ __launch_bounds__(256) void assign_exact_few_kernel(const T* __restri
   constexpr int RB = EXACT_FEW_RB, KT = 256, DC = 32;
   // the row group's rows, staged once (D <= EXACT_FEW_MAXD, zero-padded to the chunk): a
   // per-chunk slice had put two dependent global loads (index, row) on every chunk
-  __shared__ __attribute__((aligned(16))) T s_x[EXACT_FEW_MAXD][RB];
+  // the row group's rows: dynamic LDS sized by the launch (Dp x RB): a static D = 1024
+  // image (64 KiB in fp64) had left room for one workgroup per CU
+  extern __shared__ __attribute__((aligned(16))) char few_smem[];
+  T(*s_x)[RB] = reinterpret_cast<T(*)[RB]>(few_smem);
   __shared__ T s_c[DC][KT + 1];
   __shared__ T s_rb[4][RB];
   __shared__ int s_rk[4][RB];
@@ -748,17 +751,20 @@ int tdc_assign_exact(int dtype, const void* X, int64_t N, int64_t ldx, int D, co
   if (few) {
     if (!rowidx) return (int)hipErrorInvalidValue;
     // both launches read the listed count; exactly one of them has work
-    const int64_t cap = (int64_t)(num_cus > 0 ? num_cus : 256) * 4;
     int64_t fb;
     // K split: the grid covers the row groups of up to EXACT_FEW_MAX rows or, when fewer are
     // listed, their 256-centroid chunks (a few hundred workgroups either way)
-    fb = cap;
+    // two workgroups per CU: the listed count is read on the device, the few busy
+    // workgroups split their row groups over K (exact_few_splits), the rest leave at once
+    fb = (int64_t)(num_cus > 0 ? num_cus : 256) * 2;
+    const int dpad = (D + 31) / 32 * 32;
+    const size_t few_lds = (size_t)dpad * EXACT_FEW_RB * (dtype == TDC_F64 ? 8 : 4);
     char* parts = (char*)few_parts(dtype == TDC_F64 ? 8 : 4);
     if (!parts) return (int)hipErrorOutOfMemory;
     int* part_k = (int*)(parts + (size_t)EXACT_FEW_PARTS * 8);
     const int mb = (EXACT_FEW_PARTS + 255) / 256;
     if (dtype == TDC_F32) {
-      hipLaunchKernelGGL(assign_exact_few_kernel<float>, dim3((unsigned)fb), dim3(256), 0, s,
+      hipLaunchKernelGGL(assign_exact_few_kernel<float>, dim3((unsigned)fb), dim3(256), few_lds, s,
                          (const float*)X, ldx, D, (const float*)C, K, labels, (float*)mind, rowidx,
                          nptr, (float*)parts, part_k);
       TDC_CHECK_LAUNCH();
@@ -766,7 +772,7 @@ int tdc_assign_exact(int dtype, const void* X, int64_t N, int64_t ldx, int D, co
                          (int)fb, labels, (float*)mind, rowidx, nptr, (const float*)parts,
                          (const int*)part_k);
     } else if (dtype == TDC_F64) {
-      hipLaunchKernelGGL(assign_exact_few_kernel<double>, dim3((unsigned)fb), dim3(256), 0, s,
+      hipLaunchKernelGGL(assign_exact_few_kernel<double>, dim3((unsigned)fb), dim3(256), few_lds, s,
                          (const double*)X, ldx, D, (const double*)C, K, labels, (double*)mind,
                          rowidx, nptr, (double*)parts, part_k);
       TDC_CHECK_LAUNCH();

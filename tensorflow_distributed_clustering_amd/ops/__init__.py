@@ -1053,9 +1053,20 @@ class HipX3Lloyd(_LocalOpsBase):
                                pre, self.xnhl[:n] if pre is not None else None, est)
             if pre is not None and self._pre_ev is None and \
                     not torch.cuda.is_current_stream_capturing():
-                self._pre_host.copy_(self.amb_count[2:3], non_blocking=True)
-                self._pre_ev = torch.cuda.Event()
-                self._pre_ev.record()
+                # the count goes to the host on a side stream (a D2H blit on the compute
+                # stream held it ~38 us per step, profiles/fp64_2m_ksplit_kernel_stats_r06h.txt),
+                # from a device snapshot that is rewritten only after this copy has landed
+                if getattr(self, "_copy_stream", None) is None:
+                    self._copy_stream = torch.cuda.Stream(device=self.device)
+                    self._pre_snap = torch.zeros(1, dtype=torch.int32, device=self.device)
+                self._pre_snap.copy_(self.amb_count[2:3])
+                ev0 = torch.cuda.Event()
+                ev0.record()
+                self._copy_stream.wait_event(ev0)
+                with torch.cuda.stream(self._copy_stream):
+                    self._pre_host.copy_(self._pre_snap, non_blocking=True)
+                    self._pre_ev = torch.cuda.Event()
+                    self._pre_ev.record(self._copy_stream)
                 self._pre_n = n
         else:
             self.ops.x3_prep(self.cnorm, self.cnhl, self.k, self.cstat, self.amb_count)
