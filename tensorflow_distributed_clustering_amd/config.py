@@ -42,13 +42,13 @@ class ClusterConfig:
     fuzzifier       FCM m. ``None`` = compat value D (`:121,129`).
     fcm_nan_to_zero compat: membership NaN (point on a centroid) -> 0 (`:125-126`);
                     False gives the correct one-hot membership.
-    fcm_distances   bf16 FCM on the matrix cores (D >= 64): 'x3' (default) runs the
-                    fp32-faithful bf16x3 distances in the accumulate pass; 'one' runs ONE
-                    bf16 product per distance with each row's two nearest centroids
-                    corrected to bf16x3 (0.87x the step at fcm10m, but at a random-row
-                    init on that data the centroid error against the fp64 oracle is
-                    9.4e-3 ('one') vs 9.0e-4 ('x3') of max|c|, profiles/bench_fcm10m_*_r05h;
-                    the stats pass runs one product + fix-up either way).
+    fcm_distances   bf16 FCM on the matrix cores (D >= 64): 'x3' (default) runs bf16x3
+                    distances (16 of fp32's 24 mantissa bits per operand) in both passes;
+                    'one' runs ONE bf16 product per distance with each row's two nearest
+                    centroids corrected to bf16x3 (0.8x the step at fcm10m, but wrong where a
+                    third centroid sits inside the one-product error of a tight blob: on the
+                    fcm10m data 4.0e-2 ('one') vs 3.1e-5 ('x3') of max|c| against the fp64
+                    oracle, profiles/bench_fcm10m_*_std025_r06h).
     empty_cluster   'keep' (default) | 'nan' (globally empty -> NaN, the segment-sum
                     notebook) | 'nan_any' (empty on ANY rank -> NaN, the script's
                     reduce_mean poisoning) | 'reseed' | 'zero'

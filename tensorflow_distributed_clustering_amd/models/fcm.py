@@ -43,7 +43,8 @@ FCM_FP32_MIN_LOG2_W = -100.0
 
 def fcm_dtype(cfg: ClusterConfig, m: Optional[float] = None) -> torch.dtype:
     """Row / membership dtype: fp32 for fp32 and bf16/fp8 configs (bf16 selects the MFMA
-    towers, whose distances are bf16x3 -- fp32-faithful -- and whose W^T X weights are bf16).
+    towers, whose distances are bf16x3 -- 16 mantissa bits per operand -- and whose W^T X
+    weights are bf16; fp32 from K = 64, D = 64 is promoted to the fp64 matrix-core path).
 
     With the reference's fuzzifier m = D (`distribuitedClustering.py:121,129`) the weights
     u^m of a point's typical memberships u ~ 1/K fall to K^-m: 2^-144 at K=64, D=24, below
