@@ -145,8 +145,9 @@ def test_delta_matches_full_50_iterations(gpu):
     rd, ed = _fit(x, k, 50, update="delta")
     assert ef.update_mode == "full" and ed.update_mode == "delta"
     st = ed.update_stats()
-    # warm-up step + 50: full at the first step and every 32 steps since the reset
-    assert st["steps"] == 51 and st["full_steps"] == 2, st
+    # warm-up step + 50: the warm-up is full, the delta state is reset after it (timed
+    # iteration 1 re-sums every row, as the reference's first iteration), then every 32 steps
+    assert st["steps"] == 51 and st["full_steps"] == 3, st
     assert st["moved_rows"] / max(1.0, st["moved_steps"]) < 0.05 * n
     np.testing.assert_allclose(rd.centers, rf.centers, rtol=1e-5, atol=1e-5)
     assert (rd.labels == rf.labels).float().mean().item() >= 0.999

@@ -28,6 +28,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
+#include <map>
 #include <vector>
 
 #include "assign_mfma_impl.h"
@@ -47,8 +49,14 @@ template <int DP, int P, int NST, int WAVES, int QT, bool PERSIST, bool RELOAD>
 __global__ __launch_bounds__(WAVES * 64, 2)
 void ring3p_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
                    const __bf16* __restrict__ Cm2, const float* __restrict__ cnorm, int ntiles,
-                   int32_t* __restrict__ labels, int64_t nblk, int stagger, int stag_blocks) {
+                   int32_t* __restrict__ labels, int64_t nblk, int stagger, int stag_blocks,
+                   unsigned long long* __restrict__ stamps = nullptr) {
   static_assert(!RELOAD || (PERSIST && NST == 2), "reload: persistent, two-slot ring");
+  // stamps (diagnostic build only, non-persistent): per block, from wave 0 lane 0 --
+  // s_memtime at entry, after the prologue barrier (points + first ring stage landed), after
+  // the K loop, and the CU id (HW_ID bits 8-15 | XCC_ID << 8)
+  unsigned long long st0 = 0, st1 = 0;
+  if (stamps) st0 = __builtin_amdgcn_s_memtime();
   constexpr int BNL = 16 * QT;
   constexpr int CPR = DP / 8;
   constexpr int KS = DP / 32;
@@ -155,6 +163,7 @@ void ring3p_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
     for (int t = 0; t < NST - 1; ++t) issue(t < ntiles ? t : ntiles - 1, t);
     asm volatile("s_waitcnt vmcnt(%0)" ::"i"((NST - 2) * VPS) : "memory");
     __builtin_amdgcn_s_barrier();
+    if (stamps) st1 = __builtin_amdgcn_s_memtime();
 
     float best[P];
     int bt[P];
@@ -247,6 +256,18 @@ void ring3p_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 
+    if (stamps) {
+      const unsigned long long st2 = __builtin_amdgcn_s_memtime();
+      unsigned hw, xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      if (tid == 0) {
+        stamps[blk * 4 + 0] = st0;
+        stamps[blk * 4 + 1] = st1;
+        stamps[blk * 4 + 2] = st2;
+        stamps[blk * 4 + 3] = (unsigned long long)(((hw >> 8) & 0xffu) | ((xcc & 0xfu) << 8));
+      }
+    }
     const int64_t pbase = blk * PER + (int64_t)w * (P * 16);
 #pragma unroll
     for (int p = 0; p < P; ++p) {
@@ -481,14 +502,73 @@ static void prod(const Bufs& b, hipStream_t s) {
                      (int64_t)DP, b.c, b.cn, b.kp / 64, b.lab, nullptr);
 }
 
+static unsigned long long* g_stamps = nullptr;
+
 template <bool PERSIST, bool RELOAD>
-static void var(const Bufs& b, hipStream_t s, int stagger, int slots = 2) {
+static void var(const Bufs& b, hipStream_t s, int stagger, int slots = 2, bool stamp = false) {
   const int64_t per = 4 * 8 * 16;
   const int64_t nblk = (b.n + per - 1) / per;
   const int64_t grid = PERSIST ? std::min<int64_t>(nblk, (int64_t)g_cus * slots) : nblk;
   hipLaunchKernelGGL((ring3p_kernel<128, 8, 2, 4, 4, PERSIST, RELOAD>), dim3((unsigned)grid),
                      dim3(256), 0, s, b.x, b.n, (int64_t)DP, b.c, b.cn, b.kp / 64, b.lab, nblk,
-                     stagger, g_cus * 2);
+                     stagger, g_cus * 2, stamp ? g_stamps : nullptr);
+}
+
+// per-block stamps -> where the prologue cycles go and whether co-resident blocks' prologues
+// overlap (printed summary)
+static void analyse_stamps(int64_t nblk) {
+  std::vector<unsigned long long> h((size_t)nblk * 4);
+  CK(hipMemcpy(h.data(), g_stamps, h.size() * 8, hipMemcpyDeviceToHost));
+  struct B { unsigned long long s0, s1, s2; unsigned cu; };
+  std::vector<B> v;
+  v.reserve(nblk);
+  unsigned long long tmin = ~0ull, tmax = 0;
+  for (int64_t i = 0; i < nblk; ++i) {
+    B b{h[4 * i], h[4 * i + 1], h[4 * i + 2], (unsigned)h[4 * i + 3]};
+    if (b.s1 < b.s0 || b.s2 < b.s1) continue;
+    v.push_back(b);
+    tmin = std::min(tmin, b.s0);
+    tmax = std::max(tmax, b.s2);
+  }
+  double pro = 0, loop = 0;
+  std::vector<double> pr;
+  for (auto& b : v) {
+    pro += (double)(b.s1 - b.s0);
+    loop += (double)(b.s2 - b.s1);
+    pr.push_back((double)(b.s1 - b.s0));
+  }
+  std::sort(pr.begin(), pr.end());
+  const double n = (double)v.size();
+  printf("  stamps: %zu blocks, span %.3g cycles; prologue (entry -> first barrier) mean %.0f "
+         "p10 %.0f p50 %.0f p90 %.0f cycles; K loop mean %.0f cycles; prologue share of block "
+         "time %.1f %%\n",
+         v.size(), (double)(tmax - tmin), pro / n, pr[(size_t)(0.1 * n)], pr[(size_t)(0.5 * n)],
+         pr[(size_t)(0.9 * n)], loop / n, 100.0 * pro / (pro + loop));
+  // per CU: how much of each block's prologue overlaps another block's K loop on that CU
+  std::map<unsigned, std::vector<B>> cu;
+  for (auto& b : v) cu[b.cu].push_back(b);
+  double ov = 0, ov2 = 0, tot = 0;
+  size_t ncu = cu.size();
+  for (auto& kv : cu) {
+    auto& bl = kv.second;
+    std::sort(bl.begin(), bl.end(), [](const B& a, const B& c) { return a.s0 < c.s0; });
+    for (size_t i = 0; i < bl.size(); ++i) {
+      const double a0 = (double)bl[i].s0, a1 = (double)bl[i].s1;
+      double covered = 0, both = 0;  // other block in its loop / in its own prologue
+      for (size_t j = (i > 8 ? i - 8 : 0); j < std::min(bl.size(), i + 8); ++j) {
+        if (j == i) continue;
+        const double l0 = std::max(a0, (double)bl[j].s1), l1 = std::min(a1, (double)bl[j].s2);
+        if (l1 > l0) covered += l1 - l0;
+        const double p0 = std::max(a0, (double)bl[j].s0), p1 = std::min(a1, (double)bl[j].s1);
+        if (p1 > p0) both += p1 - p0;
+      }
+      ov += covered;
+      ov2 += both;
+      tot += a1 - a0;
+    }
+  }
+  printf("  per CU (%zu CUs): %.1f %% of prologue cycles run beside another block's K loop, "
+         "%.1f %% beside another block's prologue\n", ncu, 100.0 * ov / tot, 100.0 * ov2 / tot);
 }
 
 template <int P, int NST, int QT>
@@ -576,6 +656,19 @@ int main(int argc, char** argv) {
   CK(hipMemset(l1, 0xff, N * 4));          \
   __VA_ARGS__;                             \
   check(NAME);
+  {
+    const int64_t nblk = (N + 511) / 512;
+    CK(hipMalloc(&g_stamps, (size_t)nblk * 4 * 8));
+    CK(hipMemset(g_stamps, 0, (size_t)nblk * 4 * 8));
+    for (int i = 0; i < 3; ++i) var<false, false>(b1, 0, 0);
+    TRY("copy + stamps", (var<false, false>(b1, 0, 0, 2, true)))
+    analyse_stamps(nblk);
+    for (int i = 0; i < 3; ++i) var<false, false>(b1, 0, 0);
+    TRY("copy + stamps (again)", (var<false, false>(b1, 0, 0, 2, true)))
+    analyse_stamps(nblk);
+    TRY("stagger 100 + stamps", (var<false, false>(b1, 0, 100, 2, true)))
+    analyse_stamps(nblk);
+  }
   TRY("ring2x P4 NST2 QT2", (r2x<4, 2, 2>(b1, 0)))
   TRY("ring2x P4 NST3 QT2", (r2x<4, 3, 2>(b1, 0)))
   TRY("ring2x P4 NST2 QT1", (r2x<4, 2, 1>(b1, 0)))
