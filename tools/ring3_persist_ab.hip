@@ -45,13 +45,19 @@ using namespace tdc;
     }                                                                                   \
   } while (0)
 
-template <int DP, int P, int NST, int WAVES, int QT, bool PERSIST, bool RELOAD>
+// PF > 0 (non-persistent): in each of the block's last PF stages every wave touches a share of
+// the rows of block blockIdx.x + pf_stride (the block the dispatcher most likely starts next
+// on this XCD: blocks go round-robin over the 8 XCDs) with 4-byte LDS-DMA loads into a sink,
+// one 128-B line per lane, so that block's point prologue hits the XCD's L2 instead of HBM
+template <int DP, int P, int NST, int WAVES, int QT, bool PERSIST, bool RELOAD, int PF = 0>
 __global__ __launch_bounds__(WAVES * 64, 2)
 void ring3p_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
                    const __bf16* __restrict__ Cm2, const float* __restrict__ cnorm, int ntiles,
                    int32_t* __restrict__ labels, int64_t nblk, int stagger, int stag_blocks,
-                   unsigned long long* __restrict__ stamps = nullptr) {
+                   unsigned long long* __restrict__ stamps = nullptr, int pf_stride = 0) {
   static_assert(!RELOAD || (PERSIST && NST == 2), "reload: persistent, two-slot ring");
+  static_assert(PF == 0 || !PERSIST, "prefetch: one block per workgroup");
+  static_assert(PF == 0 || NST == 2, "prefetch: the stage-end wait must be vmcnt(0)");
   // stamps (diagnostic build only, non-persistent): per block, from wave 0 lane 0 --
   // s_memtime at entry, after the prologue barrier (points + first ring stage landed), after
   // the K loop, and the CU id (HW_ID bits 8-15 | XCC_ID << 8)
@@ -70,7 +76,7 @@ void ring3p_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
   constexpr int VPS = PPW + 1;
   constexpr unsigned EMB = QT * 4 <= 16 ? 15u : 31u;
   constexpr int PER = WAVES * P * 16;
-  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE_B];
+  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE_B + (PF ? WAVES * 256 : 0)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -78,6 +84,26 @@ void ring3p_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
   const int r = lane & 15;
   const int g = lane >> 4;
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  // prefetch lines: PER rows x DP x 2 B of the next block = PER * DP / 64 lines of 128 B,
+  // split over the waves and the PF stages (lane = one line)
+  constexpr int LINES = PER * DP * 2 / 128;
+  constexpr int LPS = PF ? (LINES + WAVES * PF * 64 - 1) / (WAVES * PF * 64) : 0;  // instrs/stage
+  const int64_t pfb = (int64_t)blockIdx.x + pf_stride;
+  const bool pf_on = PF && pf_stride > 0 && pfb < nblk;
+  const __bf16* pf_base = X + (pf_on ? pfb * PER * ldx : 0);
+  const int64_t pf_lines = pf_on ? min((int64_t)LINES, ((N - pfb * PER) * ldx * 2 + 127) / 128) : 0;
+  auto prefetch = [&](int j) __attribute__((always_inline)) {  // j: 0 .. PF-1
+#pragma unroll
+    for (int i = 0; i < LPS; ++i) {
+      int64_t line = ((int64_t)(j * LPS + i) * WAVES + w) * 64 + lane;
+      if (line >= pf_lines) line = pf_lines - 1;
+      const unsigned voffp = (unsigned)(line * 128);
+      const unsigned dst = lds0 + NST * STAGE_B + w * 256;
+      asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dword %1, %2"
+                   :: "s"(__builtin_amdgcn_readfirstlane(dst)), "v"(voffp), "s"(pf_base)
+                   : "memory", "m0");
+    }
+  };
 
   if (stagger > 0 && (int)blockIdx.x < stag_blocks) {
     unsigned h = (unsigned)blockIdx.x * 2654435761u;
@@ -177,6 +203,10 @@ void ring3p_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
       constexpr int slot = decltype(slot_c)::value;
       // RELOAD: the block's last stage issues no refill (uniform branch)
       const bool last = RELOAD && t == ntiles - 1;
+      if constexpr (PF > 0) {
+        // the oldest load of the stage, so the stage-end vmcnt wait finds it landed first
+        if (pf_on && t >= ntiles - PF) prefetch(t - (ntiles - PF));
+      }
       if (!last) {
         const int tn = t + NST - 1;
         issue(tn < ntiles ? tn : ntiles - 1, (slot + NST - 1) % NST);
@@ -504,6 +534,15 @@ static void prod(const Bufs& b, hipStream_t s) {
 
 static unsigned long long* g_stamps = nullptr;
 
+template <int PF>
+static void pfv(const Bufs& b, hipStream_t s, int stride) {
+  const int64_t per = 4 * 8 * 16;
+  const int64_t nblk = (b.n + per - 1) / per;
+  hipLaunchKernelGGL((ring3p_kernel<128, 8, 2, 4, 4, false, false, PF>), dim3((unsigned)nblk),
+                     dim3(256), 0, s, b.x, b.n, (int64_t)DP, b.c, b.cn, b.kp / 64, b.lab, nblk, 0,
+                     0, nullptr, stride);
+}
+
 template <bool PERSIST, bool RELOAD>
 static void var(const Bufs& b, hipStream_t s, int stagger, int slots = 2, bool stamp = false) {
   const int64_t per = 4 * 8 * 16;
@@ -669,22 +708,22 @@ int main(int argc, char** argv) {
     TRY("stagger 100 + stamps", (var<false, false>(b1, 0, 100, 2, true)))
     analyse_stamps(nblk);
   }
-  TRY("ring2x P4 NST2 QT2", (r2x<4, 2, 2>(b1, 0)))
-  TRY("ring2x P4 NST3 QT2", (r2x<4, 3, 2>(b1, 0)))
-  TRY("ring2x P4 NST2 QT1", (r2x<4, 2, 1>(b1, 0)))
-  TRY("ring2x P2 NST3 QT2", (r2x<2, 3, 2>(b1, 0)))
-  TRY("persist + reload", (var<true, true>(b1, 0, 0)))
+  const int res = g_cus * 2;
+  TRY("prefetch PF=4 stride res", (pfv<4>(b1, 0, res)))
+  TRY("prefetch PF=8 stride res", (pfv<8>(b1, 0, res)))
+  TRY("prefetch PF=2 stride res", (pfv<2>(b1, 0, res)))
   const double flop = 2.0 * (double)N * Kp * DP;
   for (int round = 0; round < 3; ++round) {
     const float t0 = timeit([&] { prod(b0, 0); }, reps);
-    const float t1 = timeit([&] { r2x<4, 2, 2>(b1, 0); }, reps);
-    const float t2 = timeit([&] { r2x<4, 3, 2>(b1, 0); }, reps);
-    const float t3 = timeit([&] { r2x<4, 2, 1>(b1, 0); }, reps);
-    const float t4 = timeit([&] { r2x<2, 3, 2>(b1, 0); }, reps);
-    const float t5 = timeit([&] { var<false, false>(b1, 0, 0); }, reps);
-    printf("round %d: prod ring3 %.3f ms (%.0f TF/s) | ring2x P4N2Q2 %.3f | P4N3Q2 %.3f | "
-           "P4N2Q1 %.3f | P2N3Q2 %.3f | ring3 copy %.3f\n",
-           round, t0, flop / t0 / 1e9, t1, t2, t3, t4, t5);
+    const float t1 = timeit([&] { var<false, false>(b1, 0, 0); }, reps);
+    const float t2 = timeit([&] { pfv<2>(b1, 0, res); }, reps);
+    const float t3 = timeit([&] { pfv<4>(b1, 0, res); }, reps);
+    const float t4 = timeit([&] { pfv<8>(b1, 0, res); }, reps);
+    const float t5 = timeit([&] { pfv<4>(b1, 0, res * 2); }, reps);
+    const float t6 = timeit([&] { pfv<16>(b1, 0, res); }, reps);
+    printf("round %d: prod ring3 %.3f ms (%.0f TF/s) | copy %.3f | L2-prefetch next block PF=2 %.3f "
+           "| PF=4 %.3f | PF=8 %.3f | PF=4 stride 2res %.3f | PF=16 %.3f\n",
+           round, t0, flop / t0 / 1e9, t1, t2, t3, t4, t5, t6);
     fflush(stdout);
   }
   return 0;
