@@ -708,22 +708,18 @@ int main(int argc, char** argv) {
     TRY("stagger 100 + stamps", (var<false, false>(b1, 0, 100, 2, true)))
     analyse_stamps(nblk);
   }
-  const int res = g_cus * 2;
-  TRY("prefetch PF=4 stride res", (pfv<4>(b1, 0, res)))
-  TRY("prefetch PF=8 stride res", (pfv<8>(b1, 0, res)))
-  TRY("prefetch PF=2 stride res", (pfv<2>(b1, 0, res)))
-  const double flop = 2.0 * (double)N * Kp * DP;
+  // tail: the launch is 38.15 rounds of 512 resident blocks at 10M; time the same kernel over
+  // whole rounds (multiples of 512 blocks) and per row
+  const int64_t rows_round = (int64_t)g_cus * 2 * 512;
+  const int64_t n_whole = N / rows_round * rows_round;
+  Bufs bw{dx, n_whole, dc, dcn, Kp, l1};
   for (int round = 0; round < 3; ++round) {
     const float t0 = timeit([&] { prod(b0, 0); }, reps);
-    const float t1 = timeit([&] { var<false, false>(b1, 0, 0); }, reps);
-    const float t2 = timeit([&] { pfv<2>(b1, 0, res); }, reps);
-    const float t3 = timeit([&] { pfv<4>(b1, 0, res); }, reps);
-    const float t4 = timeit([&] { pfv<8>(b1, 0, res); }, reps);
-    const float t5 = timeit([&] { pfv<4>(b1, 0, res * 2); }, reps);
-    const float t6 = timeit([&] { pfv<16>(b1, 0, res); }, reps);
-    printf("round %d: prod ring3 %.3f ms (%.0f TF/s) | copy %.3f | L2-prefetch next block PF=2 %.3f "
-           "| PF=4 %.3f | PF=8 %.3f | PF=4 stride 2res %.3f | PF=16 %.3f\n",
-           round, t0, flop / t0 / 1e9, t1, t2, t3, t4, t5, t6);
+    const float t1 = timeit([&] { prod(bw, 0); }, reps);
+    printf("round %d: prod N=%lld %.4f ms (%.3f ns/row) | N=%lld (whole rounds) %.4f ms (%.3f ns/row) "
+           "-> tail cost %.1f us\n",
+           round, (long long)N, t0, t0 * 1e6 / N, (long long)n_whole, t1, t1 * 1e6 / n_whole,
+           (t0 - t1 * (double)N / n_whole) * 1e3);
     fflush(stdout);
   }
   return 0;
