@@ -271,7 +271,7 @@ __device__ __forceinline__ float x1_eps(float hx, float lx, const float* cstat, 
 }
 
 template <int DP, int P, int NST, int WAVES, int QT, bool TOP2 = false>
-__global__ __launch_bounds__(WAVES * 64, ((DP >= 128 && P >= 8) ? 2 : WAVES == 6 ? 3 : (WAVES % 4 == 0 ? (WAVES / 4 > 1 ? WAVES / 4 : 3) : 2)))
+__global__ __launch_bounds__(WAVES * 64, ((DP >= 128 && (P >= 8 || (TOP2 && P >= 6))) ? 2 : WAVES == 6 ? 3 : (WAVES % 4 == 0 ? (WAVES / 4 > 1 ? WAVES / 4 : 3) : 2)))
 void assign_mfma_bf16_ring3_kernel(const __bf16* __restrict__ X, int64_t N, int64_t ldx,
                                    const __bf16* __restrict__ Cm2, const float* __restrict__ cnorm,
                                    int ntiles, int32_t* __restrict__ labels,
