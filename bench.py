@@ -126,6 +126,9 @@ def parse(argv=None):
     ap.add_argument("--fcm-distances", default="x3", choices=["one", "x3"],
                     help="bf16 FCM distances: one product + two-nearest fix-up, or bf16x3 "
                          "(ClusterConfig.fcm_distances)")
+    ap.add_argument("--fcm-path", default="", choices=["", "tower", "wide", "wide64"],
+                    help="FCM A/B: force the SIMT tower, the wide path, or the fp64 matrix-core "
+                         "path for any dtype (ops.FCM_FORCE_PATH; default: the measured routing)")
     ap.add_argument("--no-x3-prefilter", action="store_true",
                     help="fp32/fp64 K-Means: run the bf16x3 pass over every row (no one-product "
                          "prefilter; A/B of HipX3Lloyd.prefilter)")
@@ -175,6 +178,9 @@ def main(argv=None):
               (sys.argv[1:] if argv is None else list(argv))
         sys.exit(subprocess.call(cmd))
 
+    if a.fcm_path:
+        import tensorflow_distributed_clustering_amd.ops as _ops
+        _ops.FCM_FORCE_PATH = a.fcm_path
     comm = init_comm("cuda" if torch.cuda.is_available() else "cpu")
     dev = comm.device
     world, rank = comm.world_size, comm.rank

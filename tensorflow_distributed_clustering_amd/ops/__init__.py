@@ -25,7 +25,6 @@ Variants (picked by :func:`make_lloyd_ops`):
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
@@ -1676,6 +1675,11 @@ FCM_PRECISION = {
 }
 
 
+# A/B switch of make_fcm_ops (bench.py --fcm-path): "" = the measured routing; "tower" /
+# "wide" / "wide64" (fp64 wide path for any input dtype) force a path where it applies
+FCM_FORCE_PATH = ""
+
+
 def make_fcm_ops(x: torch.Tensor, k: int, dtype: str = "fp64", m: float = 2.0,
                  nan_to_zero: bool = True, backend: str = "auto", distances: str = "x3"):
     """FCM tower for (dtype, K, D).  fp64 / fp32: the fused small-K*D kernel; from K = 64
@@ -1705,7 +1709,7 @@ def make_fcm_ops(x: torch.Tensor, k: int, dtype: str = "fp64", m: float = 2.0,
             return ops
         if fcm_mfma_wide_dim(d) is not None:
             return HipMfmaWideFCM(x, k, m, nan_to_zero)
-    force = os.environ.get("TDC_FCM_PATH", "")  # A/B only: tower | wide | wide64
+    force = FCM_FORCE_PATH  # A/B only (bench.py --fcm-path): tower | wide | wide64
     if force == "tower" and d <= 256:
         return HipTowerFCM(x, k, dtype, m, nan_to_zero)
     if force in ("wide", "wide64"):

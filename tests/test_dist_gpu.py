@@ -117,6 +117,18 @@ def test_fcm_two_ranks_match_one(gpu):
     np.testing.assert_array_equal(l2, l1)
 
 
+@pytest.mark.parametrize("dtype,d,k", [("fp64", 128, 256), ("fp32", 64, 128)])
+def test_fcm_f64_mfma_two_ranks_match_one(gpu, dtype, d, k):
+    """FCM on the fp64 matrix-core path (fused row statistics; fp32 rows promoted) at
+    world 2: each rank's partial W^T X / sum W through the packed all-reduce reproduces the
+    one-rank fit."""
+    c1, l1, b1 = _run(1, dtype, 40_001, d, k, iters=3, method="fcm", extra={"fuzzifier": 2.0})
+    c2, l2, b2 = _run(2, dtype, 40_001, d, k, iters=3, method="fcm", extra={"fuzzifier": 2.0})
+    assert b1 == b2 == "hip_fcm_wide"
+    np.testing.assert_allclose(c2, c1, rtol=1e-9, atol=1e-9)
+    assert (l1 == l2).mean() > 0.9999
+
+
 def test_bounded_two_ranks_match_lloyd(gpu):
     """algorithm='bounded' on 2 ranks: per-rank pruning, one all-reduce of the deltas per
     step, replicated fp64 totals -> the single-rank Lloyd result."""
