@@ -249,8 +249,18 @@ __global__ __launch_bounds__(WAVES * 64, 1) void assign_bigd_kernel(
   float pm = INFINITY, pm2 = INFINITY;
   auto epi_elem = [&](int j) __attribute__((always_inline)) {
     const float v = __uint_as_float((__float_as_uint(accp[j]) & ~EMB) | (unsigned)j);
-    if constexpr (TOP2) pm2 = __builtin_amdgcn_fmed3f(pm, pm2, v);  // pm <= pm2 kept
-    pm = __builtin_fminf(pm, v);
+    if constexpr (TOP2) {
+      // pm <= pm2 kept.  asm as in ring3's top-2 epilogue (assign_mfma_impl.h): the builtins
+      // canonicalise the tagged v first (one more VALU per score); v is never a signalling
+      // NaN (tag bits only in normal values)
+      float r1, r2;
+      asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r2) : "v"(pm), "v"(pm2), "v"(v));
+      asm("v_min_f32 %0, %1, %2" : "=v"(r1) : "v"(pm), "v"(v));
+      pm2 = r2;
+      pm = r1;
+    } else {
+      pm = __builtin_fminf(pm, v);
+    }
   };
   auto epi_fold = [&]() __attribute__((always_inline)) {
     const bool up = pm < best;
