@@ -129,6 +129,9 @@ def parse(argv=None):
     ap.add_argument("--fcm-path", default="", choices=["", "tower", "wide", "wide64"],
                     help="FCM A/B: force the SIMT tower, the wide path, or the fp64 matrix-core "
                          "path for any dtype (ops.FCM_FORCE_PATH; default: the measured routing)")
+    ap.add_argument("--fp8-recheck", type=float, default=0.0,
+                    help="fp8 K-Means: exact re-check of rows whose fp8 margin to the runner-up "
+                         "is within this relative tau (ClusterConfig.fp8_recheck; 0 = off)")
     ap.add_argument("--no-x3-prefilter", action="store_true",
                     help="fp32/fp64 K-Means: run the bf16x3 pass over every row (no one-product "
                          "prefilter; A/B of HipX3Lloyd.prefilter)")
@@ -198,7 +201,8 @@ def main(argv=None):
                             seed=a.seed, compute_inertia=False, algorithm=a.algorithm,
                             fuzzifier=a.fuzzifier, update=a.update,
                             delta_refresh=a.delta_refresh, deterministic=a.deterministic,
-                            comm_mode=a.comm_mode, fcm_distances=a.fcm_distances)
+                            comm_mode=a.comm_mode, fcm_distances=a.fcm_distances,
+                            fp8_recheck=a.fp8_recheck)
     if a.mode == "minibatch":
         from tensorflow_distributed_clustering_amd.models.minibatch import MiniBatchStepper
         eng = MiniBatchStepper(x, cfg.replace(batch_size=a.batch_size or (1 << 20)), comm,
@@ -353,6 +357,8 @@ def main(argv=None):
             out["config"]["algorithm"] = a.algorithm
         if a.deterministic:
             out["config"]["deterministic"] = True
+        if a.fp8_recheck:
+            out["config"]["fp8_recheck"] = a.fp8_recheck
         if a.method == "fcm":
             out["config"]["fuzzifier"] = a.fuzzifier if a.fuzzifier is not None else a.dim
             out["active_frac_last_step"] = getattr(eng, "active_frac", None)

@@ -8,7 +8,7 @@ import sys
 
 
 def short(name):
-    m = re.search(r"(tdc::\w+(<[^>]*>)?|\w+_kernel\w*)", name)
+    m = re.search(r"(tdc::(?:\w+::)*\w+(<[^>]*>)?|\w+_kernel\w*)", name)
     return (m.group(1) if m else name)[:70]
 
 

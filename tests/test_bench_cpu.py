@@ -56,6 +56,9 @@ def test_bench_update_full_and_witness():
     assert dd["update"]["mode"] == "delta" and df["update"]["mode"] == "full"
     assert df["check"]["agree_fp64_sample"] >= 0.99
     assert dd["check"]["inertia"] == pytest.approx(df["check"]["inertia"], rel=1e-9)
+    # an opt-in variant is named in the config (--fp8-recheck: the fp8 kernels only)
+    dr = _run(args + ["--fp8-recheck", "0.05"])
+    assert dr["config"]["fp8_recheck"] == 0.05 and "fp8_recheck" not in dd["config"]
 
 
 def test_bench_headline_is_strong_scaling_at_10m(tmp_path):
