@@ -10,6 +10,11 @@ timed region.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N
 
+Warm-up: W steps, continued (untimed, same count on every rank) until the warm-up has run
+``--settle-ms`` (250) on the GPU -- the clock ramps over the first ~50 ms of MFMA load --
+then back to the init snapshot; the JSON's ``warmup`` is W, ``warmup_steps_run`` /
+``warmup_ms`` what ran.
+
 Data: synthetic Gaussian blobs generated on each GPU (counter-based, world-size
 invariant), random-row centroid init.  The default ``headline`` preset is STRONG scaling:
 N = 10M points in total, split over the ranks (1.25M rows per GPU at N=8), exactly the
@@ -129,6 +134,11 @@ def parse(argv=None):
     ap.add_argument("--fcm-path", default="", choices=["", "tower", "wide", "wide64"],
                     help="FCM A/B: force the SIMT tower, the wide path, or the fp64 matrix-core "
                          "path for any dtype (ops.FCM_FORCE_PATH; default: the measured routing)")
+    ap.add_argument("--settle-ms", type=float, default=250.0,
+                    help="GPU: after the W warm-up steps keep stepping (untimed) until the "
+                         "warm-up has run this many ms, so the timed steps start at the "
+                         "settled clock (the clock ramps over the first ~50 ms of MFMA load); "
+                         "0 = exactly W warm-up steps")
     ap.add_argument("--fp8-recheck", type=float, default=0.0,
                     help="fp8 K-Means: exact re-check of rows whose fp8 margin to the runner-up "
                          "is within this relative tau (ClusterConfig.fp8_recheck; 0 = off)")
@@ -248,8 +258,24 @@ def main(argv=None):
     # computation_time (scripts/distribuitedClustering.py:277-280) -- the high-motion
     # first iterations and the delta update's first full step are inside the window
     snap = eng.snapshot() if (hasattr(eng, "snapshot") and not a.warm_start) else None
+    t_w = time.perf_counter()
     for _ in range(a.warmup):
         eng.step()
+    warm_steps = a.warmup
+    # clock settle: the GPU raises its clock over the first ~50 ms of sustained MFMA load
+    # (the headline assign runs 2.1-2.4 ms per call at first and 1.81 ms from ~50 ms on,
+    # profiles/clock_ramp_r06w.txt), so W short warm-up steps would leave the timed steps
+    # inside the ramp.  The warm-up keeps stepping, untimed, until it has run --settle-ms;
+    # every rank runs the same number of steps (one flag all-reduce per extra step); the
+    # timed steps still start from the init snapshot below
+    while a.warmup > 0 and a.settle_ms > 0 and dev.type == "cuda" and warm_steps < 20000:
+        torch.cuda.synchronize(dev)
+        short = (time.perf_counter() - t_w) * 1e3 < a.settle_ms
+        if comm.max_scalar(1.0 if short else 0.0) == 0.0:
+            break
+        eng.step()
+        warm_steps += 1
+    warm_ms = (time.perf_counter() - t_w) * 1e3
     if snap is not None:
         eng.rewind(snap)
 
@@ -319,6 +345,8 @@ def main(argv=None):
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
+            "warmup_steps_run": warm_steps,
+            "warmup_ms": warm_ms,
             "ms_per_step": ms,
             "timed_from": "warm" if snap is None else "init",
             "ms_per_step_steady": ms_steady,
