@@ -134,11 +134,11 @@ def parse(argv=None):
     ap.add_argument("--fcm-path", default="", choices=["", "tower", "wide", "wide64"],
                     help="FCM A/B: force the SIMT tower, the wide path, or the fp64 matrix-core "
                          "path for any dtype (ops.FCM_FORCE_PATH; default: the measured routing)")
-    ap.add_argument("--settle-ms", type=float, default=250.0,
-                    help="GPU: after the W warm-up steps keep stepping (untimed) until the "
-                         "warm-up has run this many ms, so the timed steps start at the "
-                         "settled clock (the clock ramps over the first ~50 ms of MFMA load); "
-                         "0 = exactly W warm-up steps")
+    ap.add_argument("--settle-ms", type=float, default=None,
+                    help="after the W warm-up steps keep stepping (untimed) until the warm-up "
+                         "has run this many ms, so the timed steps start at the settled GPU "
+                         "clock (it ramps over the first ~50 ms of MFMA load); default 250 on "
+                         "a GPU, 0 on the CPU; 0 = exactly W warm-up steps")
     ap.add_argument("--fp8-recheck", type=float, default=0.0,
                     help="fp8 K-Means: exact re-check of rows whose fp8 margin to the runner-up "
                          "is within this relative tau (ClusterConfig.fp8_recheck; 0 = off)")
@@ -268,9 +268,11 @@ def main(argv=None):
     # inside the ramp.  The warm-up keeps stepping, untimed, until it has run --settle-ms;
     # every rank runs the same number of steps (one flag all-reduce per extra step); the
     # timed steps still start from the init snapshot below
-    while a.warmup > 0 and a.settle_ms > 0 and dev.type == "cuda" and warm_steps < 20000:
-        torch.cuda.synchronize(dev)
-        short = (time.perf_counter() - t_w) * 1e3 < a.settle_ms
+    settle_ms = a.settle_ms if a.settle_ms is not None else (250.0 if dev.type == "cuda" else 0.0)
+    while a.warmup > 0 and settle_ms > 0 and warm_steps < 20000:
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        short = (time.perf_counter() - t_w) * 1e3 < settle_ms
         if comm.max_scalar(1.0 if short else 0.0) == 0.0:
             break
         eng.step()

@@ -61,6 +61,20 @@ def test_bench_update_full_and_witness():
     assert dr["config"]["fp8_recheck"] == 0.05 and "fp8_recheck" not in dd["config"]
 
 
+def test_bench_settle_warmup_same_steps_on_every_rank():
+    """--settle-ms: the warm-up keeps stepping until it has run that long, every rank the
+    same number of steps (a mismatch would hang the collectives), and the timed steps still
+    start from the init (the same fit as with exactly W warm-up steps)."""
+    args = ["--gpus", "2", "--steps", "3", "--warmup", "2", "--n-per-gpu", "40000", "--k", "12",
+            "--dim", "6", "--dtype", "fp32", "--scaling", "weak"]
+    d0 = _run(args)
+    d1 = _run(args + ["--settle-ms", "300"])
+    assert d0["warmup_steps_run"] == 2 and d1["warmup"] == 2
+    assert d1["warmup_steps_run"] > 2 and d1["warmup_ms"] >= 300
+    assert d1["timed_from"] == "init"
+    assert d1["check"]["inertia"] == pytest.approx(d0["check"]["inertia"], rel=1e-9)
+
+
 def test_bench_headline_is_strong_scaling_at_10m(tmp_path):
     """The default preset measures BASELINE.json's metric: N = 10M points in TOTAL, split
     over the ranks (strong scaling), so --gpus 1/2/4 time the same problem and reach the
