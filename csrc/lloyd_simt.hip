@@ -548,36 +548,39 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(const T* __restrict__
 // part_d / part_k; exact_few_merge_kernel then takes the per-row minimum over the splits in
 // ascending k order (ties: the lower index, as the unsplit scan).
 constexpr int EXACT_FEW_RB = 8, EXACT_FEW_PARTS = 8192;
-__device__ __forceinline__ int exact_few_splits(int n, int nkc, int grid) {
-  const int rg = (n + EXACT_FEW_RB - 1) / EXACT_FEW_RB;
+// rows per workgroup by the listed count (read on the device): few rows want short
+// per-thread chains over more workgroups, many rows the centroid slice reused over 8 rows
+// (fp64 D=128 K=1024, few + merge: 60 rows 36.1 us at 8 -> 18.0 at 2; 240 rows 37.0 -> 21.4
+// at 2 or 4; 1000 rows 43.4 / 41.2 at 8 / 4; 4000 rows 126 at 8, 140 at 4;
+// profiles/few_rows_rb_ab_r06aa.txt).  force (A/B harness): 0 = by count, else that RB.
+__device__ __forceinline__ int exact_few_rb(int n, int force) {
+  return force ? force : (n <= 160 ? 2 : n <= 1536 ? 4 : EXACT_FEW_RB);
+}
+__device__ __forceinline__ int exact_few_splits(int n, int nkc, int grid, int rb) {
+  const int rg = (n + rb - 1) / rb;
   int sp = rg > 0 ? grid / rg : 1;
   if (sp > nkc) sp = nkc;
   if (sp < 1) sp = 1;
-  if ((int64_t)sp * rg * EXACT_FEW_RB > EXACT_FEW_PARTS) sp = 1;
+  if ((int64_t)sp * rg * rb > EXACT_FEW_PARTS) sp = 1;
   return sp;
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void assign_exact_few_kernel(const T* __restrict__ X, int64_t ldx,
-                                                               int D, const T* __restrict__ C, int K,
-                                                               int32_t* __restrict__ labels,
-                                                               T* __restrict__ mind,
-                                                               const int32_t* __restrict__ rowidx,
-                                                               const int* __restrict__ nptr,
-                                                               T* __restrict__ part_d,
-                                                               int* __restrict__ part_k) {
-  constexpr int RB = EXACT_FEW_RB, KT = 256, DC = 32;
+template <typename T, int RB>
+__device__ __forceinline__ void exact_few_body(const T* __restrict__ X, int64_t ldx, int D,
+                                               const T* __restrict__ C, int K,
+                                               int32_t* __restrict__ labels,
+                                               T* __restrict__ mind,
+                                               const int32_t* __restrict__ rowidx, int n,
+                                               T* __restrict__ part_d, int* __restrict__ part_k,
+                                               char* few_smem, T (*s_c)[257],
+                                               T (*s_rb)[EXACT_FEW_RB],
+                                               int (*s_rk)[EXACT_FEW_RB]) {
+  constexpr int KT = 256, DC = 32;
   // the row group's rows, staged once (D <= EXACT_FEW_MAXD, zero-padded to the chunk): a
-  // per-chunk slice had put two dependent global loads (index, row) on every chunk
-  // the row group's rows: dynamic LDS sized by the launch (Dp x RB): a static D = 1024
-  // image (64 KiB in fp64) had left room for one workgroup per CU
-  extern __shared__ __attribute__((aligned(16))) char few_smem[];
+  // per-chunk slice had put two dependent global loads (index, row) on every chunk; in
+  // dynamic LDS sized by the launch (Dp x EXACT_FEW_RB): a static D = 1024 image (64 KiB
+  // in fp64) had left room for one workgroup per CU
   T(*s_x)[RB] = reinterpret_cast<T(*)[RB]>(few_smem);
-  __shared__ T s_c[DC][KT + 1];
-  __shared__ T s_rb[4][RB];
-  __shared__ int s_rk[4][RB];
-  const int n = *nptr;
-  if (n > EXACT_FEW_MAX) return;  // assign_exact_kernel has them
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // (k0, dc) chunks in one flat sequence; the next chunk's centroid slice (16-B loads when
   // rows allow) and row values are loaded into registers while the current one is computed
@@ -587,7 +590,7 @@ __global__ __launch_bounds__(256) void assign_exact_few_kernel(const T* __restri
   const bool vec_ok = D % VEC == 0 && ((uintptr_t)C % 16) == 0;
   vecT cv[NV];
   const int Dp = nd * DC;
-  const int S = part_d ? exact_few_splits(n, nkc, (int)gridDim.x) : 1;
+  const int S = part_d ? exact_few_splits(n, nkc, (int)gridDim.x, RB) : 1;
   const int kcs = (nkc + S - 1) / S;  // 256-centroid chunks per split
   const int64_t items = (int64_t)((n + RB - 1) / RB) * S;
   auto load = [&](int64_t r0, int ci) __attribute__((always_inline)) {
@@ -699,6 +702,33 @@ __global__ __launch_bounds__(256) void assign_exact_few_kernel(const T* __restri
   }
 }
 
+template <typename T>
+__global__ __launch_bounds__(256) void assign_exact_few_kernel(const T* __restrict__ X, int64_t ldx,
+                                                               int D, const T* __restrict__ C, int K,
+                                                               int32_t* __restrict__ labels,
+                                                               T* __restrict__ mind,
+                                                               const int32_t* __restrict__ rowidx,
+                                                               const int* __restrict__ nptr,
+                                                               T* __restrict__ part_d,
+                                                               int* __restrict__ part_k,
+                                                               int force_rb) {
+  extern __shared__ __attribute__((aligned(16))) char few_smem[];
+  __shared__ T s_c[32][257];
+  __shared__ T s_rb[4][EXACT_FEW_RB];
+  __shared__ int s_rk[4][EXACT_FEW_RB];
+  const int n = *nptr;
+  if (n > EXACT_FEW_MAX) return;  // assign_exact_kernel has them
+  const int rb = exact_few_rb(n, force_rb);  // uniform: every workgroup reads the same n
+  if (rb == 1)
+    exact_few_body<T, 1>(X, ldx, D, C, K, labels, mind, rowidx, n, part_d, part_k, few_smem, s_c, s_rb, s_rk);
+  else if (rb == 2)
+    exact_few_body<T, 2>(X, ldx, D, C, K, labels, mind, rowidx, n, part_d, part_k, few_smem, s_c, s_rb, s_rk);
+  else if (rb == 4)
+    exact_few_body<T, 4>(X, ldx, D, C, K, labels, mind, rowidx, n, part_d, part_k, few_smem, s_c, s_rb, s_rk);
+  else
+    exact_few_body<T, EXACT_FEW_RB>(X, ldx, D, C, K, labels, mind, rowidx, n, part_d, part_k, few_smem, s_c, s_rb, s_rk);
+}
+
 // the per-row minimum over the K splits of assign_exact_few_kernel (nothing to do at S = 1)
 template <typename T>
 __global__ __launch_bounds__(256) void exact_few_merge_kernel(int K, int few_grid,
@@ -707,10 +737,11 @@ __global__ __launch_bounds__(256) void exact_few_merge_kernel(int K, int few_gri
                                                               const int32_t* __restrict__ rowidx,
                                                               const int* __restrict__ nptr,
                                                               const T* __restrict__ part_d,
-                                                              const int* __restrict__ part_k) {
+                                                              const int* __restrict__ part_k,
+                                                              int force_rb) {
   const int n = *nptr;
   if (n > EXACT_FEW_MAX) return;
-  const int S = exact_few_splits(n, (K + 255) / 256, few_grid);
+  const int S = exact_few_splits(n, (K + 255) / 256, few_grid, exact_few_rb(n, force_rb));
   if (S <= 1) return;
   for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 256) {
     T b = part_d[r * S];
@@ -766,19 +797,19 @@ int tdc_assign_exact(int dtype, const void* X, int64_t N, int64_t ldx, int D, co
     if (dtype == TDC_F32) {
       hipLaunchKernelGGL(assign_exact_few_kernel<float>, dim3((unsigned)fb), dim3(256), few_lds, s,
                          (const float*)X, ldx, D, (const float*)C, K, labels, (float*)mind, rowidx,
-                         nptr, (float*)parts, part_k);
+                         nptr, (float*)parts, part_k, 0);
       TDC_CHECK_LAUNCH();
       hipLaunchKernelGGL(exact_few_merge_kernel<float>, dim3((unsigned)mb), dim3(256), 0, s, K,
                          (int)fb, labels, (float*)mind, rowidx, nptr, (const float*)parts,
-                         (const int*)part_k);
+                         (const int*)part_k, 0);
     } else if (dtype == TDC_F64) {
       hipLaunchKernelGGL(assign_exact_few_kernel<double>, dim3((unsigned)fb), dim3(256), few_lds, s,
                          (const double*)X, ldx, D, (const double*)C, K, labels, (double*)mind,
-                         rowidx, nptr, (double*)parts, part_k);
+                         rowidx, nptr, (double*)parts, part_k, 0);
       TDC_CHECK_LAUNCH();
       hipLaunchKernelGGL(exact_few_merge_kernel<double>, dim3((unsigned)mb), dim3(256), 0, s, K,
                          (int)fb, labels, (double*)mind, rowidx, nptr, (const double*)parts,
-                         (const int*)part_k);
+                         (const int*)part_k, 0);
     } else {
       return (int)hipErrorInvalidValue;
     }
