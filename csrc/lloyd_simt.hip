@@ -409,6 +409,54 @@ template <> struct ExactCfg<double> { static constexpr int MR = 4; };
 // assign_exact_few_kernel instead: the 128-row tiles would leave all but a handful of CUs idle.
 constexpr int EXACT_FEW_MAX = 32768, EXACT_FEW_MAXD = 1024;
 
+constexpr int EXACT_FEW_RB = 8, EXACT_FEW_PARTS = 8192;
+// rows per workgroup by the listed count (read on the device): few rows want short
+// per-thread chains over more workgroups, many rows the centroid slice reused over 8 rows
+// (fp64 D=128 K=1024, few + merge: 60 rows 36.1 us at 8 -> 18.0 at 2; 240 rows 37.0 -> 21.4
+// at 2 or 4; 1000 rows 43.4 / 41.2 at 8 / 4; 4000 rows 126 at 8, 140 at 4;
+// profiles/few_rows_rb_ab_r06aa.txt).  force (A/B harness): 0 = by count, else that RB.
+__device__ __forceinline__ int exact_few_rb(int n, int force) {
+  return force ? force : (n <= 160 ? 2 : n <= 1536 ? 4 : EXACT_FEW_RB);
+}
+__device__ __forceinline__ int exact_few_splits(int n, int nkc, int grid, int rb) {
+  const int rg = (n + rb - 1) / rb;
+  int sp = rg > 0 ? grid / rg : 1;
+  if (sp > nkc) sp = nkc;
+  if (sp < 1) sp = 1;
+  if ((int64_t)sp * rg * rb > EXACT_FEW_PARTS) sp = 1;
+  return sp;
+}
+
+
+// the per-row minimum over the K splits of assign_exact_few_kernel (nothing to do at S = 1),
+// grid-stride over the listed rows: exact_few_merge_kernel, or the empty launch of
+// assign_exact_kernel when the listed rows were few (one launch fewer per step)
+template <typename T>
+__device__ __forceinline__ void exact_few_merge_rows(int K, int few_grid, int n, int force_rb,
+                                                     int32_t* __restrict__ labels,
+                                                     T* __restrict__ mind,
+                                                     const int32_t* __restrict__ rowidx,
+                                                     const T* __restrict__ part_d,
+                                                     const int* __restrict__ part_k) {
+  const int S = exact_few_splits(n, (K + 255) / 256, few_grid, exact_few_rb(n, force_rb));
+  if (S <= 1) return;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    T b = part_d[r * S];
+    int k = part_k[r * S];
+    for (int sp = 1; sp < S; ++sp) {  // ascending k: strict < keeps the lower index
+      const T v = part_d[r * S + sp];
+      if (v < b) {
+        b = v;
+        k = part_k[r * S + sp];
+      }
+    }
+    const int64_t orow = rowidx[r];
+    labels[orow] = k;
+    if (mind) mind[orow] = b;
+  }
+}
+
 // rowidx (nullable): row i of the launch is row rowidx[i] of X (and of labels / mind), with
 // the row count read from the device (nptr) -- the full re-scan of the rows the fp32/fp64
 // MFMA assignment could not certify (assign_x3.hip), sized on the device
@@ -420,7 +468,9 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(const T* __restrict__
                                                            T* __restrict__ mind,
                                                            const int32_t* __restrict__ rowidx,
                                                            const int* __restrict__ nptr,
-                                                           int few_max) {
+                                                           int few_max, int few_grid = 0,
+                                                           const T* __restrict__ part_d = nullptr,
+                                                           const int* __restrict__ part_k = nullptr) {
   constexpr int MR = ExactCfg<T>::MR;
   constexpr int R = 16 * MR, KT = 128, DC = 32;
   constexpr int PX = R + 4, PC = KT + 4;  // row pitch (16-B aligned, spreads the store banks)
@@ -430,7 +480,10 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(const T* __restrict__
   constexpr bool F32 = sizeof(T) == 4;
   if (nptr) {
     N = *nptr;
-    if (N <= few_max) return;  // assign_exact_few_kernel has them
+    if (N <= few_max) {  // assign_exact_few_kernel has them; merge its K splits here
+      if (part_d) exact_few_merge_rows<T>(K, few_grid, (int)N, 0, labels, mind, rowidx, part_d, part_k);
+      return;
+    }
   }
   for (int64_t r0 = (int64_t)blockIdx.x * R; r0 < N; r0 += (int64_t)gridDim.x * R) {
     T best[MR];
@@ -547,24 +600,6 @@ __global__ __launch_bounds__(256) void assign_exact_kernel(const T* __restrict__
 // workgroup: it depends only on the device-side count), each writing its (min, index) to
 // part_d / part_k; exact_few_merge_kernel then takes the per-row minimum over the splits in
 // ascending k order (ties: the lower index, as the unsplit scan).
-constexpr int EXACT_FEW_RB = 8, EXACT_FEW_PARTS = 8192;
-// rows per workgroup by the listed count (read on the device): few rows want short
-// per-thread chains over more workgroups, many rows the centroid slice reused over 8 rows
-// (fp64 D=128 K=1024, few + merge: 60 rows 36.1 us at 8 -> 18.0 at 2; 240 rows 37.0 -> 21.4
-// at 2 or 4; 1000 rows 43.4 / 41.2 at 8 / 4; 4000 rows 126 at 8, 140 at 4;
-// profiles/few_rows_rb_ab_r06aa.txt).  force (A/B harness): 0 = by count, else that RB.
-__device__ __forceinline__ int exact_few_rb(int n, int force) {
-  return force ? force : (n <= 160 ? 2 : n <= 1536 ? 4 : EXACT_FEW_RB);
-}
-__device__ __forceinline__ int exact_few_splits(int n, int nkc, int grid, int rb) {
-  const int rg = (n + rb - 1) / rb;
-  int sp = rg > 0 ? grid / rg : 1;
-  if (sp > nkc) sp = nkc;
-  if (sp < 1) sp = 1;
-  if ((int64_t)sp * rg * rb > EXACT_FEW_PARTS) sp = 1;
-  return sp;
-}
-
 template <typename T, int RB>
 __device__ __forceinline__ void exact_few_body(const T* __restrict__ X, int64_t ldx, int D,
                                                const T* __restrict__ C, int K,
@@ -729,7 +764,6 @@ __global__ __launch_bounds__(256) void assign_exact_few_kernel(const T* __restri
     exact_few_body<T, EXACT_FEW_RB>(X, ldx, D, C, K, labels, mind, rowidx, n, part_d, part_k, few_smem, s_c, s_rb, s_rk);
 }
 
-// the per-row minimum over the K splits of assign_exact_few_kernel (nothing to do at S = 1)
 template <typename T>
 __global__ __launch_bounds__(256) void exact_few_merge_kernel(int K, int few_grid,
                                                               int32_t* __restrict__ labels,
@@ -741,22 +775,7 @@ __global__ __launch_bounds__(256) void exact_few_merge_kernel(int K, int few_gri
                                                               int force_rb) {
   const int n = *nptr;
   if (n > EXACT_FEW_MAX) return;
-  const int S = exact_few_splits(n, (K + 255) / 256, few_grid, exact_few_rb(n, force_rb));
-  if (S <= 1) return;
-  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 256) {
-    T b = part_d[r * S];
-    int k = part_k[r * S];
-    for (int sp = 1; sp < S; ++sp) {  // ascending k: strict < keeps the lower index
-      const T v = part_d[r * S + sp];
-      if (v < b) {
-        b = v;
-        k = part_k[r * S + sp];
-      }
-    }
-    const int64_t orow = rowidx[r];
-    labels[orow] = k;
-    if (mind) mind[orow] = b;
-  }
+  exact_few_merge_rows<T>(K, few_grid, n, force_rb, labels, mind, rowidx, part_d, part_k);
 }
 
 // split scratch of the few-rows re-scan, one per device (allocated on first use, before
@@ -779,42 +798,48 @@ int tdc_assign_exact(int dtype, const void* X, int64_t N, int64_t ldx, int D, co
                      const int32_t* rowidx, const int* nptr) {
   if (N <= 0) return 0;
   const bool few = nptr && D <= EXACT_FEW_MAXD;
+  // K split: the grid covers the row groups of up to EXACT_FEW_MAX rows or, when fewer are
+  // listed, their 256-centroid chunks (a few hundred workgroups either way); two workgroups
+  // per CU: the listed count is read on the device, the few busy workgroups split their row
+  // groups over K (exact_few_splits), the rest leave at once
+  const int64_t fb = (int64_t)(num_cus > 0 ? num_cus : 256) * 2;
+  char* parts = nullptr;
+  int* part_k = nullptr;
+  // with N > EXACT_FEW_MAX the tiled launch below also runs (and returns at once when the
+  // listed rows were few): it does the K-split merge then, one launch fewer per step
+  const bool tiled = !few || N > EXACT_FEW_MAX;
   if (few) {
     if (!rowidx) return (int)hipErrorInvalidValue;
     // both launches read the listed count; exactly one of them has work
-    int64_t fb;
-    // K split: the grid covers the row groups of up to EXACT_FEW_MAX rows or, when fewer are
-    // listed, their 256-centroid chunks (a few hundred workgroups either way)
-    // two workgroups per CU: the listed count is read on the device, the few busy
-    // workgroups split their row groups over K (exact_few_splits), the rest leave at once
-    fb = (int64_t)(num_cus > 0 ? num_cus : 256) * 2;
     const int dpad = (D + 31) / 32 * 32;
     const size_t few_lds = (size_t)dpad * EXACT_FEW_RB * (dtype == TDC_F64 ? 8 : 4);
-    char* parts = (char*)few_parts(dtype == TDC_F64 ? 8 : 4);
+    parts = (char*)few_parts(dtype == TDC_F64 ? 8 : 4);
     if (!parts) return (int)hipErrorOutOfMemory;
-    int* part_k = (int*)(parts + (size_t)EXACT_FEW_PARTS * 8);
+    part_k = (int*)(parts + (size_t)EXACT_FEW_PARTS * 8);
     const int mb = (EXACT_FEW_PARTS + 255) / 256;
     if (dtype == TDC_F32) {
       hipLaunchKernelGGL(assign_exact_few_kernel<float>, dim3((unsigned)fb), dim3(256), few_lds, s,
                          (const float*)X, ldx, D, (const float*)C, K, labels, (float*)mind, rowidx,
                          nptr, (float*)parts, part_k, 0);
       TDC_CHECK_LAUNCH();
-      hipLaunchKernelGGL(exact_few_merge_kernel<float>, dim3((unsigned)mb), dim3(256), 0, s, K,
-                         (int)fb, labels, (float*)mind, rowidx, nptr, (const float*)parts,
-                         (const int*)part_k, 0);
+      if (!tiled)
+        hipLaunchKernelGGL(exact_few_merge_kernel<float>, dim3((unsigned)mb), dim3(256), 0, s, K,
+                           (int)fb, labels, (float*)mind, rowidx, nptr, (const float*)parts,
+                           (const int*)part_k, 0);
     } else if (dtype == TDC_F64) {
       hipLaunchKernelGGL(assign_exact_few_kernel<double>, dim3((unsigned)fb), dim3(256), few_lds, s,
                          (const double*)X, ldx, D, (const double*)C, K, labels, (double*)mind,
                          rowidx, nptr, (double*)parts, part_k, 0);
       TDC_CHECK_LAUNCH();
-      hipLaunchKernelGGL(exact_few_merge_kernel<double>, dim3((unsigned)mb), dim3(256), 0, s, K,
-                         (int)fb, labels, (double*)mind, rowidx, nptr, (const double*)parts,
-                         (const int*)part_k, 0);
+      if (!tiled)
+        hipLaunchKernelGGL(exact_few_merge_kernel<double>, dim3((unsigned)mb), dim3(256), 0, s, K,
+                           (int)fb, labels, (double*)mind, rowidx, nptr, (const double*)parts,
+                           (const int*)part_k, 0);
     } else {
       return (int)hipErrorInvalidValue;
     }
     TDC_CHECK_LAUNCH();
-    if (N <= EXACT_FEW_MAX) return 0;
+    if (!tiled) return 0;
   }
   const int64_t rows_per_tile = 16 * (dtype == TDC_F64 ? ExactCfg<double>::MR : ExactCfg<float>::MR);
   int64_t blocks = (N + rows_per_tile - 1) / rows_per_tile;
@@ -826,11 +851,13 @@ int tdc_assign_exact(int dtype, const void* X, int64_t N, int64_t ldx, int D, co
   if (dtype == TDC_F32)
     hipLaunchKernelGGL(assign_exact_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s,
                        (const float*)X, N, ldx, D, (const float*)C, K, labels, (float*)mind,
-                       rowidx, nptr, few ? EXACT_FEW_MAX : -1);
+                       rowidx, nptr, few ? EXACT_FEW_MAX : -1, (int)fb, (const float*)parts,
+                       (const int*)part_k);
   else if (dtype == TDC_F64)
     hipLaunchKernelGGL(assign_exact_kernel<double>, dim3((unsigned)blocks), dim3(256), 0, s,
                        (const double*)X, N, ldx, D, (const double*)C, K, labels, (double*)mind,
-                       rowidx, nptr, few ? EXACT_FEW_MAX : -1);
+                       rowidx, nptr, few ? EXACT_FEW_MAX : -1, (int)fb, (const double*)parts,
+                       (const int*)part_k);
   else
     return (int)hipErrorInvalidValue;
   TDC_CHECK_LAUNCH();
