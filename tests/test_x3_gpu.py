@@ -198,14 +198,17 @@ def test_x3_streamed_and_delta(gpu):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
-@pytest.mark.parametrize("m", [1, 1700, 40000])
-def test_listed_rescan_matches_exact(gpu, dtype, m):
+@pytest.mark.parametrize("n,m", [(60000, 1), (60000, 100), (60000, 700), (60000, 1700),
+                                 (60000, 40000), (20000, 100), (20000, 700), (20000, 5000)])
+def test_listed_rescan_matches_exact(gpu, dtype, n, m):
     """The listed full re-scan (x3_recheck's listF part): short lists run on the few-rows
-    kernel (<= 32768 rows), long ones on the 128-row tiles; both give the labels of the
-    full exact tiles on the listed rows and leave the other rows alone."""
+    kernel (<= 32768 rows; 2 / 4 / 8 rows per workgroup by the listed count: m = 100 / 700 /
+    1700+), long ones on the 128-row tiles; the K-split merge runs in the tiled launch
+    (n > 32768) or in its own kernel (n = 20000).  All give the labels of the full exact
+    tiles on the listed rows and leave the other rows alone."""
     from tensorflow_distributed_clustering_amd import _native
     ops = _native.require()
-    n, d, k = 60000, 100, 300
+    d, k = 100, 700  # three 256-centroid chunks: K splits of 1 to 3
     x, c = _blobs(n, d, k, seed=m, dtype=dtype)
     xg, C = x.to(gpu), c.to(gpu).contiguous()
     want = torch.empty(n, dtype=torch.int32, device=gpu)
