@@ -2,8 +2,10 @@
 //
 // Reference per GPU per iteration (scripts/distribuitedClustering.py:108-137): [N,K,D]
 // difference tiles -> d -> t = d^(-2/(m-1)) -> u = t / sum_k t -> NaN -> 0 -> W = u^m ->
-// MatMul(W, X) (cuBLAS DGEMM) and Sum(W).  Both matrix products run here on
-// v_mfma_f32_32x32x16_bf16 with fp32-grade operands from a hi/lo bf16 split
+// MatMul(W, X) (cuBLAS DGEMM) and Sum(W).  Both matrix products run here on the bf16
+// matrix cores (the bf16x3 stats pass on v_mfma_f32_16x16x32_bf16, the one-product stats
+// pass and the accumulate pass on v_mfma_f32_32x32x16_bf16) with fp32-grade operands from a
+// hi/lo bf16 split
 // (x = xh + xl, -2c = ch + cl, each lo = bf16(v - hi)):
 //   x.(-2c) ~= xh.ch + xh.cl + xl.ch      (three MFMAs; the dropped xl.cl is 2^-16 relative)
 //   sum_i w_ik x_i = W^T Xh + W^T Xl      (W = u^m rounded to bf16; sum_i w_ik from the same
@@ -93,60 +95,63 @@ __device__ __forceinline__ float mw(float u, float m) {
 // ---------------------------------------------------------------------------------------
 // pass 1: per-row statistics
 // ---------------------------------------------------------------------------------------
-// WAVES waves x one 32-point tile each share every centroid stage (8 waves: 2 per SIMD, so
-// one wave's epilogue VALU runs beside the other's MFMAs); within a wave the epilogue of
-// half q-1 is issued after the MFMAs of half q (software pipeline, as the Lloyd kernels).
+// WAVES waves x 32 points share every 64-centroid stage (8 waves: 2 per SIMD, so one wave's
+// epilogue VALU runs beside the other's MFMAs); within a wave the epilogue of half q-1 is
+// issued after the MFMAs of half q (software pipeline, as the Lloyd kernels).  On
+// v_mfma_f32_16x16x32_bf16, the Lloyd kernels' ring3 shape: the chip holds a higher clock
+// under it (MI355X_MICROARCH.md "DVFS give-back" item 7); against the 32x32x16 form of the
+// same pass 0.645 vs 0.690 ms at N=1M, K=1024, D=128 (profiles/fcm_stats_shape_ab_r06am.txt).
+// A wave's 32 points are two 16-point tiles and each 32-centroid half two 16-centroid tiles,
+// so a lane holds 4 centroids of two points (C layout: lane l, register i = centroid
+// 4 (l >> 4) + i of point l & 15); the row statistics are combined over the 4 lane groups
+// at the end.
 template <int DP, int MODE, int WAVES>
 __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats_kernel(
     const __bf16* __restrict__ Xh, const __bf16* __restrict__ Xl, const float* __restrict__ xx,
     int64_t N, const __bf16* __restrict__ Ch, const __bf16* __restrict__ Cl,
     const float* __restrict__ cc, int K, int nstages, MParam prm, int32_t* __restrict__ labels,
     float* __restrict__ rowinfo) {
-  constexpr int NT = WAVES * 64;
   constexpr int BN = 64;
   constexpr int CPR = DP / 8;
-  constexpr int KS = DP / 16;
-  constexpr int HALF = DP / 2;
-  constexpr int IMGB = BN * DP * 2;           // bytes of one (hi or lo) stage image
+  constexpr int KS = DP / 32;                 // 32-deep k-steps
+  constexpr int IMGB = BN * DP * 2;
+  constexpr unsigned TB = 7u;                 // tag bits: (centroid tile, register)
   __shared__ __attribute__((aligned(16))) char s_c[2][2 * IMGB];
   __shared__ __attribute__((aligned(16))) float s_n[2][BN];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int64_t row0 = (int64_t)blockIdx.x * (WAVES * 32) + (int64_t)w * 32 + r;
+  const int r = lane & 15, g = lane >> 4;
+  const int64_t wrow = (int64_t)blockIdx.x * (WAVES * 32) + (int64_t)w * 32;
 
-  bf16x8 bh[KS], bl[KS];
-  float xn, zf;
-  {
-    const int64_t row = row0 < N ? row0 : N - 1;
-    const bf16x8* sh = reinterpret_cast<const bf16x8*>(Xh + row * DP + h * HALF);
-    const bf16x8* sl = reinterpret_cast<const bf16x8*>(Xl + row * DP + h * HALF);
+  bf16x8 bh[2][KS], bl[2][KS];
+  float xn[2], zf[2];
+#pragma unroll
+  for (int pt = 0; pt < 2; ++pt) {
+    int64_t row = wrow + 16 * pt + r;
+    if (row >= N) row = N - 1;
+    const bf16x8* sh = reinterpret_cast<const bf16x8*>(Xh + row * DP + 8 * g);
+    const bf16x8* sl = reinterpret_cast<const bf16x8*>(Xl + row * DP + 8 * g);
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) {
-      bh[kk] = sh[kk];
-      bl[kk] = sl[kk];
+      bh[pt][kk] = sh[4 * kk];
+      bl[pt][kk] = sl[4 * kk];
     }
-    xn = xx[row];
-    zf = ZERO_FLOOR * xn;
+    xn[pt] = xx[row];
+    zf[pt] = ZERO_FLOOR * xn[pt];
   }
 
-  // Centroid stages arrive by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction,
-  // lane l -> M0 + 16 l): the XOR swizzle of the stage image is applied on the source side
-  // (coff is an involution in the chunk index), so no staging registers, no ds_write and
-  // no vmcnt wait in the middle of the stage.  Issued by inline asm in the saddr + voffset
-  // form (stage base in SGPRs); the compiler does not count these loads, the explicit
-  // vmcnt(0) before each stage's barrier does.
-  constexpr int PPI = IMGB / 1024;              // 1-KiB pieces per (hi or lo) image
-  constexpr int PPW = 2 * PPI / WAVES;          // pieces per wave per stage
+  // stage loads: as fcm_mfma_stats_kernel
+  constexpr int PPI = IMGB / 1024;
+  constexpr int PPW = 2 * PPI / WAVES;
   static_assert(IMGB % 1024 == 0 && (2 * PPI) % WAVES == 0 && PPI % PPW == 0, "stage pieces");
   constexpr int G = CPR < 16 ? CPR : 16;
   constexpr int RPB = 16 / G;
-  const int wu = __builtin_amdgcn_readfirstlane(w);  // wave index in SGPRs (DMA destinations)
-  const int hlw = (wu * PPW) / PPI;             // this wave's image
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const int hlw = (wu * PPW) / PPI;
   unsigned voff[PPW];
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
-    const int q = ((w * PPW + i) % PPI) * 64 + lane;  // destination chunk in the image
+    const int q = ((w * PPW + i) % PPI) * 64 + lane;
     const int row = q / CPR, cs = q % CPR;
     voff[i] = (unsigned)(row * DP * 2 + 16 * (cs ^ ((row / RPB) & (G - 1))));
   }
@@ -175,65 +180,65 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  float S = 0.f, best = INFINITY;
-  int bt = 0;
+  float S[2] = {0.f, 0.f}, best[2] = {INFINITY, INFINITY};
+  int bt[2] = {0, 0};
 
-  // MFMAs of half Q of the stage in buffer cb/ns into ACC (init = ||c||^2 rows)
+  // MFMAs of half Q (32 centroids = two 16-centroid tiles ct) of the stage in cb/ns
 #define TDC_PHASE(ACC, Q)                                                                 \
   {                                                                                       \
-    const int crow = (Q) * 32 + r;                                                        \
-    f32x16 init;                                                                          \
-    _Pragma("unroll") for (int g4 = 0; g4 < 4; ++g4) {                                    \
-      const f32x4 n4 = *reinterpret_cast<const f32x4*>(&ns[(Q) * 32 + 8 * g4 + 4 * h]);   \
-      _Pragma("unroll") for (int e = 0; e < 4; ++e) init[4 * g4 + e] = n4[e];             \
+    f32x4 n4[2];                                                                          \
+    bf16x8 ah[2][KS], al[2][KS];                                                          \
+    _Pragma("unroll") for (int ct = 0; ct < 2; ++ct) {                                    \
+      n4[ct] = *reinterpret_cast<const f32x4*>(&ns[(Q) * 32 + ct * 16 + 4 * g]);          \
+      const int crow = (Q) * 32 + ct * 16 + r;                                            \
+      _Pragma("unroll") for (int kk = 0; kk < KS; ++kk) {                                 \
+        ah[ct][kk] = as_bf16x8(*reinterpret_cast<const uint4*>(cb + coff<DP>(crow, 4 * kk + g))); \
+        al[ct][kk] = as_bf16x8(*reinterpret_cast<const uint4*>(cb + IMGB + coff<DP>(crow, 4 * kk + g))); \
+      }                                                                                   \
     }                                                                                     \
-    /* every fragment of the half is read up front: with a one-step prefetch the        \
-       compiler re-used the registers and waited for each pair right before its MFMAs,    \
-       exposing the LDS latency on every k-step */                                        \
-    bf16x8 ah[KS], al[KS];                                                                \
-    _Pragma("unroll") for (int kk = 0; kk < KS; ++kk) {                                   \
-      ah[kk] = as_bf16x8(*reinterpret_cast<const uint4*>(cb + coff<DP>(crow, h * (CPR / 2) + kk))); \
-      al[kk] = as_bf16x8(*reinterpret_cast<const uint4*>(cb + IMGB + coff<DP>(crow, h * (CPR / 2) + kk))); \
-    }                                                                                     \
-    __builtin_amdgcn_sched_barrier(0); /* keep the reads ahead of the MFMAs */            \
-    _Pragma("unroll") for (int kk = 0; kk < KS; ++kk) {                                   \
-      ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[kk], bh[kk], kk == 0 ? init : ACC, 0, 0, 0); \
-      ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[kk], bl[kk], ACC, 0, 0, 0);       \
-      ACC = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[kk], bh[kk], ACC, 0, 0, 0);       \
-    }                                                                                     \
+    __builtin_amdgcn_sched_barrier(0);                                                    \
+    _Pragma("unroll") for (int kk = 0; kk < KS; ++kk)                                     \
+      _Pragma("unroll") for (int ct = 0; ct < 2; ++ct)                                    \
+        _Pragma("unroll") for (int pt = 0; pt < 2; ++pt) {                                \
+          ACC[ct][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[ct][kk], bh[pt][kk], kk == 0 ? n4[ct] : ACC[ct][pt], 0, 0, 0); \
+          ACC[ct][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[ct][kk], bl[pt][kk], ACC[ct][pt], 0, 0, 0); \
+          ACC[ct][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[ct][kk], bh[pt][kk], ACC[ct][pt], 0, 0, 0); \
+        }                                                                                 \
   }
-  // epilogue of half Q of stage T_: register i = centroid (i&3)+8(i>>2)+4h (ascending);
-  // d2 clamped at the zero floor (a row whose min d2 is at the floor is "on a centroid");
-  // pad centroids (last stage only) masked
+  // epilogue of half Q of stage T_: register i of tile ct = centroid ct*16 + 4g + i of the
+  // half; the tag (ct, i) orders them ascending for this lane group
 #define TDC_EPI(ACC, Q, T_)                                                               \
   {                                                                                       \
-    const int kvalid = K - ((T_) * BN + (Q) * 32 + 4 * h);                                \
-    float mpk = INFINITY, sp = 0.f;                                                       \
-    if (kvalid >= 28) {                                                                   \
-      _Pragma("unroll") for (int i = 0; i < 16; ++i) {                                    \
-        const float d2 = fmaxf(ACC[i] + xn, zf);                                          \
-        sp += mt<MODE>(d2, prm.expo);                                                     \
-        mpk = __builtin_fminf(mpk, __uint_as_float((__float_as_uint(d2) & ~15u) | (unsigned)i)); \
+    const int kvalid = K - ((T_) * BN + (Q) * 32 + 4 * g);                                \
+    _Pragma("unroll") for (int pt = 0; pt < 2; ++pt) {                                    \
+      float mpk = INFINITY, sp = 0.f;                                                     \
+      if (kvalid >= 20) { /* every centroid of this lane group valid (all but the last stage) */ \
+        _Pragma("unroll") for (int ct = 0; ct < 2; ++ct)                                  \
+          _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                 \
+            const float d2 = fmaxf(ACC[ct][pt][i] + xn[pt], zf[pt]);                      \
+            sp += mt<MODE>(d2, prm.expo);                                                 \
+            mpk = __builtin_fminf(mpk, __uint_as_float((__float_as_uint(d2) & ~TB) | (unsigned)(ct * 4 + i))); \
+          }                                                                               \
+      } else {                                                                            \
+        _Pragma("unroll") for (int ct = 0; ct < 2; ++ct)                                  \
+          _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                 \
+            const bool v = ct * 16 + i < kvalid;                                          \
+            const float d2 = fmaxf(ACC[ct][pt][i] + xn[pt], zf[pt]);                      \
+            sp += v ? mt<MODE>(d2, prm.expo) : 0.f;                                       \
+            const float pk = __uint_as_float((__float_as_uint(d2) & ~TB) | (unsigned)(ct * 4 + i)); \
+            mpk = v ? __builtin_fminf(mpk, pk) : mpk;                                     \
+          }                                                                               \
       }                                                                                   \
-    } else {                                                                              \
-      _Pragma("unroll") for (int i = 0; i < 16; ++i) {                                    \
-        const bool v = (i & 3) + 8 * (i >> 2) < kvalid;                                   \
-        const float d2 = fmaxf(ACC[i] + xn, zf);                                          \
-        sp += v ? mt<MODE>(d2, prm.expo) : 0.f;                                           \
-        const float pk = __uint_as_float((__float_as_uint(d2) & ~15u) | (unsigned)i);     \
-        mpk = v ? __builtin_fminf(mpk, pk) : mpk;                                         \
-      }                                                                                   \
+      S[pt] += sp;                                                                        \
+      const bool up = mpk < best[pt];                                                     \
+      best[pt] = up ? mpk : best[pt];                                                     \
+      bt[pt] = up ? (2 * (T_) + (Q)) : bt[pt];                                            \
     }                                                                                     \
-    S += sp;                                                                              \
-    const bool up = mpk < best;                                                           \
-    best = up ? mpk : best;                                                               \
-    bt = up ? (2 * (T_) + (Q)) : bt;                                                      \
   }
 
-  f32x16 acc0, acc1;
+  f32x4 acc0[2][2], acc1[2][2];
   for (int t = 0; t < nstages; ++t) {
     const int buf = t & 1;
-    // buffer buf ^ 1 was last read in stage t - 1, before that stage's barrier
     if (t + 1 < nstages) TDC_STAGE_LOAD(t + 1, buf ^ 1)
     const char* cb = s_c[buf];
     const float* ns = s_n[buf];
@@ -241,7 +246,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats_kernel(
     if (t > 0) TDC_EPI(acc1, 1, t - 1)
     TDC_PHASE(acc1, 1)
     TDC_EPI(acc0, 0, t)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // stage t + 1 landed (this wave's part)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
   TDC_EPI(acc1, 1, nstages - 1)
@@ -249,19 +254,29 @@ __global__ __launch_bounds__(WAVES * 64, 1) void fcm_mfma_stats_kernel(
 #undef TDC_EPI
 #undef TDC_STAGE_LOAD
 
-  S += __shfl_xor(S, 32, 64);
-  const unsigned e0 = __float_as_uint(best) & 15u;
-  const int l0 = bt * 32 + (int)(e0 & 3) + 8 * (int)(e0 >> 2) + 4 * h;
-  const float v0 = __uint_as_float(__float_as_uint(best) & ~15u);
-  const float v1 = __shfl_xor(v0, 32, 64);
-  const int l1 = __shfl_xor(l0, 32, 64);
-  const bool other = (v1 < v0) || (v1 == v0 && l1 < l0);
-  if (h == 0 && row0 < N) {
-    // on a centroid: the nearest distance is at the floor (one zero-distance centroid is
-    // assumed for the one-hot case; the exact tower counts duplicates)
-    const bool on = (other ? v1 : v0) <= __uint_as_float(__float_as_uint(zf) & ~15u);
-    labels[row0] = (on && prm.nz) ? 0 : (other ? l1 : l0);
-    rowinfo[row0] = on ? (prm.nz ? 0.f : -1.f) : __builtin_amdgcn_rcpf(S);
+  // combine the 4 lane groups of each point: sum of t, nearest (lowest index on ties)
+#pragma unroll
+  for (int pt = 0; pt < 2; ++pt) {
+    float s = S[pt];
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    const unsigned e = __float_as_uint(best[pt]) & TB;
+    float v = __uint_as_float(__float_as_uint(best[pt]) & ~TB);
+    int l = bt[pt] * 32 + (int)(e >> 2) * 16 + 4 * g + (int)(e & 3);
+#pragma unroll
+    for (int o = 16; o <= 32; o <<= 1) {
+      const float ov = __shfl_xor(v, o, 64);
+      const int ol = __shfl_xor(l, o, 64);
+      const bool other = (ov < v) || (ov == v && ol < l);
+      v = other ? ov : v;
+      l = other ? ol : l;
+    }
+    const int64_t row = wrow + 16 * pt + r;
+    if (g == 0 && row < N) {
+      const bool on = v <= __uint_as_float(__float_as_uint(zf[pt]) & ~TB);
+      labels[row] = (on && prm.nz) ? 0 : l;
+      rowinfo[row] = on ? (prm.nz ? 0.f : -1.f) : __builtin_amdgcn_rcpf(s);
+    }
   }
 }
 
