@@ -646,7 +646,8 @@ void assign_bf16_indexed(const at::Tensor& X, const at::Tensor& rowidx, const at
 void update_sorted_indexed(const at::Tensor& X, const at::Tensor& rowidx, const at::Tensor& labels,
                            at::Tensor& sums, at::Tensor& counts, at::Tensor& work,
                            const std::optional<at::Tensor>& cnt_hi,
-                           const std::optional<at::Tensor>& cnt_lo, bool work_clean) {
+                           const std::optional<at::Tensor>& cnt_lo, bool work_clean,
+                           const std::optional<at::Tensor>& zero_first) {
   check_cuda(X, "X");
   check_rows(X, "X");
   const int64_t B = labels.numel();
@@ -662,13 +663,22 @@ void update_sorted_indexed(const at::Tensor& X, const at::Tensor& rowidx, const 
                   work.numel() >= tdc_update_sorted_workspace(B, (int)sums.size(0)),
               "tdc.update_sorted_indexed: workspace too small");
   check_split(cnt_hi, cnt_lo, sums.size(0), "update_sorted_indexed");
+  // zero_first (the caller's all-reduce buffer): cleared by the histogram kernel, before
+  // anything accumulates into it (one fill launch fewer per mini-batch step)
+  int64_t zbytes = 0;
+  if (zero_first.has_value() && zero_first->defined()) {
+    TORCH_CHECK(zero_first->is_contiguous() && zero_first->device() == X.device() &&
+                    (zero_first->numel() * zero_first->element_size()) % 4 == 0,
+                "tdc.update_sorted_indexed: zero_first must be a contiguous device buffer of 4-byte words");
+    zbytes = zero_first->numel() * zero_first->element_size();
+  }
   const DevGuard guard(X.device());
   check(tdc_update_sorted(dcode(X.scalar_type()), dcode(sums.scalar_type()), X.data_ptr(), B,
                           X.stride(0), (int)sums.size(1), labels.data_ptr<int32_t>(),
                           (int)sums.size(0), sums.data_ptr(), counts.data_ptr(),
                           work.data_ptr<int>(), num_cus(X.device().index()), cur_stream(),
                           rowidx.data_ptr<int32_t>(), static_cast<float*>(opt_ptr(cnt_hi)),
-                          static_cast<float*>(opt_ptr(cnt_lo)), nullptr, 0, 0.0,
+                          static_cast<float*>(opt_ptr(cnt_lo)), opt_ptr(zero_first), zbytes, 0.0,
                           work_clean ? 1 : 0),
         "update_sorted_indexed");
 }
@@ -1235,7 +1245,7 @@ TORCH_LIBRARY(tdc, m) {
   m.def("kpp_step(Tensor X, Tensor cand, Tensor(a!) closest, int mode, Tensor(b!) pots) -> ()");
   m.def("finalize(Tensor? sums, Tensor? counts, Tensor(a!) C, int policy, Tensor(b!)? shift, Tensor(c!)? Cm2, Tensor(d!)? cnorm, Tensor(e!)? drift=None, Tensor(f!)? maxdrift=None, float fixed_scale=0.0) -> ()");
   m.def("assign_bf16_indexed(Tensor X, Tensor rowidx, Tensor Cm2, Tensor cnorm, Tensor(a!) labels, Tensor(b!)? mind) -> ()");
-  m.def("update_sorted_indexed(Tensor X, Tensor rowidx, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work, Tensor(d!)? cnt_hi=None, Tensor(e!)? cnt_lo=None, bool work_clean=False) -> ()");
+  m.def("update_sorted_indexed(Tensor X, Tensor rowidx, Tensor labels, Tensor(a!) sums, Tensor(b!) counts, Tensor(c!) work, Tensor(d!)? cnt_hi=None, Tensor(e!)? cnt_lo=None, bool work_clean=False, Tensor(f!)? zero_first=None) -> ()");
   m.def("assign_bf16_top2(Tensor X, Tensor? rowidx, Tensor Cm2, Tensor cnorm, Tensor(a!) labels, Tensor(b!) mind, Tensor(c!) mind2) -> ()");
   m.def("bounds_filter(Tensor labels, Tensor(a!) ub, Tensor(b!) lb, Tensor drift, Tensor maxdrift, float slack, Tensor(c!) active, Tensor(d!) count) -> ()");
   m.def("bounds_scatter(Tensor active, Tensor count, Tensor blab, Tensor d1, Tensor d2, Tensor(a!) labels, Tensor(b!) ub, Tensor(c!) lb, Tensor(d!) moved_idx, Tensor(e!) moved_old, Tensor(f!) moved_new, Tensor(g!) mcount) -> ()");

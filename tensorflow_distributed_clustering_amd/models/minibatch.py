@@ -117,12 +117,14 @@ class MiniBatchStepper:
         return self.resident and self.device.type == "cuda" and sup is not None and sup()
 
     def step(self):
-        self.buf.zero_()
         if self._indexed():
             idx = torch.randint(self.n_local, (self.batch_rows,), generator=self.gen,
                                 device=self.device, dtype=torch.int32)
-            self.local.step_indexed(self.C, idx, self.blabels, None, self.sums, self.counts)
+            # the all-reduce buffer is cleared by the update's first kernel (no fill launch)
+            self.local.step_indexed(self.C, idx, self.blabels, None, self.sums, self.counts,
+                                    zero_first=self.buf)
         else:
+            self.buf.zero_()
             batch = self.next_batch()
             self.local.bind(batch).step(self.C, self.blabels[: batch.shape[0]], None, self.sums,
                                         self.counts)

@@ -197,13 +197,15 @@ class NativeUpdate:
     def supports_indexed(self) -> bool:
         return self.kind == "sorted" and not self.deterministic
 
-    def indexed(self, x, rowidx, labels, sums, counts):
-        """Partials of the rows ``x[rowidx]`` without gathering them (mini-batches)."""
+    def indexed(self, x, rowidx, labels, sums, counts, zero_first=None):
+        """Partials of the rows ``x[rowidx]`` without gathering them (mini-batches).
+        ``zero_first``: a buffer (the step's all-reduce buffer, holding sums / counts) the
+        first update kernel clears before anything accumulates into it."""
         need = int(self.ops.update_sorted_workspace(rowidx.shape[0], sums.shape[0]))
         if self.work is None or self.work.numel() < need:
             self.work = self._workspace(rowidx.shape[0], sums.shape[0], x.device)
         self.ops.update_sorted_indexed(x, rowidx, labels, sums, counts, self.work,
-                                       *(self.count_split or (None, None)), True)
+                                       *(self.count_split or (None, None)), True, zero_first)
 
 
 # ----------------------------------------------------------------- delta update
@@ -565,11 +567,12 @@ class HipBf16Lloyd(_LocalOpsBase):
     def supports_indexed(self) -> bool:
         return self.dp in (64, 128, 256) and self.update.supports_indexed()
 
-    def step_indexed(self, C, rowidx, labels, mind, sums, counts):
+    def step_indexed(self, C, rowidx, labels, mind, sums, counts, zero_first=None):
         """Assign + partials of the shard rows ``rowidx`` (int32 [B]); the batch is never
-        copied out of the shard (the kernels load row rowidx[i] for point i)."""
+        copied out of the shard (the kernels load row rowidx[i] for point i).
+        ``zero_first``: see NativeUpdate.indexed (sums / counts need no clearing then)."""
         self.ops.assign_bf16_indexed(self.x, rowidx, self.cm2, self.cnorm, labels, mind)
-        self.update.indexed(self.x, rowidx, labels, sums, counts)
+        self.update.indexed(self.x, rowidx, labels, sums, counts, zero_first)
 
     def sculley(self, sums, counts, C, v, shift):
         """Native mini-batch centre update + next-assignment operand prep (one launch)."""

@@ -385,6 +385,13 @@ def test_indexed_assign_and_update(gpu, n, b, d, k):
     s_ref, c_ref = ref.cluster_sums(xb[:, :d].double(), lab_g, k, acc_dtype=torch.float64)
     assert torch.equal(c_i.double(), c_ref)
     torch.testing.assert_close(s_i.double(), s_ref, rtol=1e-4, atol=1e-3)
+    # the mini-batch step's form: [sums | counts] buffer full of stale values, cleared by
+    # the update's first kernel (zero_first) before anything accumulates into it
+    buf = torch.full((k * d + k,), 7.0, dtype=torch.float32, device=gpu)
+    s_z, c_z = buf[: k * d].view(k, d), buf[k * d:]
+    ops.update_sorted_indexed(lo.x, idx, lab_i, s_z, c_z, work, None, None, True, buf)
+    assert torch.equal(c_z.double(), c_ref)
+    torch.testing.assert_close(s_z.double(), s_ref, rtol=1e-4, atol=1e-3)
 
 
 @pytest.mark.parametrize("d,k", [(128, 1024), (128, 64), (100, 300)])
